@@ -1,0 +1,290 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front-ends of the two CPU checkers.
+
+* ``Oracle``: the C restatement (oracle/thcm_oracle.c -> oracle/_build/liboracle.so).
+* ``run_reference``: the reference's own THCM Fortran (compiled in place by
+  oracle/ref/Makefile into oracle/_ref/libthcm_ref.so), driven in a fresh subprocess
+  per configuration because THCM keeps global Fortran module state (a singleton,
+  src/ocean/THCM.H:76-84).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  The product (i-emic_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_ORACLE = os.path.join(HERE, "_build", "liboracle.so")
+LIB_REF = os.path.join(HERE, "_ref", "libthcm_ref.so")
+
+
+def build(ref: bool = True) -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if ref and os.path.isdir("/root/reference/src/ocean"):
+        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "ref")], check=True)
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("n", C.c_int), ("m", C.c_int), ("l", C.c_int),
+                ("xmin_deg", C.c_double), ("xmax_deg", C.c_double),
+                ("ymin_deg", C.c_double), ("ymax_deg", C.c_double),
+                ("periodic", C.c_int), ("hdim", C.c_double), ("qz", C.c_double),
+                ("tres", C.c_int), ("sres", C.c_int), ("ite", C.c_int), ("its", C.c_int),
+                ("iza", C.c_int), ("forcing_type", C.c_int), ("ih", C.c_int),
+                ("vmix", C.c_int), ("coriolis_on", C.c_int), ("alphaT", C.c_double),
+                ("alphaS", C.c_double), ("int_sign", C.c_int), ("nic", C.c_int),
+                ("mic", C.c_int)]
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_ORACLE):
+            build(ref=False)
+        lib = C.CDLL(LIB_ORACLE)
+        lib.orc_create.restype = C.c_void_p
+        lib.orc_create.argtypes = [C.POINTER(_Cfg), C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        lib.orc_destroy.argtypes = [C.c_void_p]
+        lib.orc_set_par.argtypes = [C.c_void_p, C.c_int, C.c_double]
+        lib.orc_get_par.argtypes = [C.c_void_p, C.c_int]
+        lib.orc_get_par.restype = C.c_double
+        lib.orc_nrows.argtypes = [C.c_void_p]
+        lib.orc_rowintcon.argtypes = [C.c_void_p]
+        lib.orc_graph_nnz.argtypes = [C.c_void_p]
+        lib.orc_graph_nnz.restype = C.c_int64
+        lib.orc_graph.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        lib.orc_fortran_matrix.restype = C.c_int64
+        lib.orc_fortran_matrix.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                           C.POINTER(C.c_double)]
+        lib.orc_fortran_rhs.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        lib.orc_jacobian.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_double)]
+        lib.orc_rhs.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        lib.orc_intcond_coeff.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        lib.orc_csr_spmv.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_double)]
+        _lib = lib
+    return _lib
+
+
+def cfg_struct(d: dict) -> _Cfg:
+    return _Cfg(d["n"], d["m"], d["l"], d["xmin_deg"], d["xmax_deg"], d["ymin_deg"],
+                d["ymax_deg"], d["periodic"], d["hdim"], d["qz"], d["tres"], d["sres"],
+                d["ite"], d["its"], d["iza"], d["forcing_type"], d["ih"], d["vmix"],
+                d["coriolis_on"], d["alphaT"], d["alphaS"], d["int_sign"], d["nic"], d["mic"])
+
+
+class Oracle:
+    """C restatement of the THCM hot path (see oracle/thcm_oracle.c)."""
+
+    def __init__(self, cfgdict: dict, landm: np.ndarray, pars=(), spert=None):
+        lib = _load()
+        self.lib = lib
+        self.d = dict(cfgdict)
+        self._cfg = cfg_struct(cfgdict)
+        lm = np.ascontiguousarray(landm, dtype=np.int32)
+        n, m = cfgdict["n"], cfgdict["m"]
+        sp = np.full(n * m, float(cfgdict["sres"])) if spert is None else np.ascontiguousarray(spert, dtype=np.float64)
+        self.h = lib.orc_create(C.byref(self._cfg), _p(lm, C.c_int), _p(sp, C.c_double))
+        if not self.h:
+            raise RuntimeError("orc_create failed")
+        for idx, v in pars:
+            lib.orc_set_par(self.h, int(idx), float(v))
+        self.N = lib.orc_nrows(self.h)
+        self.rowintcon = lib.orc_rowintcon(self.h)
+        nnz = lib.orc_graph_nnz(self.h)
+        self.rowptr = np.zeros(self.N + 1, dtype=np.int64)
+        self.col = np.zeros(nnz, dtype=np.int32)
+        lib.orc_graph(self.h, _p(self.rowptr, C.c_int64), _p(self.col, C.c_int))
+
+    def __del__(self):
+        try:
+            self.lib.orc_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_par(self, idx, v):
+        self.lib.orc_set_par(self.h, int(idx), float(v))
+
+    def get_par(self, idx):
+        return self.lib.orc_get_par(self.h, int(idx))
+
+    def jacobian(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        val = np.zeros(len(self.col))
+        B = np.zeros(self.N)
+        self.lib.orc_jacobian(self.h, _p(x, C.c_double), _p(val, C.c_double), _p(B, C.c_double))
+        return val, B
+
+    def rhs(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        F = np.zeros(self.N)
+        self.lib.orc_rhs(self.h, _p(x, C.c_double), _p(F, C.c_double))
+        return F
+
+    def fortran_rhs(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        B = np.zeros(self.N)
+        self.lib.orc_fortran_rhs(self.h, _p(x, C.c_double), _p(B, C.c_double))
+        return B
+
+    def fortran_matrix(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        nnz = self.lib.orc_fortran_matrix(self.h, _p(x, C.c_double), None, None, None, None)
+        beg = np.zeros(self.N + 1, dtype=np.int32)
+        jco = np.zeros(nnz, dtype=np.int32)
+        co = np.zeros(nnz)
+        coB = np.zeros(self.N)
+        self.lib.orc_fortran_matrix(self.h, _p(x, C.c_double), _p(beg, C.c_int),
+                                    _p(jco, C.c_int), _p(co, C.c_double), _p(coB, C.c_double))
+        return beg, jco, co, coB
+
+    def intcond_coeff(self):
+        c = np.zeros(self.N)
+        self.lib.orc_intcond_coeff(self.h, _p(c, C.c_double))
+        return c
+
+    def spmv(self, val, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(self.N)
+        self.lib.orc_csr_spmv(self.N, _p(self.rowptr, C.c_int64), _p(self.col, C.c_int),
+                              _p(val, C.c_double), _p(x, C.c_double), _p(y, C.c_double))
+        return y
+
+
+# ------------------------------------------------------------------------------------
+# reference (Fortran) runner: one subprocess per configuration
+
+_REF_SCRIPT = r'''
+import ctypes as C, sys, numpy as np
+lib = C.CDLL(sys.argv[1])
+d = np.load(sys.argv[2], allow_pickle=False)
+class Cfg(C.Structure):
+    _fields_ = [(k, t) for k, t in [("n",C.c_int),("m",C.c_int),("l",C.c_int),
+        ("xmin_deg",C.c_double),("xmax_deg",C.c_double),("ymin_deg",C.c_double),("ymax_deg",C.c_double),
+        ("periodic",C.c_int),("hdim",C.c_double),("qz",C.c_double),("itopo",C.c_int),("flat",C.c_int),
+        ("rd_mask",C.c_int),("tres",C.c_int),("sres",C.c_int),("iza",C.c_int),("ite",C.c_int),
+        ("its",C.c_int),("rd_spertm",C.c_int),("coupled_T",C.c_int),("coupled_S",C.c_int),
+        ("forcing_type",C.c_int),("ih",C.c_int),("vmix",C.c_int),("tap",C.c_int),
+        ("rho_mixing",C.c_int),("coriolis_on",C.c_int),("alphaT",C.c_double),("alphaS",C.c_double),
+        ("maskfile",C.c_char*256),("spertfile",C.c_char*256)]]
+cfg = Cfg()
+ints = d["cfg_int"]; dbls = d["cfg_dbl"]
+names_i = ["n","m","l","periodic","itopo","flat","rd_mask","tres","sres","iza","ite","its",
+           "rd_spertm","coupled_T","coupled_S","forcing_type","ih","vmix","tap","rho_mixing","coriolis_on"]
+names_d = ["xmin_deg","xmax_deg","ymin_deg","ymax_deg","hdim","qz","alphaT","alphaS"]
+for k, v in zip(names_i, ints): setattr(cfg, k, int(v))
+for k, v in zip(names_d, dbls): setattr(cfg, k, float(v))
+cfg.maskfile = bytes(d["maskfile"]).rstrip(b"\0")
+cfg.spertfile = b"no_mask_specified"
+landm = np.ascontiguousarray(d["landm"], dtype=np.int32)
+use_landm = bool(d["use_landm"])
+lib.thcmref_init.argtypes = [C.POINTER(Cfg), C.c_void_p]
+rc = lib.thcmref_init(C.byref(cfg), landm.ctypes.data if use_landm else None)
+assert rc == 0, rc
+lib.thcmref_set_par.argtypes = [C.c_int, C.c_double]
+for idx, v in d["pars"]:
+    lib.thcmref_set_par(int(idx), float(v))
+nrows = C.c_int(); cap = C.c_int()
+lib.thcmref_sizes(C.byref(nrows), C.byref(cap))
+N = nrows.value
+out = {}
+L = np.zeros(landm.size, dtype=np.int32)
+lib.thcmref_landm(L.ctypes.data_as(C.c_void_p))
+out["landm_local"] = L
+iv = np.zeros(N, dtype=np.float64); ii = np.zeros(N, dtype=np.int32)
+lib.thcmref_intcond.argtypes = [C.c_void_p, C.c_void_p]
+ln = lib.thcmref_intcond(iv.ctypes.data, ii.ctypes.data)
+out["intcond_val"] = iv[:ln]; out["intcond_ind"] = ii[:ln]
+lib.thcmref_matrix.argtypes = [C.c_void_p] * 5
+lib.thcmref_rhs.argtypes = [C.c_void_p] * 2
+pidx = np.arange(31)
+out["par"] = np.array([0.0] + [0.0]*30)
+lib.thcmref_get_par.restype = C.c_double
+lib.thcmref_get_par.argtypes = [C.c_int]
+for p in range(1, 31):
+    out["par"][p] = lib.thcmref_get_par(p)
+for s in range(int(d["nstates"])):
+    x = np.ascontiguousarray(d["x%d" % s])
+    beg = np.zeros(N + 1, dtype=np.int32); jco = np.zeros(cap.value, dtype=np.int32)
+    co = np.zeros(cap.value); coB = np.zeros(N)
+    nnz = lib.thcmref_matrix(x.ctypes.data, beg.ctypes.data, jco.ctypes.data, co.ctypes.data, coB.ctypes.data)
+    B = np.zeros(N)
+    lib.thcmref_rhs(x.ctypes.data, B.ctypes.data)
+    out["beg%d" % s] = beg; out["jco%d" % s] = jco[:nnz]; out["co%d" % s] = co[:nnz]
+    out["coB%d" % s] = coB; out["B%d" % s] = B
+np.savez(sys.argv[3], **out)
+'''
+
+
+def reference_available() -> bool:
+    return os.path.exists(LIB_REF)
+
+
+def run_reference(cfgdict: dict, landm, pars, states, use_landm: bool = True,
+                  timeout: float = 600.0) -> dict:
+    """Run the reference THCM Fortran (init, setparcs, matrix, rhs) in a fresh process.
+
+    Returns dict with per-state Fortran CSR (beg/jco/co, 1-based), coB, rhs B, the local
+    land mask after init, intcond scaling and par(1..30)."""
+    if not reference_available():
+        raise RuntimeError("reference library not built (make -C oracle ref)")
+    with tempfile.TemporaryDirectory() as td:
+        inp = os.path.join(td, "in.npz")
+        outp = os.path.join(td, "out.npz")
+        ints = [cfgdict[k] for k in ["n", "m", "l", "periodic", "itopo", "flat", "rd_mask", "tres",
+                                     "sres", "iza", "ite", "its", "rd_spertm", "coupled_T",
+                                     "coupled_S", "forcing_type", "ih", "vmix", "tap",
+                                     "rho_mixing", "coriolis_on"]]
+        dbls = [cfgdict[k] for k in ["xmin_deg", "xmax_deg", "ymin_deg", "ymax_deg", "hdim",
+                                     "qz", "alphaT", "alphaS"]]
+        mf = np.frombuffer(cfgdict["maskfile"].encode().ljust(256, b"\0"), dtype=np.uint8)
+        arrs = dict(cfg_int=np.array(ints, dtype=np.int64), cfg_dbl=np.array(dbls),
+                    maskfile=mf, landm=np.ascontiguousarray(landm, dtype=np.int32).reshape(-1),
+                    use_landm=np.array(int(use_landm)),
+                    pars=np.array(list(pars), dtype=np.float64).reshape(-1, 2),
+                    nstates=np.array(len(states)))
+        for s, x in enumerate(states):
+            arrs["x%d" % s] = np.ascontiguousarray(x, dtype=np.float64)
+        np.savez(inp, **arrs)
+        script = os.path.join(td, "run.py")
+        with open(script, "w") as f:
+            f.write(_REF_SCRIPT)
+        subprocess.run([sys.executable, script, LIB_REF, inp, outp], check=True, cwd=td,
+                       timeout=timeout, stdout=subprocess.DEVNULL)
+        with np.load(outp, allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
+
+
+def fortran_to_graph(rowptr, col, beg, jco, co, rowintcon=-1):
+    """Restates THCM.C:1074-1155: place the 1-based Fortran CSR rows into the maximal
+    graph (rows sorted by column); unfilled slots stay explicit zeros."""
+    N = len(rowptr) - 1
+    val = np.zeros(len(col))
+    for r in range(N):
+        if r == rowintcon:
+            continue
+        b, e = int(rowptr[r]), int(rowptr[r + 1])
+        cols = col[b:e]
+        fb, fe = int(beg[r]) - 1, int(beg[r + 1]) - 1
+        fc = jco[fb:fe] - 1
+        pos = np.searchsorted(cols, fc)
+        if np.any(pos >= len(cols)) or np.any(cols[np.minimum(pos, len(cols) - 1)] != fc):
+            raise AssertionError(f"row {r}: Fortran entry outside maximal graph")
+        val[b + pos] = co[fb:fe]
+    return val
