@@ -1,0 +1,179 @@
+/*
+ * assembly.hip -- Jacobian, residual and forcing assembly on the device.
+ *
+ * Replaces the THCM Fortran assembly behind THCM::evaluate (src/ocean/THCM.C:949-1192):
+ *   matrix_ (usrc.F90:432-504) + the C++ copy into the maximal graph (THCM.C:1074-1155)
+ *   -> k_jacobian: one thread per (cell, equation) writes its slots of the stencil-ELL
+ *   rhs_ (usrc.F90:506-586) + sign flip (THCM.C:1003) -> k_rhs: Picard coefficients are
+ *   formed in registers and contracted with the state in fillcolA order (matAvec,
+ *   matetc.F90:147-166); no matrix is stored.
+ *   forcing (forcing.F90:4-218) -> k_forcing (+ k_qint for the flux corrections).
+ * Compiled with -ffp-contract=off: values are bit-identical to the reference.
+ */
+#include "common.h"
+
+namespace iemic {
+
+__device__ __forceinline__ void cell_ijk(const Geo& g, int64_t c, int& i, int& j, int& k)
+{
+    i = (int)(c % g.n) + 1;
+    j = (int)((c / g.n) % g.m) + 1;
+    k = (int)(c / ((int64_t)g.n * g.m)) + 1;
+}
+
+template <int R>
+__device__ __forceinline__ void jac_row(const Geo& g, const double* __restrict__ x, int i, int j,
+                                        int k, int64_t cell, int64_t ncell, int64_t rowintcon,
+                                        double* __restrict__ val)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    double A[NS];
+    bool fz;
+    assemble_row<R, true>(g, x, i, j, k, A, fz);
+    const bool dense_row = (NUN * cell + R) == rowintcon; /* replaced by intcond_S */
+#pragma unroll
+    for (int s = 0; s < NS; s++) val[(int64_t)(B + s) * ncell + cell] = dense_row ? 0.0 : A[s];
+}
+
+__global__ void __launch_bounds__(128) k_jacobian(Geo g, const double* __restrict__ x,
+                                                  double* __restrict__ val, int64_t ncell,
+                                                  int64_t rowintcon)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    int i, j, k;
+    cell_ijk(g, cell, i, j, k);
+    switch (blockIdx.y) {
+    case UU: jac_row<UU>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    case VV: jac_row<VV>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    case WW: jac_row<WW>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    case PP: jac_row<PP>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    case TT: jac_row<TT>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    default: jac_row<SS>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    }
+}
+
+/* fillcolB times Mass (THCM.C:1150-1153), B = 0 at rowintcon */
+__global__ void k_diagB(Geo g, double* __restrict__ B, int64_t ncell, int64_t rowintcon)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    int i, j, k;
+    cell_ijk(g, cell, i, j, k);
+    double b[NUN];
+    diagB_cell(g, i, j, k, b);
+    for (int v = 0; v < NUN; v++) {
+        const int64_t row = NUN * cell + v;
+        B[row] = (row == rowintcon) ? 0.0 : b[v];
+    }
+}
+
+__global__ void __launch_bounds__(128) k_rhs(Geo g, const double* __restrict__ x,
+                                             const double* __restrict__ frc,
+                                             double* __restrict__ F, int64_t ncell)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    int i, j, k;
+    cell_ijk(g, cell, i, j, k);
+    double f;
+    switch (blockIdx.y) {
+    case UU: f = rhs_row_value<UU>(g, x, frc, i, j, k, cell); break;
+    case VV: f = rhs_row_value<VV>(g, x, frc, i, j, k, cell); break;
+    case WW: f = rhs_row_value<WW>(g, x, frc, i, j, k, cell); break;
+    case PP: f = rhs_row_value<PP>(g, x, frc, i, j, k, cell); break;
+    case TT: f = rhs_row_value<TT>(g, x, frc, i, j, k, cell); break;
+    default: f = rhs_row_value<SS>(g, x, frc, i, j, k, cell); break;
+    }
+    F[NUN * cell + blockIdx.y] = f;
+}
+
+/* deterministic block partial sums of a*b (for the intcond dot) */
+__global__ void k_dot_partial(const double* __restrict__ a, const double* __restrict__ b,
+                              int64_t n, double* __restrict__ part)
+{
+    __shared__ double sm[256];
+    double s = 0.0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+         q += (int64_t)gridDim.x * blockDim.x)
+        s += a[q] * b[q];
+    sm[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = sm[0];
+}
+/* F[rowintcon] = intSign*(coeff . x - intCorrection)  (THCM.C:1005-1018) */
+__global__ void k_intcond_finish(const double* __restrict__ part, int nb, double* __restrict__ F,
+                                 int64_t row, int sign)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double s = 0.0;
+        for (int q = 0; q < nb; q++) s += part[q];
+        F[row] = sign * (s - 0.0);
+    }
+}
+
+__global__ void k_qint(Geo g, const double* __restrict__ ftab, double* __restrict__ qcor,
+                       int need_t, int need_s)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    forcing_qint(g, ftab, qcor, need_t, need_s);
+}
+
+__global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* __restrict__ qcor,
+                          double* __restrict__ frc, int64_t ncell)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    int i, j, k;
+    cell_ijk(g, cell, i, j, k);
+    double f[NUN];
+    forcing_cell(g, ftab, qcor, i, j, k, f);
+    for (int v = 0; v < NUN; v++) frc[NUN * cell + v] = f[v];
+}
+
+/* ------------------------------------------------------------------------------------ */
+int assemble_jacobian(iemic_ctx* c, const double* x_dev)
+{
+    Geo g = c->geo();
+    dim3 blk(128), grd((unsigned)((c->ncell + 127) / 128), NUN);
+    hipLaunchKernelGGL(k_jacobian, grd, blk, 0, c->stream, g, x_dev, c->d_val.p, c->ncell,
+                       (int64_t)c->rowintcon);
+    hipLaunchKernelGGL(k_diagB, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0, c->stream,
+                       g, c->d_B.p, c->ncell, (int64_t)c->rowintcon);
+    HIP_OK(hipGetLastError());
+    c->jac_valid = 1;
+    return 0;
+}
+
+int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev)
+{
+    Geo g = c->geo();
+    dim3 blk(128), grd((unsigned)((c->ncell + 127) / 128), NUN);
+    hipLaunchKernelGGL(k_rhs, grd, blk, 0, c->stream, g, x_dev, c->d_frc.p, F_dev, c->ncell);
+    if (c->rowintcon >= 0) {
+        const int nb = 256;
+        hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(256), 0, c->stream, c->d_intc.p, x_dev,
+                           c->nrows, c->d_red.p);
+        hipLaunchKernelGGL(k_intcond_finish, dim3(1), dim3(64), 0, c->stream, c->d_red.p, nb, F_dev,
+                           (int64_t)c->rowintcon, c->cfg.int_sign);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int compute_forcing(iemic_ctx* c)
+{
+    Geo g = c->geo();
+    hipLaunchKernelGGL(k_qint, dim3(1), dim3(64), 0, c->stream, g, c->d_ftab.p, c->d_qcor.p,
+                       c->cfg.tres == 0 ? 1 : 0, c->cfg.sres == 0 ? 1 : 0);
+    hipLaunchKernelGGL(k_forcing, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0,
+                       c->stream, g, c->d_ftab.p, c->d_qcor.p, c->d_frc.p, c->ncell);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace iemic

@@ -1,0 +1,122 @@
+/*
+ * common.h -- device context shared by the assembly, Krylov and preconditioner units.
+ */
+#ifndef IEMIC_COMMON_H
+#define IEMIC_COMMON_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/iemic.h"
+#include "stencil.h"
+#include "host_setup.h"
+
+namespace iemic {
+
+void set_error(const std::string& s);
+
+#define HIP_OK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::iemic::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));     \
+            return IEMIC_EDEVICE;                                                      \
+        }                                                                              \
+    } while (0)
+
+template <typename T> struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t count)
+    {
+        free();
+        n = count;
+        if (count == 0) return 0;
+        if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            n = 0;
+            return IEMIC_ENOMEM;
+        }
+        return 0;
+    }
+    void free()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DevBuf() { free(); }
+};
+
+/* Block Gauss-Seidel preconditioner state (prec.hip). */
+struct BlockGS {
+    int ready = 0;
+    int ncol = 0;                    /* active (ocean) columns                          */
+    DevBuf<int> col_of_ij;           /* (i,j) -> active column index or -1              */
+    DevBuf<int> ij_of_col;           /* active column -> j*n + i                        */
+    DevBuf<int> kb;                  /* deepest ocean layer (1-based) per active column */
+    DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
+    DevBuf<double> dinv;             /* 2x2 inverse of the U/V diagonal block, 4/cell   */
+    DevBuf<double> schur_inv;        /* dense ncol x ncol inverse of the 2-D Schur      */
+    DevBuf<double> schur;            /* dense ncol x ncol Schur (work)                  */
+    DevBuf<int> piv;
+    DevBuf<double> wk1, wk2, wk3, rr; /* N-length work vectors                          */
+    DevBuf<double> colv, colv2;      /* ncol work                                       */
+    int ts_sweeps = 3;
+    int kind = 0;                    /* 1: block-Jacobi, 2: block Gauss-Seidel           */
+};
+
+struct Krylov {
+    int m = 0;                       /* allocated basis size                            */
+    DevBuf<double> V, Z;             /* (m+1) x N and m x N                             */
+    DevBuf<double> w, r, partial, hbuf;
+    double* hhost = nullptr;         /* pinned host copy of dot results                 */
+};
+
+}  // namespace iemic
+
+struct iemic_ctx {
+    iemic_grid cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n = 0, m = 0, l = 0;
+    int64_t ncell = 0, nrows = 0;
+    int rowintcon = -1;
+    iemic::host::Setup su;           /* grid tables, parameters, effective mask */
+    /* device tables */
+    iemic::DevBuf<int> d_landm;
+    iemic::DevBuf<double> d_tab;     /* cos_y | cos_yv | tan_yv | sin_yv | amh_y | bmh_y |
+                                        amh_yv | bmh_yv | bmhy_yv | dfzT | dfzW          */
+    iemic::DevBuf<double> d_ftab;    /* forcing tables wfun(yv), temfun(y), salfun(y), spert */
+    iemic::DevBuf<double> d_frc;     /* Frc (forcing.F90), before boundaries zeroing     */
+    iemic::DevBuf<double> d_qcor;    /* qint corrections                                 */
+    iemic::DevBuf<double> d_intc;    /* intcond coefficients (THCM.C:2549)               */
+    /* state and operator */
+    iemic::DevBuf<double> d_x, d_F, d_B, d_val; /* d_val: NSLOT x ncell                    */
+    iemic::DevBuf<double> d_tmp1, d_tmp2, d_red;
+    int jac_valid = 0;
+    iemic::BlockGS gs;
+    iemic::Krylov kr;
+    iemic::Geo geo() const;
+};
+
+namespace iemic {
+/* assembly.hip */
+int assemble_jacobian(iemic_ctx* c, const double* x_dev);
+int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev);
+int compute_forcing(iemic_ctx* c);
+/* krylov.hip */
+int spmv(iemic_ctx* c, const double* x, double* y, hipStream_t s);
+double dot(iemic_ctx* c, const double* a, const double* b, int64_t n);
+int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
+           iemic_solve_info* info);
+/* prec.hip */
+int prec_compute(iemic_ctx* c, const iemic_krylov* opt);
+int prec_apply(iemic_ctx* c, const double* r, double* z);
+}  // namespace iemic
+
+#endif

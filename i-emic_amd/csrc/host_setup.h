@@ -1,0 +1,246 @@
+/*
+ * host_setup.h -- one-time set-up of the 1-D metric tables, parameters and land mask.
+ *
+ * Restates the serial set-up path of the THCM constructor (src/ocean/THCM.C:178-798):
+ *   init_ border handling of the land mask       usrc.F90:83-107
+ *   grid                                         grid.F90:2-95
+ *   QTnd / QSnd                                  usrc.F90:125-127
+ *   stpnt + vmix_par                             usrc.F90:1136-1180, mix_imp.f vmix_par
+ *   forcing profiles wfun/temfun/salfun          forcing.F90:489-533
+ *   intcond coefficients                         thcm_utils.F90:285-312
+ * Only 1-D tables (length m+2, l+2) and scalars are produced here; they are evaluated
+ * with the same libm the reference uses so that the per-cell device arithmetic is
+ * bit-identical.  Pure C++ (shared by the device library and its CPU unit test).
+ */
+#ifndef IEMIC_HOST_SETUP_H
+#define IEMIC_HOST_SETUP_H
+
+#include <cmath>
+#include <vector>
+
+#include "../../include/iemic.h"
+#include "stencil.h"
+
+namespace iemic {
+namespace host {
+
+constexpr double pi_ = 3.14159265358979323846;     /* par.F90:14, THCM.C PI_ */
+constexpr double omegadim = 7.292e-05, r0dim = 6.37e+06, udim = 0.1e+00, gdim = 9.8e+00;
+constexpr double rhodim = 1.024e+03, deltas = 1.0, s0 = 35.0, cp0 = 4.2e+03;
+constexpr double ah = 2.5e+05, av = 1.0e-03, kappah = 1.0e+03, kappav = 1.0e-04;
+constexpr double zmin = -1.0, zmax = 0.0;
+
+inline double fz(double z, double qz)
+{
+    double th = std::tanh(qz * (z + 1));
+    double tth = std::tanh(qz);
+    if (qz > 1.0) return -1 + th / tth;
+    return z + (1. - qz) * z * (1 - z);
+}
+inline double dfdz(double z, double qz)
+{
+    double ch = std::cosh(qz * (z + 1));
+    double tth = std::tanh(qz);
+    if (qz > 1.0) return qz / (tth * ch * ch);
+    return 1.0 + (1. - qz) * (1. - 2. * z);
+}
+inline double amh(double y, int ih) { return ih == 0 ? 1.0 : 1. + 10.0 * std::exp(-5 * y * y); }
+inline double bmh(double y, int ih) { return ih == 0 ? 1.0 : 1.0 + 10.0 * std::exp(-5 * y * y); }
+inline double bmhy(double y, int ih) { return ih == 0 ? 0.0 : -10. * 10.0 * y * std::exp(-5 * y * y); }
+inline double wfun(double yy)
+{
+    return 0.2 - 0.8 * std::sin(6 * std::fabs(yy)) - 0.5 * (1 - std::tanh(10 * std::fabs(yy))) -
+           0.5 * (1 - std::tanh(10 * (pi_ / 2 - std::fabs(yy))));
+}
+
+struct Setup {
+    iemic_grid cfg;
+    int n = 0, m = 0, l = 0;
+    double xmin = 0, xmax = 0, ymin = 0, ymax = 0, dx = 0, dy = 0, dz = 0;
+    std::vector<double> y, yv, dfzT, dfzW;
+    std::vector<int> landm;          /* local mask after init_ border handling */
+    std::vector<double> tab;         /* Geo table block (see geo())            */
+    double par[31] = {0};
+    double qtnd = 0, qsnd = 0;
+    int rowintcon = -1;
+
+    void init(const iemic_grid& g, const int* landm_in)
+    {
+        cfg = g;
+        n = g.n; m = g.m; l = g.l;
+        xmin = g.xmin * pi_ / 180.0;
+        xmax = g.xmax * pi_ / 180.0;
+        ymin = g.ymin * pi_ / 180.0;
+        ymax = g.ymax * pi_ / 180.0;
+        const size_t nl = (size_t)(n + 2) * (m + 2) * (l + 2);
+        landm.assign(landm_in, landm_in + nl);
+        for (int k = 0; k <= l + 1; k++)
+            for (int j = 0; j <= m + 1; j++)
+                for (int i = 0; i <= n + 1; i++) {
+                    int& v = landm[((size_t)k * (m + 2) + j) * (n + 2) + i];
+                    if (!g.periodic && v == 3) v = OCEAN;
+                    if (!g.periodic && (i == 0 || i == n + 1)) v = LAND;
+                    if (j == 0 || j == m + 1 || k == 0 || k == l + 1) v = LAND;
+                }
+        rowintcon = -1;
+        if (g.sres == 0) {
+            int Nic = g.int_i == -1 ? n - 1 : g.int_i;
+            int Mic = g.int_j == -1 ? m - 1 : g.int_j;
+            rowintcon = NUN * ((l - 1) * n * m + n * Mic + Nic) + SS;
+        }
+        grid();
+        stpnt();
+    }
+
+    void grid()
+    {
+        const int M2 = m + 2;
+        dx = (xmax - xmin) / n;
+        dy = (ymax - ymin) / m;
+        dz = (zmax - zmin) / l;
+        y.assign(M2, 0.0);
+        yv.assign(M2, 0.0);
+        for (int j = 1; j <= m; j++) {
+            y[j] = ((double)j - 0.5) * dy + ymin;
+            yv[j] = ((double)j) * dy + ymin;
+        }
+        y[0] = y[1] - dy;
+        y[m + 1] = y[m] + dy;
+        yv[0] = ymin;
+        dfzT.assign(l + 2, 0.0);
+        dfzW.assign(l + 2, 0.0);
+        for (int k = 1; k <= l; k++) {
+            double ze = ((double)k - 0.5) * dz + zmin;
+            double zwe = ((double)k) * dz + zmin;
+            dfzT[k] = dfdz(ze, cfg.qz);
+            dfzW[k] = dfdz(zwe, cfg.qz);
+        }
+        dfzW[0] = dfdz(zmin, cfg.qz);
+        const int ih = cfg.ih;
+        tab.assign((size_t)9 * M2 + 2 * (l + 2), 0.0);
+        for (int j = 0; j <= m + 1; j++) {
+            tab[j] = std::cos(y[j]);
+            tab[4 * M2 + j] = amh(y[j], ih);
+            tab[5 * M2 + j] = bmh(y[j], ih);
+        }
+        for (int j = 0; j <= m; j++) {
+            tab[M2 + j] = std::cos(yv[j]);
+            tab[2 * M2 + j] = std::tan(yv[j]);
+            tab[3 * M2 + j] = std::sin(yv[j]);
+            tab[6 * M2 + j] = amh(yv[j], ih);
+            tab[7 * M2 + j] = bmh(yv[j], ih);
+            tab[8 * M2 + j] = bmhy(yv[j], ih);
+        }
+        for (int k = 0; k <= l + 1; k++) {
+            tab[9 * M2 + k] = dfzT[k];
+            tab[9 * M2 + (l + 2) + k] = dfzW[k];
+        }
+        double dzne = dz * dfzT[l];
+        qtnd = r0dim / (udim * cp0 * rhodim * cfg.hdim * dzne);
+        qsnd = s0 * r0dim / (deltas * udim * cfg.hdim * dzne);
+    }
+
+    void stpnt()
+    {
+        const double hdim = cfg.hdim;
+        par[P_AL_T] = 0.1 / (2 * omegadim * rhodim * hdim * udim * dz * dfzT[l]);
+        par[P_RAYL] = cfg.alpha_t * gdim * hdim / (2 * omegadim * udim * r0dim);
+        par[P_EK_V] = av / (2 * omegadim * hdim * hdim);
+        par[P_EK_H] = ah / (2 * omegadim * r0dim * r0dim);
+        par[P_ROSB] = udim / (2 * omegadim * r0dim);
+        par[P_HMTP] = 0.0;
+        par[P_SUNP] = 0.0;
+        par[P_PE_H] = kappah / (udim * r0dim);
+        par[P_PE_V] = kappav * r0dim / (udim * hdim * hdim);
+        par[P_P_VC] = 2.5e+04 * par[P_PE_V];
+        par[P_LAMB] = cfg.alpha_s / cfg.alpha_t;
+        par[P_SALT] = 0.0;
+        par[P_WIND] = 0.0;
+        par[P_TEMP] = 0.0;
+        par[P_BIOT] = r0dim / (75. * 3600. * 24. * udim);
+        par[P_COMB] = 0.0;
+        par[P_NLES] = 0.0;
+        par[P_CMPR] = 0.0;
+        par[P_ALPC] = 1.0;
+        par[P_ENER] = 1.0e+02;
+        par[P_MIXP] = 0.0;
+        par[P_MKAP] = 0.0;
+        par[P_SPL1] = 2.0e+03;
+        par[P_SPL2] = 0.01;
+        if (cfg.vmix == 0) {
+            par[P_MIXP] = 0.0;
+            par[P_P_VC] = 0.0;
+            par[P_ALPC] = 1.0;
+            par[P_ENER] = 1.0e+2;
+            par[P_MKAP] = 0.0;
+        }
+    }
+
+    /* [wfun(yv) | temfun(y) | salfun(y) | spert(n*m)] for the current par (forcing.F90) */
+    std::vector<double> forcing_tables() const
+    {
+        const int M2 = m + 2;
+        std::vector<double> t((size_t)3 * M2 + (size_t)n * m, 0.0);
+        for (int j = 0; j <= m; j++) t[j] = wfun(yv[j]);
+        for (int j = 0; j <= m + 1; j++) {
+            double yy = y[j];
+            double tf, sf;
+            if (cfg.forcing_type == 2) {
+                tf = std::cos(pi_ * (yy - ymin) / (ymax - ymin));
+                sf = tf;
+            } else {
+                tf = std::cos(pi_ * yy / ymax) + par[P_CMPR] * std::sin(pi_ * yy / ymax);
+                if (cfg.forcing_type == 1)
+                    sf = (std::cos(pi_ * yy / ymax) + par[P_FPER] * yy / ymax) / std::cos(yy);
+                else
+                    sf = std::cos(pi_ * yy / ymax) + par[P_FPER] * yy / ymax;
+            }
+            t[M2 + j] = tf;
+            t[2 * M2 + j] = sf;
+        }
+        /* spert = real(SRES) (global.F90:590-611, no perturbation mask) */
+        for (int q = 0; q < n * m; q++) t[3 * M2 + q] = (double)cfg.sres;
+        return t;
+    }
+
+    std::vector<double> intcond_coeff() const
+    {
+        std::vector<double> ic((size_t)NUN * n * m * l, 0.0);
+        for (int k = 1; k <= l; k++)
+            for (int j = 1; j <= m; j++)
+                for (int i = 1; i <= n; i++)
+                    if (landm[((size_t)k * (m + 2) + j) * (n + 2) + i] == OCEAN)
+                        ic[(size_t)NUN * (((size_t)(k - 1) * m + (j - 1)) * n + (i - 1)) + SS] =
+                            std::cos(y[j]) * dfzT[k];
+        return ic;
+    }
+
+    /* Geo over externally owned copies of landm / tab */
+    Geo geo(const int* landm_p, const double* tab_p) const
+    {
+        Geo g{};
+        g.n = n; g.m = m; g.l = l;
+        g.periodic = cfg.periodic;
+        g.tres = cfg.tres; g.sres = cfg.sres; g.coriolis_on = cfg.coriolis_on;
+        g.dx = dx; g.dy = dy; g.dz = dz;
+        g.landm = landm_p;
+        const int M2 = m + 2;
+        g.cos_y = tab_p;
+        g.cos_yv = tab_p + M2;
+        g.tan_yv = tab_p + 2 * M2;
+        g.sin_yv = tab_p + 3 * M2;
+        g.amh_y = tab_p + 4 * M2;
+        g.bmh_y = tab_p + 5 * M2;
+        g.amh_yv = tab_p + 6 * M2;
+        g.bmh_yv = tab_p + 7 * M2;
+        g.bmhy_yv = tab_p + 8 * M2;
+        g.dfzT = tab_p + 9 * M2;
+        g.dfzW = tab_p + 9 * M2 + (l + 2);
+        for (int i = 0; i < 31; i++) g.par[i] = par[i];
+        return g;
+    }
+};
+
+}  // namespace host
+}  // namespace iemic
+#endif

@@ -1,0 +1,373 @@
+/*
+ * krylov.hip -- stencil-ELL SpMV and the flexible GMRES driver.
+ *
+ *  - k_spmv replaces Epetra_CrsMatrix::Apply (Ocean::applyMatrix, src/ocean/Ocean.C:1352-1357)
+ *    on the maximal graph: one thread per cell computes its 6 rows from 104 slot-major
+ *    values (coalesced) and implicit neighbour columns.  The dense integral-condition row
+ *    (SRES = 0, THCM.C:2121-2198) is a separate fused dot.
+ *  - fgmres restates Belos BlockGmresSolMgr as configured by Ocean::initializeBelos
+ *    (Ocean.C:961-1020): flexible (right) preconditioning, x0 = 0, residual relative to
+ *    ||b|| (the preconditioned initial residual for right preconditioning), classical
+ *    Gram-Schmidt with one full re-orthogonalisation pass (DGKS-like), Givens updates of
+ *    the least-squares problem, restarts, and the explicit residual check of
+ *    Ocean::solve (Ocean.C:1140-1150).
+ */
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+
+#include "common.h"
+
+namespace iemic {
+
+/* ---- SpMV ------------------------------------------------------------------------ */
+template <int R>
+__device__ __forceinline__ double row_dot(const double* __restrict__ val, const double* __restrict__ x,
+                                          int64_t cell, int64_t ncell, const int64_t* nb)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const Slot sl = SLOTS[B + s];
+        const int o = (sl.dk + 1) * 9 + (sl.dj + 1) * 3 + (sl.di + 1);
+        acc += val[(int64_t)(B + s) * ncell + cell] * x[NUN * nb[o] + sl.var];
+    }
+    return acc;
+}
+
+/* neighbour cell index for the 27 offsets; out-of-domain -> own cell (value slot is 0) */
+__device__ __forceinline__ void neighbours(int n, int m, int l, int periodic, int64_t cell,
+                                           int64_t* nb)
+{
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    int ii[3], jj[3], kk[3];
+    ii[0] = i - 1; ii[1] = i; ii[2] = i + 1;
+    if (periodic) {
+        if (ii[0] < 0) ii[0] = n - 1;
+        if (ii[2] >= n) ii[2] = 0;
+    } else {
+        if (ii[0] < 0) ii[0] = i;
+        if (ii[2] >= n) ii[2] = i;
+    }
+    jj[0] = j > 0 ? j - 1 : j; jj[1] = j; jj[2] = j < m - 1 ? j + 1 : j;
+    kk[0] = k > 0 ? k - 1 : k; kk[1] = k; kk[2] = k < l - 1 ? k + 1 : k;
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++)
+#pragma unroll
+            for (int d = 0; d < 3; d++)
+                nb[a * 9 + b * 3 + d] = ((int64_t)kk[a] * m + jj[b]) * n + ii[d];
+}
+
+__global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic,
+                                              const double* __restrict__ val,
+                                              const double* __restrict__ x,
+                                              double* __restrict__ y, int64_t ncell)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    int64_t nb[27];
+    neighbours(n, m, l, periodic, cell, nb);
+    double r0 = row_dot<UU>(val, x, cell, ncell, nb);
+    double r1 = row_dot<VV>(val, x, cell, ncell, nb);
+    double r2 = row_dot<WW>(val, x, cell, ncell, nb);
+    double r3 = row_dot<PP>(val, x, cell, ncell, nb);
+    double r4 = row_dot<TT>(val, x, cell, ncell, nb);
+    double r5 = row_dot<SS>(val, x, cell, ncell, nb);
+    double* yc = y + NUN * cell;
+    yc[0] = r0; yc[1] = r1; yc[2] = r2; yc[3] = r3; yc[4] = r4; yc[5] = r5;
+}
+
+/* ---- reductions / BLAS-1 ------------------------------------------------------------ */
+constexpr int RED_BLOCKS = 512;
+
+__device__ __forceinline__ double block_sum(double v, double* sm)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sm[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += sm[w];
+    return t;
+}
+
+/* partial[i * gridDim.x + blk] = sum over the block's range of V_i . w, i < nvec */
+__global__ void __launch_bounds__(256) k_mdot(const double* __restrict__ V, int64_t ldv, int nvec,
+                                              const double* __restrict__ w, int64_t N,
+                                              double* __restrict__ partial)
+{
+    __shared__ double sm[8];
+    const int i = blockIdx.y;
+    if (i >= nvec) return;
+    const double* vi = V + (int64_t)i * ldv;
+    double s = 0.0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x)
+        s += vi[q] * w[q];
+    double t = block_sum(s, sm);
+    if (threadIdx.x == 0) partial[(int64_t)i * gridDim.x + blockIdx.x] = t;
+}
+/* out[i] = sum_b partial[i*nb + b]  (fixed order: deterministic) */
+__global__ void k_mdot_final(const double* __restrict__ partial, int nb, int nvec,
+                             double* __restrict__ out)
+{
+    __shared__ double sm[8];
+    const int i = blockIdx.x;
+    if (i >= nvec) return;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) s += partial[(int64_t)i * nb + b];
+    double t = block_sum(s, sm);
+    if (threadIdx.x == 0) out[i] = t;
+}
+/* w -= sum_i h_i V_i */
+__global__ void __launch_bounds__(256) k_mupdate(const double* __restrict__ V, int64_t ldv, int nvec,
+                                                 const double* __restrict__ h,
+                                                 double* __restrict__ w, int64_t N)
+{
+    __shared__ double hs[1024];
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) hs[i] = h[i];
+    __syncthreads();
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = w[q];
+        for (int i = 0; i < nvec; i++) acc -= hs[i] * V[(int64_t)i * ldv + q];
+        w[q] = acc;
+    }
+}
+/* x += sum_i y_i Z_i */
+__global__ void __launch_bounds__(256) k_mupdate_add(const double* __restrict__ Z, int64_t ldz, int nvec,
+                                                     const double* __restrict__ y,
+                                                     double* __restrict__ x, int64_t N)
+{
+    __shared__ double ys[1024];
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) ys[i] = y[i];
+    __syncthreads();
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = x[q];
+        for (int i = 0; i < nvec; i++) acc += ys[i] * Z[(int64_t)i * ldz + q];
+        x[q] = acc;
+    }
+}
+__global__ void k_scale_copy(const double* __restrict__ a, double s, double* __restrict__ b, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x)
+        b[q] = s * a[q];
+}
+__global__ void k_axpby(double a, const double* __restrict__ x, double b, const double* __restrict__ y,
+                        double* __restrict__ out, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x)
+        out[q] = a * x[q] + b * y[q];
+}
+
+static inline unsigned grid_for(int64_t N)
+{
+    int64_t b = (N + 255) / 256;
+    return (unsigned)std::min<int64_t>(b, 2048);
+}
+
+int spmv(iemic_ctx* c, const double* x, double* y, hipStream_t s)
+{
+    if (!c->jac_valid) {
+        set_error("spmv: no Jacobian assembled");
+        return IEMIC_ESTATE;
+    }
+    hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0, s, c->n,
+                       c->m, c->l, c->cfg.periodic, c->d_val.p, x, y, c->ncell);
+    if (c->rowintcon >= 0) {
+        /* dense intcond row: y[rowintcon] = intSign * coeff . x */
+        hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, 1), dim3(256), 0, s, c->d_intc.p, (int64_t)0, 1,
+                           x, c->nrows, c->d_red.p);
+        hipLaunchKernelGGL(k_mdot_final, dim3(1), dim3(256), 0, s, c->d_red.p, RED_BLOCKS, 1,
+                           c->d_red.p + RED_BLOCKS);
+        hipLaunchKernelGGL(k_scale_copy, dim3(1), dim3(1), 0, s, c->d_red.p + RED_BLOCKS,
+                           (double)c->cfg.int_sign, y + c->rowintcon, (int64_t)1);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+/* dot products of nvec vectors V_i (stride ldv) with w; result on host in out[] */
+static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const double* w,
+                     double* out)
+{
+    const int64_t N = c->nrows;
+    hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec), dim3(256), 0, c->stream, V, ldv, nvec, w, N,
+                       c->kr.partial.p);
+    hipLaunchKernelGGL(k_mdot_final, dim3(nvec), dim3(256), 0, c->stream, c->kr.partial.p, RED_BLOCKS,
+                       nvec, c->kr.hbuf.p);
+    HIP_OK(hipMemcpyAsync(c->kr.hhost, c->kr.hbuf.p, sizeof(double) * nvec, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < nvec; i++) out[i] = c->kr.hhost[i];
+    return 0;
+}
+
+double dot(iemic_ctx* c, const double* a, const double* b, int64_t n)
+{
+    (void)n;
+    double r = 0.0;
+    if (mdot_host(c, a, 0, 1, b, &r)) return NAN;
+    return r;
+}
+
+static int ensure_krylov(iemic_ctx* c, int m)
+{
+    if (c->kr.m >= m && c->kr.V.p) return 0;
+    const int64_t N = c->nrows;
+    int rc = 0;
+    rc |= c->kr.V.alloc((size_t)(m + 1) * N);
+    rc |= c->kr.Z.alloc((size_t)m * N);
+    rc |= c->kr.w.alloc(N);
+    rc |= c->kr.r.alloc(N);
+    rc |= c->kr.partial.alloc((size_t)RED_BLOCKS * (m + 2));
+    rc |= c->kr.hbuf.alloc(m + 2);
+    if (rc) {
+        set_error("fgmres: out of device memory for the Krylov basis");
+        return IEMIC_ENOMEM;
+    }
+    if (c->kr.hhost) (void)hipHostFree(c->kr.hhost);
+    HIP_OK(hipHostMalloc(&c->kr.hhost, sizeof(double) * (m + 2)));
+    c->kr.m = m;
+    return 0;
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
+{
+    const int m = std::max(1, std::min(opt->krylov_dim, 1000));
+    const int64_t N = c->nrows;
+    int rc = ensure_krylov(c, m);
+    if (rc) return rc;
+    iemic_solve_info inf{};
+    auto T0 = std::chrono::steady_clock::now();
+    double* V = c->kr.V.p;
+    double* Z = c->kr.Z.p;
+    double* w = c->kr.w.p;
+    double* r = c->kr.r.p;
+    const unsigned G = grid_for(N);
+    std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
+
+    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * N, c->stream));
+    double bnorm = std::sqrt(std::max(0.0, dot(c, b, b, N)));
+    if (!(bnorm > 0)) {
+        inf.converged = 1;
+        if (info) *info = inf;
+        return 0;
+    }
+    /* r = b (x0 = 0) */
+    HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+    double beta = bnorm, res = 1.0;
+    int it = 0;
+    for (int cycle = 0; cycle <= opt->max_restarts; cycle++) {
+        hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r, 1.0 / beta, V, N);
+        std::fill(g.begin(), g.end(), 0.0);
+        g[0] = beta;
+        int j = 0;
+        bool conv = false;
+        for (; j < m; j++) {
+            double* vj = V + (int64_t)j * N;
+            double* zj = Z + (int64_t)j * N;
+            double* vn = V + (int64_t)(j + 1) * N;
+            auto tp = std::chrono::steady_clock::now();
+            if (opt->prec > 0) {
+                rc = prec_apply(c, vj, zj);
+                if (rc) return rc;
+            } else {
+                HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+            }
+            HIP_OK(hipStreamSynchronize(c->stream));
+            inf.t_prec_ms += ms_since(tp);
+            tp = std::chrono::steady_clock::now();
+            rc = spmv(c, zj, vn, c->stream);
+            if (rc) return rc;
+            HIP_OK(hipStreamSynchronize(c->stream));
+            inf.t_spmv_ms += ms_since(tp);
+            tp = std::chrono::steady_clock::now();
+            /* CGS2 */
+            rc = mdot_host(c, V, N, j + 1, vn, h.data());
+            if (rc) return rc;
+            HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, h.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice,
+                                  c->stream));
+            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1, c->kr.hbuf.p, vn, N);
+            rc = mdot_host(c, V, N, j + 1, vn, h2.data());
+            if (rc) return rc;
+            HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, h2.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice,
+                                  c->stream));
+            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1, c->kr.hbuf.p, vn, N);
+            for (int i = 0; i <= j; i++) h[i] += h2[i];
+            double hn2 = 0.0;
+            rc = mdot_host(c, vn, 0, 1, vn, &hn2);
+            if (rc) return rc;
+            double hn = std::sqrt(std::max(0.0, hn2));
+            if (hn > 0)
+                hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn, 1.0 / hn, vn, N);
+            inf.t_orth_ms += ms_since(tp);
+            for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
+            H[(size_t)(j + 1) * m + j] = hn;
+            for (int i = 0; i < j; i++) {
+                double a = H[(size_t)i * m + j], bb = H[(size_t)(i + 1) * m + j];
+                H[(size_t)i * m + j] = cs[i] * a + sn[i] * bb;
+                H[(size_t)(i + 1) * m + j] = -sn[i] * a + cs[i] * bb;
+            }
+            double a = H[(size_t)j * m + j], bb = H[(size_t)(j + 1) * m + j];
+            double d = std::sqrt(a * a + bb * bb);
+            cs[j] = d > 0 ? a / d : 1.0;
+            sn[j] = d > 0 ? bb / d : 0.0;
+            H[(size_t)j * m + j] = d;
+            H[(size_t)(j + 1) * m + j] = 0.0;
+            g[j + 1] = -sn[j] * g[j];
+            g[j] = cs[j] * g[j];
+            res = std::fabs(g[j + 1]) / bnorm;
+            it++;
+            if (res <= opt->tol || hn == 0.0) {
+                j++;
+                conv = true;
+                break;
+            }
+        }
+        /* y = H \ g ; x += Z y */
+        int k = j;
+        for (int i = k - 1; i >= 0; i--) {
+            double t = g[i];
+            for (int q = i + 1; q < k; q++) t -= H[(size_t)i * m + q] * y[q];
+            y[i] = t / H[(size_t)i * m + i];
+        }
+        HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, y.data(), sizeof(double) * k, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z, N, k, c->kr.hbuf.p, x, N);
+        if (conv || cycle == opt->max_restarts) break;
+        /* r = b - J x */
+        rc = spmv(c, x, r, c->stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, r, r, N);
+        beta = std::sqrt(std::max(0.0, dot(c, r, r, N)));
+        res = beta / bnorm;
+        if (res <= opt->tol) break;
+    }
+    /* explicit residual (Ocean.C:1140-1150) */
+    rc = spmv(c, x, w, c->stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, w, w, N);
+    double e2 = dot(c, w, w, N);
+    inf.iters = it;
+    inf.implicit_rel_res = res;
+    inf.explicit_rel_res = std::sqrt(std::max(0.0, e2)) / bnorm;
+    inf.converged = res <= opt->tol;
+    inf.t_total_ms = ms_since(T0);
+    HIP_OK(hipGetLastError());
+    if (info) *info = inf;
+    return 0;
+}
+
+}  // namespace iemic

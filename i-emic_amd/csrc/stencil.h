@@ -1,0 +1,971 @@
+/*
+ * stencil.h -- THCM 6-DOF stencil on the device "stencil-ELL" layout.
+ *
+ * One row of the Jacobian (or of the Picard operator used by the residual) is computed
+ * per (cell, variable) directly into its slots of the reference's maximal graph
+ * (src/ocean/THCM.C:2241-2539), without ever materialising the Fortran An(27,6,6,cell)
+ * array.  The arithmetic restates, operation by operation, the atoms of
+ * src/ocean/spf.F90, lin/nlin_jac/nlin_rhs of src/ocean/usrc.F90:588-995, usol
+ * (usrc.F90:997-1104), boundaries (src/ocean/boundary.F90:2-393) and the fillcolA
+ * threshold (assemble.F90:115), so that values are bit-identical to the reference
+ * compiled without FMA contraction.  Compile with -ffp-contract=off.
+ *
+ * Layout: slot-major SoA, val[slot * ncell + cell] (coalesced across cells).  Slot order
+ * inside a row is the insertion order of THCM::CreateMaximalGraph; 104 slots per cell
+ * (U 24, V 22, W 7, P 11, T 20, S 20).  Column indices are implicit: (di,dj,dk,var)
+ * relative to the cell, periodic wrap in x.
+ */
+#ifndef IEMIC_STENCIL_H
+#define IEMIC_STENCIL_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define HD __host__ __device__ __forceinline__
+#else
+#define HD inline
+#endif
+
+namespace iemic {
+
+enum { UU = 0, VV = 1, WW = 2, PP = 3, TT = 4, SS = 5 };  /* 0-based (par.F90:70-75 minus 1) */
+enum { OCEAN = 0, LAND = 1 };
+constexpr int NUN = 6;
+constexpr int NSLOT = 104;
+
+/* par.F90:38-67 */
+enum { P_AL_T = 1, P_RAYL, P_EK_V, P_EK_H, P_ROSB, P_MIXP, P_RESC, P_SPL1, P_HMTP, P_SUNP,
+       P_PE_H, P_PE_V, P_P_VC, P_LAMB, P_SALT, P_WIND, P_TEMP, P_BIOT, P_COMB, P_ARCL,
+       P_NLES, P_IFRICB, P_CONT, P_ENER, P_ALPC, P_CMPR, P_FPER, P_SPER, P_MKAP, P_SPL2 };
+
+/* usr.F90:150-152 */
+constexpr double ALPT1 = 2.93, ALPT2 = 8.3e-02, ALPT3 = 6.6e-04;
+
+struct Slot { int8_t di, dj, dk, var; };
+
+/* THCM::CreateMaximalGraph insertion order (THCM.C:2298-2482) */
+constexpr Slot SLOTS[NSLOT] = {
+    /* U row (24) */
+    {0,0,0,UU},{-1,0,0,UU},{1,0,0,UU},{0,-1,0,UU},{0,1,0,UU},{0,0,-1,UU},{0,0,1,UU},
+    {0,0,0,VV},{-1,0,0,VV},{1,0,0,VV},{0,-1,0,VV},{0,1,0,VV},
+    {0,0,0,WW},{1,0,0,WW},{1,1,0,WW},{0,1,0,WW},{0,0,-1,WW},{1,0,-1,WW},{1,1,-1,WW},{0,1,-1,WW},
+    {0,0,0,PP},{1,0,0,PP},{0,1,0,PP},{1,1,0,PP},
+    /* V row (22) */
+    {0,0,0,VV},{-1,0,0,VV},{1,0,0,VV},{0,-1,0,VV},{0,1,0,VV},{0,0,-1,VV},{0,0,1,VV},
+    {0,0,0,UU},{-1,0,0,UU},{1,0,0,UU},
+    {0,0,0,WW},{1,0,0,WW},{1,1,0,WW},{0,1,0,WW},{0,0,-1,WW},{1,0,-1,WW},{1,1,-1,WW},{0,1,-1,WW},
+    {0,0,0,PP},{1,0,0,PP},{0,1,0,PP},{1,1,0,PP},
+    /* W row (7) */
+    {0,0,0,WW},{0,0,0,PP},{0,0,1,PP},{0,0,0,TT},{0,0,1,TT},{0,0,0,SS},{0,0,1,SS},
+    /* P row (11) */
+    {0,0,0,PP},{0,0,0,UU},{-1,0,0,UU},{0,-1,0,UU},{-1,-1,0,UU},
+    {0,0,0,VV},{-1,0,0,VV},{0,-1,0,VV},{-1,-1,0,VV},{0,0,0,WW},{0,0,-1,WW},
+    /* T row (20) */
+    {0,0,0,TT},{-1,0,0,TT},{1,0,0,TT},{0,-1,0,TT},{0,1,0,TT},{0,0,-1,TT},{0,0,1,TT},
+    {0,0,0,UU},{-1,0,0,UU},{-1,-1,0,UU},{0,-1,0,UU},
+    {0,0,0,VV},{-1,0,0,VV},{-1,-1,0,VV},{0,-1,0,VV},{0,0,0,WW},{0,0,-1,WW},
+    {0,0,0,SS},{0,0,-1,SS},{0,0,1,SS},
+    /* S row (20) */
+    {0,0,0,SS},{-1,0,0,SS},{1,0,0,SS},{0,-1,0,SS},{0,1,0,SS},{0,0,-1,SS},{0,0,1,SS},
+    {0,0,0,UU},{-1,0,0,UU},{-1,-1,0,UU},{0,-1,0,UU},
+    {0,0,0,VV},{-1,0,0,VV},{-1,-1,0,VV},{0,-1,0,VV},{0,0,0,WW},{0,0,-1,WW},
+    {0,0,0,TT},{0,0,-1,TT},{0,0,1,TT},
+};
+constexpr int ROW_BEGIN[NUN + 1] = {0, 24, 46, 53, 64, 84, 104};
+
+/* Fortran stencil position kk (1..27) of an offset (assemble.F90:142-179) */
+HD constexpr int pos_of(int di, int dj, int dk)
+{
+    return (dk == 0 ? 0 : (dk < 0 ? 9 : 18)) + 3 * (di + 1) + (dj + 1) + 1;
+}
+/* slot index (global 0..103) of (row, position, column var), or -1 */
+HD constexpr int slot_of(int row, int pos, int col)
+{
+    for (int s = ROW_BEGIN[row]; s < ROW_BEGIN[row + 1]; s++)
+        if (SLOTS[s].var == col && pos_of(SLOTS[s].di, SLOTS[s].dj, SLOTS[s].dk) == pos) return s;
+    return -1;
+}
+/* rank of a slot in fillcolA order (kk ascending, column var ascending) within its row */
+HD constexpr int fortran_rank(int s)
+{
+    int row = 0;
+    while (s >= ROW_BEGIN[row + 1]) row++;
+    int key = pos_of(SLOTS[s].di, SLOTS[s].dj, SLOTS[s].dk) * 8 + SLOTS[s].var;
+    int r = 0;
+    for (int t = ROW_BEGIN[row]; t < ROW_BEGIN[row + 1]; t++) {
+        int kt = pos_of(SLOTS[t].di, SLOTS[t].dj, SLOTS[t].dk) * 8 + SLOTS[t].var;
+        if (kt < key) r++;
+    }
+    return r;
+}
+
+/* ---- per-context geometry (grid.F90, usrc.F90 stpnt/init) ------------------------- */
+struct Geo {
+    int n, m, l;                    /* local (sub)domain                                */
+    int periodic;
+    int tres, sres, coriolis_on;
+    double dx, dy, dz;
+    const int* landm;               /* (0:n+1,0:m+1,0:l+1), i fastest                   */
+    /* per-j tables (index j = 0..m+1; yv-based ones valid 0..m) */
+    const double* cos_y;            /* cos(y(j))                                        */
+    const double* cos_yv;           /* cos(yv(j))                                       */
+    const double* tan_yv;           /* tan(yv(j))                                       */
+    const double* sin_yv;           /* sin(yv(j))                                       */
+    const double* amh_y;            /* amh(y(j),ih)                                     */
+    const double* bmh_y;
+    const double* amh_yv;
+    const double* bmh_yv;
+    const double* bmhy_yv;
+    /* per-k tables */
+    const double* dfzT;             /* dfzT(k), k = 1..l (index 0 unused)               */
+    const double* dfzW;             /* dfzW(k), k = 0..l                                */
+    double par[31];                 /* par(1..30)                                       */
+};
+
+HD int LM(const Geo& g, int i, int j, int k)
+{
+    return g.landm[((int64_t)k * (g.m + 2) + j) * (g.n + 2) + i];
+}
+/* 0-based row of variable v at 1-based (i,j,k) (find_row2, matetc.F90:123) */
+HD int64_t frow(const Geo& g, int i, int j, int k, int v)
+{
+    return (int64_t)NUN * (((int64_t)(k - 1) * g.m + (j - 1)) * g.n + (i - 1)) + v;
+}
+
+/* ---- usol (usrc.F90:997-1104): padded staggered state, closed forms ---------------- */
+HD bool land_in(const Geo& g, int i, int j, int k)
+{
+    return i >= 1 && i <= g.n && j >= 1 && j <= g.m && k >= 1 && k <= g.l && LM(g, i, j, k) == 1;
+}
+/* u, v arrays: (0:n,0:m,0:l+1) */
+HD double uv_arr(const Geo& g, const double* x, int var, int i, int j, int k)
+{
+    const int n = g.n, m = g.m, l = g.l;
+    double v = 0.0;
+    auto after3 = [&](int ii, int jj, int kk) -> double {
+        /* value of u(ii,jj,kk) after steps 1-3, 1<=ii<=n, 1<=jj<=m, 1<=kk<=l */
+        if (jj == m) return 0.0;
+        if (!g.periodic && ii == n) return 0.0;
+        return x[frow(g, ii, jj, kk, var)];
+    };
+    if (i >= 1 && i <= n && j >= 1 && j <= m && k >= 1 && k <= l) v = after3(i, j, k);
+    else if (i == 0 && j >= 1 && j <= m && k >= 1 && k <= l)
+        v = g.periodic ? x[frow(g, n, j, k, var)] : 0.0;
+    else if (i >= 1 && i <= n && j >= 1 && j <= m && (k == 0 || k == l + 1))
+        v = after3(i, j, k == 0 ? 1 : l);
+    else v = 0.0;
+    if (k >= 1 && k <= l &&
+        (land_in(g, i, j, k) || land_in(g, i + 1, j, k) || land_in(g, i, j + 1, k) ||
+         land_in(g, i + 1, j + 1, k)))
+        v = 0.0;
+    return v;
+}
+/* w array: (0:n+1,0:m+1,0:l) */
+HD double w_arr(const Geo& g, const double* x, int i, int j, int k)
+{
+    const int n = g.n, m = g.m, l = g.l;
+    if (j < 1 || j > m || k < 1 || k > l) return 0.0;
+    if (i >= 1 && i <= n) return k == l ? 0.0 : x[frow(g, i, j, k, WW)];
+    if (g.periodic && i == 0) return x[frow(g, n, j, k, WW)];
+    if (g.periodic && i == n + 1) return x[frow(g, 1, j, k, WW)];
+    return 0.0;
+}
+/* t, s arrays: (0:n+1,0:m+1,0:l+1) */
+HD double ts_arr(const Geo& g, const double* x, int var, int i, int j, int k)
+{
+    const int n = g.n, m = g.m, l = g.l;
+    bool ii = i >= 1 && i <= n, jj = j >= 1 && j <= m, kk = k >= 1 && k <= l;
+    if (ii && jj && kk) return x[frow(g, i, j, k, var)];
+    if ((i == 0 || i == n + 1) && jj && kk) {
+        int src = g.periodic ? (i == 0 ? n : 1) : (i == 0 ? 1 : n);
+        return x[frow(g, src, j, k, var)];
+    }
+    if (ii && (j == 0 || j == m + 1) && kk) return x[frow(g, i, j == 0 ? 1 : m, k, var)];
+    if (ii && jj && (k == 0 || k == l + 1)) return x[frow(g, i, j, k == 0 ? 1 : l, var)];
+    return 0.0;
+}
+
+/* ================================================================================
+ * Row assembly.  A[s] holds the slots of row R (s = 0 .. NS-1, local index).
+ * ================================================================================ */
+template <int R> struct RowInfo {
+    static constexpr int B = ROW_BEGIN[R];
+    static constexpr int NS = ROW_BEGIN[R + 1] - ROW_BEGIN[R];
+};
+
+/* local slot of (pos, col) in row R or -1 */
+template <int R> HD constexpr int ls(int pos, int col)
+{
+    return slot_of(R, pos, col) < 0 ? -1 : slot_of(R, pos, col) - ROW_BEGIN[R];
+}
+
+struct CellCtx {
+    int i, j, k;             /* 1-based */
+    double wet;              /* (double)(1 - landm(i,j,l)) */
+    int wet_i;
+};
+
+/* ---- linear atoms (spf.F90 uderiv/vderiv/pderiv/tderiv/coriolis/gradp) ------------ */
+HD double at_uxx(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double cc = 1.0 / (g.cos_yv[c.j] * g.dx);
+    cc = cc * cc;
+    double a2 = g.amh_yv[c.j] * cc, a8 = g.amh_yv[c.j] * cc;
+    if (p == 2) return a2;
+    if (p == 8) return a8;
+    if (p == 5) return -(a2 + a8);
+    return 0.0;
+}
+HD double at_uyy(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double r = 1.0 / g.dy;
+    r = r * r;
+    double a4 = r * g.bmh_y[c.j] * g.cos_y[c.j] / g.cos_yv[c.j];
+    double a6 = r * g.bmh_y[c.j + 1] * g.cos_y[c.j + 1] / g.cos_yv[c.j];
+    if (p == 4) return a4;
+    if (p == 6) return a6;
+    if (p == 5) return -(a4 + a6);
+    return 0.0;
+}
+HD double at_zz(const Geo& g, const CellCtx& c, int p) /* uderiv(4) == vderiv(4) */
+{
+    double r = 1.0 / g.dz;
+    r = r * r;
+    double h1 = 1. / (g.dfzT[c.k] * g.dfzW[c.k]);
+    double h2 = 1. / (g.dfzT[c.k] * g.dfzW[c.k - 1]);
+    double a14 = h2 * r, a23 = h1 * r;
+    if (p == 14) return a14;
+    if (p == 23) return a23;
+    if (p == 5) return -(a14 + a23);
+    return 0.0;
+}
+HD double at_ucsi(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1 || p != 5) return 0.0;
+    double t2 = 1 - g.tan_yv[c.j] * g.tan_yv[c.j];
+    return g.bmh_yv[c.j] * t2 + g.tan_yv[c.j] * g.bmhy_yv[c.j];
+}
+HD double at_vxs(const Geo& g, const CellCtx& c, int p) /* uderiv(6) */
+{
+    if (c.j > g.m - 1) return 0.0;
+    double t2 = g.tan_yv[c.j], c2 = g.cos_yv[c.j];
+    if (p == 2) return (g.bmhy_yv[c.j] - (g.amh_yv[c.j] + g.bmh_yv[c.j]) * t2) / (g.dx * c2);
+    if (p == 8) return -(g.bmhy_yv[c.j] - (g.amh_yv[c.j] + g.bmh_yv[c.j]) * t2) / (g.dx * c2);
+    return 0.0;
+}
+HD double at_cor(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1 || p != 5) return 0.0;
+    return g.sin_yv[c.j] * g.coriolis_on;
+}
+HD double at_px(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double cc = 1. / (2 * g.cos_yv[c.j] * g.dx);
+    if (p == 5 || p == 6) return -cc;
+    if (p == 8 || p == 9) return cc;
+    return 0.0;
+}
+HD double at_vxx(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double cc = 1.0 / (g.cos_yv[c.j] * g.dx);
+    cc = cc * cc;
+    if (p == 2 || p == 8) return g.bmh_yv[c.j] * cc;
+    if (p == 5) return -2 * g.bmh_yv[c.j] * cc;
+    return 0.0;
+}
+HD double at_vyy(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double r = 1.0 / g.dy;
+    r = r * r;
+    double a4 = r * g.amh_y[c.j] * g.cos_y[c.j] / g.cos_yv[c.j];
+    double a6 = r * g.amh_y[c.j + 1] * g.cos_y[c.j + 1] / g.cos_yv[c.j];
+    if (p == 4) return a4;
+    if (p == 6) return a6;
+    if (p == 5) return -(a4 + a6);
+    return 0.0;
+}
+HD double at_vcsi(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1 || p != 5) return 0.0;
+    return g.bmh_yv[c.j] - g.amh_yv[c.j] * g.tan_yv[c.j] * g.tan_yv[c.j] +
+           g.bmhy_yv[c.j] * g.tan_yv[c.j];
+}
+HD double at_uxs(const Geo& g, const CellCtx& c, int p) /* vderiv(6) */
+{
+    if (c.j > g.m - 1) return 0.0;
+    double t2 = g.tan_yv[c.j], c2 = g.cos_yv[c.j];
+    if (p == 2) return -((g.amh_yv[c.j] + g.bmh_yv[c.j]) * t2 - g.bmhy_yv[c.j]) / (g.dx * c2);
+    if (p == 8) return ((g.amh_yv[c.j] + g.bmh_yv[c.j]) * t2 - g.bmhy_yv[c.j]) / (g.dx * c2);
+    return 0.0;
+}
+HD double at_py(const Geo& g, const CellCtx& c, int p)
+{
+    if (c.j > g.m - 1) return 0.0;
+    double d = 1. / (2 * g.dy);
+    if (p == 5 || p == 8) return -d;
+    if (p == 6 || p == 9) return d;
+    return 0.0;
+}
+HD double at_pz(const Geo& g, const CellCtx& c, int p)
+{
+    double dzi = 1. / g.dz;
+    if (p == 5) return -dzi / g.dfzW[c.k];
+    if (p == 23) return dzi / g.dfzW[c.k];
+    return 0.0;
+}
+HD double at_tbc(const Geo&, const CellCtx& c, int p)
+{
+    if (p == 23 || p == 5) return 1.0 * c.wet_i;
+    return 0.0;
+}
+HD double at_uxc(const Geo& g, const CellCtx& c, int p)
+{
+    double cc = 1.0 / (2 * g.cos_y[c.j] * g.dx);
+    if (p == 2 || p == 1) return -cc;
+    if (p == 4 || p == 5) return cc;
+    return 0.0;
+}
+HD double at_vyc(const Geo& g, const CellCtx& c, int p)
+{
+    double cc = 1. / (2 * g.cos_y[c.j] * g.dy);
+    if (p == 4 || p == 1) return -g.cos_yv[c.j - 1] * cc;
+    if (p == 2 || p == 5) return g.cos_yv[c.j] * cc;
+    return 0.0;
+}
+HD double at_wzc(const Geo& g, const CellCtx& c, int p)
+{
+    double dzi = 1.0 / g.dz;
+    if (p == 5) return dzi / g.dfzT[c.k];
+    if (p == 14) return -dzi / g.dfzT[c.k];
+    return 0.0;
+}
+HD double at_tc(const Geo& g, const CellCtx& c, int p) { return (p == 5 && c.k == g.l) ? 1.0 : 0.0; }
+HD double at_txx(const Geo& g, const CellCtx& c, int p)
+{
+    double cc = 1.0 / (g.cos_y[c.j] * g.dx);
+    cc = cc * cc;
+    if (p == 2 || p == 8) return cc * c.wet_i;
+    if (p == 5) return -2 * cc * c.wet_i;
+    return 0.0;
+}
+HD double at_tyy(const Geo& g, const CellCtx& c, int p)
+{
+    double r = 1.0 / g.dy;
+    r = r * r;
+    double a4 = (r * g.cos_yv[c.j - 1] / g.cos_y[c.j]) * c.wet_i;
+    double a6 = (r * g.cos_yv[c.j] / g.cos_y[c.j]) * c.wet_i;
+    if (p == 4) return a4;
+    if (p == 6) return a6;
+    if (p == 5) return -(a4 + a6);
+    return 0.0;
+}
+HD double at_tzz(const Geo& g, const CellCtx& c, int p)
+{
+    double r = 1.0 / g.dz;
+    r = r * r;
+    double h1 = 1. / (g.dfzT[c.k] * g.dfzW[c.k]);
+    double h2 = 1. / (g.dfzT[c.k] * g.dfzW[c.k - 1]);
+    double a14 = h2 * r * c.wet_i;
+    double a23 = (c.k <= g.l - 1) ? h1 * r * c.wet_i : 0.0;
+    if (p == 14) return a14;
+    if (p == 23) return a23;
+    if (p == 5) return -(a14 + a23);
+    return 0.0;
+}
+
+/* lin (usrc.F90:650-772): value of Al(pos, R, col) for ocean-only (coupled = 0) */
+template <int R> HD double lin_val(const Geo& g, const CellCtx& c, int pos, int col)
+{
+    const double* par = g.par;
+    const double EV = par[P_EK_V], EH = par[P_EK_H];
+    const double ph = (1 - par[P_MIXP]) * par[P_PE_H], pv = par[P_PE_V];
+    const double lambda = par[P_LAMB], xes = par[P_NLES], bi = par[P_BIOT], Ra = par[P_RAYL];
+    if (R == UU) {
+        if (col == UU)
+            return -EH * (at_uxx(g, c, pos) + at_uyy(g, c, pos) + at_ucsi(g, c, pos)) -
+                   EV * at_zz(g, c, pos);
+        if (col == VV) return -at_cor(g, c, pos) - EH * at_vxs(g, c, pos);
+        if (col == PP) return at_px(g, c, pos);
+    } else if (R == VV) {
+        if (col == UU) return at_cor(g, c, pos) - EH * at_uxs(g, c, pos);
+        if (col == VV)
+            return -EH * (at_vxx(g, c, pos) + at_vyy(g, c, pos) + at_vcsi(g, c, pos)) -
+                   EV * at_zz(g, c, pos);
+        if (col == PP) return at_py(g, c, pos);
+    } else if (R == WW) {
+        if (col == PP) return at_pz(g, c, pos);
+        if (col == TT) return -Ra * (1. + xes * ALPT1) * at_tbc(g, c, pos) / 2.;
+        if (col == SS) return lambda * Ra * at_tbc(g, c, pos) / 2.;
+    } else if (R == PP) {
+        if (col == UU) return at_uxc(g, c, pos);
+        if (col == VV) return at_vyc(g, c, pos);
+        if (col == WW) return at_wzc(g, c, pos);
+    } else if (R == TT) {
+        if (col == TT)
+            return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
+                   g.tres * bi * at_tc(g, c, pos);
+    } else if (R == SS) {
+        if (col == SS)
+            return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
+                   g.sres * bi * at_tc(g, c, pos);
+    }
+    return 0.0;
+}
+
+/* ---- nonlinear atoms (spf.F90 unlin/vnlin/wnlin/tnlin) ------------------------------ */
+struct Fld {
+    const Geo* g;
+    const double* x;
+    HD double u(int i, int j, int k) const { return uv_arr(*g, x, UU, i, j, k); }
+    HD double v(int i, int j, int k) const { return uv_arr(*g, x, VV, i, j, k); }
+    HD double w(int i, int j, int k) const { return w_arr(*g, x, i, j, k); }
+    HD double t(int var, int i, int j, int k) const { return ts_arr(*g, x, var, i, j, k); }
+};
+
+/* unlin(type) at position p */
+HD double at_unlin(const Geo& g, const Fld& f, const CellCtx& c, int type, int p)
+{
+    const int i = c.i, j = c.j, k = c.k;
+    switch (type) {
+    case 1:
+    case 2: {
+        double cc = 1.0 / (2 * g.cos_yv[j] * g.dx);
+        double s = type == 1 ? 1.0 : 2.0;
+        if (p == 8) return (i <= g.n - 1) ? (type == 1 ? f.u(i + 1, j, k) * cc : 2 * f.u(i + 1, j, k) * cc) : 0.0;
+        if (p == 2) return (i >= 2) ? (type == 1 ? -f.u(i - 1, j, k) * cc : -2 * f.u(i - 1, j, k) * cc) : 0.0;
+        (void)s;
+        return 0.0;
+    }
+    case 3:
+    case 4: {
+        double cc = 1.0 / (2 * g.cos_yv[j] * g.dy);
+        if (p == 4) {
+            if (j < 2) return 0.0;
+            double q = type == 3 ? f.v(i, j - 1, k) : f.u(i, j - 1, k);
+            return -q * g.cos_yv[j - 1] * cc;
+        }
+        if (p == 6) {
+            if (j > g.m - 1) return 0.0;
+            double q = type == 3 ? f.v(i, j + 1, k) : f.u(i, j + 1, k);
+            return q * g.cos_yv[j + 1] * cc;
+        }
+        return 0.0;
+    }
+    case 5: {
+        double td = 1.0 / (8 * g.dfzT[k] * g.dz);
+        double a23 = (f.w(i, j, k) + f.w(i, j + 1, k) + f.w(i + 1, j, k) + f.w(i + 1, j + 1, k)) * td;
+        double a14 = -(f.w(i, j, k - 1) + f.w(i, j + 1, k - 1) + f.w(i + 1, j, k - 1) +
+                       f.w(i + 1, j + 1, k - 1)) * td;
+        if (p == 23) return a23;
+        if (p == 14) return a14;
+        if (p == 5) return a14 + a23;
+        return 0.0;
+    }
+    case 6: {
+        double td = 1.0 / (8 * g.dfzT[k] * g.dz);
+        if (p == 5 || p == 6 || p == 8 || p == 9) return (f.u(i, j, k) + f.u(i, j, k + 1)) * td;
+        if (p == 14 || p == 15 || p == 17 || p == 18) return -(f.u(i, j, k) + f.u(i, j, k - 1)) * td;
+        return 0.0;
+    }
+    case 7:
+        return p == 5 ? f.v(i, j, k) * g.tan_yv[j] : 0.0;
+    case 8:
+        return p == 5 ? f.u(i, j, k) * g.tan_yv[j] : 0.0;
+    }
+    return 0.0;
+}
+HD double at_vnlin(const Geo& g, const Fld& f, const CellCtx& c, int type, int p)
+{
+    const int i = c.i, j = c.j, k = c.k;
+    switch (type) {
+    case 1:
+    case 2: {
+        double cc = 1.0 / (2 * g.cos_yv[j] * g.dx);
+        if (p == 8) {
+            if (i > g.n - 1) return 0.0;
+            return (type == 1 ? f.u(i + 1, j, k) : f.v(i + 1, j, k)) * cc;
+        }
+        if (p == 2) {
+            if (i < 2) return 0.0;
+            return -(type == 1 ? f.u(i - 1, j, k) : f.v(i - 1, j, k)) * cc;
+        }
+        return 0.0;
+    }
+    case 3: {
+        double cc = 1.0 / (2 * g.cos_yv[j] * g.dy);
+        if (p == 6) return (j <= g.m - 1) ? f.v(i, j + 1, k) * g.cos_yv[j + 1] * cc : 0.0;
+        if (p == 4) return (j >= 2) ? -f.v(i, j - 1, k) * g.cos_yv[j - 1] * cc : 0.0;
+        return 0.0;
+    }
+    case 4: {
+        double cc = 1.0 / (2 * g.cos_yv[j] * g.dy);
+        if (p == 6) return (j <= g.m - 1) ? 2 * f.v(i, j + 1, k) * g.cos_yv[j + 1] * cc : 0.0;
+        if (p == 4) return (j >= 2) ? -2 * f.v(i, j - 1, k) * g.cos_yv[j - 1] * cc : 0.0;
+        return 0.0;
+    }
+    case 5:
+        return at_unlin(g, f, c, 5, p);
+    case 6: {
+        double td = 1.0 / (8 * g.dfzT[k] * g.dz);
+        if (p == 5 || p == 6 || p == 8 || p == 9) return (f.v(i, j, k) + f.v(i, j, k + 1)) * td;
+        if (p == 14 || p == 15 || p == 17 || p == 18) return -(f.v(i, j, k) + f.v(i, j, k - 1)) * td;
+        return 0.0;
+    }
+    case 7:
+        return p == 5 ? f.u(i, j, k) * g.tan_yv[j] : 0.0;
+    case 8:
+        return p == 5 ? 2 * f.u(i, j, k) * g.tan_yv[j] : 0.0;
+    }
+    return 0.0;
+}
+HD double at_wnlin(const Geo& g, const Fld& f, const CellCtx& c, int type, int p)
+{
+    if (c.k > g.l - 1 || (p != 5 && p != 23)) return 0.0;
+    double t0 = f.t(TT, c.i, c.j, c.k), t1 = f.t(TT, c.i, c.j, c.k + 1);
+    switch (type) {
+    case 1:
+        return (t0 + t1) / 2.;
+    case 2:
+        return p == 23 ? t1 / 4. : (t0 + 2 * t1) / 4.;
+    case 3: {
+        double s = t0 + t1;
+        return 0.375 * (s * s);
+    }
+    case 4:
+        return p == 5 ? 0.125 * (t0 * t0 + 3 * t1 * t0 + 3 * t1 * t1) : 0.125 * t1 * t1;
+    }
+    return 0.0;
+}
+HD double at_tnlin(const Geo& g, const Fld& f, const CellCtx& c, int type, int var, int p)
+{
+    const int i = c.i, j = c.j, k = c.k;
+    const double wet = c.wet;
+    switch (type) {
+    case 2: {
+        double cc = 1.0 / (4 * g.cos_y[j] * g.dx);
+        if (p == 2 || p == 1) return -(f.t(var, i, j, k) + f.t(var, i - 1, j, k)) * cc * wet;
+        if (p == 4 || p == 5) return (f.t(var, i + 1, j, k) + f.t(var, i, j, k)) * cc * wet;
+        return 0.0;
+    }
+    case 3: {
+        double cc = 1.0 / (4 * g.cos_y[j] * g.dx);
+        double a2 = -(f.u(i - 1, j, k) + f.u(i - 1, j - 1, k)) * cc * wet;
+        double a8 = (f.u(i, j, k) + f.u(i, j - 1, k)) * cc * wet;
+        if (p == 2) return a2;
+        if (p == 8) return a8;
+        if (p == 5) return a2 + a8;
+        return 0.0;
+    }
+    case 4: {
+        double cc = 1.0 / (4 * g.cos_y[j] * g.dy);
+        if (p == 4 || p == 1) return -cc * (f.t(var, i, j, k) + f.t(var, i, j - 1, k)) * g.cos_yv[j - 1] * wet;
+        if (p == 5 || p == 2) return cc * (f.t(var, i, j + 1, k) + f.t(var, i, j, k)) * g.cos_yv[j] * wet;
+        return 0.0;
+    }
+    case 5: {
+        double cc = 1.0 / (4 * g.cos_y[j] * g.dy);
+        double a4 = -(f.v(i, j - 1, k) + f.v(i - 1, j - 1, k)) * cc * g.cos_yv[j - 1] * wet;
+        double a6 = (f.v(i, j, k) + f.v(i - 1, j, k)) * cc * g.cos_yv[j] * wet;
+        if (p == 4) return a4;
+        if (p == 6) return a6;
+        if (p == 5) return a4 + a6;
+        return 0.0;
+    }
+    case 6: {
+        double td = 1.0 / (2 * g.dz);
+        if (p == 14) return -td * wet * (f.t(var, i, j, k) + f.t(var, i, j, k - 1)) / g.dfzT[k];
+        if (p == 5)
+            return (k <= g.l - 1) ? td * wet * (f.t(var, i, j, k + 1) + f.t(var, i, j, k)) / g.dfzT[k]
+                                  : 0.0;
+        return 0.0;
+    }
+    case 7: {
+        double td = 1.0 / (2 * g.dz);
+        double a14 = -f.w(i, j, k - 1) * wet * td / g.dfzT[k];
+        double a23 = f.w(i, j, k) * wet * td / g.dfzT[k];
+        if (p == 14) return a14;
+        if (p == 23) return a23;
+        if (p == 5) return a14 + a23;
+        return 0.0;
+    }
+    }
+    return 0.0;
+}
+
+/* nlin_jac (usrc.F90:873-995) / nlin_rhs (775-870) added to the linear value */
+template <int R, bool JAC>
+HD double nlin_add(const Geo& g, const Fld& f, const CellCtx& c, int pos, int col, double a)
+{
+    const double epsr = g.par[P_ROSB], Ra = g.par[P_RAYL], xes = g.par[P_NLES];
+    if (R == UU) {
+        if (JAC) {
+            if (col == UU)
+                return a + epsr * (at_unlin(g, f, c, 2, pos) + at_unlin(g, f, c, 3, pos) +
+                                   at_unlin(g, f, c, 5, pos) + at_unlin(g, f, c, 7, pos));
+            if (col == VV) return a + epsr * (at_unlin(g, f, c, 4, pos) + at_unlin(g, f, c, 8, pos));
+            if (col == WW) return a + epsr * at_unlin(g, f, c, 6, pos);
+        } else if (col == UU) {
+            return a + epsr * (at_unlin(g, f, c, 1, pos) + at_unlin(g, f, c, 3, pos) +
+                               at_unlin(g, f, c, 5, pos) + at_unlin(g, f, c, 7, pos));
+        }
+    } else if (R == VV) {
+        if (JAC) {
+            if (col == UU) return a + epsr * (at_vnlin(g, f, c, 8, pos) + at_vnlin(g, f, c, 2, pos));
+            if (col == VV)
+                return a + epsr * (at_vnlin(g, f, c, 1, pos) + at_vnlin(g, f, c, 4, pos) +
+                                   at_vnlin(g, f, c, 5, pos));
+            if (col == WW) return a + epsr * at_vnlin(g, f, c, 6, pos);
+        } else {
+            if (col == UU) return a + epsr * at_vnlin(g, f, c, 7, pos);
+            if (col == VV)
+                return a + epsr * (at_vnlin(g, f, c, 1, pos) + at_vnlin(g, f, c, 3, pos) +
+                                   at_vnlin(g, f, c, 5, pos));
+        }
+    } else if (R == WW) {
+        if (col == TT)
+            return a - Ra * xes * ALPT2 * at_wnlin(g, f, c, JAC ? 1 : 2, pos) +
+                   Ra * xes * ALPT3 * at_wnlin(g, f, c, JAC ? 3 : 4, pos);
+    } else if (R == TT || R == SS) {
+        const int X = R;
+        if (JAC) {
+            if (col == UU) return a + at_tnlin(g, f, c, 2, X, pos);
+            if (col == VV) return a + at_tnlin(g, f, c, 4, X, pos);
+            if (col == WW) return a + at_tnlin(g, f, c, 6, X, pos);
+            if (col == X)
+                return a + at_tnlin(g, f, c, 3, X, pos) + at_tnlin(g, f, c, 5, X, pos) +
+                       at_tnlin(g, f, c, 7, X, pos);
+        } else if (col == X) {
+            return a + at_tnlin(g, f, c, 3, X, pos) + at_tnlin(g, f, c, 5, X, pos) +
+                   at_tnlin(g, f, c, 7, X, pos);
+        }
+    }
+    return a;
+}
+
+/* ---- boundaries (boundary.F90:2-393) restricted to row R --------------------------- */
+template <int R>
+HD void boundaries_row(const Geo& g, const CellCtx& c, double* A, bool& frc_zero)
+{
+    const int i = c.i, j = c.j, k = c.k, n = g.n, m = g.m;
+    constexpr int NS = RowInfo<R>::NS;
+#define L_(a, b, cc) LM(g, a, b, cc)
+    const int southw = L_(i - 1, j - 1, k), west = L_(i - 1, j, k), nwest = L_(i - 1, j + 1, k);
+    const int south = L_(i, j - 1, k), center = L_(i, j, k), north = L_(i, j + 1, k);
+    const int southe = L_(i + 1, j - 1, k), east = L_(i + 1, j, k), neast = L_(i + 1, j + 1, k);
+    const int southwb = L_(i - 1, j - 1, k - 1), westb = L_(i - 1, j, k - 1), nwestb = L_(i - 1, j + 1, k - 1);
+    const int southb = L_(i, j - 1, k - 1), bottom = L_(i, j, k - 1), northb = L_(i, j + 1, k - 1);
+    const int southeb = L_(i + 1, j - 1, k - 1), eastb = L_(i + 1, j, k - 1), neastb = L_(i + 1, j + 1, k - 1);
+    const int southwt = L_(i - 1, j - 1, k + 1), westt = L_(i - 1, j, k + 1), nwestt = L_(i - 1, j + 1, k + 1);
+    const int southt = L_(i, j - 1, k + 1), top = L_(i, j, k + 1), northt = L_(i, j + 1, k + 1);
+    const int southet = L_(i + 1, j - 1, k + 1), eastt = L_(i + 1, j, k + 1), neastt = L_(i + 1, j + 1, k + 1);
+    int southee = -1, easteast = -1, northee = -1, nnorthee = -1, nnwest = -1, nnorth = -1, nneast = -1;
+    if (i < n) {
+        southee = L_(i + 2, j - 1, k);
+        easteast = L_(i + 2, j, k);
+        northee = L_(i + 2, j + 1, k);
+        if (j < m) nnorthee = L_(i + 2, j + 2, k);
+    }
+    if (j < m) {
+        nnwest = L_(i, j + 2, k);
+        nnorth = L_(i, j + 2, k);
+        nneast = L_(i, j + 2, k);
+    }
+#undef L_
+    /* helpers on this row's slots */
+    auto addc = [&](int dst, int src, int col) {
+        int d = ls<R>(dst, col), s = ls<R>(src, col);
+        if (d >= 0 && s >= 0) A[d] = A[d] + A[s];
+    };
+    auto zeroc = [&](int pos, int col) {
+        int d = ls<R>(pos, col);
+        if (d >= 0) A[d] = 0.0;
+    };
+    auto zerop = [&](int pos) {
+        for (int col = 0; col < NUN; col++) zeroc(pos, col);
+    };
+    auto zerorow = [&](int row) {
+        if (row == R)
+            for (int s = 0; s < NS; s++) A[s] = 0.0;
+    };
+    auto setv = [&](int pos, int col, double v) {
+        int d = ls<R>(pos, col);
+        if (d >= 0) A[d] = v;
+    };
+
+    if (center == OCEAN) {
+        if (bottom == LAND) {
+            if (westb == LAND && southwb == LAND && southb == LAND) { addc(1, 10, UU); addc(1, 10, VV); }
+            zeroc(10, UU); zeroc(10, VV);
+            if (westb == LAND && neastb == LAND && northb == LAND) { addc(2, 11, UU); addc(2, 11, VV); }
+            zeroc(11, UU); zeroc(11, VV);
+            if (eastb == LAND && southeb == LAND && southb == LAND) { addc(4, 13, UU); addc(4, 13, VV); }
+            zeroc(13, UU); zeroc(13, VV);
+            if (eastb == LAND && neastb == LAND && northb == LAND) { addc(5, 14, UU); addc(5, 14, VV); }
+            addc(5, 14, TT); addc(5, 14, SS);
+            zerop(14);
+        }
+        if (southwb == LAND) zerop(10);
+        if (westb == LAND) zerop(11);
+        if (nwestb == LAND) zerop(12);
+        if (southb == LAND) zerop(13);
+        if (northb == LAND) zerop(15);
+        if (southeb == LAND) zerop(16);
+        if (eastb == LAND) zerop(17);
+        if (neastb == LAND) zerop(18);
+        if (top == LAND) {
+            if (westt == LAND && southwt == LAND && southt == LAND) { addc(1, 19, UU); addc(1, 19, VV); }
+            zeroc(19, UU); zeroc(19, VV);
+            if (westt == LAND && nwestt == LAND && northt == LAND) { addc(2, 20, UU); addc(2, 20, VV); }
+            zeroc(20, UU); zeroc(20, VV);
+            if (eastt == LAND && southet == LAND && southt == LAND) { addc(4, 22, UU); addc(4, 22, VV); }
+            zeroc(22, UU); zeroc(22, VV);
+            if (eastt == LAND && neastt == LAND && northt == LAND) { addc(5, 23, UU); addc(5, 23, VV); }
+            addc(5, 23, TT); addc(5, 23, SS);
+            zerop(23);
+            if (R == WW) frc_zero = true;
+            zerorow(WW);
+            setv(5, WW, 1.0e-10);
+            setv(6, WW, 1.0e-10);
+            setv(8, WW, 1.0e-10);
+            setv(9, WW, 1.0e-10);
+            if (R == WW) setv(5, WW, 1.0);
+        }
+        if (southwt == LAND) zerop(19);
+        if (westt == LAND) zerop(20);
+        if (nwestt == LAND) zerop(21);
+        if (southt == LAND) zerop(22);
+        if (northt == LAND) zerop(24);
+        if (southet == LAND) zerop(25);
+        if (eastt == LAND) zerop(26);
+        if (neastt == LAND) zerop(27);
+        if (southw == LAND) { zeroc(1, UU); zeroc(1, VV); }
+        if (west == LAND) {
+            addc(5, 2, TT); addc(5, 2, SS);
+            zerop(2);
+            zeroc(1, UU); zeroc(1, VV);
+        }
+        if (nwest == LAND) {
+            zeroc(2, UU); zeroc(2, VV); zeroc(3, UU); zeroc(3, VV);
+        } else if (j < m) {
+            if (nnwest == LAND) { zeroc(3, UU); zeroc(3, VV); }
+        }
+        if (south == LAND) {
+            addc(5, 4, SS); addc(5, 4, TT);
+            zerop(4);
+            zeroc(1, UU); zeroc(1, VV);
+        }
+        if (north == LAND) {
+            zeroc(2, UU); zeroc(2, VV);
+            if (R == PP) { setv(2, UU, 0.0); setv(2, VV, 0.0); setv(5, UU, 0.0); setv(5, VV, 0.0); }
+            if (R == VV) frc_zero = true;
+            zerorow(VV);
+            zeroc(5, VV);
+            if (R == VV) setv(5, VV, 1.0);
+            if (R == UU) frc_zero = true;
+            zerorow(UU);
+            zeroc(5, UU);
+            if (R == UU) setv(5, UU, 1.0);
+            addc(5, 6, SS); addc(5, 6, TT);
+            zerop(6);
+        } else if (j < m) {
+            if (nnorth == LAND) { zeroc(3, UU); zeroc(3, VV); zeroc(6, UU); zeroc(6, VV); }
+        }
+        if (southe == LAND) {
+            zeroc(4, UU); zeroc(4, VV); zeroc(7, UU); zeroc(7, VV);
+        } else if (i < n) {
+            if (southee == LAND) { zeroc(7, UU); zeroc(7, VV); }
+        }
+        if (east == LAND) {
+            zeroc(4, UU); zeroc(4, VV);
+            if (R == PP) { setv(4, UU, 0.0); setv(4, VV, 0.0); setv(5, UU, 0.0); setv(5, VV, 0.0); }
+            if (R == UU) frc_zero = true;
+            zerorow(UU);
+            zeroc(5, UU);
+            if (R == UU) setv(5, UU, 1.0);
+            if (R == VV) frc_zero = true;
+            zerorow(VV);
+            zeroc(5, VV);
+            if (R == VV) setv(5, VV, 1.0);
+            addc(5, 8, SS); addc(5, 8, TT);
+            zerop(8);
+            zeroc(7, UU); zeroc(7, VV);
+        } else if (i < n) {
+            if (easteast == LAND) { zeroc(7, UU); zeroc(7, VV); zeroc(8, UU); zeroc(8, VV); }
+        }
+        if (neast == LAND) {
+            if (R == UU) frc_zero = true;
+            zerorow(UU);
+            zeroc(5, UU);
+            if (R == UU) setv(5, UU, 1.0);
+            if (R == VV) frc_zero = true;
+            zerorow(VV);
+            zeroc(5, VV);
+            if (R == VV) setv(5, VV, 1.0);
+            zeroc(7, UU); zeroc(7, VV);
+        } else if (i < n || j < m) {
+            if (i < n) {
+                if (northee == LAND) {
+                    zeroc(8, UU); zeroc(8, VV); zeroc(9, UU); zeroc(9, VV);
+                } else if (j < m) {
+                    if (nnorthee == LAND) { zeroc(9, UU); zeroc(9, VV); }
+                }
+            }
+            if (j < m) {
+                if (nneast == LAND) { zeroc(6, UU); zeroc(6, VV); zeroc(9, UU); zeroc(9, VV); }
+            }
+        }
+    } else {
+        for (int s = 0; s < NS; s++) A[s] = 0.0;
+        frc_zero = true;
+        setv(5, R, 1.0);
+    }
+}
+
+/* Full row: lin + nonlinear + boundaries + fillcolA threshold.  Returns slots in A. */
+template <int R, bool JAC>
+HD void assemble_row(const Geo& g, const double* x, int i, int j, int k, double* A, bool& frc_zero)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    CellCtx c;
+    c.i = i; c.j = j; c.k = k;
+    c.wet_i = 1 - LM(g, i, j, g.l);
+    c.wet = (double)c.wet_i;
+    Fld f{&g, x};
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+    for (int s = 0; s < NS; s++) {
+        const Slot sl = SLOTS[B + s];
+        const int pos = pos_of(sl.di, sl.dj, sl.dk);
+        double a = lin_val<R>(g, c, pos, sl.var);
+        A[s] = nlin_add<R, JAC>(g, f, c, pos, sl.var, a);
+    }
+    frc_zero = false;
+    boundaries_row<R>(g, c, A, frc_zero);
+    for (int s = 0; s < NS; s++) A[s] = (A[s] > 1.0e-10 || A[s] < -1.0e-10) ? A[s] : 0.0;
+}
+
+/* Column (0-based global row index) of slot s of cell (i,j,k) (1-based), or -1 when the
+ * neighbour is outside the domain (such slots hold 0). */
+HD int64_t slot_col(const Geo& g, int s, int i, int j, int k)
+{
+    const Slot sl = SLOTS[s];
+    int ii = i + sl.di, jj = j + sl.dj, kk = k + sl.dk;
+    if (g.periodic) {
+        if (ii == 0) ii = g.n;
+        else if (ii == g.n + 1) ii = 1;
+    }
+    if (ii < 1 || ii > g.n || jj < 1 || jj > g.m || kk < 1 || kk > g.l) return -1;
+    return frow(g, ii, jj, kk, sl.var);
+}
+
+
+/* ---- residual row (rhs_, usrc.F90:506-586 + THCM.C:1003) -------------------------- */
+template <int R>
+HD double rhs_row_value(const Geo& g, const double* x, const double* frc, int i, int j, int k,
+                        int64_t cell)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    double A[NS];
+    bool fz;
+    assemble_row<R, false>(g, x, i, j, k, A, fz);
+    /* matAvec in fillcolA order: v2 = coA(v)*v1(jcoA(v)) + v2 */
+    double au = 0.0;
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+    for (int r = 0; r < NS; r++) {
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+        for (int s = 0; s < NS; s++) {
+            if (fortran_rank(B + s) == r) {
+                if (A[s] != 0.0) {
+                    const int64_t col = slot_col(g, B + s, i, j, k);
+                    if (col >= 0) au = A[s] * x[col] + au;
+                }
+            }
+        }
+    }
+    const int64_t row = NUN * cell + R;
+    const double f = fz ? 0.0 : frc[row];
+    /* B = -Au - mix + Frc - p0*(1-par(RESC))*ures; B *= (1-landm); F = -B */
+    const double b = -au - 0.0 + f - 0.0 * (1 - g.par[P_RESC]) * 0.0;
+    return -(b * (1 - LM(g, i, j, k)));
+}
+
+/* fillcolB (assemble.F90:18-54) times Mass = 1 (THCM.C:1150-1153) */
+HD void diagB_cell(const Geo& g, int i, int j, int k, double* b)
+{
+    for (int v = 0; v < NUN; v++) b[v] = 0.0;
+    if (LM(g, i, j, k) == OCEAN) {
+        if (LM(g, i + 1, j, k) != LAND) b[UU] = -g.par[P_ROSB];
+        if (LM(g, i, j + 1, k) != LAND) b[VV] = -g.par[P_ROSB];
+        b[TT] = -1.0;
+        b[SS] = -1.0;
+    }
+}
+
+/* ---- forcing (forcing.F90:4-218, ocean-only idealized: iza = 2, ite = its = 1) ----
+ * ftab = [wfun(yv) (m+2) | temfun(y) (m+2) | salfun(y) (m+2) | spert (n*m)]          */
+HD void forcing_qint(const Geo& g, const double* ftab, double* qcor, int need_t, int need_s)
+{
+    /* qint (forcing.F90:536-548 -> THCM.C:2704-2737): sequential, reference order */
+    const int n = g.n, m = g.m, l = g.l;
+    const double* temf = ftab + (m + 2);
+    const double* salf = ftab + 2 * (m + 2);
+    const double* spert = ftab + 3 * (m + 2);
+    double ls = 0.0, lt = 0.0, le = 0.0, lz = 0.0, lp = 0.0;
+    for (int j = 1; j <= m; j++)
+        for (int i = 1; i <= n; i++) {
+            const int lm = LM(g, i, j, l);
+            const double cy = g.cos_y[j];
+            lt = temf[j] * cy * (1 - lm) + lt;
+            le = (salf[j] * (1 - lm)) * cy * (1 - lm) + le;
+            lz = 0.0 * cy * (1 - lm) + lz;
+            lp = spert[(j - 1) * n + (i - 1)] * cy * (1 - lm) + lp;
+            ls = cy * (1 - lm) + ls;
+        }
+    qcor[0] = need_t ? lt / ls : 0.0;   /* temcor         */
+    qcor[1] = need_s ? le / ls : 0.0;   /* salcor         */
+    qcor[2] = need_s ? lz / ls : 0.0;   /* adapted_salcor */
+    qcor[3] = need_s ? lp / ls : 0.0;   /* spertcor       */
+}
+HD void forcing_cell(const Geo& g, const double* ftab, const double* qcor, int i, int j, int k,
+                     double* f)
+{
+    const int n = g.n, m = g.m, l = g.l;
+    const double* par = g.par;
+    const double* wfun_yv = ftab;
+    const double* temf = ftab + (m + 2);
+    const double* salf = ftab + 2 * (m + 2);
+    const double* spert = ftab + 3 * (m + 2);
+    const int TRES = g.tres, SRES = g.sres;
+    for (int v = 0; v < NUN; v++) f[v] = 0.0;
+    if (k == l) {
+        const double sigma = par[P_COMB] * par[P_WIND] * par[P_AL_T];
+        if (j <= m - 1) {
+            f[UU] = sigma * wfun_yv[j];
+            f[VV] = sigma * 0.0;
+        }
+        const double etabi = par[P_COMB] * par[P_TEMP] * ((double)(1 - TRES) + TRES * par[P_BIOT]);
+        f[TT] = etabi * (temf[j] - qcor[0]);
+        const double gamma = par[P_COMB] * par[P_SALT] * ((double)(1 - SRES) + SRES * par[P_BIOT]);
+        const double emip = salf[j] * (1 - LM(g, i, j, l));
+        f[SS] = gamma * (1 - par[P_HMTP]) * (emip - qcor[1]) +
+                gamma * par[P_HMTP] * (0.0 - qcor[2]) +
+                par[P_SPER] * ((double)(1 - SRES) + SRES * par[P_BIOT]) *
+                    (spert[(j - 1) * n + (i - 1)] - qcor[3]);
+    }
+    if (k <= l - 1)
+        f[WW] = -par[P_COMB] * (1 - LM(g, i, j, k)) * par[P_RAYL] *
+                (par[P_LAMB] * (0.0 + 0.0) / 2. - (0.0 + 0.0) / 2.);
+}
+
+}  // namespace iemic
+#endif

@@ -1,0 +1,125 @@
+"""ctypes binding of the device library's C ABI (include/iemic.h).
+
+The library is built in-tree (``make -C i-emic_amd``) into ``i-emic_amd/lib/libiemic_amd.so``.
+There is no CPU fallback: if the library or a GPU is missing, every call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libiemic_amd.so")
+
+IEMIC_ENODEV = -19
+
+
+class Grid(C.Structure):
+    """iemic_grid (include/iemic.h)."""
+    _fields_ = [("n", C.c_int), ("m", C.c_int), ("l", C.c_int),
+                ("xmin", C.c_double), ("xmax", C.c_double), ("ymin", C.c_double),
+                ("ymax", C.c_double), ("periodic", C.c_int), ("hdim", C.c_double),
+                ("qz", C.c_double), ("tres", C.c_int), ("sres", C.c_int),
+                ("forcing_type", C.c_int), ("ih", C.c_int), ("vmix", C.c_int),
+                ("coriolis_on", C.c_int), ("alpha_t", C.c_double), ("alpha_s", C.c_double),
+                ("int_sign", C.c_int), ("int_i", C.c_int), ("int_j", C.c_int),
+                ("analyze_jacobian", C.c_int), ("max_mask_fixes", C.c_int),
+                ("device", C.c_int)]
+
+
+class Krylov(C.Structure):
+    _fields_ = [("tol", C.c_double), ("krylov_dim", C.c_int), ("max_restarts", C.c_int),
+                ("prec", C.c_int), ("ts_sweeps", C.c_int)]
+
+
+class SolveInfo(C.Structure):
+    _fields_ = [("iters", C.c_int), ("converged", C.c_int),
+                ("implicit_rel_res", C.c_double), ("explicit_rel_res", C.c_double),
+                ("t_prec_ms", C.c_double), ("t_spmv_ms", C.c_double),
+                ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double)]
+
+
+class NewtonInfo(C.Structure):
+    _fields_ = [("norm_f0", C.c_double), ("norm_f1", C.c_double), ("solve", SolveInfo),
+                ("t_jac_ms", C.c_double), ("t_rhs_ms", C.c_double), ("t_prec_ms", C.c_double),
+                ("t_solve_ms", C.c_double), ("t_total_ms", C.c_double)]
+
+
+def grid_from_config(cfg, device: int = 0, analyze_jacobian: bool = True) -> Grid:
+    return Grid(cfg.n, cfg.m, cfg.l, cfg.xmin, cfg.xmax, cfg.ymin, cfg.ymax, int(cfg.periodic),
+                cfg.hdim, cfg.qz, cfg.tres, cfg.sres, cfg.forcing_type,
+                cfg.inhomogeneous_mixing, cfg.mixing, cfg.coriolis, cfg.alpha_t, cfg.alpha_s,
+                cfg.int_sign, cfg.integral_i, cfg.integral_j, int(analyze_jacobian), 5, device)
+
+
+_lib = None
+
+P = C.POINTER
+PD, PI, P64 = P(C.c_double), P(C.c_int), P(C.c_int64)
+
+
+def ptr(a, t=C.c_double):
+    return a.ctypes.data_as(P(t))
+
+
+def lib():
+    """Load the in-tree device library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"device library not built: {LIB_PATH} (run make -C i-emic_amd)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    sig = {
+        "iemic_create": (C.c_int, [P(vp), P(Grid), PI]),
+        "iemic_destroy": (None, [vp]),
+        "iemic_device_count": (C.c_int, []),
+        "iemic_last_error": (C.c_char_p, []),
+        "iemic_set_par": (C.c_int, [vp, C.c_int, C.c_double]),
+        "iemic_get_par": (C.c_int, [vp, C.c_int, PD]),
+        "iemic_nrows": (C.c_int, [vp]),
+        "iemic_graph_nnz": (C.c_int64, [vp]),
+        "iemic_rowintcon": (C.c_int, [vp]),
+        "iemic_landm": (C.c_int, [vp, PI]),
+        "iemic_set_state": (C.c_int, [vp, PD]),
+        "iemic_get_state": (C.c_int, [vp, PD]),
+        "iemic_jacobian": (C.c_int, [vp]),
+        "iemic_rhs": (C.c_int, [vp, PD]),
+        "iemic_diag_b": (C.c_int, [vp, PD]),
+        "iemic_export_csr": (C.c_int, [vp, P64, PI, PD]),
+        "iemic_spmv": (C.c_int, [vp, PD, PD]),
+        "iemic_spmv_dev": (C.c_int, [vp, vp, vp, vp]),
+        "iemic_prec_compute": (C.c_int, [vp, P(Krylov)]),
+        "iemic_prec_apply": (C.c_int, [vp, PD, PD]),
+        "iemic_solve": (C.c_int, [vp, PD, PD, P(Krylov), P(SolveInfo)]),
+        "iemic_solve_dev": (C.c_int, [vp, vp, vp, P(Krylov), P(SolveInfo)]),
+        "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
+        "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+EXPORTED = ("iemic_create", "iemic_destroy", "iemic_device_count", "iemic_last_error",
+            "iemic_set_par", "iemic_get_par", "iemic_nrows", "iemic_graph_nnz",
+            "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",
+            "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
+            "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
+            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv")
+
+
+class IemicError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().iemic_last_error()
+        raise IemicError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,186 @@
+"""Ocean-shaped host interface over the device library.
+
+Mirrors the Model surface the reference's Continuation and transient Newton drive
+(``src/ocean/Ocean.H``; calls listed in SURVEY.md §8b.1): ``computeRHS``,
+``computeJacobian``, ``solve``, ``applyMatrix``, ``applyPrecon``, ``buildPreconditioner``,
+``getState/getSolution/getRHS('C'|'V')``, ``setPar/getPar``, ``preProcess``,
+``postProcess``.  Parameter names are THCM's (``THCM::par2int``, THCM.C:1754-1807) and
+Belos settings keep Ocean's names ("FGMRES iterations", "FGMRES tolerance",
+"FGMRES restarts"; defaults Ocean.C:2232-2237).
+
+Everything computes on the GPU through the C ABI; the state, Jacobian, residual and
+Krylov basis stay resident in HBM.  Errors raise ``IemicError`` (the reference throws).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import IemicError, check, lib, ptr
+from .config import PAR_INDEX, THCMConfig, landmask
+
+__all__ = ["Ocean", "IemicError"]
+
+
+class Ocean:
+    """One THCM ocean model instance on one GPU (Ocean.C:63-213)."""
+
+    def __init__(self, cfg: THCMConfig, landm: Optional[np.ndarray] = None, device: int = 0,
+                 analyze_jacobian: bool = True, solver_params: Optional[dict] = None):
+        self.cfg = cfg
+        L = landmask(cfg) if landm is None else landm
+        L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
+        self._grid = _lib.grid_from_config(cfg, device=device, analyze_jacobian=analyze_jacobian)
+        h = C.c_void_p()
+        rc = lib().iemic_create(C.byref(h), C.byref(self._grid), ptr(L, C.c_int))
+        check(rc, "iemic_create")
+        self._h = h
+        self.N = lib().iemic_nrows(h)
+        # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
+        sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
+              "Preconditioner": 2, "TS sweeps": 3}
+        if solver_params:
+            sp.update(solver_params)
+        self.solver_params = sp
+        self._recomp_prec = True
+        for idx, v in cfg.par_list():
+            self.setPar(idx, v)
+        self._x = np.zeros(self.N)
+        self._F = np.zeros(self.N)
+        self._sol = np.zeros(self.N)
+        self.last_solve = None
+
+    # ---- lifecycle -----------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().iemic_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- parameters (THCM::setParameter / getParameter) ------------------------------
+    def setPar(self, par, value: float) -> None:
+        idx = PAR_INDEX[par] if isinstance(par, str) else int(par)
+        check(lib().iemic_set_par(self._h, idx, float(value)), "iemic_set_par")
+
+    def getPar(self, par) -> float:
+        idx = PAR_INDEX[par] if isinstance(par, str) else int(par)
+        v = C.c_double()
+        check(lib().iemic_get_par(self._h, idx, C.byref(v)), "iemic_get_par")
+        return v.value
+
+    # ---- state --------------------------------------------------------------------
+    def setState(self, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        assert x.shape == (self.N,)
+        check(lib().iemic_set_state(self._h, ptr(x)), "iemic_set_state")
+        self._x = x.copy()
+
+    def getState(self, mode: str = "C") -> np.ndarray:
+        x = np.zeros(self.N)
+        check(lib().iemic_get_state(self._h, ptr(x)), "iemic_get_state")
+        return x
+
+    def getRHS(self, mode: str = "C") -> np.ndarray:
+        return self._F.copy() if mode == "C" else self._F
+
+    def getSolution(self, mode: str = "C") -> np.ndarray:
+        return self._sol.copy() if mode == "C" else self._sol
+
+    # ---- Model API -----------------------------------------------------------------
+    def computeRHS(self) -> np.ndarray:
+        """F(state) (Ocean::computeRHS, Ocean.C:1267-1274)."""
+        check(lib().iemic_rhs(self._h, ptr(self._F)), "iemic_rhs")
+        return self._F
+
+    def computeJacobian(self) -> None:
+        """J(state) + diag(B) (Ocean::computeJacobian, Ocean.C:1287-1299)."""
+        check(lib().iemic_jacobian(self._h), "iemic_jacobian")
+
+    def applyMatrix(self, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(self.N) if y is None else y
+        check(lib().iemic_spmv(self._h, ptr(x), ptr(y)), "iemic_spmv")
+        return y
+
+    def diagB(self) -> np.ndarray:
+        B = np.zeros(self.N)
+        check(lib().iemic_diag_b(self._h, ptr(B)), "iemic_diag_b")
+        return B
+
+    def _krylov(self) -> _lib.Krylov:
+        sp = self.solver_params
+        return _lib.Krylov(float(sp["FGMRES tolerance"]), int(sp["FGMRES iterations"]),
+                           int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
+                           int(sp["TS sweeps"]))
+
+    def buildPreconditioner(self, force: bool = False) -> None:
+        """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""
+        if self._recomp_prec or force:
+            k = self._krylov()
+            check(lib().iemic_prec_compute(self._h, C.byref(k)), "iemic_prec_compute")
+            self._recomp_prec = False
+
+    def applyPrecon(self, r: np.ndarray) -> np.ndarray:
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros(self.N)
+        check(lib().iemic_prec_apply(self._h, ptr(r), ptr(z)), "iemic_prec_apply")
+        return z
+
+    def solve(self, rhs: np.ndarray) -> np.ndarray:
+        """J x = rhs with FGMRES (Ocean::solve, Ocean.C:1060-1137)."""
+        self.buildPreconditioner()
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        k = self._krylov()
+        info = _lib.SolveInfo()
+        check(lib().iemic_solve(self._h, ptr(rhs), ptr(self._sol), C.byref(k), C.byref(info)),
+              "iemic_solve")
+        self.last_solve = info
+        return self._sol
+
+    def preProcess(self) -> None:
+        """Ocean::preProcess (Ocean.C:790-801): refactor the preconditioner next solve."""
+        self._recomp_prec = True
+
+    def postProcess(self) -> None:
+        pass
+
+    # ---- fused device-resident Newton step -------------------------------------------
+    def newtonStep(self) -> _lib.NewtonInfo:
+        """F, J, preconditioner, J dx = -F, x += dx, F (transient/Newton.H:92-99)."""
+        k = self._krylov()
+        info = _lib.NewtonInfo()
+        check(lib().iemic_newton_step(self._h, C.byref(k), C.byref(info)), "iemic_newton_step")
+        return info
+
+    # ---- inspection -----------------------------------------------------------------
+    def exportCSR(self):
+        nnz = lib().iemic_graph_nnz(self._h)
+        rowptr = np.zeros(self.N + 1, dtype=np.int64)
+        col = np.zeros(nnz, dtype=np.int32)
+        val = np.zeros(nnz)
+        check(lib().iemic_export_csr(self._h, ptr(rowptr, C.c_int64), ptr(col, C.c_int), ptr(val)),
+              "iemic_export_csr")
+        return rowptr, col, val
+
+    def landmask(self) -> np.ndarray:
+        c = self.cfg
+        out = np.zeros((c.l + 2) * (c.m + 2) * (c.n + 2), dtype=np.int32)
+        check(lib().iemic_landm(self._h, ptr(out, C.c_int)), "iemic_landm")
+        return out
+
+    @property
+    def rowintcon(self) -> int:
+        return lib().iemic_rowintcon(self._h)
+
+    def time_spmv(self, nrep: int = 20) -> float:
+        ms = C.c_double()
+        check(lib().iemic_time_spmv(self._h, int(nrep), C.byref(ms)), "iemic_time_spmv")
+        return ms.value

@@ -1,0 +1,142 @@
+/*
+ * iemic.h -- C ABI of the MI355X-native Newton-Krylov core for the THCM ocean model.
+ *
+ * Drop-in boundary.  The reference splits this path across three seams;
+ * this ABI replaces the two lower ones and is what the Ocean-shaped C++ host
+ * (i-emic_amd/csrc/ocean.hpp) and the Python mirror (i-emic_amd/iemic/) bind:
+ *
+ *   THCM Fortran ABI (assembly)      src/ocean/THCM.C:47-174, usrc.F90:6-586
+ *     init_ / setparcs_ / matrix_ / rhs_ / fillcolb_        -> iemic_create / iemic_set_par /
+ *                                                              iemic_jacobian / iemic_rhs
+ *   Epetra_CrsMatrix storage + Apply  THCM.C:739-751, Ocean.C:1352-1357
+ *                                                           -> iemic_spmv / iemic_export_csr
+ *   mrilucpp_* factor/apply           src/mrilucpp/Ifpack_MRILU.cpp:22-39,
+ *                                     mrilucpp.F90:120-553   -> iemic_prec_compute / iemic_prec_apply
+ *   Belos BlockGmresSolMgr (FGMRES)   Ocean.C:961-1137        -> iemic_solve
+ *
+ * Conventions
+ *  - Return codes: 0 on success, negative errno-style values on failure; the ABI never
+ *    throws and never falls back to the CPU: without a usable gfx950 device every
+ *    compute entry point returns IEMIC_ENODEV.
+ *  - Vectors are fp64 in the reference's global row order
+ *    row = 6*((k*m + j)*n + i) + var, var in {u,v,w,p,T,S} (FIND_ROW2, THCMdefs.H:21).
+ *  - Pointers are host pointers unless the function name ends in _dev (device pointers
+ *    into memory the caller allocated on the context's device, e.g. torch tensors).
+ *  - A context is single-host-thread and not re-entrant, like the reference THCM
+ *    singleton; independent contexts may coexist (one per GPU / rank).
+ */
+#ifndef IEMIC_H
+#define IEMIC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IEMIC_ENODEV  (-19)
+#define IEMIC_EINVAL  (-22)
+#define IEMIC_ENOMEM  (-12)
+#define IEMIC_EDEVICE (-5)
+#define IEMIC_ESTATE  (-71)
+
+typedef struct iemic_ctx iemic_ctx;
+
+/* THCM ParameterList subset used by the hot path (THCM.C:189-265; defaults 2748-2813). */
+typedef struct {
+    int n, m, l;                 /* "Global Grid-Size n/m/l"                         */
+    double xmin, xmax, ymin, ymax;/* "Global Bound ..." in degrees                   */
+    int periodic;                /* "Periodic"                                       */
+    double hdim, qz;             /* "Depth hdim", "Grid Stretching qz"               */
+    int tres, sres;              /* "Restoring Temperature/Salinity Profile"         */
+    int forcing_type;            /* "Forcing Type"                                   */
+    int ih;                      /* "Inhomogeneous Mixing"                           */
+    int vmix;                    /* "Mixing" (only 0 implemented: SURVEY §8f row 1)  */
+    int coriolis_on;             /* "Coriolis Force"                                 */
+    double alpha_t, alpha_s;     /* "Linear EOS: alpha T/S"                          */
+    int int_sign;                /* "Salinity Integral Sign"                         */
+    int int_i, int_j;            /* "Integral row coordinate i/j" (-1: default)      */
+    int analyze_jacobian;        /* Ocean "Analyze Jacobian" mask fix (Ocean.C:505)  */
+    int max_mask_fixes;          /* Ocean "Max mask fixes" (default 5)               */
+    int device;                  /* HIP device ordinal                               */
+} iemic_grid;
+
+/* Krylov settings (Ocean.C:961-1020, getDefaultInitParameters 2232-2237). */
+typedef struct {
+    double tol;                  /* "FGMRES tolerance" (relative to ||b||, x0 = 0)   */
+    int krylov_dim;              /* "FGMRES iterations" = restart length             */
+    int max_restarts;            /* "FGMRES restarts"                                */
+    int prec;                    /* 0: none, 1: block Gauss-Seidel (default)         */
+    int ts_sweeps;               /* symmetric red-black sweeps on the T/S block      */
+} iemic_krylov;
+
+typedef struct {
+    int iters;                   /* total Arnoldi steps                              */
+    int converged;
+    double implicit_rel_res;     /* Givens estimate / ||b||                          */
+    double explicit_rel_res;     /* ||b - J x|| / ||b||  (Ocean.C:1140-1150)         */
+    double t_prec_ms, t_spmv_ms, t_orth_ms, t_total_ms;
+} iemic_solve_info;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+/* landm: (n+2)(m+2)(l+2) ints, i fastest, the global mask m_global::get_landm returns
+ * (THCM.C:391).  The context applies init_'s border handling (usrc.F90:83-107), builds
+ * grid metrics, stpnt parameters, forcing and the maximal graph, and (if requested)
+ * runs the Ocean mask-fix cycle (Ocean.C:496-569, analyzeJacobian1). */
+int  iemic_create(iemic_ctx** ctx, const iemic_grid* grid, const int* landm);
+void iemic_destroy(iemic_ctx* ctx);
+int  iemic_device_count(void);
+const char* iemic_last_error(void);
+
+/* ---- parameters (setparcs_/getparcs_, usrc.F90:163-198; index 1..30 = par2int) --- */
+int  iemic_set_par(iemic_ctx* ctx, int idx, double value);
+int  iemic_get_par(iemic_ctx* ctx, int idx, double* value);
+
+/* ---- geometry queries ------------------------------------------------------------ */
+int     iemic_nrows(const iemic_ctx* ctx);
+int64_t iemic_graph_nnz(const iemic_ctx* ctx);       /* Epetra maximal-graph nnz       */
+int     iemic_rowintcon(const iemic_ctx* ctx);       /* -1 when SRES != 0              */
+int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local mask   */
+
+/* ---- state ------------------------------------------------------------------------ */
+int iemic_set_state(iemic_ctx* ctx, const double* x);     /* host -> device state     */
+int iemic_get_state(iemic_ctx* ctx, double* x);
+
+/* ---- assembly (THCM::evaluate, THCM.C:949-1192) --------------------------------- */
+int iemic_jacobian(iemic_ctx* ctx);                 /* J(state) + diag(B) on device */
+int iemic_rhs(iemic_ctx* ctx, double* F);           /* F(state); F may be NULL      */
+int iemic_diag_b(iemic_ctx* ctx, double* B);
+/* Epetra-identical CSR of J: rows sorted by column, 0-based, explicit zeros kept. */
+int iemic_export_csr(iemic_ctx* ctx, int64_t* rowptr, int* col, double* val);
+
+/* ---- operators (Epetra_Operator Apply / ApplyInverse) --------------------------- */
+int iemic_spmv(iemic_ctx* ctx, const double* x, double* y);          /* y = J x     */
+int iemic_spmv_dev(iemic_ctx* ctx, const double* x, double* y, void* stream);
+int iemic_prec_compute(iemic_ctx* ctx, const iemic_krylov* opt);    /* factor once */
+int iemic_prec_apply(iemic_ctx* ctx, const double* r, double* z);
+
+/* ---- linear solve J x = b (Ocean::solve) ---------------------------------------- */
+int iemic_solve(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* opt,
+                iemic_solve_info* info);
+/* device-resident variant: b, x are device pointers of length nrows */
+int iemic_solve_dev(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* opt,
+                    iemic_solve_info* info);
+
+/* ---- one Newton step on the resident state (transient/Newton.H:92-99 form) -----
+ * F(x); J(x); precond compute; solve J dx = -F; x += dx; F(x).  Returns ||F|| before /
+ * after and the solve info.  Everything stays on the device. */
+typedef struct {
+    double norm_f0, norm_f1;
+    iemic_solve_info solve;
+    double t_jac_ms, t_rhs_ms, t_prec_ms, t_solve_ms, t_total_ms;
+} iemic_newton_info;
+int iemic_newton_step(iemic_ctx* ctx, const iemic_krylov* opt, iemic_newton_info* info);
+
+/* ---- profiling helpers (bench): time n launches of the SpMV kernel with HIP events
+ * on the stream it runs on; returns mean kernel milliseconds. */
+int iemic_time_spmv(iemic_ctx* ctx, int nrep, double* ms_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IEMIC_H */

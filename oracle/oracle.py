@@ -288,3 +288,91 @@ def fortran_to_graph(rowptr, col, beg, jco, co, rowintcon=-1):
             raise AssertionError(f"row {r}: Fortran entry outside maximal graph")
         val[b + pos] = co[fb:fe]
     return val
+
+
+# ------------------------------------------------------------------------------------
+# CPU linear solve (krylov_oracle.c)
+
+def _load_krylov():
+    lib = _load()
+    if not hasattr(lib, "_krylov_ready"):
+        P64, PI, PD = C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_double)
+        lib.orc_bcsr_build.restype = C.c_int64
+        lib.orc_bcsr_build.argtypes = [C.c_int, P64, PI, PD, P64, PI, PD, C.c_int64]
+        lib.orc_bilu0_factor.argtypes = [C.c_int, P64, PI, PD, PI, PI, PD]
+        lib.orc_bilu0_apply.argtypes = [C.c_int, P64, PI, PD, PI, PI, PD, PD, PD]
+        lib.orc_fgmres.argtypes = [C.c_int, P64, PI, PD, P64, PI, PD, PI, PI, PD, PD, PD,
+                                   C.c_double, C.c_int, C.c_int, PD, PD]
+        lib._krylov_ready = True
+    return lib
+
+
+def cell_orders(n, m, l, kind="natural"):
+    """Cell elimination orders: 'natural' (FIND_ROW2 order) or 'color8'
+    ((i%2, j%2, k%2) colour classes, natural order inside each)."""
+    ncell = n * m * l
+    c = np.arange(ncell)
+    if kind == "natural":
+        order = c
+    elif kind == "color8":
+        i, j, k = c % n, (c // n) % m, c // (n * m)
+        col = (i % 2) + 2 * (j % 2) + 4 * (k % 2)
+        order = np.lexsort((c, col))
+    else:
+        raise KeyError(kind)
+    order = np.ascontiguousarray(order, dtype=np.int32)
+    rank = np.empty(ncell, dtype=np.int32)
+    rank[order] = np.arange(ncell, dtype=np.int32)
+    return order, rank
+
+
+class BILU0:
+    def __init__(self, rowptr, col, val, ncell, order, rank):
+        lib = _load_krylov()
+        self.lib = lib
+        self.ncell = ncell
+        nb = lib.orc_bcsr_build(ncell, _p(rowptr, C.c_int64), _p(col, C.c_int), _p(val, C.c_double),
+                                None, None, None, 0)
+        self.bptr = np.zeros(ncell + 1, dtype=np.int64)
+        self.bcol = np.zeros(nb, dtype=np.int32)
+        self.bval = np.zeros(nb * 36)
+        lib.orc_bcsr_build(ncell, _p(rowptr, C.c_int64), _p(col, C.c_int), _p(val, C.c_double),
+                           _p(self.bptr, C.c_int64), _p(self.bcol, C.c_int),
+                           _p(self.bval, C.c_double), nb)
+        self.order, self.rank = order, rank
+        self.dinv = np.zeros(ncell * 36)
+        rc = lib.orc_bilu0_factor(ncell, _p(self.bptr, C.c_int64), _p(self.bcol, C.c_int),
+                                  _p(self.bval, C.c_double), _p(order, C.c_int), _p(rank, C.c_int),
+                                  _p(self.dinv, C.c_double))
+        if rc:
+            raise RuntimeError(f"BILU0: singular pivot at cell {rc - 1}")
+
+    def apply(self, r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros_like(r)
+        self.lib.orc_bilu0_apply(self.ncell, _p(self.bptr, C.c_int64), _p(self.bcol, C.c_int),
+                                 _p(self.bval, C.c_double), _p(self.order, C.c_int),
+                                 _p(self.rank, C.c_int), _p(self.dinv, C.c_double),
+                                 _p(r, C.c_double), _p(z, C.c_double))
+        return z
+
+
+def fgmres(rowptr, col, val, b, prec=None, tol=1e-8, m=500, maxit=500):
+    lib = _load_krylov()
+    N = len(rowptr) - 1
+    x = np.zeros(N)
+    rel = C.c_double()
+    hist = np.zeros(maxit + 1)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    if prec is None:
+        it = lib.orc_fgmres(N // 6, _p(rowptr, C.c_int64), _p(col, C.c_int), _p(val, C.c_double),
+                            None, None, None, None, None, None, _p(b, C.c_double),
+                            _p(x, C.c_double), tol, m, maxit, C.byref(rel), _p(hist, C.c_double))
+    else:
+        it = lib.orc_fgmres(N // 6, _p(rowptr, C.c_int64), _p(col, C.c_int), _p(val, C.c_double),
+                            _p(prec.bptr, C.c_int64), _p(prec.bcol, C.c_int),
+                            _p(prec.bval, C.c_double), _p(prec.order, C.c_int),
+                            _p(prec.rank, C.c_int), _p(prec.dinv, C.c_double),
+                            _p(b, C.c_double), _p(x, C.c_double), tol, m, maxit, C.byref(rel),
+                            _p(hist, C.c_double))
+    return x, it, rel.value, hist[:it]
