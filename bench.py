@@ -1,0 +1,228 @@
+"""Newton-step benchmark of the THCM ocean hot path (BASELINE.json metric).
+
+One step = one full Newton step of the 2-degree global ocean (192x76x16, 1,400,832
+unknowns) on the GPU: residual F, Jacobian assembly, preconditioner
+set-up, FGMRES solve of J dx = -F to the relative tolerance 1e-8 (Belos semantics,
+Ocean.C:1060-1137), x += dx and the new residual (transient/Newton.H:92-99).  Every step
+restarts from the same synthetic state (splitmix64 seed 20261015, resident in HBM; the
+reset is a device-to-device copy inside the timed region).
+
+Multi-GPU (``--gpus N`` under torch.distributed.run): round 1 runs N independent
+replicas, one per GPU (no domain decomposition yet); the step time
+is the max over ranks.
+
+Prints ONE JSON line (rank 0) with the metric, the SpMV roofline of the same run (HIP
+events on the library's stream) and the CPU baseline (the oracle port, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def spmv_bytes(nnz: int, n: int) -> int:
+    """CSR-equivalent algorithmic bytes of one SpMV."""
+    return 12 * nnz + 20 * n + 4
+
+
+def stencil_ell_bytes(ncell: int, nslot: int, n: int) -> int:
+    """Bytes the implicit-index stencil-ELL SpMV must move: values + x + y."""
+    return 8 * ncell * nslot + 16 * n
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="global2")
+    p.add_argument("--prec", type=int, default=1, help="0 none, 1 block Jacobi, 2 block GS")
+    p.add_argument("--tol", type=float, default=1e-8)
+    p.add_argument("--krylov", type=int, default=500)
+    p.add_argument("--restarts", type=int, default=0)
+    p.add_argument("--ts-sweeps", type=int, default=3)
+    p.add_argument("--spmv-reps", type=int, default=100)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-iters", type=int, default=24)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, L, x, gpu_iters: int, krylov_dim: int, prec: int):
+    """The oracle port timed on the host cores over a bounded sample of the same step:
+    full F and J assembly of the 2-degree problem, the preconditioner set-up, and two
+    FGMRES runs of K1 and K2 iterations (K = --cpu-iters) from which the cost of
+    iteration j (a + b*j, CGS2) is fitted and summed over the GPU's iteration count."""
+    from oracle import oracle as orc
+    lib = orc._load_krylov()
+    import ctypes as C
+    PD = C.POINTER(C.c_double)
+    lib.orc_bj_compute.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int), PD, PD]
+    lib.orc_fgmres_bj.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int), PD, PD, PD,
+                                  PD, C.c_double, C.c_int, C.c_int, PD, PD]
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
+    t = time.perf_counter()
+    val, _ = o.jacobian(x)
+    t_jac = time.perf_counter() - t
+    t = time.perf_counter()
+    F = o.rhs(x)
+    t_rhs = time.perf_counter() - t
+    ncell = cfg.ncell
+    P64, PI = C.POINTER(C.c_int64), C.POINTER(C.c_int)
+    dinv = np.zeros(ncell * 36)
+    t = time.perf_counter()
+    lib.orc_bj_compute(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
+                       val.ctypes.data_as(PD), dinv.ctypes.data_as(PD))
+    t_prec = time.perf_counter() - t
+    b = np.ascontiguousarray(-F)
+
+    def run(k):
+        xs = np.zeros(cfg.nrows)
+        rel = C.c_double()
+        t0 = time.perf_counter()
+        lib.orc_fgmres_bj(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
+                          val.ctypes.data_as(PD), dinv.ctypes.data_as(PD), b.ctypes.data_as(PD),
+                          xs.ctypes.data_as(PD), 1e-300, k, k, C.byref(rel), None)
+        return time.perf_counter() - t0
+
+    k2 = max(4, args_cpu_iters)
+    k1 = max(2, k2 // 3)
+    t1, t2 = run(k1), run(k2)
+    # t(K) = c0 + a*K + b*K(K-1)/2 with c0 = 2 SpMV (initial + final residual) ~ 2a
+    A = np.array([[k1 + 2, k1 * (k1 - 1) / 2], [k2 + 2, k2 * (k2 - 1) / 2]])
+    a, bq = np.linalg.solve(A, np.array([t1, t2]))
+    a = max(a, 0.0)
+    bq = max(bq, 0.0)
+    est = 0.0
+    for it in range(gpu_iters):
+        est += a + bq * (it % max(1, krylov_dim))
+    est += 2 * a
+    total = t_jac + 2 * t_rhs + t_prec + est
+    return {
+        "value": total * 1e3, "unit": "ms/Newton-step", "cores": cores, "kind": "port",
+        "sample": (f"oracle C port (OpenMP {cores} threads), same 2-degree state: F and J "
+                   f"assembly timed in full ({t_jac*1e3:.0f} + {t_rhs*1e3:.0f} ms), block-Jacobi "
+                   f"set-up {t_prec*1e3:.0f} ms, CPU FGMRES timed for {k1} and {k2} iterations "
+                   f"({t1:.2f} s, {t2:.2f} s) and extrapolated to the GPU's {gpu_iters} "
+                   f"iterations (iteration j costs a+b*j, a={a*1e3:.1f} ms, b={bq*1e3:.3f} ms)"),
+        "norm_f0": float(np.linalg.norm(F)),
+    }
+
+
+args_cpu_iters = 24
+
+
+def main():
+    global args_cpu_iters
+    args = parse()
+    args_cpu_iters = args.cpu_iters
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from iemic import _lib
+    from iemic import config as cf
+    from iemic.ocean import Ocean
+
+    cfg = cf.preset(args.config, mixing=0)
+    sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
+          "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
+          "TS sweeps": args.ts_sweeps}
+    oc = Ocean(cfg, device=local, solver_params=sp)
+    L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
+    x0h = cf.synthetic_state(cfg, L)
+    x0 = torch.from_numpy(x0h).to(dev)
+    L_ = _lib.lib()
+    torch.cuda.synchronize()
+
+    def step():
+        _lib.check(L_.iemic_set_state_dev(oc._h, x0.data_ptr()), "set_state_dev")
+        return oc.newtonStep()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    infos = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        infos.append(step())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ms = dt / args.steps * 1e3
+    if dist:
+        tt = torch.tensor([ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = float(tt.item())
+
+    # SpMV roofline on the Jacobian of the last step (HIP events on the library stream)
+    oc.setState(x0h)
+    oc.computeJacobian()
+    spmv_ms = oc.time_spmv(args.spmv_reps)
+    nnz = int(L_.iemic_graph_nnz(oc._h))
+    bsp = spmv_bytes(nnz, cfg.nrows)
+    achieved = bsp / (spmv_ms * 1e-3) / 1e9
+    ell = stencil_ell_bytes(cfg.ncell, 104, cfg.nrows)
+
+    last = infos[-1]
+    s = last.solve
+    out = {
+        "metric": "Newton-step wall time + SpMV achieved HBM GB/s, 2deg global ocean",
+        "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (splitmix64 seed 20261015 state; Combined Forcing 0.5)",
+        "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing=0, one Newton "
+                               f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
+                   "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
+                   "krylov_dim": args.krylov, "restarts": args.restarts,
+                   "parallelism": "replicas" if world > 1 else "single"},
+        "newton": {"iters": s.iters, "converged": s.converged,
+                   "explicit_rel_res": s.explicit_rel_res, "norm_f0": last.norm_f0,
+                   "norm_f1": last.norm_f1, "t_rhs_ms": last.t_rhs_ms,
+                   "t_jac_ms": last.t_jac_ms, "t_prec_ms": last.t_prec_ms,
+                   "t_solve_ms": last.t_solve_ms, "t_solve_prec_ms": s.t_prec_ms,
+                   "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms},
+        "spmv_gbps": round(achieved, 1),
+        "roofline": {"kernel": "k_spmv", "bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes": bsp, "stencil_ell_bytes": ell,
+                     "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
+                     "launch_us": round(spmv_ms * 1e3, 2)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(cfg, L, x0h, s.iters, args.krylov, args.prec)
+        out["newton"]["norm_f0_rel_diff_vs_oracle"] = abs(last.norm_f0 - cb.pop("norm_f0")) / last.norm_f0
+        out["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

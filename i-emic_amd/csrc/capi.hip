@@ -229,46 +229,10 @@ extern "C" int iemic_landm(const iemic_ctx* c, int* out)
 }
 
 /* Maximal-graph rows (THCM.C:2288-2521): sorted, de-duplicated columns */
-static void graph_row(const iemic_ctx* c, int64_t row, std::vector<int64_t>& cols, std::vector<int>& slot)
-{
-    cols.clear();
-    slot.clear();
-    Geo g = c->geo();
-    const int64_t cell = row / NUN;
-    const int var = (int)(row % NUN);
-    const int i = (int)(cell % c->n) + 1, j = (int)((cell / c->n) % c->m) + 1,
-              k = (int)(cell / ((int64_t)c->n * c->m)) + 1;
-    if (row == c->rowintcon) {
-        for (int64_t q = 0; q < c->ncell; q++) {
-            cols.push_back(NUN * q + SS);
-            slot.push_back(-1);
-        }
-        return;
-    }
-    std::vector<std::pair<int64_t, int>> e;
-    for (int s = ROW_BEGIN[var]; s < ROW_BEGIN[var + 1]; s++) {
-        int64_t col = slot_col(g, s, i, j, k);
-        if (col >= 0) e.push_back({col, s});
-    }
-    std::sort(e.begin(), e.end());
-    for (size_t a = 0; a < e.size(); a++)
-        if (a == 0 || e[a].first != e[a - 1].first) {
-            cols.push_back(e[a].first);
-            slot.push_back(e[a].second);
-        }
-}
-
 extern "C" int64_t iemic_graph_nnz(const iemic_ctx* c)
 {
     if (!c) return IEMIC_EINVAL;
-    int64_t nnz = 0;
-    std::vector<int64_t> cols;
-    std::vector<int> slot;
-    for (int64_t r = 0; r < c->nrows; r++) {
-        graph_row(c, r, cols, slot);
-        nnz += (int64_t)cols.size();
-    }
-    return nnz;
+    return c->su.to_csr(nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int iemic_set_state(iemic_ctx* c, const double* x)
@@ -276,6 +240,15 @@ extern "C" int iemic_set_state(iemic_ctx* c, const double* x)
     CTX_CHECK(c);
     if (!x) return IEMIC_EINVAL;
     HIP_OK(hipMemcpy(c->d_x.p, x, sizeof(double) * c->nrows, hipMemcpyHostToDevice));
+    c->jac_valid = 0;
+    return 0;
+}
+extern "C" int iemic_set_state_dev(iemic_ctx* c, const double* x_dev)
+{
+    CTX_CHECK(c);
+    if (!x_dev) return IEMIC_EINVAL;
+    HIP_OK(hipMemcpyAsync(c->d_x.p, x_dev, sizeof(double) * c->nrows, hipMemcpyDeviceToDevice,
+                          c->stream));
     c->jac_valid = 0;
     return 0;
 }
@@ -327,21 +300,7 @@ extern "C" int iemic_export_csr(iemic_ctx* c, int64_t* rowptr, int* col, double*
         ic.resize(c->nrows);
         HIP_OK(hipMemcpy(ic.data(), c->d_intc.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost));
     }
-    std::vector<int64_t> cols;
-    std::vector<int> slot;
-    int64_t pos = 0;
-    for (int64_t r = 0; r < c->nrows; r++) {
-        rowptr[r] = pos;
-        graph_row(c, r, cols, slot);
-        const int64_t cell = r / NUN;
-        for (size_t a = 0; a < cols.size(); a++) {
-            col[pos] = (int)cols[a];
-            if (slot[a] >= 0) val[pos] = v[(size_t)slot[a] * c->ncell + cell];
-            else val[pos] = c->cfg.int_sign * ic[cols[a]];
-            pos++;
-        }
-    }
-    rowptr[c->nrows] = pos;
+    c->su.to_csr(v.data(), ic.data(), rowptr, col, val);
     return 0;
 }
 

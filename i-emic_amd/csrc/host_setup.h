@@ -15,7 +15,9 @@
 #ifndef IEMIC_HOST_SETUP_H
 #define IEMIC_HOST_SETUP_H
 
+#include <algorithm>
 #include <cmath>
+#include <utility>
 #include <vector>
 
 #include "../../include/iemic.h"
@@ -213,6 +215,64 @@ struct Setup {
                         ic[(size_t)NUN * (((size_t)(k - 1) * m + (j - 1)) * n + (i - 1)) + SS] =
                             std::cos(y[j]) * dfzT[k];
         return ic;
+    }
+
+    /* Row `row` of the maximal graph (THCM::CreateMaximalGraph, THCM.C:2288-2491, columns
+     * sorted as Epetra stores them): columns and the stencil slot feeding each.  Several
+     * slots can name the same column (tiny periodic grids); `slot` keeps all of them, in
+     * `first` the position of the column they add into.  The intcond row (SRES = 0) is
+     * dense over all S unknowns (THCM.C:2475-2486); its slots are -1. */
+    void graph_row(int64_t row, std::vector<int64_t>& cols, std::vector<std::pair<int, int>>& slot) const
+    {
+        cols.clear();
+        slot.clear();
+        const int64_t ncell = (int64_t)n * m * l;
+        if (row == rowintcon) {
+            for (int64_t q = 0; q < ncell; q++) cols.push_back(NUN * q + SS);
+            return;
+        }
+        Geo g = geo(nullptr, tab.data());
+        const int64_t cell = row / NUN;
+        const int var = (int)(row % NUN);
+        const int i = (int)(cell % n) + 1, j = (int)((cell / n) % m) + 1, k = (int)(cell / ((int64_t)n * m)) + 1;
+        std::vector<std::pair<int64_t, int>> e;
+        for (int s = ROW_BEGIN[var]; s < ROW_BEGIN[var + 1]; s++) {
+            int64_t col = slot_col(g, s, i, j, k);
+            if (col >= 0) e.push_back({col, s});
+        }
+        std::sort(e.begin(), e.end());
+        for (size_t a = 0; a < e.size(); a++) {
+            if (a == 0 || e[a].first != e[a - 1].first) cols.push_back(e[a].first);
+            slot.push_back({(int)cols.size() - 1, e[a].second});
+        }
+    }
+
+    /* Epetra-identical CSR of the Jacobian from slot-major stencil values (+ dense
+     * intcond row with coefficients intSign*ic).  rowptr/col/val may be null (count). */
+    int64_t to_csr(const double* v, const double* ic, int64_t* rowptr, int* col, double* val) const
+    {
+        const int64_t ncell = (int64_t)n * m * l, nrows = NUN * ncell;
+        std::vector<int64_t> cols;
+        std::vector<std::pair<int, int>> slot;
+        int64_t pos = 0;
+        for (int64_t r = 0; r < nrows; r++) {
+            if (rowptr) rowptr[r] = pos;
+            graph_row(r, cols, slot);
+            if (col)
+                for (size_t a = 0; a < cols.size(); a++) col[pos + a] = (int)cols[a];
+            if (val) {
+                const int64_t cell = r / NUN;
+                if (r == rowintcon)
+                    for (size_t a = 0; a < cols.size(); a++) val[pos + a] = cfg.int_sign * ic[cols[a]];
+                else {
+                    for (size_t a = 0; a < cols.size(); a++) val[pos + a] = 0.0;
+                    for (auto& ps : slot) val[pos + ps.first] += v[(size_t)ps.second * ncell + cell];
+                }
+            }
+            pos += (int64_t)cols.size();
+        }
+        if (rowptr) rowptr[nrows] = pos;
+        return pos;
     }
 
     /* Geo over externally owned copies of landm / tab */

@@ -86,6 +86,7 @@ def lib():
         "iemic_landm": (C.c_int, [vp, PI]),
         "iemic_set_state": (C.c_int, [vp, PD]),
         "iemic_get_state": (C.c_int, [vp, PD]),
+        "iemic_set_state_dev": (C.c_int, [vp, vp]),
         "iemic_jacobian": (C.c_int, [vp]),
         "iemic_rhs": (C.c_int, [vp, PD]),
         "iemic_diag_b": (C.c_int, [vp, PD]),
@@ -110,6 +111,7 @@ def lib():
 EXPORTED = ("iemic_create", "iemic_destroy", "iemic_device_count", "iemic_last_error",
             "iemic_set_par", "iemic_get_par", "iemic_nrows", "iemic_graph_nnz",
             "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",
+            "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
             "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv")

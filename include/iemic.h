@@ -101,6 +101,8 @@ int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local 
 /* ---- state ------------------------------------------------------------------------ */
 int iemic_set_state(iemic_ctx* ctx, const double* x);     /* host -> device state     */
 int iemic_get_state(iemic_ctx* ctx, double* x);
+/* device -> device state copy on the library stream (x_dev: N doubles in HBM) */
+int iemic_set_state_dev(iemic_ctx* ctx, const double* x_dev);
 
 /* ---- assembly (THCM::evaluate, THCM.C:949-1192) --------------------------------- */
 int iemic_jacobian(iemic_ctx* ctx);                 /* J(state) + diag(B) on device */

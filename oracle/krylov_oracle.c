@@ -218,21 +218,68 @@ void orc_bilu0_apply(int ncell, const int64_t* bptr, const int* bcol, const doub
     }
 }
 
-/* ---- FGMRES ---------------------------------------------------------------------- */
+/* ---- preconditioners behind one callback --------------------------------------- */
+typedef void (*orc_prec_fn)(const void* ctx, const double* r, double* z);
+
 typedef struct {
     int ncell;
-    const int64_t *rowptr, *bptr;
-    const int *col, *bcol, *order, *rank;
-    const double *val, *bval, *dinv;
-} sys_t;
+    const int64_t* bptr;
+    const int *bcol, *order, *rank;
+    const double *bval, *dinv;
+} bilu_t;
 
-static void apply_prec(const sys_t* s, const double* r, double* z)
+static void bilu_apply_cb(const void* ctx, const double* r, double* z)
 {
-    if (!s->bval) {
-        memcpy(z, r, sizeof(double) * s->ncell * NB);
-        return;
-    }
+    const bilu_t* s = (const bilu_t*)ctx;
     orc_bilu0_apply(s->ncell, s->bptr, s->bcol, s->bval, s->order, s->rank, s->dinv, r, z);
+}
+
+/* Block Jacobi: inverse of each cell's 6x6 diagonal block (identity if singular) --
+ * the CPU twin of prec.hip k_bj_compute/k_bj_apply. */
+void orc_bj_compute(int ncell, const int64_t* rowptr, const int* col, const double* val,
+                    double* dinv)
+{
+#pragma omp parallel for schedule(static)
+    for (int cell = 0; cell < ncell; cell++) {
+        double A[BB] = {0};
+        for (int a = 0; a < NB; a++) {
+            const int64_t row = (int64_t)cell * NB + a;
+            for (int64_t p = rowptr[row]; p < rowptr[row + 1]; p++) {
+                const int c = col[p];
+                if (c / NB == cell) A[a * NB + c % NB] += val[p];
+            }
+        }
+        double* D = dinv + (int64_t)cell * BB;
+        if (inv6(A, D)) {
+            for (int q = 0; q < BB; q++) D[q] = 0.0;
+            for (int a = 0; a < NB; a++) D[a * NB + a] = 1.0;
+        }
+    }
+}
+
+typedef struct {
+    int ncell;
+    const double* dinv;
+} bj_t;
+
+static void bj_apply_cb(const void* ctx, const double* r, double* z)
+{
+    const bj_t* s = (const bj_t*)ctx;
+#pragma omp parallel for schedule(static)
+    for (int cell = 0; cell < s->ncell; cell++) {
+        const double* D = s->dinv + (int64_t)cell * BB;
+        for (int a = 0; a < NB; a++) {
+            double acc = 0.0;
+            for (int c = 0; c < NB; c++) acc += D[a * NB + c] * r[(int64_t)cell * NB + c];
+            z[(int64_t)cell * NB + a] = acc;
+        }
+    }
+}
+
+void orc_bj_apply(int ncell, const double* dinv, const double* r, double* z)
+{
+    bj_t s = {ncell, dinv};
+    bj_apply_cb(&s, r, z);
 }
 
 static double dot(int n, const double* a, const double* b)
@@ -245,13 +292,10 @@ static double dot(int n, const double* a, const double* b)
 
 /* Right-preconditioned FGMRES(m) with restarts, CGS2.  Tolerance relative to ||b||
  * (x0 = 0).  Returns iterations; *relres = ||b - A x|| / ||b|| (true residual). */
-int orc_fgmres(int ncell, const int64_t* rowptr, const int* col, const double* val,
-               const int64_t* bptr, const int* bcol, const double* bval, const int* order,
-               const int* rank, const double* dinv, const double* b, double* x, double tol,
-               int m, int maxit, double* relres, double* hist)
+static int fgmres_core(int N, const int64_t* rowptr, const int* col, const double* val,
+                       orc_prec_fn prec, const void* pctx, const double* b, double* x,
+                       double tol, int m, int maxit, double* relres, double* hist)
 {
-    int N = ncell * NB;
-    sys_t s = {ncell, rowptr, bptr, col, bcol, order, rank, val, bval, dinv};
     double* V = (double*)malloc(sizeof(double) * (size_t)N * (m + 1));
     double* Z = (double*)malloc(sizeof(double) * (size_t)N * m);
     double* H = (double*)calloc((size_t)(m + 1) * m, sizeof(double));
@@ -280,7 +324,8 @@ int orc_fgmres(int ncell, const int64_t* rowptr, const int* col, const double* v
             double* vj = V + (size_t)j * N;
             double* zj = Z + (size_t)j * N;
             double* w = V + (size_t)(j + 1) * N;
-            apply_prec(&s, vj, zj);
+            if (prec) prec(pctx, vj, zj);
+            else memcpy(zj, vj, sizeof(double) * N);
             orc_csr_spmv(N, rowptr, col, val, zj, w);
             for (int i = 0; i <= j; i++) hcol[i] = 0.0;
             for (int pass = 0; pass < 2; pass++) {
@@ -338,4 +383,24 @@ int orc_fgmres(int ncell, const int64_t* rowptr, const int* col, const double* v
     *relres = sqrt(dot(N, r, r)) / bnorm;
     free(V); free(Z); free(H); free(cs); free(sn); free(g); free(hcol); free(r);
     return it;
+}
+
+int orc_fgmres(int ncell, const int64_t* rowptr, const int* col, const double* val,
+               const int64_t* bptr, const int* bcol, const double* bval, const int* order,
+               const int* rank, const double* dinv, const double* b, double* x, double tol,
+               int m, int maxit, double* relres, double* hist)
+{
+    bilu_t s = {ncell, bptr, bcol, order, rank, bval, dinv};
+    return fgmres_core(ncell * NB, rowptr, col, val, bval ? bilu_apply_cb : NULL, &s, b, x, tol,
+                       m, maxit, relres, hist);
+}
+
+/* FGMRES with the block-Jacobi preconditioner (dinv from orc_bj_compute) */
+int orc_fgmres_bj(int ncell, const int64_t* rowptr, const int* col, const double* val,
+                  const double* dinv, const double* b, double* x, double tol, int m, int maxit,
+                  double* relres, double* hist)
+{
+    bj_t s = {ncell, dinv};
+    return fgmres_core(ncell * NB, rowptr, col, val, bj_apply_cb, &s, b, x, tol, m, maxit,
+                       relres, hist);
 }

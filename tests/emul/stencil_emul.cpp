@@ -106,6 +106,14 @@ void emul_rhs(void* h, const double* x, double* F)
     }
 }
 
+/* Epetra-shaped CSR of emulated slot values (same routine as iemic_export_csr) */
+int64_t emul_to_csr(void* h, const double* v, int64_t* rowptr, int* col, double* val)
+{
+    Emul* e = (Emul*)h;
+    std::vector<double> ic = e->su.intcond_coeff();
+    return e->su.to_csr(v, ic.data(), rowptr, col, val);
+}
+
 /* slot -> column map helper for CSR conversion in tests */
 int64_t emul_slot_col(void* h, int s, int64_t cell)
 {

@@ -1,0 +1,112 @@
+"""Test helpers: golden fixtures, mask fix-up, the CPU emulation harness wrapper."""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+from iemic import _lib
+from iemic import config as cf
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+EMUL_LIB = os.path.join(HERE, "_build", "libstencil_emul.so")
+P = C.POINTER
+
+
+def manifest() -> dict:
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def golden(name: str) -> dict:
+    with np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def golden_landm(name: str) -> np.ndarray:
+    c = cf.preset(name, mixing=0)
+    g = golden(name)
+    return g["landm_local"].astype(np.int32).reshape(c.l + 2, c.m + 2, c.n + 2)
+
+
+def state(cfg, landm, kind: str, g: dict | None = None) -> np.ndarray:
+    if kind == "zero":
+        return np.zeros(cfg.nrows)
+    if kind == "synthetic":
+        return cf.synthetic_state(cfg, landm)
+    return g[f"{kind}_x"]
+
+
+def mask_fix(orc, cfg, L, max_fix: int = 5):
+    """Ocean::analyzeJacobian1 (Ocean.C:1877-1938) restated on the oracle: pressure rows
+    with at most two entries |v| > 1e-10 at the zero state become land."""
+    L = L.copy()
+    for _ in range(max_fix):
+        o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
+        val, _ = o.jacobian(np.zeros(o.N))
+        bad = []
+        for cell in range(cfg.ncell):
+            row = 6 * cell + 3
+            v = val[o.rowptr[row]:o.rowptr[row + 1]]
+            i, j, k = cell % cfg.n, (cell // cfg.n) % cfg.m, cell // (cfg.n * cfg.m)
+            if v.sum() == 1:
+                continue
+            if np.sum(np.abs(v) > 1e-10) <= 2:
+                bad.append((i, j, k))
+        if not bad:
+            return L
+        for i, j, k in bad:
+            L[k + 1, j + 1, i + 1] = 1
+    return L
+
+
+class Emul:
+    """ctypes wrapper of tests/emul/stencil_emul.cpp."""
+
+    def __init__(self, cfg, landm):
+        lib = C.CDLL(EMUL_LIB)
+        lib.emul_create.restype = C.c_void_p
+        lib.emul_create.argtypes = [P(_lib.Grid), P(C.c_int)]
+        lib.emul_destroy.argtypes = [C.c_void_p]
+        lib.emul_set_par.argtypes = [C.c_void_p, C.c_int, C.c_double]
+        lib.emul_jacobian.argtypes = [C.c_void_p] + [P(C.c_double)] * 3
+        lib.emul_rhs.argtypes = [C.c_void_p] + [P(C.c_double)] * 2
+        lib.emul_to_csr.restype = C.c_int64
+        lib.emul_to_csr.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int64), P(C.c_int),
+                                    P(C.c_double)]
+        self.lib = lib
+        self.cfg = cfg
+        g = _lib.grid_from_config(cfg, analyze_jacobian=False)
+        L = np.ascontiguousarray(landm.reshape(-1), dtype=np.int32)
+        self.h = lib.emul_create(C.byref(g), _lib.ptr(L, C.c_int))
+        for idx, v in cfg.par_list():
+            lib.emul_set_par(self.h, idx, v)
+
+    def __del__(self):
+        try:
+            self.lib.emul_destroy(self.h)
+        except Exception:
+            pass
+
+    def jacobian_csr(self, x):
+        c = self.cfg
+        slots = np.zeros(104 * c.ncell)
+        B = np.zeros(c.nrows)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        self.lib.emul_jacobian(self.h, _lib.ptr(x), _lib.ptr(slots), _lib.ptr(B))
+        nnz = self.lib.emul_to_csr(self.h, _lib.ptr(slots), None, None, None)
+        rowptr = np.zeros(c.nrows + 1, dtype=np.int64)
+        col = np.zeros(nnz, dtype=np.int32)
+        val = np.zeros(nnz)
+        self.lib.emul_to_csr(self.h, _lib.ptr(slots), _lib.ptr(rowptr, C.c_int64),
+                             _lib.ptr(col, C.c_int), _lib.ptr(val))
+        return rowptr, col, val, B
+
+    def rhs(self, x):
+        F = np.zeros(self.cfg.nrows)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        self.lib.emul_rhs(self.h, _lib.ptr(x), _lib.ptr(F))
+        return F
