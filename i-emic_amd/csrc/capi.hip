@@ -36,6 +36,16 @@ extern "C" int iemic_device_count(void)
 
 Geo iemic_ctx::geo() const { return su.geo(d_landm.p, d_tab.p); }
 
+iemic_ctx::~iemic_ctx()
+{
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (h_red) (void)hipHostFree(h_red);
+    h_red = nullptr;
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+    /* device buffers are members: released after this body, with the stream drained */
+}
+
 namespace {
 
 int upload_forcing_tables(iemic_ctx* c)
@@ -49,11 +59,10 @@ int upload_forcing_tables(iemic_ctx* c)
 
 int upload_landm(iemic_ctx* c)
 {
-    HIP_OK(hipMemcpy(c->d_landm.p, c->su.landm.data(), sizeof(int) * c->su.landm.size(),
-                     hipMemcpyHostToDevice));
+    int rc = h2d(c, c->d_landm.p, c->su.landm.data(), sizeof(int) * c->su.landm.size());
+    if (rc) return rc;
     std::vector<double> ic = c->su.intcond_coeff();
-    HIP_OK(hipMemcpy(c->d_intc.p, ic.data(), sizeof(double) * ic.size(), hipMemcpyHostToDevice));
-    return 0;
+    return h2d(c, c->d_intc.p, ic.data(), sizeof(double) * ic.size());
 }
 
 /* Ocean::analyzeJacobian1 (Ocean.C:273-340) + THCM::getLandMask(fix) (THCM.C:1298-1330):
@@ -61,14 +70,14 @@ int upload_landm(iemic_ctx* c)
 int mask_fix(iemic_ctx* c)
 {
     const int n = c->n, m = c->m;
-    HIP_OK(hipMemset(c->d_tmp1.p, 0, sizeof(double) * c->nrows));
+    HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nrows, c->stream));
     const int pb = ROW_BEGIN[PP], pn = ROW_BEGIN[PP + 1] - ROW_BEGIN[PP];
     std::vector<double> pv((size_t)pn * c->ncell);
     for (int cyc = 0; cyc < std::max(1, c->cfg.max_mask_fixes); cyc++) {
         int rc = assemble_jacobian(c, c->d_tmp1.p);
         if (rc) return rc;
-        HIP_OK(hipMemcpy(pv.data(), c->d_val.p + (size_t)pb * c->ncell, sizeof(double) * pv.size(),
-                         hipMemcpyDeviceToHost));
+        if ((rc = d2h(c, pv.data(), c->d_val.p + (size_t)pb * c->ncell, sizeof(double) * pv.size())))
+            return rc;
         int nfix = 0;
         for (int64_t cell = 0; cell < c->ncell; cell++) {
             if (NUN * cell + PP == c->rowintcon) continue;
@@ -143,14 +152,17 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
     rc |= c->d_tmp1.alloc(c->nrows);
     rc |= c->d_tmp2.alloc(c->nrows);
     rc |= c->d_red.alloc(2048);
+    rc |= c->d_part.alloc((size_t)RED_BLOCKS * (MAX_KRYLOV + 2));
+    rc |= c->d_hbuf.alloc((size_t)2 * (MAX_KRYLOV + 2));
+    if (!rc && hipHostMalloc(&c->h_red, sizeof(double) * 2 * (MAX_KRYLOV + 2)) != hipSuccess) rc = 1;
     if (rc) {
         set_error("iemic_create: out of device memory");
         delete c;
         return IEMIC_ENOMEM;
     }
-    (void)hipMemset(c->d_x.p, 0, sizeof(double) * c->nrows);
+    (void)hipMemsetAsync(c->d_x.p, 0, sizeof(double) * c->nrows, c->stream);
     if (c->d_tab.alloc(c->su.tab.size()) ||
-        hipMemcpy(c->d_tab.p, c->su.tab.data(), sizeof(double) * c->su.tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        h2d(c, c->d_tab.p, c->su.tab.data(), sizeof(double) * c->su.tab.size()) != 0) {
         set_error("iemic_create: cannot upload metric tables");
         delete c;
         return IEMIC_EDEVICE;
@@ -182,20 +194,16 @@ extern "C" void iemic_destroy(iemic_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    if (c->kr.hhost) (void)hipHostFree(c->kr.hhost);
-    (void)hipStreamDestroy(c->stream);
-    delete c;
+    delete c; /* ~iemic_ctx drains the stream before any buffer is released */
 }
 
 #define CTX_CHECK(c)                                   \
-    do {                                               \
-        if (!(c)) return IEMIC_EINVAL;                 \
-        if (hipSetDevice((c)->device) != hipSuccess) { \
-            set_error("hipSetDevice failed");          \
-            return IEMIC_EDEVICE;                      \
-        }                                              \
-    } while (0)
+    if (!(c)) return IEMIC_EINVAL;                     \
+    if (hipSetDevice((c)->device) != hipSuccess) {     \
+        set_error("hipSetDevice failed");              \
+        return IEMIC_EDEVICE;                          \
+    }                                                  \
+    StreamGuard stream_guard_{(c)}
 
 extern "C" int iemic_set_par(iemic_ctx* c, int idx, double value)
 {
@@ -239,7 +247,8 @@ extern "C" int iemic_set_state(iemic_ctx* c, const double* x)
 {
     CTX_CHECK(c);
     if (!x) return IEMIC_EINVAL;
-    HIP_OK(hipMemcpy(c->d_x.p, x, sizeof(double) * c->nrows, hipMemcpyHostToDevice));
+    int rc = h2d(c, c->d_x.p, x, sizeof(double) * c->nrows);
+    if (rc) return rc;
     c->jac_valid = 0;
     return 0;
 }
@@ -255,7 +264,7 @@ extern "C" int iemic_set_state_dev(iemic_ctx* c, const double* x_dev)
 extern "C" int iemic_get_state(iemic_ctx* c, double* x)
 {
     CTX_CHECK(c);
-    HIP_OK(hipMemcpy(x, c->d_x.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost));
+    return d2h(c, x, c->d_x.p, sizeof(double) * c->nrows);
     return 0;
 }
 
@@ -282,7 +291,8 @@ extern "C" int iemic_diag_b(iemic_ctx* c, double* B)
 {
     CTX_CHECK(c);
     if (!c->jac_valid) return IEMIC_ESTATE;
-    HIP_OK(hipMemcpy(B, c->d_B.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost));
+    int rc = d2h(c, B, c->d_B.p, sizeof(double) * c->nrows);
+    if (rc) return rc;
     return 0;
 }
 
@@ -294,11 +304,12 @@ extern "C" int iemic_export_csr(iemic_ctx* c, int64_t* rowptr, int* col, double*
         return IEMIC_ESTATE;
     }
     std::vector<double> v((size_t)NSLOT * c->ncell);
-    HIP_OK(hipMemcpy(v.data(), c->d_val.p, sizeof(double) * v.size(), hipMemcpyDeviceToHost));
+    int rc = d2h(c, v.data(), c->d_val.p, sizeof(double) * v.size());
+    if (rc) return rc;
     std::vector<double> ic;
     if (c->rowintcon >= 0) {
         ic.resize(c->nrows);
-        HIP_OK(hipMemcpy(ic.data(), c->d_intc.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost));
+        if ((rc = d2h(c, ic.data(), c->d_intc.p, sizeof(double) * c->nrows))) return rc;
     }
     c->su.to_csr(v.data(), ic.data(), rowptr, col, val);
     return 0;
@@ -307,8 +318,9 @@ extern "C" int iemic_export_csr(iemic_ctx* c, int64_t* rowptr, int* col, double*
 extern "C" int iemic_spmv(iemic_ctx* c, const double* x, double* y)
 {
     CTX_CHECK(c);
-    HIP_OK(hipMemcpy(c->d_tmp1.p, x, sizeof(double) * c->nrows, hipMemcpyHostToDevice));
-    int rc = spmv(c, c->d_tmp1.p, c->d_tmp2.p, c->stream);
+    int rc = h2d(c, c->d_tmp1.p, x, sizeof(double) * c->nrows);
+    if (rc) return rc;
+    rc = spmv(c, c->d_tmp1.p, c->d_tmp2.p, c->stream);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(y, c->d_tmp2.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -333,8 +345,9 @@ extern "C" int iemic_prec_compute(iemic_ctx* c, const iemic_krylov* opt)
 extern "C" int iemic_prec_apply(iemic_ctx* c, const double* r, double* z)
 {
     CTX_CHECK(c);
-    HIP_OK(hipMemcpy(c->d_tmp1.p, r, sizeof(double) * c->nrows, hipMemcpyHostToDevice));
-    int rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);
+    int rc = h2d(c, c->d_tmp1.p, r, sizeof(double) * c->nrows);
+    if (rc) return rc;
+    rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(z, c->d_tmp2.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -356,11 +369,11 @@ extern "C" int iemic_solve(iemic_ctx* c, const double* b, double* x, const iemic
     if (!opt || !b || !x) return IEMIC_EINVAL;
     DevBuf<double> db, dx;
     if (db.alloc(c->nrows) || dx.alloc(c->nrows)) return IEMIC_ENOMEM;
-    HIP_OK(hipMemcpy(db.p, b, sizeof(double) * c->nrows, hipMemcpyHostToDevice));
-    int rc = fgmres(c, db.p, dx.p, opt, info);
+    int rc = h2d(c, db.p, b, sizeof(double) * c->nrows);
     if (rc) return rc;
-    HIP_OK(hipMemcpy(x, dx.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost));
-    return 0;
+    rc = fgmres(c, db.p, dx.p, opt, info);
+    if (rc) return rc;
+    return d2h(c, x, dx.p, sizeof(double) * c->nrows);
 }
 
 namespace iemic {

@@ -73,9 +73,11 @@ struct BlockGS {
 struct Krylov {
     int m = 0;                       /* allocated basis size                            */
     DevBuf<double> V, Z;             /* (m+1) x N and m x N                             */
-    DevBuf<double> w, r, partial, hbuf;
-    double* hhost = nullptr;         /* pinned host copy of dot results                 */
+    DevBuf<double> w, r;
 };
+
+constexpr int RED_BLOCKS = 512;      /* partial-sum blocks of the reductions            */
+constexpr int MAX_KRYLOV = 1000;     /* largest Krylov dimension                        */
 
 }  // namespace iemic
 
@@ -98,13 +100,43 @@ struct iemic_ctx {
     /* state and operator */
     iemic::DevBuf<double> d_x, d_F, d_B, d_val; /* d_val: NSLOT x ncell                    */
     iemic::DevBuf<double> d_tmp1, d_tmp2, d_red;
+    /* reduction buffers (allocated at create): partial sums, results, pinned host copy */
+    iemic::DevBuf<double> d_part, d_hbuf;
+    double* h_red = nullptr;
     int jac_valid = 0;
     iemic::BlockGS gs;
     iemic::Krylov kr;
     iemic::Geo geo() const;
+    iemic_ctx() = default;
+    iemic_ctx(const iemic_ctx&) = delete;
+    iemic_ctx& operator=(const iemic_ctx&) = delete;
+    ~iemic_ctx();
 };
 
 namespace iemic {
+/* Stream-ordered copies: every transfer goes through the context's stream and is complete
+ * on return (the stream is non-blocking, so the legacy null stream must never be used). */
+inline int h2d(iemic_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!bytes) return 0;
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+inline int d2h(iemic_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!bytes) return 0;
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+/* Drains the stream when an entry point returns, also on error paths, so no kernel of
+ * this context is still in flight when control goes back to the caller. */
+struct StreamGuard {
+    iemic_ctx* c;
+    ~StreamGuard() { if (c && c->stream) (void)hipStreamSynchronize(c->stream); }
+};
+
 /* assembly.hip */
 int assemble_jacobian(iemic_ctx* c, const double* x_dev);
 int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev);

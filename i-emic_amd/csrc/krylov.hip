@@ -81,7 +81,6 @@ __global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic,
 }
 
 /* ---- reductions / BLAS-1 ------------------------------------------------------------ */
-constexpr int RED_BLOCKS = 512;
 
 __device__ __forceinline__ double block_sum(double v, double* sm)
 {
@@ -200,13 +199,13 @@ static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const
 {
     const int64_t N = c->nrows;
     hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec), dim3(256), 0, c->stream, V, ldv, nvec, w, N,
-                       c->kr.partial.p);
-    hipLaunchKernelGGL(k_mdot_final, dim3(nvec), dim3(256), 0, c->stream, c->kr.partial.p, RED_BLOCKS,
-                       nvec, c->kr.hbuf.p);
-    HIP_OK(hipMemcpyAsync(c->kr.hhost, c->kr.hbuf.p, sizeof(double) * nvec, hipMemcpyDeviceToHost,
+                       c->d_part.p);
+    hipLaunchKernelGGL(k_mdot_final, dim3(nvec), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS,
+                       nvec, c->d_hbuf.p);
+    HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * nvec, hipMemcpyDeviceToHost,
                           c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < nvec; i++) out[i] = c->kr.hhost[i];
+    for (int i = 0; i < nvec; i++) out[i] = c->h_red[i];
     return 0;
 }
 
@@ -227,15 +226,22 @@ static int ensure_krylov(iemic_ctx* c, int m)
     rc |= c->kr.Z.alloc((size_t)m * N);
     rc |= c->kr.w.alloc(N);
     rc |= c->kr.r.alloc(N);
-    rc |= c->kr.partial.alloc((size_t)RED_BLOCKS * (m + 2));
-    rc |= c->kr.hbuf.alloc(m + 2);
     if (rc) {
         set_error("fgmres: out of device memory for the Krylov basis");
         return IEMIC_ENOMEM;
     }
-    if (c->kr.hhost) (void)hipHostFree(c->kr.hhost);
-    HIP_OK(hipHostMalloc(&c->kr.hhost, sizeof(double) * (m + 2)));
     c->kr.m = m;
+    return 0;
+}
+
+/* coefficients -> device through the pinned staging area (the previous use of the area
+ * has completed: every caller synchronised the stream since) */
+static int upload_coeffs(iemic_ctx* c, const double* h, int n)
+{
+    double* st = c->h_red + (MAX_KRYLOV + 2);
+    for (int i = 0; i < n; i++) st[i] = h[i];
+    HIP_OK(hipMemcpyAsync(c->d_hbuf.p + (MAX_KRYLOV + 2), st, sizeof(double) * n,
+                          hipMemcpyHostToDevice, c->stream));
     return 0;
 }
 
@@ -246,7 +252,7 @@ static double ms_since(std::chrono::steady_clock::time_point t0)
 
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
 {
-    const int m = std::max(1, std::min(opt->krylov_dim, 1000));
+    const int m = std::max(1, std::min(opt->krylov_dim, MAX_KRYLOV));
     const int64_t N = c->nrows;
     int rc = ensure_krylov(c, m);
     if (rc) return rc;
@@ -298,14 +304,14 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             /* CGS2 */
             rc = mdot_host(c, V, N, j + 1, vn, h.data());
             if (rc) return rc;
-            HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, h.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice,
-                                  c->stream));
-            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1, c->kr.hbuf.p, vn, N);
+            if ((rc = upload_coeffs(c, h.data(), j + 1))) return rc;
+            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1,
+                               c->d_hbuf.p + (MAX_KRYLOV + 2), vn, N);
             rc = mdot_host(c, V, N, j + 1, vn, h2.data());
             if (rc) return rc;
-            HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, h2.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice,
-                                  c->stream));
-            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1, c->kr.hbuf.p, vn, N);
+            if ((rc = upload_coeffs(c, h2.data(), j + 1))) return rc;
+            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1,
+                               c->d_hbuf.p + (MAX_KRYLOV + 2), vn, N);
             for (int i = 0; i <= j; i++) h[i] += h2[i];
             double hn2 = 0.0;
             rc = mdot_host(c, vn, 0, 1, vn, &hn2);
@@ -344,8 +350,11 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             for (int q = i + 1; q < k; q++) t -= H[(size_t)i * m + q] * y[q];
             y[i] = t / H[(size_t)i * m + i];
         }
-        HIP_OK(hipMemcpyAsync(c->kr.hbuf.p, y.data(), sizeof(double) * k, hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z, N, k, c->kr.hbuf.p, x, N);
+        if (k > 0) {
+            if ((rc = upload_coeffs(c, y.data(), k))) return rc;
+            hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z, N, k,
+                               c->d_hbuf.p + (MAX_KRYLOV + 2), x, N);
+        }
         if (conv || cycle == opt->max_restarts) break;
         /* r = b - J x */
         rc = spmv(c, x, r, c->stream);

@@ -28,7 +28,7 @@ def Ocean():
 
 def make(Ocean, orc, name, **kw):
     c = cf.preset(name, mixing=0)
-    L0 = golden_landm(name)
+    L0 = golden_landm(name) if name != "global2" else cf.init_landmask(c, cf.landmask(c))
     oc = Ocean(c, landm=L0, **kw)
     L = mask_fix(orc, c, L0)
     o = orc.Oracle(c.ref_dict(), L, c.par_list())
