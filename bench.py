@@ -47,29 +47,33 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="global2")
-    p.add_argument("--prec", type=int, default=1, help="0 none, 1 block Jacobi, 2 block GS")
+    p.add_argument("--prec", type=int, default=2, help="0 none, 1 block Jacobi, 2 block GS")
+    p.add_argument("--amp-ts", type=float, default=1e-3,
+                   help="T/S amplitude of the synthetic state (DESIGN.md: benchmark state)")
     p.add_argument("--tol", type=float, default=1e-8)
     p.add_argument("--krylov", type=int, default=500)
     p.add_argument("--restarts", type=int, default=0)
     p.add_argument("--ts-sweeps", type=int, default=3)
     p.add_argument("--spmv-reps", type=int, default=100)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-iters", type=int, default=24)
+    p.add_argument("--cpu-iters", type=int, default=48)
     return p.parse_args()
 
 
-def cpu_baseline(cfg, L, x, gpu_iters: int, krylov_dim: int, prec: int):
+def cpu_baseline(cfg, L, x, gpu_iters: int, krylov_dim: int, prec: int, ts_sweeps: int):
     """The oracle port timed on the host cores over a bounded sample of the same step:
     full F and J assembly of the 2-degree problem, the preconditioner set-up, and two
-    FGMRES runs of K1 and K2 iterations (K = --cpu-iters) from which the cost of
-    iteration j (a + b*j, CGS2) is fitted and summed over the GPU's iteration count."""
+    FGMRES runs of K1 and K2 iterations (K2 = --cpu-iters) with the same preconditioner,
+    from which the cost of iteration j (a + b*j: CGS2 grows with j) is fitted and summed
+    over the GPU's iteration count."""
+    import ctypes as C
+
     from oracle import oracle as orc
     lib = orc._load_krylov()
-    import ctypes as C
-    PD = C.POINTER(C.c_double)
-    lib.orc_bj_compute.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int), PD, PD]
-    lib.orc_fgmres_bj.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int), PD, PD, PD,
-                                  PD, C.c_double, C.c_int, C.c_int, PD, PD]
+    PD, P64, PI = C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int)
+    lib.orc_bj_compute.argtypes = [C.c_int, P64, PI, PD, PD]
+    lib.orc_fgmres_bj.argtypes = [C.c_int, P64, PI, PD, PD, PD, PD, C.c_double, C.c_int, C.c_int,
+                                  PD, PD]
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
     t = time.perf_counter()
@@ -79,41 +83,46 @@ def cpu_baseline(cfg, L, x, gpu_iters: int, krylov_dim: int, prec: int):
     F = o.rhs(x)
     t_rhs = time.perf_counter() - t
     ncell = cfg.ncell
-    P64, PI = C.POINTER(C.c_int64), C.POINTER(C.c_int)
-    dinv = np.zeros(ncell * 36)
-    t = time.perf_counter()
-    lib.orc_bj_compute(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
-                       val.ctypes.data_as(PD), dinv.ctypes.data_as(PD))
-    t_prec = time.perf_counter() - t
     b = np.ascontiguousarray(-F)
+    t = time.perf_counter()
+    if prec == 2:
+        P = orc.BlockGS(o, val, ts_sweeps)
+        pname = f"block Gauss-Seidel ({ts_sweeps} T/S sweeps, band-LU Schur)"
+    else:
+        dinv = np.zeros(ncell * 36)
+        lib.orc_bj_compute(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
+                           val.ctypes.data_as(PD), dinv.ctypes.data_as(PD))
+        pname = "block Jacobi"
+    t_prec = time.perf_counter() - t
 
     def run(k):
-        xs = np.zeros(cfg.nrows)
-        rel = C.c_double()
         t0 = time.perf_counter()
-        lib.orc_fgmres_bj(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
-                          val.ctypes.data_as(PD), dinv.ctypes.data_as(PD), b.ctypes.data_as(PD),
-                          xs.ctypes.data_as(PD), 1e-300, k, k, C.byref(rel), None)
+        if prec == 2:
+            P.fgmres(b, tol=1e-300, m=k, maxit=k)
+        else:
+            xs = np.zeros(cfg.nrows)
+            rel = C.c_double()
+            lib.orc_fgmres_bj(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
+                              val.ctypes.data_as(PD), dinv.ctypes.data_as(PD),
+                              b.ctypes.data_as(PD), xs.ctypes.data_as(PD), 1e-300, k, k,
+                              C.byref(rel), None)
         return time.perf_counter() - t0
 
     k2 = max(4, args_cpu_iters)
     k1 = max(2, k2 // 3)
+    run(2)  # warm-up: first-touch of the basis arrays
     t1, t2 = run(k1), run(k2)
-    # t(K) = c0 + a*K + b*K(K-1)/2 with c0 = 2 SpMV (initial + final residual) ~ 2a
+    # t(K) = a*(K+2) + b*K(K-1)/2   (K iterations + initial and final residual SpMVs)
     A = np.array([[k1 + 2, k1 * (k1 - 1) / 2], [k2 + 2, k2 * (k2 - 1) / 2]])
     a, bq = np.linalg.solve(A, np.array([t1, t2]))
-    a = max(a, 0.0)
-    bq = max(bq, 0.0)
-    est = 0.0
-    for it in range(gpu_iters):
-        est += a + bq * (it % max(1, krylov_dim))
-    est += 2 * a
+    a, bq = max(a, 0.0), max(bq, 0.0)
+    est = sum(a + bq * (it % max(1, krylov_dim)) for it in range(gpu_iters)) + 2 * a
     total = t_jac + 2 * t_rhs + t_prec + est
     return {
-        "value": total * 1e3, "unit": "ms/Newton-step", "cores": cores, "kind": "port",
-        "sample": (f"oracle C port (OpenMP {cores} threads), same 2-degree state: F and J "
-                   f"assembly timed in full ({t_jac*1e3:.0f} + {t_rhs*1e3:.0f} ms), block-Jacobi "
-                   f"set-up {t_prec*1e3:.0f} ms, CPU FGMRES timed for {k1} and {k2} iterations "
+        "value": round(total * 1e3, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
+        "sample": (f"oracle C port (OpenMP {cores} threads), same state: F and J assembly timed "
+                   f"in full ({t_jac*1e3:.0f} + {t_rhs*1e3:.0f} ms), {pname} set-up "
+                   f"{t_prec*1e3:.0f} ms, CPU FGMRES timed for {k1} and {k2} iterations "
                    f"({t1:.2f} s, {t2:.2f} s) and extrapolated to the GPU's {gpu_iters} "
                    f"iterations (iteration j costs a+b*j, a={a*1e3:.1f} ms, b={bq*1e3:.3f} ms)"),
         "norm_f0": float(np.linalg.norm(F)),
@@ -149,7 +158,7 @@ def main():
           "TS sweeps": args.ts_sweeps}
     oc = Ocean(cfg, device=local, solver_params=sp)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
-    x0h = cf.synthetic_state(cfg, L)
+    x0h = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
     x0 = torch.from_numpy(x0h).to(dev)
     L_ = _lib.lib()
     torch.cuda.synchronize()
@@ -193,7 +202,8 @@ def main():
         "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (splitmix64 seed 20261015 state; Combined Forcing 0.5)",
+        "data": (f"synthetic (splitmix64 seed 20261015 state, u,v,w,p ~ U(+-1e-3), T,S ~ "
+                 f"U(+-{args.amp_ts:g}); Combined Forcing 0.5)"),
         "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing=0, one Newton "
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
@@ -215,7 +225,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(cfg, L, x0h, s.iters, args.krylov, args.prec)
+        cb = cpu_baseline(cfg, L, x0h, s.iters, args.krylov, args.prec, args.ts_sweeps)
         out["newton"]["norm_f0_rel_diff_vs_oracle"] = abs(last.norm_f0 - cb.pop("norm_f0")) / last.norm_f0
         out["cpu_baseline"] = cb
     if rank == 0:

@@ -52,22 +52,26 @@ template <typename T> struct DevBuf {
     ~DevBuf() { free(); }
 };
 
-/* Block Gauss-Seidel preconditioner state (prec.hip). */
+/* Preconditioner state (prec.hip: block Jacobi, prec_gs.hip: block Gauss-Seidel). */
 struct BlockGS {
     int ready = 0;
-    int ncol = 0;                    /* active (ocean) columns                          */
-    DevBuf<int> col_of_ij;           /* (i,j) -> active column index or -1              */
-    DevBuf<int> ij_of_col;           /* active column -> j*n + i                        */
-    DevBuf<int> kb;                  /* deepest ocean layer (1-based) per active column */
-    DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
-    DevBuf<double> dinv;             /* 2x2 inverse of the U/V diagonal block, 4/cell   */
-    DevBuf<double> schur_inv;        /* dense ncol x ncol inverse of the 2-D Schur      */
-    DevBuf<double> schur;            /* dense ncol x ncol Schur (work)                  */
-    DevBuf<int> piv;
-    DevBuf<double> wk1, wk2, wk3, rr; /* N-length work vectors                          */
-    DevBuf<double> colv, colv2;      /* ncol work                                       */
-    int ts_sweeps = 3;
     int kind = 0;                    /* 1: block-Jacobi, 2: block Gauss-Seidel           */
+    int ts_sweeps = 3;               /* symmetric red-black sweeps on the T/S block     */
+    DevBuf<double> dinv;             /* block-Jacobi: 6x6 inverses, slot-major          */
+    /* structure (rebuilt when the identity-row pattern changes) */
+    std::vector<uint8_t> known_h;    /* identity rows the structure was built for       */
+    int ncol = 0, bl = 0, bu = 0;    /* active water columns, Schur band widths          */
+    DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
+    DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index (band order) or -1       */
+    DevBuf<int> ij_of_col;           /* Schur index -> j*n+i                            */
+    DevBuf<uint8_t> pinned;          /* Schur index pinned to 0 (null-space pins)       */
+    /* numeric factors */
+    DevBuf<double> uvinv, tsinv;     /* 2x2 inverses per cell (U/V and T/S blocks)      */
+    DevBuf<double> pw;               /* per P row: weight of the depth integral         */
+    DevBuf<double> band;             /* Schur band, row-wise, width 2*bl+bu+1           */
+    DevBuf<int> piv, info;
+    DevBuf<double> sinv;             /* dense Schur inverse, ncol x ncol row-major      */
+    DevBuf<double> rr, bts, colv, colv2; /* work                                         */
 };
 
 struct Krylov {

@@ -404,3 +404,17 @@ int orc_fgmres_bj(int ncell, const int64_t* rowptr, const int* col, const double
     return fgmres_core(ncell * NB, rowptr, col, val, bj_apply_cb, &s, b, x, tol, m, maxit,
                        relres, hist);
 }
+
+/* FGMRES with the block Gauss-Seidel preconditioner of prec_oracle.c */
+void orc_gs_apply(void* h, const double* r, double* z);
+static void gs_apply_cb(const void* ctx, const double* r, double* z)
+{
+    orc_gs_apply((void*)ctx, r, z);
+}
+int orc_fgmres_gs(int ncell, const int64_t* rowptr, const int* col, const double* val, void* gs,
+                  const double* b, double* x, double tol, int m, int maxit, double* relres,
+                  double* hist)
+{
+    return fgmres_core(ncell * NB, rowptr, col, val, gs_apply_cb, gs, b, x, tol, m, maxit, relres,
+                       hist);
+}

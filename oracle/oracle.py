@@ -376,3 +376,68 @@ def fgmres(rowptr, col, val, b, prec=None, tol=1e-8, m=500, maxit=500):
                             _p(b, C.c_double), _p(x, C.c_double), tol, m, maxit, C.byref(rel),
                             _p(hist, C.c_double))
     return x, it, rel.value, hist[:it]
+
+
+# ------------------------------------------------------------------------------------
+# block Gauss-Seidel preconditioner (prec_oracle.c) -- CPU twin of prec_gs.hip
+
+def _load_gs():
+    lib = _load_krylov()
+    if not hasattr(lib, "_gs_ready"):
+        P64, PI, PD = C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_double)
+        lib.orc_gs_create.restype = C.c_void_p
+        lib.orc_gs_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, P64, PI, PD, C.c_int64,
+                                      C.c_int, PD, C.c_int]
+        lib.orc_gs_destroy.argtypes = [C.c_void_p]
+        lib.orc_gs_apply.argtypes = [C.c_void_p, PD, PD]
+        lib.orc_gs_ncol.argtypes = [C.c_void_p]
+        lib.orc_gs_band.argtypes = [C.c_void_p]
+        lib.orc_fgmres_gs.argtypes = [C.c_int, P64, PI, PD, C.c_void_p, PD, PD, C.c_double,
+                                      C.c_int, C.c_int, PD, PD]
+        lib._gs_ready = True
+    return lib
+
+
+class BlockGS:
+    """CPU block Gauss-Seidel preconditioner on the oracle's CSR Jacobian."""
+
+    def __init__(self, o: "Oracle", val, ts_sweeps: int = 3):
+        lib = _load_gs()
+        self.lib = lib
+        d = o.d
+        self.o = o
+        self.val = np.ascontiguousarray(val, dtype=np.float64)
+        self.intc = np.ascontiguousarray(o.intcond_coeff())
+        self.h = lib.orc_gs_create(d["n"], d["m"], d["l"], d["periodic"],
+                                   _p(o.rowptr, C.c_int64), _p(o.col, C.c_int),
+                                   _p(self.val, C.c_double), o.rowintcon, d["int_sign"],
+                                   _p(self.intc, C.c_double), ts_sweeps)
+        if not self.h:
+            raise RuntimeError("BlockGS: singular Schur complement")
+        self.ncol = lib.orc_gs_ncol(self.h)
+        self.band = lib.orc_gs_band(self.h)
+
+    def __del__(self):
+        try:
+            self.lib.orc_gs_destroy(self.h)
+        except Exception:
+            pass
+
+    def apply(self, r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros_like(r)
+        self.lib.orc_gs_apply(self.h, _p(r, C.c_double), _p(z, C.c_double))
+        return z
+
+    def fgmres(self, b, tol=1e-8, m=500, maxit=500):
+        o = self.o
+        N = len(o.rowptr) - 1
+        x = np.zeros(N)
+        rel = C.c_double()
+        hist = np.zeros(maxit + 1)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        it = self.lib.orc_fgmres_gs(N // 6, _p(o.rowptr, C.c_int64), _p(o.col, C.c_int),
+                                    _p(self.val, C.c_double), self.h, _p(b, C.c_double),
+                                    _p(x, C.c_double), tol, m, maxit, C.byref(rel),
+                                    _p(hist, C.c_double))
+        return x, it, rel.value, hist[:it]
