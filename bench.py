@@ -214,7 +214,8 @@ def main():
                    "norm_f1": last.norm_f1, "t_rhs_ms": last.t_rhs_ms,
                    "t_jac_ms": last.t_jac_ms, "t_prec_ms": last.t_prec_ms,
                    "t_solve_ms": last.t_solve_ms, "t_solve_prec_ms": s.t_prec_ms,
-                   "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms},
+                   "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms,
+                   "dgks_reorth": s.reorth},
         "spmv_gbps": round(achieved, 1),
         "roofline": {"kernel": "k_spmv", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -68,8 +68,11 @@ struct BlockGS {
     /* numeric factors */
     DevBuf<double> uvinv, tsinv;     /* 2x2 inverses per cell (U/V and T/S blocks)      */
     DevBuf<double> pw;               /* per P row: weight of the depth integral         */
+    DevBuf<uint8_t> nearknown;       /* per cell: some active row couples to a known row */
+    DevBuf<double> tsoff;            /* compact T/S off-diagonal couplings, 16 x ncell  */
     DevBuf<double> band;             /* Schur band, row-wise, width 2*bl+bu+1           */
     DevBuf<int> piv, info;
+    DevBuf<double> lpan;             /* band-LU panel multipliers                       */
     DevBuf<double> sinv;             /* dense Schur inverse, ncol x ncol row-major      */
     DevBuf<double> rr, bts, colv, colv2; /* work                                         */
 };

@@ -94,15 +94,17 @@ __device__ __forceinline__ double block_sum(double v, double* sm)
     return t;
 }
 
-/* partial[i * gridDim.x + blk] = sum over the block's range of V_i . w, i < nvec */
+/* partial[i * gridDim.x + blk] = sum over the block's range of V_i . w, i < nvec;
+ * with extra != null, row i == nvec is extra . w (the norm of w in the same launch) */
 __global__ void __launch_bounds__(256) k_mdot(const double* __restrict__ V, int64_t ldv, int nvec,
                                               const double* __restrict__ w, int64_t N,
-                                              double* __restrict__ partial)
+                                              double* __restrict__ partial,
+                                              const double* __restrict__ extra = nullptr)
 {
     __shared__ double sm[8];
     const int i = blockIdx.y;
-    if (i >= nvec) return;
-    const double* vi = V + (int64_t)i * ldv;
+    if (i > nvec || (i == nvec && !extra)) return;
+    const double* vi = i == nvec ? extra : V + (int64_t)i * ldv;
     double s = 0.0;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
          q += (int64_t)gridDim.x * blockDim.x)
@@ -137,6 +139,36 @@ __global__ void __launch_bounds__(256) k_mupdate(const double* __restrict__ V, i
         w[q] = acc;
     }
 }
+/* w -= sum_i h_i V_i and partial[blk] = block's sum of the new w^2 (grid = RED_BLOCKS) */
+__global__ void __launch_bounds__(256) k_mupdate_norm(const double* __restrict__ V, int64_t ldv,
+                                                      int nvec, const double* __restrict__ h,
+                                                      double* __restrict__ w, int64_t N,
+                                                      double* __restrict__ partial)
+{
+    __shared__ double hs[1024];
+    __shared__ double sm[8];
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) hs[i] = h[i];
+    __syncthreads();
+    double ss = 0.0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = w[q];
+        int i = 0;
+        for (; i + 4 <= nvec; i += 4) {
+            const double* v = V + (int64_t)i * ldv + q;
+            acc -= hs[i] * v[0];
+            acc -= hs[i + 1] * v[ldv];
+            acc -= hs[i + 2] * v[2 * ldv];
+            acc -= hs[i + 3] * v[3 * ldv];
+        }
+        for (; i < nvec; i++) acc -= hs[i] * V[(int64_t)i * ldv + q];
+        w[q] = acc;
+        ss += acc * acc;
+    }
+    const double t = block_sum(ss, sm);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
 /* x += sum_i y_i Z_i */
 __global__ void __launch_bounds__(256) k_mupdate_add(const double* __restrict__ Z, int64_t ldz, int nvec,
                                                      const double* __restrict__ y,
@@ -217,6 +249,30 @@ double dot(iemic_ctx* c, const double* a, const double* b, int64_t n)
     return r;
 }
 
+/* One Gram-Schmidt pass over the nvec basis vectors: h = V^T w, ww0 = w.w (before),
+ * w -= V h, ww1 = w.w (after).  The coefficients stay on the device between the two
+ * launches; one device-to-host copy + synchronisation returns h, ww0, ww1. */
+static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, double* w, double* h,
+                     double* ww0, double* ww1)
+{
+    const int64_t N = c->nrows;
+    hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec + 1), dim3(256), 0, c->stream, V, ldv, nvec,
+                       w, N, c->d_part.p, (const double*)w);
+    hipLaunchKernelGGL(k_mdot_final, dim3(nvec + 1), dim3(256), 0, c->stream, c->d_part.p,
+                       RED_BLOCKS, nvec + 1, c->d_hbuf.p);
+    hipLaunchKernelGGL(k_mupdate_norm, dim3(RED_BLOCKS), dim3(256), 0, c->stream, V, ldv, nvec,
+                       c->d_hbuf.p, w, N, c->d_part.p);
+    hipLaunchKernelGGL(k_mdot_final, dim3(1), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS, 1,
+                       c->d_hbuf.p + nvec + 1);
+    HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (nvec + 2), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < nvec; i++) h[i] = c->h_red[i];
+    *ww0 = c->h_red[nvec];
+    *ww1 = c->h_red[nvec + 1];
+    return 0;
+}
+
 static int ensure_krylov(iemic_ctx* c, int m)
 {
     if (c->kr.m >= m && c->kr.V.p) return 0;
@@ -264,6 +320,13 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     double* r = c->kr.r.p;
     const unsigned G = grid_for(N);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
+    int inf_reorth = 0;
+    struct Events {
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ~Events() { for (auto& x : e) if (x) (void)hipEventDestroy(x); }
+    } evs;
+    hipEvent_t* ev = evs.e;
+    for (int q = 0; q < 3; q++) HIP_OK(hipEventCreate(&ev[q]));
 
     HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * N, c->stream));
     double bnorm = std::sqrt(std::max(0.0, dot(c, b, b, N)));
@@ -286,40 +349,48 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             double* vj = V + (int64_t)j * N;
             double* zj = Z + (int64_t)j * N;
             double* vn = V + (int64_t)(j + 1) * N;
-            auto tp = std::chrono::steady_clock::now();
+            /* prec and SpMV are timed with events (no extra host synchronisation) */
+            HIP_OK(hipEventRecord(ev[0], c->stream));
             if (opt->prec > 0) {
                 rc = prec_apply(c, vj, zj);
                 if (rc) return rc;
             } else {
                 HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
             }
-            HIP_OK(hipStreamSynchronize(c->stream));
-            inf.t_prec_ms += ms_since(tp);
-            tp = std::chrono::steady_clock::now();
+            HIP_OK(hipEventRecord(ev[1], c->stream));
             rc = spmv(c, zj, vn, c->stream);
             if (rc) return rc;
-            HIP_OK(hipStreamSynchronize(c->stream));
-            inf.t_spmv_ms += ms_since(tp);
-            tp = std::chrono::steady_clock::now();
-            /* CGS2 */
-            rc = mdot_host(c, V, N, j + 1, vn, h.data());
-            if (rc) return rc;
-            if ((rc = upload_coeffs(c, h.data(), j + 1))) return rc;
-            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1,
-                               c->d_hbuf.p + (MAX_KRYLOV + 2), vn, N);
-            rc = mdot_host(c, V, N, j + 1, vn, h2.data());
-            if (rc) return rc;
-            if ((rc = upload_coeffs(c, h2.data(), j + 1))) return rc;
-            hipLaunchKernelGGL(k_mupdate, dim3(G), dim3(256), 0, c->stream, V, N, j + 1,
-                               c->d_hbuf.p + (MAX_KRYLOV + 2), vn, N);
-            for (int i = 0; i <= j; i++) h[i] += h2[i];
+            HIP_OK(hipEventRecord(ev[2], c->stream));
+            auto tp = std::chrono::steady_clock::now();
+            /* DGKS (Belos' default orthogonalisation): one classical Gram-Schmidt pass
+             * h = V^T w (with ||w||^2 in the same launch), w -= V h (with ||w||^2 fused),
+             * and a second pass only when the norm dropped below 1/sqrt(2) of its value
+             * (dep_tol, BelosDGKSOrthoManager).  One host synchronisation per pass. */
             double hn2 = 0.0;
-            rc = mdot_host(c, vn, 0, 1, vn, &hn2);
-            if (rc) return rc;
+            {
+                double ww0 = 0.0;
+                rc = orth_pass(c, V, N, j + 1, vn, h.data(), &ww0, &hn2);
+                if (rc) return rc;
+                if (hn2 < 0.5 * ww0) {
+                    double dummy = 0.0;
+                    rc = orth_pass(c, V, N, j + 1, vn, h2.data(), &dummy, &hn2);
+                    if (rc) return rc;
+                    for (int i = 0; i <= j; i++) h[i] += h2[i];
+                    inf_reorth++;
+                }
+            }
             double hn = std::sqrt(std::max(0.0, hn2));
             if (hn > 0)
                 hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn, 1.0 / hn, vn, N);
-            inf.t_orth_ms += ms_since(tp);
+            {
+                float a1 = 0.f, a2 = 0.f;
+                (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
+                (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
+                inf.t_prec_ms += a1;
+                inf.t_spmv_ms += a2;
+                /* host time of the orthogonalisation includes waiting for prec + SpMV */
+                inf.t_orth_ms += ms_since(tp) - a1 - a2;
+            }
             for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
             H[(size_t)(j + 1) * m + j] = hn;
             for (int i = 0; i < j; i++) {
@@ -370,6 +441,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, w, w, N);
     double e2 = dot(c, w, w, N);
     inf.iters = it;
+    inf.reorth = inf_reorth;
     inf.implicit_rel_res = res;
     inf.explicit_rel_res = std::sqrt(std::max(0.0, e2)) / bnorm;
     inf.converged = res <= opt->tol;

@@ -182,111 +182,232 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
     row[c2 - c + bl] += s;
 }
 
-/* Band LU with partial pivoting, one workgroup; row i holds columns [i-bl, i+bl+bu]. */
+/* Band LU with partial pivoting (LAPACK gbtrf semantics), one workgroup of 1024 threads,
+ * right-looking and blocked by panels of NBP columns: the panel is factorised in LDS
+ * (partial pivoting, full panel-row interchanges), row swaps and U12 = L11^-1 A12 follow,
+ * and the trailing window is updated once per panel (A22 -= L21 U12) instead of once per
+ * column.  U stays in the band (row i holds columns [i-bl, i+bl+bu] at offset
+ * j - i + bl); the panel multipliers go to lpan[panel][NBP + bl][NBP], so a solve applies,
+ * panel by panel, the panel's interchanges and then its multipliers. */
+constexpr int NBP = 16;
+
 __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int ncol, int bl, int bu,
-                                                  int* __restrict__ piv, int* __restrict__ info)
+                                                  int* __restrict__ piv, int* __restrict__ info,
+                                                  double* __restrict__ lpan)
 {
+    extern __shared__ double lds[];
     const int W = 2 * bl + bu + 1;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6, nwave = nthr >> 6;
+    double* P = lds;                              /* (NBP + bl) x NBP panel          */
+    double* U = lds + (NBP + bl) * NBP;           /* NBP x (bl + bu) block row U12   */
+    __shared__ int s_lp[NBP];
     __shared__ int s_p;
     __shared__ double s_best;
-    const int tid = threadIdx.x;
-    if (tid == 0) *info = 0;
-    for (int k = 0; k < ncol; k++) {
-        const int iend = min(k + bl, ncol - 1), jend = min(k + bl + bu, ncol - 1);
-        if (tid < 64) {
-            double best = -1.0;
-            int bi = k;
-            for (int i = k + tid; i <= iend; i += 64) {
-                const double v = fabs(ab[(int64_t)i * W + (k - i + bl)]);
-                if (v > best) { best = v; bi = i; }
-            }
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ob = __shfl_down(best, off, 64);
-                const int oi = __shfl_down(bi, off, 64);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            if (tid == 0) { s_p = bi; s_best = best; }
+    __shared__ int s_info;
+    if (tid == 0) s_info = 0;
+    auto A = [&](int i, int j) -> double& { return ab[(int64_t)i * W + (j - i + bl)]; };
+    for (int k0 = 0; k0 < ncol; k0 += NBP) {
+        const int nbk = min(NBP, ncol - k0);
+        const int pend = min(k0 + nbk - 1 + bl, ncol - 1);
+        const int nprow = pend - k0 + 1;
+        /* load the panel */
+        for (int e = tid; e < nprow * NBP; e += nthr) {
+            const int r = e / NBP, t = e % NBP;
+            P[e] = (t < nbk && r <= t + bl) ? A(k0 + r, k0 + t) : 0.0;
         }
         __syncthreads();
-        const int p = s_p;
-        if (s_best == 0.0) {
-            if (tid == 0) { piv[k] = k; if (*info == 0) *info = k + 1; }
+        /* factorise the panel */
+        for (int t = 0; t < nbk; t++) {
+            const int rlast = min(t + bl, nprow - 1);
+            if (wave == 0) {
+                double best = -1.0;
+                int bi = t;
+                for (int r = t + lane; r <= rlast; r += 64) {
+                    const double v = fabs(P[r * NBP + t]);
+                    if (v > best) { best = v; bi = r; }
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const double ob = __shfl_down(best, off, 64);
+                    const int oi = __shfl_down(bi, off, 64);
+                    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+                }
+                if (lane == 0) { s_p = bi; s_best = best; }
+            }
             __syncthreads();
-            continue;
-        }
-        if (p != k)
-            for (int j = k + tid; j <= jend; j += blockDim.x) {
-                double* a = ab + (int64_t)k * W + (j - k + bl);
-                double* b = ab + (int64_t)p * W + (j - p + bl);
-                const double t = *a; *a = *b; *b = t;
+            const int rp = s_p;
+            if (s_best == 0.0) {
+                if (tid == 0) {
+                    s_lp[t] = t;
+                    piv[k0 + t] = k0 + t;
+                    if (s_info == 0) s_info = k0 + t + 1;
+                }
+                __syncthreads();
+                continue;
             }
-        if (tid == 0) piv[k] = p;
+            if (rp != t && tid < nbk) {
+                const double x = P[t * NBP + tid];
+                P[t * NBP + tid] = P[rp * NBP + tid];
+                P[rp * NBP + tid] = x;
+            }
+            if (tid == 0) { s_lp[t] = rp; piv[k0 + t] = k0 + rp; }
+            __syncthreads();
+            const double pivot = P[t * NBP + t];
+            for (int r = t + 1 + tid; r <= rlast; r += nthr) P[r * NBP + t] /= pivot;
+            __syncthreads();
+            const int ncl = nbk - t - 1;
+            for (int e = tid; e < (rlast - t) * ncl; e += nthr) {
+                const int r = t + 1 + e / ncl, cc = t + 1 + e % ncl;
+                P[r * NBP + cc] -= P[r * NBP + t] * P[t * NBP + cc];
+            }
+            __syncthreads();
+        }
+        /* U11 back to the band; the multipliers (L11, L21 with the panel's row
+         * interchanges applied, LAPACK getrf convention) go to the panel store */
+        double* Lp = lpan + (int64_t)(k0 / NBP) * (NBP + bl) * NBP;
+        for (int e = tid; e < (NBP + bl) * NBP; e += nthr) {
+            const int r = e / NBP, t = e % NBP;
+            const bool in = r < nprow && t < nbk;
+            if (in && r <= t) A(k0 + r, k0 + t) = P[e];
+            Lp[e] = (in && r > t) ? P[e] : 0.0;
+        }
+        /* row swaps of the trailing columns, in pivot order, one thread per column */
+        const int jlo = k0 + nbk, jhi = min(k0 + nbk - 1 + bl + bu, ncol - 1);
+        for (int j = jlo + tid; j <= jhi; j += nthr)
+            for (int t = 0; t < nbk; t++) {
+                const int rp = s_lp[t];
+                if (rp == t || j > k0 + t + bl + bu) continue;
+                double& x = A(k0 + t, j);
+                double& y = A(k0 + rp, j);
+                const double tmp = x; x = y; y = tmp;
+            }
         __syncthreads();
-        const double pivot = ab[(int64_t)k * W + bl];
-        const int nr = iend - k, nc = jend - k;
-        for (int r = tid; r < nr; r += blockDim.x) ab[(int64_t)(k + 1 + r) * W + (bl - 1 - r)] /= pivot;
+        /* U12 = L11^-1 A12, one thread per column */
+        const int ncu = jhi - jlo + 1;
+        for (int jj = tid; jj < ncu; jj += nthr) {
+            const int j = jlo + jj;
+            double u[NBP];
+            for (int t = 0; t < nbk; t++) {
+                double v = (j <= k0 + t + bl + bu) ? A(k0 + t, j) : 0.0;
+                for (int q = 0; q < t; q++) v -= P[t * NBP + q] * u[q];
+                u[t] = v;
+                U[t * (bl + bu) + jj] = v;
+                if (j <= k0 + t + bl + bu) A(k0 + t, j) = v;
+            }
+        }
         __syncthreads();
-        for (int t = tid; t < nr * nc; t += blockDim.x) {
-            const int r = t / nc, cc = t % nc;
-            const int i = k + 1 + r, j = k + 1 + cc;
-            const double lik = ab[(int64_t)i * W + (k - i + bl)];
-            if (lik != 0.0) ab[(int64_t)i * W + (j - i + bl)] -= lik * ab[(int64_t)k * W + (j - k + bl)];
+        /* A22 -= L21 U12 over rows k0+nbk .. pend */
+        for (int r = nbk + wave; r < nprow; r += nwave) {
+            const int i = k0 + r;
+            double l[NBP];
+            bool any = false;
+            for (int t = 0; t < nbk; t++) { l[t] = P[r * NBP + t]; any |= l[t] != 0.0; }
+            if (!any) continue;
+            for (int jj = lane; jj < ncu; jj += 64) {
+                double acc = 0.0;
+                for (int t = 0; t < nbk; t++) acc += l[t] * U[t * (bl + bu) + jj];
+                A(i, jlo + jj) -= acc;
+            }
         }
         __syncthreads();
     }
+    if (tid == 0) *info = s_info;
 }
 
-/* Column c of the inverse: X[:, c] = U^-1 L^-1 P e_c (X row-major, ncol x ncol).  The
- * lanes of a wavefront walk the same rows, so X accesses are coalesced. */
-__global__ void __launch_bounds__(64) k_band_inv(const double* __restrict__ ab,
-                                                 const int* __restrict__ piv, int ncol, int bl,
-                                                 int bu, double* __restrict__ X)
+/* Columns [c0, c0+NB) of the inverse, X = U^-1 L^-1 P, one workgroup of 256 threads per
+ * block of NB right-hand sides (unit vectors).  Thread t owns column t % NB and every
+ * 256/NB-th row of the active window; the window lives in LDS as a ring buffer:
+ *   forward  (P, L^-1): rows k..k+bl      y is written to X (row-major, ncol x ncol)
+ *   backward (U^-1)   : rows i+1..i+bl+bu x overwrites y in X
+ * Two barriers per elimination step; the factors are read from L2. */
+template <int NB>
+__global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__ ab,
+                                                      const double* __restrict__ lpan,
+                                                      const int* __restrict__ piv, int ncol,
+                                                      int bl, int bu, double* __restrict__ X)
 {
-    const int c0 = blockIdx.x * 64;
-    const int c = c0 + threadIdx.x;
-    const bool on = c < ncol;
+    extern __shared__ double lds[];
+    constexpr int G = 256 / NB;              /* row groups */
     const int W = 2 * bl + bu + 1;
-    const int cc = on ? c : ncol - 1;
-#define XV(i) X[(int64_t)(i) * ncol + cc]
-    if (on)
-        for (int i = 0; i < ncol; i++) XV(i) = (i == c) ? 1.0 : 0.0;
-    const int k0 = max(0, c0 - bl);
-    for (int k = k0; k < ncol; k++) {
-        const int p = piv[k];
-        double bk = on ? XV(k) : 0.0;
-        if (p != k && on) {
-            const double bp = XV(p);
-            XV(p) = bk;
-            XV(k) = bp;
-            bk = bp;
+    const int col = threadIdx.x % NB, grp = threadIdx.x / NB;
+    const int c0 = blockIdx.x * NB;
+    const int c = c0 + col;
+    const bool on = c < ncol;
+    double* red = lds;                       /* G x NB partial sums */
+    double* win = lds + G * NB;              /* ring buffer         */
+    /* ---- forward, panel by panel: ring of R1 = bl + NBP + 1 rows ---- */
+    const int R1 = bl + NBP + 1;
+    const int kst = (max(0, c0 - bl - NBP + 1) / NBP) * NBP;
+    for (int r = kst + grp; r <= min(kst + NBP - 1 + bl, ncol - 1); r += G)
+        win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
+    for (int k0 = kst; k0 < ncol; k0 += NBP) {
+        const int nbk = min(NBP, ncol - k0);
+        const int pend = min(k0 + nbk - 1 + bl, ncol - 1);
+        const int nprow = pend - k0 + 1;
+        const double* Lp = lpan + (int64_t)(k0 / NBP) * (NBP + bl) * NBP;
+        __syncthreads();
+        if (grp == 0)
+            for (int t = 0; t < nbk; t++) {
+                const int rp = piv[k0 + t] - k0;
+                if (rp != t) {
+                    double* a = win + ((k0 + t) % R1) * NB + col;
+                    double* b = win + ((k0 + rp) % R1) * NB + col;
+                    const double x = *a; *a = *b; *b = x;
+                }
+            }
+        __syncthreads();
+        for (int t = 0; t < nbk; t++) {
+            const double bk = win[((k0 + t) % R1) * NB + col];
+            if (bk != 0.0)
+                for (int r = t + 1 + grp; r < nprow; r += G)
+                    win[((k0 + r) % R1) * NB + col] -= Lp[r * NBP + t] * bk;
+            __syncthreads();
         }
-        if (on && bk != 0.0) {
-            const int iend = min(k + bl, ncol - 1);
-            for (int i = k + 1; i <= iend; i++) XV(i) -= ab[(int64_t)i * W + (k - i + bl)] * bk;
-        }
+        /* rows k0 .. k0+nbk-1 are final: y -> X; bring in the rows of the next panel */
+        for (int t = grp; t < nbk; t += G)
+            if (on) X[(int64_t)(k0 + t) * ncol + c] = win[((k0 + t) % R1) * NB + col];
+        __syncthreads();
+        for (int r = pend + 1 + grp; r <= min(k0 + 2 * NBP - 1 + bl, ncol - 1); r += G)
+            win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
     }
+    /* rows above the first panel are zero in y */
+    if (grp == 0 && on)
+        for (int r = 0; r < kst; r++) X[(int64_t)r * ncol + c] = 0.0;
+    /* ---- backward: ring of R2 = bl + bu + 1 rows holding x(i+1 .. i+bl+bu) ---- */
+    const int R2 = bl + bu + 1;
+    __syncthreads();
     for (int i = ncol - 1; i >= 0; i--) {
-        if (!on) continue;
-        double s = XV(i);
         const int jend = min(i + bl + bu, ncol - 1);
         const double* ar = ab + (int64_t)i * W + (bl - i);
-        for (int j = i + 1; j <= jend; j++) s -= ar[j] * XV(j);
-        XV(i) = s / ar[i];
+        double s = 0.0;
+        for (int j = i + 1 + grp; j <= jend; j += G) s += ar[j] * win[(j % R2) * NB + col];
+        red[grp * NB + col] = s;
+        __syncthreads();
+        if (grp == 0) {
+            double t = 0.0;
+            for (int g2 = 0; g2 < G; g2++) t += red[g2 * NB + col];
+            const double y = on ? X[(int64_t)i * ncol + c] : 0.0;
+            const double x = (y - t) / ar[i];
+            win[(i % R2) * NB + col] = x;
+            if (on) X[(int64_t)i * ncol + c] = x;
+        }
+        __syncthreads();
     }
-#undef XV
 }
 
 /* ---- apply ------------------------------------------------------------------------ */
 
 /* z = r on identity rows; rr = r - A(:, known) r(known) on the others */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                        const double* __restrict__ r, double* __restrict__ z,
-                        double* __restrict__ rr, int n, int m, int l, int periodic)
+                        const uint8_t* __restrict__ nearknown, const double* __restrict__ r,
+                        double* __restrict__ z, double* __restrict__ rr, int n, int m, int l,
+                        int periodic)
 {
     const int64_t ncell = (int64_t)n * m * l;
     const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= ncell) return;
     const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    const bool nk = nearknown[cell];
     for (int R = 0; R < NUN; R++) {
         const int64_t row = NUN * cell + R;
         if (known[row]) {
@@ -295,6 +416,10 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
             continue;
         }
         double acc = r[row];
+        if (!nk) {                      /* no identity-row neighbour: nothing to subtract */
+            rr[row] = acc;
+            continue;
+        }
         for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
             const double v = val[(int64_t)s * ncell + cell];
             if (v == 0.0) continue;
@@ -308,15 +433,69 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     }
 }
 
+/* cells whose active rows couple to an identity row (coast, sea floor, rigid lid) */
+__global__ void k_nearknown(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                            uint8_t* __restrict__ nearknown, int n, int m, int l, int periodic)
+{
+    const int64_t ncell = (int64_t)n * m * l;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    bool nk = false;
+    for (int s = 0; s < NSLOT && !nk; s++) {
+        int R = 0;
+        while (s >= ROW_BEGIN[R + 1]) R++;
+        if (known[NUN * cell + R] || val[(int64_t)s * ncell + cell] == 0.0) continue;
+        int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
+        const int kk = k + SLOTS[s].dk;
+        if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
+        nk = known[NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var] != 0;
+    }
+    nearknown[cell] = nk ? 1 : 0;
+}
+
+/* T/S off-diagonal couplings of active rows to active T/S columns, compacted:
+ * per row (T, S) 6 same-variable neighbours (-i,+i,-j,+j,-k,+k) + the other variable at
+ * k-1, k+1; zero where the column is an identity row, outside, or the row is inactive. */
+constexpr int TS_NC = 16;
+__global__ void k_ts_compact(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                             double* __restrict__ tsoff, int n, int m, int l, int periodic,
+                             int64_t rowintcon)
+{
+    const int64_t ncell = (int64_t)n * m * l;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    for (int R = TT; R <= SS; R++) {
+        const int base = ROW_BEGIN[R];
+        const int other = R == TT ? SS : TT;
+        const bool act = !known[NUN * cell + R] && NUN * cell + R != rowintcon;
+        /* slots base+1..base+6: same var (-i,+i,-j,+j,-k,+k); base+18, base+19: other var k-1, k+1 */
+        const int sl[8] = {base + 1, base + 2, base + 3, base + 4, base + 5, base + 6, base + 18, base + 19};
+        for (int q = 0; q < 8; q++) {
+            double v = 0.0;
+            if (act) {
+                const int s = sl[q];
+                int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
+                const int kk = k + SLOTS[s].dk;
+                if (kk >= 0 && kk < l && hnb(ii, jj, n, m, periodic) &&
+                    !known[NUN * cidx(ii, jj, kk, n, m) + (q < 6 ? R : other)])
+                    v = val[(int64_t)s * ncell + cell];
+            }
+            tsoff[(int64_t)((R - TT) * 8 + q) * ncell + cell] = v;
+        }
+    }
+}
+
 /* 1. hydrostatic rows top-down: ptil (stored in z at the P rows) */
 __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                          const int* __restrict__ ij_of_col, int ncol, const double* __restrict__ rr,
+                          const int* __restrict__ col_of_ij, const double* __restrict__ rr,
                           double* __restrict__ z, int n, int m, int l)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncol) return;
+    /* one thread per water column, (i,j) in memory order so that lanes read adjacent cells */
+    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ij >= n * m || col_of_ij[ij] < 0) return;
     const int64_t ncell = (int64_t)n * m * l;
-    const int ij = ij_of_col[c];
     const int i = ij % n, j = ij / n;
     double pabove = 0.0;
     for (int k = l - 1; k >= 0; k--) {
@@ -397,15 +576,16 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
 
 /* 3a. Schur right-hand side per column: sum_k w_k (Duv uv* - rr_p)_k */
 __global__ void k_gs_schur_rhs(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                               const double* __restrict__ pw, const int* __restrict__ ij_of_col,
-                               const uint8_t* __restrict__ pinned, int ncol,
+                               const double* __restrict__ pw, const int* __restrict__ col_of_ij,
+                               const uint8_t* __restrict__ pinned,
                                const double* __restrict__ rr, const double* __restrict__ z,
                                double* __restrict__ rhs, int n, int m, int l, int periodic)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncol) return;
+    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ij >= n * m) return;
+    const int c = col_of_ij[ij];
+    if (c < 0) return;
     const int64_t ncell = (int64_t)n * m * l;
-    const int ij = ij_of_col[c];
     const int i = ij % n, j = ij / n;
     double s = 0.0;
     for (int k = 0; k < l; k++) {
@@ -424,8 +604,16 @@ __global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int 
     const int lane = threadIdx.x & 63;
     if (row >= nr) return;
     const double* xr = X + (int64_t)row * nr;
-    double s = 0.0;
-    for (int c = lane; c < nr; c += 64) s += xr[c] * b[c];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int c = lane;
+    for (; c + 192 < nr; c += 256) {
+        s0 += xr[c] * b[c];
+        s1 += xr[c + 64] * b[c + 64];
+        s2 += xr[c + 128] * b[c + 128];
+        s3 += xr[c + 192] * b[c + 192];
+    }
+    for (; c < nr; c += 64) s0 += xr[c] * b[c];
+    double s = (s0 + s1) + (s2 + s3);
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     if (lane == 0) y[row] = s;
 }
@@ -453,14 +641,15 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
 
 /* 4b/5. p = ptil + pbar; continuity rows bottom-up for w (top P row excluded) */
 __global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                        const int* __restrict__ ij_of_col, int ncol, const double* __restrict__ pbar,
+                        const int* __restrict__ col_of_ij, const double* __restrict__ pbar,
                         const double* __restrict__ rr, double* __restrict__ z, int n, int m, int l,
                         int periodic)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncol) return;
+    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ij >= n * m) return;
+    const int c = col_of_ij[ij];
+    if (c < 0) return;
     const int64_t ncell = (int64_t)n * m * l;
-    const int ij = ij_of_col[c];
     const int i = ij % n, j = ij / n;
     const double pb = pbar[c];
     double wbelow = 0.0;
@@ -511,36 +700,48 @@ __global__ void k_gs_bts(const double* __restrict__ val, const uint8_t* __restri
     }
 }
 
-/* 6b. one red-black half sweep on the T/S block with 2x2 cell blocks */
-__global__ void k_gs_ts_half(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                             const double* __restrict__ tsinv, const double* __restrict__ bts,
-                             double* __restrict__ z, int n, int m, int l, int periodic, int color)
+/* colour of a cell for the T/S sweeps: parity of i+j+k; on a periodic grid with odd n
+ * the wrap pairs (n-1, 0) would share a colour, so column i = n-1 gets colours 2/3 */
+__device__ __forceinline__ int ts_color(int i, int j, int k, int n, int periodic)
+{
+    if (periodic && (n & 1) && i == n - 1) return 2 + ((j + k) & 1);
+    return (i + j + k) & 1;
+}
+
+/* 6b. one red-black half sweep on the T/S block with 2x2 cell blocks (compact couplings) */
+__global__ void __launch_bounds__(256) k_gs_ts_half(const double* __restrict__ tsoff,
+                                                    const uint8_t* __restrict__ known,
+                                                    const double* __restrict__ tsinv,
+                                                    const double* __restrict__ bts,
+                                                    double* __restrict__ z, int n, int m, int l,
+                                                    int periodic, int color)
 {
     const int64_t ncell = (int64_t)n * m * l;
     const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= ncell) return;
     const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
-    if (((i + j + k) & 1) != color) return;
+    if (ts_color(i, j, k, n, periodic) != color) return;
     const bool ta = !known[NUN * cell + TT], sa = !known[NUN * cell + SS];
     if (!ta && !sa) return;
-    double res[2] = {0.0, 0.0};
-    for (int R = TT; R <= SS; R++) {
-        const int64_t row = NUN * cell + R;
-        if (known[row]) continue;
-        double acc = bts[row];
-        for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
-            const int var = SLOTS[s].var;
-            if (var != TT && var != SS) continue;
-            if (SLOTS[s].di == 0 && SLOTS[s].dj == 0 && SLOTS[s].dk == 0) continue;
-            const double v = val[(int64_t)s * ncell + cell];
-            if (v == 0.0) continue;
-            int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
-            const int kk = k + SLOTS[s].dk;
-            if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-            const int64_t col = NUN * cidx(ii, jj, kk, n, m) + var;
-            if (!known[col]) acc -= v * z[col];
-        }
-        res[R - TT] = acc;
+    /* neighbour cells (clamped where the coupling is zero anyway) */
+    int im = i - 1, ip = i + 1;
+    if (periodic) { if (im < 0) im = n - 1; if (ip >= n) ip = 0; }
+    else { if (im < 0) im = i; if (ip >= n) ip = i; }
+    const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
+    const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
+    const int64_t nb[6] = {cidx(im, j, k, n, m), cidx(ip, j, k, n, m), cidx(i, jm, k, n, m),
+                           cidx(i, jp, k, n, m), cidx(i, j, km, n, m), cidx(i, j, kp, n, m)};
+    double res[2];
+#pragma unroll
+    for (int R = 0; R < 2; R++) {
+        const int var = TT + R, oth = SS - R;
+        const double* a = tsoff + (int64_t)(R * 8) * ncell + cell;
+        double acc = bts[NUN * cell + var];
+#pragma unroll
+        for (int q = 0; q < 6; q++) acc -= a[(int64_t)q * ncell] * z[NUN * nb[q] + var];
+        acc -= a[(int64_t)6 * ncell] * z[NUN * nb[4] + oth];
+        acc -= a[(int64_t)7 * ncell] * z[NUN * nb[5] + oth];
+        res[R] = acc;
     }
     const double* D = tsinv + 4 * cell;
     if (ta) z[NUN * cell + TT] = D[0] * res[0] + D[1] * res[1];
@@ -664,6 +865,7 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
     rc |= gs.pinned.alloc(ncol);
     rc |= gs.band.alloc((size_t)ncol * W);
     rc |= gs.piv.alloc(ncol);
+    rc |= gs.lpan.alloc((size_t)((ncol + NBP - 1) / NBP) * (NBP + gs.bl) * NBP);
     rc |= gs.info.alloc(1);
     rc |= gs.sinv.alloc((size_t)ncol * ncol);
     rc |= gs.colv.alloc(ncol);
@@ -695,6 +897,8 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         rc |= gs.pw.alloc(ncell);
         rc |= gs.rr.alloc(N);
         rc |= gs.bts.alloc(N);
+        rc |= gs.nearknown.alloc(ncell);
+        rc |= gs.tsoff.alloc((size_t)TS_NC * ncell);
         if (rc) {
             set_error("block GS: out of device memory");
             return IEMIC_ENOMEM;
@@ -712,6 +916,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        ncell, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
                        gs.tsinv.p, gs.pw.p, c->n, c->m);
+    hipLaunchKernelGGL(k_nearknown, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
+                       gs.nearknown.p, c->n, c->m, c->l, c->cfg.periodic);
+    hipLaunchKernelGGL(k_ts_compact, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
+                       gs.tsoff.p, c->n, c->m, c->l, c->cfg.periodic, (int64_t)c->rowintcon);
     const int W = 2 * gs.bl + gs.bu + 1;
     HIP_OK(hipMemsetAsync(gs.band.p, 0, sizeof(double) * (size_t)gs.ncol * W, c->stream));
     const int64_t nt = (int64_t)gs.ncol * 9;
@@ -719,8 +927,17 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                        c->d_val.p, gs.known.p, gs.uvinv.p, gs.pw.p, gs.col_of_ij.p, gs.ij_of_col.p,
                        gs.pinned.p, gs.ncol, gs.bl, gs.bu, c->n, c->m, c->l, c->cfg.periodic,
                        gs.band.p);
-    hipLaunchKernelGGL(k_band_lu, dim3(1), dim3(1024), 0, c->stream, gs.band.p, gs.ncol, gs.bl, gs.bu,
-                       gs.piv.p, gs.info.p);
+    {
+        const size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * NBP + (size_t)NBP * (gs.bl + gs.bu));
+        if (lb > 150 * 1024) {
+            set_error("block GS: Schur band too wide for the LDS band LU");
+            return IEMIC_EINVAL;
+        }
+        HIP_OK(hipFuncSetAttribute((const void*)k_band_lu, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lb));
+        hipLaunchKernelGGL(k_band_lu, dim3(1), dim3(1024), lb, c->stream, gs.band.p, gs.ncol, gs.bl,
+                           gs.bu, gs.piv.p, gs.info.p, gs.lpan.p);
+    }
     int info = 0;
     HIP_OK(hipGetLastError());
     if ((rc = d2h(c, &info, gs.info.p, sizeof(int)))) return rc;
@@ -728,8 +945,34 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         set_error("block GS: singular Schur complement (pivot " + std::to_string(info - 1) + ")");
         return IEMIC_EINVAL;
     }
-    hipLaunchKernelGGL(k_band_inv, dim3((unsigned)((gs.ncol + 63) / 64)), dim3(64), 0, c->stream,
-                       gs.band.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.sinv.p);
+    {
+        /* pick the widest RHS block whose ring buffers fit in LDS */
+        const int rows = std::max(gs.bl + NBP + 1, gs.bl + gs.bu + 1);
+        auto bytes = [&](int nb) { return (size_t)(rows + 256 / nb) * nb * sizeof(double); };
+        const size_t lmax = 150 * 1024;
+        if (bytes(32) <= lmax) {
+            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<32>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(32)));
+            hipLaunchKernelGGL(k_band_inv_blk<32>, dim3((unsigned)((gs.ncol + 31) / 32)), dim3(256),
+                               bytes(32), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
+                               gs.sinv.p);
+        } else if (bytes(16) <= lmax) {
+            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(16)));
+            hipLaunchKernelGGL(k_band_inv_blk<16>, dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256),
+                               bytes(16), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
+                               gs.sinv.p);
+        } else if (bytes(8) <= lmax) {
+            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(8)));
+            hipLaunchKernelGGL(k_band_inv_blk<8>, dim3((unsigned)((gs.ncol + 7) / 8)), dim3(256),
+                               bytes(8), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
+                               gs.sinv.p);
+        } else {
+            set_error("block GS: Schur band too wide for the LDS inverse");
+            return IEMIC_EINVAL;
+        }
+    }
     HIP_OK(hipGetLastError());
     gs.ready = 1;
     return 0;
@@ -741,31 +984,34 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     const int n = c->n, m = c->m, l = c->l, per = c->cfg.periodic;
     const int64_t ncell = c->ncell;
     const unsigned gc = (unsigned)((ncell + 255) / 256);
-    const unsigned gcol = (unsigned)((gs.ncol + 63) / 64);
+    const unsigned gij = (unsigned)((n * m + 255) / 256);
     hipStream_t s = c->stream;
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nrows, s));
-    hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, r, z, gs.rr.p,
-                       n, m, l, per);
-    hipLaunchKernelGGL(k_gs_ptil, dim3(gcol), dim3(64), 0, s, c->d_val.p, gs.known.p, gs.ij_of_col.p,
-                       gs.ncol, gs.rr.p, z, n, m, l);
+    hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.nearknown.p,
+                       r, z, gs.rr.p, n, m, l, per);
+    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       gs.rr.p, z, n, m, l);
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.rr.p, z, n, m, l, per);
-    hipLaunchKernelGGL(k_gs_schur_rhs, dim3(gcol), dim3(64), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.ij_of_col.p, gs.pinned.p, gs.ncol, gs.rr.p, z, gs.colv.p, n, m, l, per);
+    hipLaunchKernelGGL(k_gs_schur_rhs, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       gs.col_of_ij.p, gs.pinned.p, gs.rr.p, z, gs.colv.p, n, m, l, per);
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
                        gs.ncol, gs.colv.p, gs.colv2.p);
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.col_of_ij.p, gs.colv2.p, z, n, m, l, per);
-    hipLaunchKernelGGL(k_gs_pw, dim3(gcol), dim3(64), 0, s, c->d_val.p, gs.known.p, gs.ij_of_col.p,
-                       gs.ncol, gs.colv2.p, gs.rr.p, z, n, m, l, per);
+    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       gs.colv2.p, gs.rr.p, z, n, m, l, per);
     hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
                        gs.bts.p, n, m, l, per);
-    for (int sw = 0; sw < std::max(1, gs.ts_sweeps); sw++) {
-        const int seq[4] = {0, 1, 1, 0};
-        for (int h = 0; h < 4; h++)
-            hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+    /* symmetric sweeps: colours forward then backward */
+    const bool four = per && (n & 1);
+    const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
+    const int* seq = four ? seq4 : seq2;
+    const int ns = four ? 8 : 4;
+    for (int sw = 0; sw < std::max(1, gs.ts_sweeps); sw++)
+        for (int h = 0; h < ns; h++)
+            hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
                                gs.tsinv.p, gs.bts.p, z, n, m, l, per, seq[h]);
-    }
     HIP_OK(hipGetLastError());
     return 0;
 }

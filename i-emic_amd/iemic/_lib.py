@@ -38,7 +38,7 @@ class SolveInfo(C.Structure):
     _fields_ = [("iters", C.c_int), ("converged", C.c_int),
                 ("implicit_rel_res", C.c_double), ("explicit_rel_res", C.c_double),
                 ("t_prec_ms", C.c_double), ("t_spmv_ms", C.c_double),
-                ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double)]
+                ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double), ("reorth", C.c_int)]
 
 
 class NewtonInfo(C.Structure):

@@ -66,7 +66,7 @@ typedef struct {
     double tol;                  /* "FGMRES tolerance" (relative to ||b||, x0 = 0)   */
     int krylov_dim;              /* "FGMRES iterations" = restart length             */
     int max_restarts;            /* "FGMRES restarts"                                */
-    int prec;                    /* 0: none, 1: block Gauss-Seidel (default)         */
+    int prec;                    /* 0: none, 1: cell block-Jacobi, 2: block Gauss-Seidel */
     int ts_sweeps;               /* symmetric red-black sweeps on the T/S block      */
 } iemic_krylov;
 
@@ -76,6 +76,7 @@ typedef struct {
     double implicit_rel_res;     /* Givens estimate / ||b||                          */
     double explicit_rel_res;     /* ||b - J x|| / ||b||  (Ocean.C:1140-1150)         */
     double t_prec_ms, t_spmv_ms, t_orth_ms, t_total_ms;
+    int reorth;                  /* DGKS second passes taken                         */
 } iemic_solve_info;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

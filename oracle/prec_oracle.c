@@ -447,15 +447,20 @@ void orc_gs_apply(void* h, const double* r, double* z)
         g->bts[row] = acc;
         z[row] = 0.0;
     }
-    const int seq[4] = {0, 1, 1, 0};
+    /* colours: parity of i+j+k; odd periodic n: column n-1 gets colours 2/3 */
+    const int four = g->periodic && (n & 1);
+    const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
+    const int* seq = four ? seq4 : seq2;
+    const int ns = four ? 8 : 4;
     int nsw = g->ts_sweeps > 1 ? g->ts_sweeps : 1;
     for (int sw = 0; sw < nsw; sw++)
-        for (int hh = 0; hh < 4; hh++) {
+        for (int hh = 0; hh < ns; hh++) {
             const int color = seq[hh];
 #pragma omp parallel for schedule(static)
             for (int64_t c = 0; c < nc; c++) {
                 int i = (int)(c % n), j = (int)((c / n) % m), k = (int)(c / ((int64_t)n * m));
-                if (((i + j + k) & 1) != color) continue;
+                int cc = (four && i == n - 1) ? 2 + ((j + k) & 1) : ((i + j + k) & 1);
+                if (cc != color) continue;
                 int ta = !kn[NUN * c + TT], sa = !kn[NUN * c + SS];
                 if (!ta && !sa) continue;
                 double res[2] = {0.0, 0.0};
