@@ -51,9 +51,10 @@ def parse():
     p.add_argument("--amp-ts", type=float, default=1e-3,
                    help="T/S amplitude of the synthetic state (DESIGN.md: benchmark state)")
     p.add_argument("--tol", type=float, default=1e-8)
-    p.add_argument("--krylov", type=int, default=500)
-    p.add_argument("--restarts", type=int, default=0)
-    p.add_argument("--ts-sweeps", type=int, default=3)
+    p.add_argument("--krylov", type=int, default=1000)
+    p.add_argument("--restarts", type=int, default=2)
+    p.add_argument("--ts-sweeps", type=int, default=12)
+    p.add_argument("--orth", default="DCGS2", choices=["DCGS2", "DGKS"])
     p.add_argument("--spmv-reps", type=int, default=100)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=48)
@@ -155,7 +156,7 @@ def main():
     cfg = cf.preset(args.config, mixing=0)
     sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
           "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
-          "TS sweeps": args.ts_sweeps}
+          "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth}
     oc = Ocean(cfg, device=local, solver_params=sp)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     x0h = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
@@ -207,7 +208,8 @@ def main():
         "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing=0, one Newton "
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
-                   "krylov_dim": args.krylov, "restarts": args.restarts,
+                   "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
+                   "ts_sweeps": args.ts_sweeps,
                    "parallelism": "replicas" if world > 1 else "single"},
         "newton": {"iters": s.iters, "converged": s.converged,
                    "explicit_rel_res": s.explicit_rel_res, "norm_f0": last.norm_f0,

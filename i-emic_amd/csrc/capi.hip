@@ -152,9 +152,9 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
     rc |= c->d_tmp1.alloc(c->nrows);
     rc |= c->d_tmp2.alloc(c->nrows);
     rc |= c->d_red.alloc(2048);
-    rc |= c->d_part.alloc((size_t)RED_BLOCKS * (MAX_KRYLOV + 2));
-    rc |= c->d_hbuf.alloc((size_t)2 * (MAX_KRYLOV + 2));
-    if (!rc && hipHostMalloc(&c->h_red, sizeof(double) * 2 * (MAX_KRYLOV + 2)) != hipSuccess) rc = 1;
+    rc |= c->d_part.alloc((size_t)RED_BLOCKS * RED_ROWS);
+    rc |= c->d_hbuf.alloc((size_t)2 * RED_ROWS);
+    if (!rc && hipHostMalloc(&c->h_red, sizeof(double) * 2 * RED_ROWS) != hipSuccess) rc = 1;
     if (rc) {
         set_error("iemic_create: out of device memory");
         delete c;

@@ -83,8 +83,9 @@ struct Krylov {
     DevBuf<double> w, r;
 };
 
-constexpr int RED_BLOCKS = 512;      /* partial-sum blocks of the reductions            */
+constexpr int RED_BLOCKS = 1024;     /* partial-sum blocks of the reductions            */
 constexpr int MAX_KRYLOV = 1000;     /* largest Krylov dimension                        */
+constexpr int RED_ROWS = 2 * MAX_KRYLOV + 4; /* reduction rows (DCGS2: 2 per basis vector + 3) */
 
 }  // namespace iemic
 

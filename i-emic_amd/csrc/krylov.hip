@@ -169,6 +169,81 @@ __global__ void __launch_bounds__(256) k_mupdate_norm(const double* __restrict__
     if (threadIdx.x == 0) partial[blockIdx.x] = t;
 }
 
+/* DCGS2 dot pass: for i < nvec, out rows 2i, 2i+1 = Q_i.u, Q_i.w; rows 2nvec..2nvec+2 =
+ * u.u, u.w, w.w.  partial[row * RED_BLOCKS + blk]; grid (RED_BLOCKS, nvec + 1). */
+__global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, int64_t ldv, int nvec,
+                                                  const double* __restrict__ u,
+                                                  const double* __restrict__ w, int64_t N,
+                                                  double* __restrict__ partial)
+{
+    __shared__ double sm[8];
+    const int i = blockIdx.y;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (i < nvec) {
+        const double* q = V + (int64_t)i * ldv;
+        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += stride) {
+            const double qe = q[e];
+            s0 += qe * u[e];
+            s1 += qe * w[e];
+        }
+        double t = block_sum(s0, sm);
+        if (threadIdx.x == 0) partial[(int64_t)(2 * i) * gridDim.x + blockIdx.x] = t;
+        __syncthreads();
+        t = block_sum(s1, sm);
+        if (threadIdx.x == 0) partial[(int64_t)(2 * i + 1) * gridDim.x + blockIdx.x] = t;
+    } else {
+        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += stride) {
+            const double ue = u[e], we = w[e];
+            s0 += ue * ue;
+            s1 += ue * we;
+            s2 += we * we;
+        }
+        const int64_t r0 = 2 * (int64_t)nvec;
+        double t = block_sum(s0, sm);
+        if (threadIdx.x == 0) partial[r0 * gridDim.x + blockIdx.x] = t;
+        __syncthreads();
+        t = block_sum(s1, sm);
+        if (threadIdx.x == 0) partial[(r0 + 1) * gridDim.x + blockIdx.x] = t;
+        __syncthreads();
+        t = block_sum(s2, sm);
+        if (threadIdx.x == 0) partial[(r0 + 2) * gridDim.x + blockIdx.x] = t;
+    }
+}
+
+/* DCGS2 update pass, one read of Q:  q_j = (u - Q a) * inv_beta,  w -= Q c + gamma * u
+ * (coef = [a (nvec) | c (nvec)]); u is overwritten by q_j. */
+__global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ V, int64_t ldv,
+                                                     int nvec, const double* __restrict__ coef,
+                                                     double inv_beta, double gamma,
+                                                     double* __restrict__ u, double* __restrict__ w,
+                                                     int64_t N)
+{
+    __shared__ double cs[2 * 1024];
+    for (int i = threadIdx.x; i < 2 * nvec; i += blockDim.x) cs[i] = coef[i];
+    __syncthreads();
+    const double* a = cs;
+    const double* cc = cs + nvec;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        double su = 0.0, sw = 0.0;
+        int i = 0;
+        for (; i + 2 <= nvec; i += 2) {
+            const double q0 = V[(int64_t)i * ldv + e], q1 = V[(int64_t)(i + 1) * ldv + e];
+            su += a[i] * q0 + a[i + 1] * q1;
+            sw += cc[i] * q0 + cc[i + 1] * q1;
+        }
+        for (; i < nvec; i++) {
+            const double q0 = V[(int64_t)i * ldv + e];
+            su += a[i] * q0;
+            sw += cc[i] * q0;
+        }
+        const double ue = u[e];
+        u[e] = (ue - su) * inv_beta;
+        w[e] = w[e] - sw - gamma * ue;
+    }
+}
+
 /* x += sum_i y_i Z_i */
 __global__ void __launch_bounds__(256) k_mupdate_add(const double* __restrict__ Z, int64_t ldz, int nvec,
                                                      const double* __restrict__ y,
@@ -294,9 +369,13 @@ static int ensure_krylov(iemic_ctx* c, int m)
  * has completed: every caller synchronised the stream since) */
 static int upload_coeffs(iemic_ctx* c, const double* h, int n)
 {
-    double* st = c->h_red + (MAX_KRYLOV + 2);
+    if (n > RED_ROWS) {
+        set_error("upload_coeffs: too many coefficients");
+        return IEMIC_EINVAL;
+    }
+    double* st = c->h_red + RED_ROWS;
     for (int i = 0; i < n; i++) st[i] = h[i];
-    HIP_OK(hipMemcpyAsync(c->d_hbuf.p + (MAX_KRYLOV + 2), st, sizeof(double) * n,
+    HIP_OK(hipMemcpyAsync(c->d_hbuf.p + RED_ROWS, st, sizeof(double) * n,
                           hipMemcpyHostToDevice, c->stream));
     return 0;
 }
@@ -320,6 +399,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     double* r = c->kr.r.p;
     const unsigned G = grid_for(N);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
+    if (2 * m + 3 > RED_ROWS) {
+        set_error("fgmres: Krylov dimension too large");
+        return IEMIC_EINVAL;
+    }
     int inf_reorth = 0;
     struct Events {
         hipEvent_t e[3] = {nullptr, nullptr, nullptr};
@@ -345,74 +428,178 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         g[0] = beta;
         int j = 0;
         bool conv = false;
-        for (; j < m; j++) {
-            double* vj = V + (int64_t)j * N;
-            double* zj = Z + (int64_t)j * N;
-            double* vn = V + (int64_t)(j + 1) * N;
-            /* prec and SpMV are timed with events (no extra host synchronisation) */
-            HIP_OK(hipEventRecord(ev[0], c->stream));
-            if (opt->prec > 0) {
-                rc = prec_apply(c, vj, zj);
-                if (rc) return rc;
-            } else {
-                HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
-            }
-            HIP_OK(hipEventRecord(ev[1], c->stream));
-            rc = spmv(c, zj, vn, c->stream);
-            if (rc) return rc;
-            HIP_OK(hipEventRecord(ev[2], c->stream));
-            auto tp = std::chrono::steady_clock::now();
-            /* DGKS (Belos' default orthogonalisation): one classical Gram-Schmidt pass
-             * h = V^T w (with ||w||^2 in the same launch), w -= V h (with ||w||^2 fused),
-             * and a second pass only when the norm dropped below 1/sqrt(2) of its value
-             * (dep_tol, BelosDGKSOrthoManager).  One host synchronisation per pass. */
-            double hn2 = 0.0;
-            {
-                double ww0 = 0.0;
-                rc = orth_pass(c, V, N, j + 1, vn, h.data(), &ww0, &hn2);
-                if (rc) return rc;
-                if (hn2 < 0.5 * ww0) {
-                    double dummy = 0.0;
-                    rc = orth_pass(c, V, N, j + 1, vn, h2.data(), &dummy, &hn2);
+        if (opt->orth == 1) {
+            for (; j < m; j++) {
+                double* vj = V + (int64_t)j * N;
+                double* zj = Z + (int64_t)j * N;
+                double* vn = V + (int64_t)(j + 1) * N;
+                /* prec and SpMV are timed with events (no extra host synchronisation) */
+                HIP_OK(hipEventRecord(ev[0], c->stream));
+                if (opt->prec > 0) {
+                    rc = prec_apply(c, vj, zj);
                     if (rc) return rc;
-                    for (int i = 0; i <= j; i++) h[i] += h2[i];
-                    inf_reorth++;
+                } else {
+                    HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+                }
+                HIP_OK(hipEventRecord(ev[1], c->stream));
+                rc = spmv(c, zj, vn, c->stream);
+                if (rc) return rc;
+                HIP_OK(hipEventRecord(ev[2], c->stream));
+                auto tp = std::chrono::steady_clock::now();
+                /* DGKS (Belos' default orthogonalisation): one classical Gram-Schmidt pass
+                 * h = V^T w (with ||w||^2 in the same launch), w -= V h (with ||w||^2 fused),
+                 * and a second pass only when the norm dropped below 1/sqrt(2) of its value
+                 * (dep_tol, BelosDGKSOrthoManager).  One host synchronisation per pass. */
+                double hn2 = 0.0;
+                {
+                    double ww0 = 0.0;
+                    rc = orth_pass(c, V, N, j + 1, vn, h.data(), &ww0, &hn2);
+                    if (rc) return rc;
+                    if (hn2 < 0.5 * ww0) {
+                        double dummy = 0.0;
+                        rc = orth_pass(c, V, N, j + 1, vn, h2.data(), &dummy, &hn2);
+                        if (rc) return rc;
+                        for (int i = 0; i <= j; i++) h[i] += h2[i];
+                        inf_reorth++;
+                    }
+                }
+                double hn = std::sqrt(std::max(0.0, hn2));
+                if (hn > 0)
+                    hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn, 1.0 / hn, vn, N);
+                {
+                    float a1 = 0.f, a2 = 0.f;
+                    (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
+                    (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
+                    inf.t_prec_ms += a1;
+                    inf.t_spmv_ms += a2;
+                    /* host time of the orthogonalisation includes waiting for prec + SpMV */
+                    inf.t_orth_ms += ms_since(tp) - a1 - a2;
+                }
+                for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
+                H[(size_t)(j + 1) * m + j] = hn;
+                for (int i = 0; i < j; i++) {
+                    double a = H[(size_t)i * m + j], bb = H[(size_t)(i + 1) * m + j];
+                    H[(size_t)i * m + j] = cs[i] * a + sn[i] * bb;
+                    H[(size_t)(i + 1) * m + j] = -sn[i] * a + cs[i] * bb;
+                }
+                double a = H[(size_t)j * m + j], bb = H[(size_t)(j + 1) * m + j];
+                double d = std::sqrt(a * a + bb * bb);
+                cs[j] = d > 0 ? a / d : 1.0;
+                sn[j] = d > 0 ? bb / d : 0.0;
+                H[(size_t)j * m + j] = d;
+                H[(size_t)(j + 1) * m + j] = 0.0;
+                g[j + 1] = -sn[j] * g[j];
+                g[j] = cs[j] * g[j];
+                res = std::fabs(g[j + 1]) / bnorm;
+                it++;
+                if (res <= opt->tol || hn == 0.0) {
+                    j++;
+                    conv = true;
+                    break;
                 }
             }
-            double hn = std::sqrt(std::max(0.0, hn2));
-            if (hn > 0)
-                hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn, 1.0 / hn, vn, N);
-            {
+
+        } else {
+            /* DCGS2 (delayed classical Gram-Schmidt with reorthogonalisation): the new
+             * vector u_j is orthogonalised once when produced and re-orthogonalised one step
+             * later in the same pass over the basis that orthogonalises the next candidate;
+             * normalisation is folded in.  One read pass (k_dcgs_dot) + one update pass
+             * (k_dcgs_update) over the basis and one host synchronisation per iteration;
+             * the Hessenberg column j-1 is final (and the residual known) at iteration j. */
+            std::vector<double> htent(m + 1), col(m + 1), coef(2 * (size_t)m + 2);
+            int ncolf = 0;                 /* finalised columns */
+            for (int jj = 0; jj <= m; jj++) {
+                double* u = V + (int64_t)jj * N;
+                double* wv = jj < m ? V + (int64_t)(jj + 1) * N : nullptr;
                 float a1 = 0.f, a2 = 0.f;
-                (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
-                (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
-                inf.t_prec_ms += a1;
-                inf.t_spmv_ms += a2;
-                /* host time of the orthogonalisation includes waiting for prec + SpMV */
+                if (jj < m) {
+                    double* zj = Z + (int64_t)jj * N;
+                    HIP_OK(hipEventRecord(ev[0], c->stream));
+                    if (opt->prec > 0) {
+                        rc = prec_apply(c, u, zj);
+                        if (rc) return rc;
+                    } else {
+                        HIP_OK(hipMemcpyAsync(zj, u, sizeof(double) * N, hipMemcpyDeviceToDevice,
+                                              c->stream));
+                    }
+                    HIP_OK(hipEventRecord(ev[1], c->stream));
+                    rc = spmv(c, zj, wv, c->stream);
+                    if (rc) return rc;
+                    HIP_OK(hipEventRecord(ev[2], c->stream));
+                }
+                auto tp = std::chrono::steady_clock::now();
+                /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1) */
+                const int nv = jj;
+                const double* wd = wv ? wv : u;
+                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, nv + 1), dim3(256), 0, c->stream, V, N,
+                                   nv, u, wd, N, c->d_part.p);
+                hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
+                                   RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
+                HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (2 * nv + 3),
+                                      hipMemcpyDeviceToHost, c->stream));
+                HIP_OK(hipStreamSynchronize(c->stream));
+                if (jj < m) {
+                    (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
+                    (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
+                    inf.t_prec_ms += a1;
+                    inf.t_spmv_ms += a2;
+                }
+                const double* hr = c->h_red;
+                double aa = 0.0, ab = 0.0;
+                for (int i = 0; i < nv; i++) {
+                    aa += hr[2 * i] * hr[2 * i];
+                    ab += hr[2 * i] * hr[2 * i + 1];
+                }
+                const double uu = hr[2 * nv], uw = hr[2 * nv + 1];
+                const double beta2 = uu - aa;
+                const double bt = beta2 > 0.0 ? std::sqrt(beta2) : 0.0;
+                if (jj >= 1) {
+                    /* finalise column jj-1: tentative + reorthogonalisation coefficients */
+                    const int q = jj - 1;
+                    for (int i = 0; i < jj; i++) col[i] = htent[i] + hr[2 * i];
+                    col[jj] = bt;
+                    for (int i = 0; i <= jj; i++) H[(size_t)i * m + q] = col[i];
+                    for (int i = 0; i < q; i++) {
+                        const double x0 = H[(size_t)i * m + q], x1 = H[(size_t)(i + 1) * m + q];
+                        H[(size_t)i * m + q] = cs[i] * x0 + sn[i] * x1;
+                        H[(size_t)(i + 1) * m + q] = -sn[i] * x0 + cs[i] * x1;
+                    }
+                    const double x0 = H[(size_t)q * m + q], x1 = H[(size_t)(q + 1) * m + q];
+                    const double d = std::sqrt(x0 * x0 + x1 * x1);
+                    cs[q] = d > 0 ? x0 / d : 1.0;
+                    sn[q] = d > 0 ? x1 / d : 0.0;
+                    H[(size_t)q * m + q] = d;
+                    H[(size_t)(q + 1) * m + q] = 0.0;
+                    g[q + 1] = -sn[q] * g[q];
+                    g[q] = cs[q] * g[q];
+                    res = std::fabs(g[q + 1]) / bnorm;
+                    ncolf = jj;
+                    it++;
+                    if (res <= opt->tol || !(bt > 0.0)) {
+                        conv = true;
+                        inf.t_orth_ms += ms_since(tp) - a1 - a2;
+                        break;
+                    }
+                }
+                if (jj == m || !(bt > 0.0)) {
+                    inf.t_orth_ms += ms_since(tp) - a1 - a2;
+                    break;
+                }
+                /* update pass: q_jj = (u - Q a)/bt,  w -= Q c + gamma u */
+                const double hjj = (uw - ab) / bt;
+                const double gamma = hjj / bt;
+                for (int i = 0; i < nv; i++) {
+                    coef[i] = hr[2 * i];
+                    coef[nv + i] = hr[2 * i + 1] - hr[2 * i] * gamma;
+                    htent[i] = hr[2 * i + 1];
+                }
+                htent[nv] = hjj;
+                if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
+                hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V, N, nv,
+                                   c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u, wv, N);
                 inf.t_orth_ms += ms_since(tp) - a1 - a2;
             }
-            for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
-            H[(size_t)(j + 1) * m + j] = hn;
-            for (int i = 0; i < j; i++) {
-                double a = H[(size_t)i * m + j], bb = H[(size_t)(i + 1) * m + j];
-                H[(size_t)i * m + j] = cs[i] * a + sn[i] * bb;
-                H[(size_t)(i + 1) * m + j] = -sn[i] * a + cs[i] * bb;
-            }
-            double a = H[(size_t)j * m + j], bb = H[(size_t)(j + 1) * m + j];
-            double d = std::sqrt(a * a + bb * bb);
-            cs[j] = d > 0 ? a / d : 1.0;
-            sn[j] = d > 0 ? bb / d : 0.0;
-            H[(size_t)j * m + j] = d;
-            H[(size_t)(j + 1) * m + j] = 0.0;
-            g[j + 1] = -sn[j] * g[j];
-            g[j] = cs[j] * g[j];
-            res = std::fabs(g[j + 1]) / bnorm;
-            it++;
-            if (res <= opt->tol || hn == 0.0) {
-                j++;
-                conv = true;
-                break;
-            }
+            j = ncolf;
         }
         /* y = H \ g ; x += Z y */
         int k = j;
@@ -424,16 +611,18 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         if (k > 0) {
             if ((rc = upload_coeffs(c, y.data(), k))) return rc;
             hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z, N, k,
-                               c->d_hbuf.p + (MAX_KRYLOV + 2), x, N);
+                               c->d_hbuf.p + RED_ROWS, x, N);
         }
-        if (conv || cycle == opt->max_restarts) break;
-        /* r = b - J x */
+        if (cycle == opt->max_restarts) break;
+        /* r = b - J x; a cycle that converged on the implicit (Givens) estimate restarts
+         * only if the true residual has not reached the tolerance */
         rc = spmv(c, x, r, c->stream);
         if (rc) return rc;
         hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, r, r, N);
         beta = std::sqrt(std::max(0.0, dot(c, r, r, N)));
         res = beta / bnorm;
         if (res <= opt->tol) break;
+        (void)conv;
     }
     /* explicit residual (Ocean.C:1140-1150) */
     rc = spmv(c, x, w, c->stream);

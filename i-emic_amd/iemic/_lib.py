@@ -31,7 +31,7 @@ class Grid(C.Structure):
 
 class Krylov(C.Structure):
     _fields_ = [("tol", C.c_double), ("krylov_dim", C.c_int), ("max_restarts", C.c_int),
-                ("prec", C.c_int), ("ts_sweeps", C.c_int)]
+                ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int)]
 
 
 class SolveInfo(C.Structure):

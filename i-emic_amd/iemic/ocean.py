@@ -41,7 +41,7 @@ class Ocean:
         self.N = lib().iemic_nrows(h)
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
-              "Preconditioner": 2, "TS sweeps": 3}
+              "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2"}
         if solver_params:
             sp.update(solver_params)
         self.solver_params = sp
@@ -119,7 +119,7 @@ class Ocean:
         sp = self.solver_params
         return _lib.Krylov(float(sp["FGMRES tolerance"]), int(sp["FGMRES iterations"]),
                            int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
-                           int(sp["TS sweeps"]))
+                           int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0)
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""

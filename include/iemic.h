@@ -68,6 +68,7 @@ typedef struct {
     int max_restarts;            /* "FGMRES restarts"                                */
     int prec;                    /* 0: none, 1: cell block-Jacobi, 2: block Gauss-Seidel */
     int ts_sweeps;               /* symmetric red-black sweeps on the T/S block      */
+    int orth;                    /* 0: DCGS2 (default), 1: DGKS (Belos' default)     */
 } iemic_krylov;
 
 typedef struct {
