@@ -68,8 +68,10 @@ struct BlockGS {
     /* numeric factors */
     DevBuf<double> uvinv, tsinv;     /* 2x2 inverses per cell (U/V and T/S blocks)      */
     DevBuf<double> pw;               /* per P row: weight of the depth integral         */
-    DevBuf<uint8_t> nearknown;       /* per cell: some active row couples to a known row */
+    DevBuf<uint64_t> kmask;          /* per cell: slots coupling to identity columns     */
     DevBuf<double> tsoff;            /* compact T/S off-diagonal couplings, 16 x ncell  */
+    DevBuf<double> tsc, tic, bc;     /* the same per colour (even n), T/S rhs per colour */
+    DevBuf<double> zt, zs, tcell;    /* T/S iterates, per-cell work                      */
     DevBuf<double> band;             /* Schur band, row-wise, width 2*bl+bu+1           */
     DevBuf<int> piv, info;
     DevBuf<double> lpan;             /* band-LU panel multipliers                       */

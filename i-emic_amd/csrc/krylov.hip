@@ -169,45 +169,81 @@ __global__ void __launch_bounds__(256) k_mupdate_norm(const double* __restrict__
     if (threadIdx.x == 0) partial[blockIdx.x] = t;
 }
 
-/* DCGS2 dot pass: for i < nvec, out rows 2i, 2i+1 = Q_i.u, Q_i.w; rows 2nvec..2nvec+2 =
- * u.u, u.w, w.w.  partial[row * RED_BLOCKS + blk]; grid (RED_BLOCKS, nvec + 1). */
+/* sum NV values over the block; result valid in thread 0 (sm: NV*(blockDim/64) doubles) */
+template <int NV>
+__device__ __forceinline__ void block_sum_n(double* v, double* sm)
+{
+#pragma unroll
+    for (int q = 0; q < NV; q++)
+        for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_down(v[q], o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NV; q++) sm[q * nw + wid] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            double t = 0.0;
+            for (int w = 0; w < nw; w++) t += sm[q * nw + w];
+            v[q] = t;
+        }
+}
+
+/* DCGS2 dot pass: rows 2i, 2i+1 = Q_i.u, Q_i.w (i < nvec); rows 2nvec..2nvec+2 = u.u, u.w,
+ * w.w.  Block y < ceil(nvec/4) handles four basis vectors so that u and w are read once
+ * per four; the last y handles the three self products.  partial[row*gridDim.x + blk]. */
 __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, int64_t ldv, int nvec,
                                                   const double* __restrict__ u,
                                                   const double* __restrict__ w, int64_t N,
                                                   double* __restrict__ partial)
 {
-    __shared__ double sm[8];
-    const int i = blockIdx.y;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    __shared__ double sm[8 * 4];
+    const int nq = (nvec + 3) / 4;
+    const int by = blockIdx.y;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    if (i < nvec) {
-        const double* q = V + (int64_t)i * ldv;
-        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += stride) {
-            const double qe = q[e];
-            s0 += qe * u[e];
-            s1 += qe * w[e];
+    const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (by < nq) {
+        const int i0 = 4 * by;
+        const int nv = min(4, nvec - i0);
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const double* q0 = V + (int64_t)i0 * ldv;
+        if (nv == 4) {
+            for (int64_t e = e0; e < N; e += stride) {
+                const double ue = u[e], we = w[e];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const double qe = q0[(int64_t)t * ldv + e];
+                    acc[2 * t] += qe * ue;
+                    acc[2 * t + 1] += qe * we;
+                }
+            }
+        } else {
+            for (int64_t e = e0; e < N; e += stride) {
+                const double ue = u[e], we = w[e];
+                for (int t = 0; t < nv; t++) {
+                    const double qe = q0[(int64_t)t * ldv + e];
+                    acc[2 * t] += qe * ue;
+                    acc[2 * t + 1] += qe * we;
+                }
+            }
         }
-        double t = block_sum(s0, sm);
-        if (threadIdx.x == 0) partial[(int64_t)(2 * i) * gridDim.x + blockIdx.x] = t;
-        __syncthreads();
-        t = block_sum(s1, sm);
-        if (threadIdx.x == 0) partial[(int64_t)(2 * i + 1) * gridDim.x + blockIdx.x] = t;
+        block_sum_n<8>(acc, sm);
+        if (threadIdx.x == 0)
+            for (int t = 0; t < 2 * nv; t++)
+                partial[(int64_t)(2 * i0 + t) * gridDim.x + blockIdx.x] = acc[t];
     } else {
-        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += stride) {
+        double acc[3] = {0, 0, 0};
+        for (int64_t e = e0; e < N; e += stride) {
             const double ue = u[e], we = w[e];
-            s0 += ue * ue;
-            s1 += ue * we;
-            s2 += we * we;
+            acc[0] += ue * ue;
+            acc[1] += ue * we;
+            acc[2] += we * we;
         }
-        const int64_t r0 = 2 * (int64_t)nvec;
-        double t = block_sum(s0, sm);
-        if (threadIdx.x == 0) partial[r0 * gridDim.x + blockIdx.x] = t;
-        __syncthreads();
-        t = block_sum(s1, sm);
-        if (threadIdx.x == 0) partial[(r0 + 1) * gridDim.x + blockIdx.x] = t;
-        __syncthreads();
-        t = block_sum(s2, sm);
-        if (threadIdx.x == 0) partial[(r0 + 2) * gridDim.x + blockIdx.x] = t;
+        block_sum_n<3>(acc, sm);
+        if (threadIdx.x == 0)
+            for (int t = 0; t < 3; t++)
+                partial[(int64_t)(2 * nvec + t) * gridDim.x + blockIdx.x] = acc[t];
     }
 }
 
@@ -531,8 +567,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1) */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
-                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, nv + 1), dim3(256), 0, c->stream, V, N,
-                                   nv, u, wd, N, c->d_part.p);
+                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, (nv + 3) / 4 + 1), dim3(256), 0,
+                                   c->stream, V, N, nv, u, wd, N, c->d_part.p);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
                 HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (2 * nv + 3),

@@ -397,61 +397,69 @@ __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__
 
 /* ---- apply ------------------------------------------------------------------------ */
 
-/* z = r on identity rows; rr = r - A(:, known) r(known) on the others */
+/* z = r on identity rows; rr = r - A(:, known) r(known) on the others (slot bitmask) */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                        const uint8_t* __restrict__ nearknown, const double* __restrict__ r,
+                        const uint64_t* __restrict__ kmask, const double* __restrict__ r,
                         double* __restrict__ z, double* __restrict__ rr, int n, int m, int l,
                         int periodic)
 {
     const int64_t ncell = (int64_t)n * m * l;
     const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
-    const bool nk = nearknown[cell];
+    double acc[NUN];
+#pragma unroll
     for (int R = 0; R < NUN; R++) {
         const int64_t row = NUN * cell + R;
-        if (known[row]) {
-            z[row] = r[row];
-            rr[row] = 0.0;
-            continue;
-        }
-        double acc = r[row];
-        if (!nk) {                      /* no identity-row neighbour: nothing to subtract */
-            rr[row] = acc;
-            continue;
-        }
-        for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
-            const double v = val[(int64_t)s * ncell + cell];
-            if (v == 0.0) continue;
-            int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
-            const int kk = k + SLOTS[s].dk;
-            if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-            const int64_t col = NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var;
-            if (known[col]) acc -= v * r[col];
-        }
-        rr[row] = acc;
+        acc[R] = r[row];
+        if (known[row]) z[row] = acc[R];
+    }
+    uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
+    if (b[0] | b[1]) {
+        const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+        for (int h = 0; h < 2; h++)
+            while (b[h]) {
+                const int s = 64 * h + __builtin_ctzll(b[h]);
+                b[h] &= b[h] - 1;
+                int R = 0;
+                while (s >= ROW_BEGIN[R + 1]) R++;
+                int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
+                const int kk = k + SLOTS[s].dk;
+                hnb(ii, jj, n, m, periodic);
+                const int64_t col = NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var;
+                acc[R] -= val[(int64_t)s * ncell + cell] * r[col];
+            }
+    }
+#pragma unroll
+    for (int R = 0; R < NUN; R++) {
+        const int64_t row = NUN * cell + R;
+        rr[row] = known[row] ? 0.0 : acc[R];
     }
 }
 
-/* cells whose active rows couple to an identity row (coast, sea floor, rigid lid) */
-__global__ void k_nearknown(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                            uint8_t* __restrict__ nearknown, int n, int m, int l, int periodic)
+/* per cell: bitmask of the slots (104 bits) through which an active row couples to an
+ * identity-row column (coast, sea floor, rigid lid); empty for most interior cells */
+__global__ void k_knownmask(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                            uint64_t* __restrict__ kmask, int n, int m, int l, int periodic)
 {
     const int64_t ncell = (int64_t)n * m * l;
     const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= ncell) return;
     const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
-    bool nk = false;
-    for (int s = 0; s < NSLOT && !nk; s++) {
-        int R = 0;
+    uint64_t b0 = 0, b1 = 0;
+    int R = 0;
+    for (int s = 0; s < NSLOT; s++) {
         while (s >= ROW_BEGIN[R + 1]) R++;
         if (known[NUN * cell + R] || val[(int64_t)s * ncell + cell] == 0.0) continue;
         int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
         const int kk = k + SLOTS[s].dk;
         if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-        nk = known[NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var] != 0;
+        if (known[NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var]) {
+            if (s < 64) b0 |= (uint64_t)1 << s;
+            else b1 |= (uint64_t)1 << (s - 64);
+        }
     }
-    nearknown[cell] = nk ? 1 : 0;
+    kmask[2 * cell] = b0;
+    kmask[2 * cell + 1] = b1;
 }
 
 /* T/S off-diagonal couplings of active rows to active T/S columns, compacted:
@@ -574,25 +582,31 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
     return acc;
 }
 
-/* 3a. Schur right-hand side per column: sum_k w_k (Duv uv* - rr_p)_k */
-__global__ void k_gs_schur_rhs(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                               const double* __restrict__ pw, const int* __restrict__ col_of_ij,
-                               const uint8_t* __restrict__ pinned,
-                               const double* __restrict__ rr, const double* __restrict__ z,
-                               double* __restrict__ rhs, int n, int m, int l, int periodic)
+/* 3a. Schur right-hand side: per P cell t = w_k (Duv uv - rr_p) (cell-parallel), then a
+ * fixed-order sum over k per column (k_col_sum).  With w_k = 1 and mode 1 the same kernel
+ * gives the continuity right-hand side rr_p - Duv uv used by the W sweep. */
+__global__ void k_gs_pcell(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                           const double* __restrict__ pw, const double* __restrict__ rr,
+                           const double* __restrict__ z, double* __restrict__ t, int n, int m,
+                           int l, int periodic, int mode)
+{
+    const int64_t ncell = (int64_t)n * m * l;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    if (known[NUN * cell + PP]) { t[cell] = 0.0; return; }
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    const double d = duv_uv(val, known, z, i, j, k, cell, n, m, periodic, ncell);
+    t[cell] = mode == 0 ? pw[cell] * (d - rr[NUN * cell + PP]) : rr[NUN * cell + PP] - d;
+}
+__global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ col_of_ij,
+                          const uint8_t* __restrict__ pinned, double* __restrict__ rhs, int nm, int l)
 {
     const int ij = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ij >= n * m) return;
+    if (ij >= nm) return;
     const int c = col_of_ij[ij];
     if (c < 0) return;
-    const int64_t ncell = (int64_t)n * m * l;
-    const int i = ij % n, j = ij / n;
     double s = 0.0;
-    for (int k = 0; k < l; k++) {
-        const int64_t pc = cidx(i, j, k, n, m);
-        if (known[NUN * pc + PP]) continue;
-        s += pw[pc] * (duv_uv(val, known, z, i, j, k, pc, n, m, periodic, ncell) - rr[NUN * pc + PP]);
-    }
+    for (int k = 0; k < l; k++) s += t[(int64_t)k * nm + ij];
     rhs[c] = pinned[c] ? 0.0 : s;
 }
 
@@ -642,8 +656,8 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
 /* 4b/5. p = ptil + pbar; continuity rows bottom-up for w (top P row excluded) */
 __global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const int* __restrict__ col_of_ij, const double* __restrict__ pbar,
-                        const double* __restrict__ rr, double* __restrict__ z, int n, int m, int l,
-                        int periodic)
+                        const double* __restrict__ crhs, double* __restrict__ z, int n, int m,
+                        int l)
 {
     const int ij = blockIdx.x * blockDim.x + threadIdx.x;
     if (ij >= n * m) return;
@@ -661,7 +675,7 @@ __global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restric
         if (pa && wa) {
             const double a = val[(int64_t)S_PW0 * ncell + cell];
             const double b = val[(int64_t)S_PWM * ncell + cell];
-            const double rhs = rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell, n, m, periodic, ncell);
+            const double rhs = crhs[cell];
             if (a != 0.0) w = (rhs - b * wbelow) / a;
             z[NUN * cell + WW] = w;
         } else if (wa) {
@@ -746,6 +760,101 @@ __global__ void __launch_bounds__(256) k_gs_ts_half(const double* __restrict__ t
     const double* D = tsinv + 4 * cell;
     if (ta) z[NUN * cell + TT] = D[0] * res[0] + D[1] * res[1];
     if (sa) z[NUN * cell + SS] = D[2] * res[0] + D[3] * res[1];
+}
+
+/* Even n: the cells of one colour are cell = 2q + ((j+k+c)&1), q = cell >> 1, so every
+ * per-cell T/S array can be stored per colour and read contiguously by a half sweep.
+ * tsc[(c*16 + e)*half + q] couplings, tic[(c*4 + e)*half + q] 2x2 inverses,
+ * bc[(c*2 + v)*half + q] right-hand sides; zt / zs: T and S iterates, natural order. */
+__global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __restrict__ tsinv,
+                          double* __restrict__ tsc, double* __restrict__ tic, int n, int m, int l)
+{
+    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    const int c = (i + j + k) & 1;
+    const int64_t q = cell >> 1;
+    for (int e = 0; e < TS_NC; e++) tsc[(int64_t)(c * TS_NC + e) * half + q] = tsoff[(int64_t)e * ncell + cell];
+    for (int e = 0; e < 4; e++) tic[(int64_t)(c * 4 + e) * half + q] = tsinv[4 * cell + e];
+}
+
+/* T/S right-hand side into the colour layout; zt = zs = 0 */
+__global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                           const double* __restrict__ rr, const double* __restrict__ z,
+                           double* __restrict__ bc, double* __restrict__ zt, double* __restrict__ zs,
+                           int n, int m, int l, int periodic)
+{
+    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    const int c = (i + j + k) & 1;
+    for (int R = TT; R <= SS; R++) {
+        const int64_t row = NUN * cell + R;
+        double acc = 0.0;
+        if (!known[row]) {
+            acc = rr[row];
+            for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
+                const int var = SLOTS[s].var;
+                if (var == TT || var == SS) continue;
+                const double v = val[(int64_t)s * ncell + cell];
+                if (v == 0.0) continue;
+                int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
+                const int kk = k + SLOTS[s].dk;
+                if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
+                const int64_t col = NUN * cidx(ii, jj, kk, n, m) + var;
+                if (!known[col]) acc -= v * z[col];
+            }
+        }
+        bc[(int64_t)(c * 2 + (R - TT)) * half + (cell >> 1)] = acc;
+    }
+    zt[cell] = 0.0;
+    zs[cell] = 0.0;
+}
+
+__global__ void __launch_bounds__(256) k_gs_ts_half_c(const double* __restrict__ tsc,
+                                                      const double* __restrict__ tic,
+                                                      const double* __restrict__ bc,
+                                                      double* __restrict__ zt, double* __restrict__ zs,
+                                                      int n, int m, int l, int periodic, int c)
+{
+    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= half) return;
+    const int64_t row = (2 * q) / n;
+    const int j = (int)(row % m), k = (int)(row / m);
+    const int64_t cell = 2 * q + ((j + k + c) & 1);
+    const int i = (int)(cell - row * n);
+    int im = i - 1, ip = i + 1;
+    if (periodic) { if (im < 0) im = n - 1; if (ip >= n) ip = 0; }
+    else { if (im < 0) im = i; if (ip >= n) ip = i; }
+    const int64_t nm = (int64_t)n * m;
+    const int64_t base = cell - i;
+    const int64_t nb[6] = {base + im, base + ip, j > 0 ? cell - n : cell, j < m - 1 ? cell + n : cell,
+                           k > 0 ? cell - nm : cell, k < l - 1 ? cell + nm : cell};
+    const double* a = tsc + (int64_t)(c * TS_NC) * half + q;
+    double rt = bc[(int64_t)(c * 2) * half + q], rs = bc[(int64_t)(c * 2 + 1) * half + q];
+#pragma unroll
+    for (int e = 0; e < 6; e++) {
+        rt -= a[(int64_t)e * half] * zt[nb[e]];
+        rs -= a[(int64_t)(8 + e) * half] * zs[nb[e]];
+    }
+    rt -= a[(int64_t)6 * half] * zs[nb[4]] + a[(int64_t)7 * half] * zs[nb[5]];
+    rs -= a[(int64_t)14 * half] * zt[nb[4]] + a[(int64_t)15 * half] * zt[nb[5]];
+    const double* D = tic + (int64_t)(c * 4) * half + q;
+    zt[cell] = D[0] * rt + D[half] * rs;
+    zs[cell] = D[2 * half] * rt + D[3 * half] * rs;
+}
+
+/* z(T,S) = zt, zs on the active rows */
+__global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __restrict__ zt,
+                             const double* __restrict__ zs, double* __restrict__ z, int64_t ncell)
+{
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= ncell) return;
+    if (!known[NUN * cell + TT]) z[NUN * cell + TT] = zt[cell];
+    if (!known[NUN * cell + SS]) z[NUN * cell + SS] = zs[cell];
 }
 
 /* ---- host: structure from the identity-row pattern ------------------------------ */
@@ -897,8 +1006,14 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         rc |= gs.pw.alloc(ncell);
         rc |= gs.rr.alloc(N);
         rc |= gs.bts.alloc(N);
-        rc |= gs.nearknown.alloc(ncell);
+        rc |= gs.kmask.alloc((size_t)2 * ncell);
         rc |= gs.tsoff.alloc((size_t)TS_NC * ncell);
+        rc |= gs.tsc.alloc((size_t)TS_NC * ncell);
+        rc |= gs.tic.alloc((size_t)4 * ncell);
+        rc |= gs.bc.alloc((size_t)2 * ncell);
+        rc |= gs.zt.alloc(ncell);
+        rc |= gs.zs.alloc(ncell);
+        rc |= gs.tcell.alloc(ncell);
         if (rc) {
             set_error("block GS: out of device memory");
             return IEMIC_ENOMEM;
@@ -916,10 +1031,13 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        ncell, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
                        gs.tsinv.p, gs.pw.p, c->n, c->m);
-    hipLaunchKernelGGL(k_nearknown, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
-                       gs.nearknown.p, c->n, c->m, c->l, c->cfg.periodic);
+    hipLaunchKernelGGL(k_knownmask, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
+                       gs.kmask.p, c->n, c->m, c->l, c->cfg.periodic);
     hipLaunchKernelGGL(k_ts_compact, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        gs.tsoff.p, c->n, c->m, c->l, c->cfg.periodic, (int64_t)c->rowintcon);
+    if ((c->n & 1) == 0)
+        hipLaunchKernelGGL(k_ts_pack, dim3(gc), dim3(256), 0, c->stream, gs.tsoff.p, gs.tsinv.p,
+                           gs.tsc.p, gs.tic.p, c->n, c->m, c->l);
     const int W = 2 * gs.bl + gs.bu + 1;
     HIP_OK(hipMemsetAsync(gs.band.p, 0, sizeof(double) * (size_t)gs.ncol * W, c->stream));
     const int64_t nt = (int64_t)gs.ncol * 9;
@@ -987,31 +1105,50 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     const unsigned gij = (unsigned)((n * m + 255) / 256);
     hipStream_t s = c->stream;
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nrows, s));
-    hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.nearknown.p,
+    hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, n, m, l, per);
     hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
                        gs.rr.p, z, n, m, l);
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.rr.p, z, n, m, l, per);
-    hipLaunchKernelGGL(k_gs_schur_rhs, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.col_of_ij.p, gs.pinned.p, gs.rr.p, z, gs.colv.p, n, m, l, per);
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       gs.rr.p, z, gs.tcell.p, n, m, l, per, 0);
+    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
+                       gs.pinned.p, gs.colv.p, n * m, l);
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
                        gs.ncol, gs.colv.p, gs.colv2.p);
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.col_of_ij.p, gs.colv2.p, z, n, m, l, per);
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       gs.rr.p, z, gs.tcell.p, n, m, l, per, 1);
     hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.colv2.p, gs.rr.p, z, n, m, l, per);
-    hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                       gs.bts.p, n, m, l, per);
-    /* symmetric sweeps: colours forward then backward */
-    const bool four = per && (n & 1);
-    const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
-    const int* seq = four ? seq4 : seq2;
-    const int ns = four ? 8 : 4;
-    for (int sw = 0; sw < std::max(1, gs.ts_sweeps); sw++)
-        for (int h = 0; h < ns; h++)
-            hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
-                               gs.tsinv.p, gs.bts.p, z, n, m, l, per, seq[h]);
+                       gs.colv2.p, gs.tcell.p, z, n, m, l);
+    const int nsw = std::max(1, gs.ts_sweeps);
+    if ((n & 1) == 0) {
+        /* colour-compacted symmetric red-black sweeps */
+        const unsigned gh = (unsigned)((ncell / 2 + 255) / 256);
+        hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                           gs.bc.p, gs.zt.p, gs.zs.p, n, m, l, per);
+        const int seq[4] = {0, 1, 1, 0};
+        for (int sw = 0; sw < nsw; sw++)
+            for (int h = 0; h < 4; h++)
+                hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
+                                   gs.zt.p, gs.zs.p, n, m, l, per, seq[h]);
+        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z,
+                           ncell);
+    } else {
+        hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                           gs.bts.p, n, m, l, per);
+        /* symmetric sweeps: colours forward then backward */
+        const bool four = per && (n & 1);
+        const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
+        const int* seq = four ? seq4 : seq2;
+        const int ns = four ? 8 : 4;
+        for (int sw = 0; sw < nsw; sw++)
+            for (int h = 0; h < ns; h++)
+                hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
+                                   gs.tsinv.p, gs.bts.p, z, n, m, l, per, seq[h]);
+    }
     HIP_OK(hipGetLastError());
     return 0;
 }

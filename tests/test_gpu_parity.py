@@ -95,7 +95,7 @@ def test_global2_full_size(oracle_lib, Ocean):
                                   "global4"])
 def test_block_gs_apply_matches_cpu(oracle_lib, Ocean, name):
     """GPU block Gauss-Seidel apply (dense Schur inverse) == CPU twin (band solve)."""
-    c, oc, o, L = make(Ocean, oracle_lib, name, solver_params={"Preconditioner": 2})
+    c, oc, o, L = make(Ocean, oracle_lib, name, solver_params={"Preconditioner": 2, "TS sweeps": 3})
     x = cf.synthetic_state(c, L, amp_ts=1e-3)
     oc.setState(x)
     oc.computeJacobian()
