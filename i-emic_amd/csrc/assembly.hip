@@ -14,54 +14,50 @@
 
 namespace iemic {
 
-__device__ __forceinline__ void cell_ijk(const Geo& g, int64_t c, int& i, int& j, int& k)
-{
-    i = (int)(c % g.n) + 1;
-    j = (int)((c / g.n) % g.m) + 1;
-    k = (int)(c / ((int64_t)g.n * g.m)) + 1;
-}
-
+/* Kernels run over the owned cells lc = 0 .. nloc-1 (ext cell own0 + lc); the Jacobian is
+ * stored slot-major over owned cells, val[s * nloc + lc]; vectors are in the ext layout. */
 template <int R>
 __device__ __forceinline__ void jac_row(const Geo& g, const double* __restrict__ x, int i, int j,
-                                        int k, int64_t cell, int64_t ncell, int64_t rowintcon,
+                                        int k, int64_t lc, int64_t nloc, int64_t rowintcon,
                                         double* __restrict__ val)
 {
     constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
     double A[NS];
     bool fz;
     assemble_row<R, true>(g, x, i, j, k, A, fz);
-    const bool dense_row = (NUN * cell + R) == rowintcon; /* replaced by intcond_S */
+    const bool dense_row = (NUN * (own0(g) + lc) + R) == rowintcon; /* replaced by intcond_S */
 #pragma unroll
-    for (int s = 0; s < NS; s++) val[(int64_t)(B + s) * ncell + cell] = dense_row ? 0.0 : A[s];
+    for (int s = 0; s < NS; s++) val[(int64_t)(B + s) * nloc + lc] = dense_row ? 0.0 : A[s];
 }
 
 __global__ void __launch_bounds__(128) k_jacobian(Geo g, const double* __restrict__ x,
-                                                  double* __restrict__ val, int64_t ncell,
+                                                  double* __restrict__ val, int64_t nloc,
                                                   int64_t rowintcon)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
     int i, j, k;
-    cell_ijk(g, cell, i, j, k);
+    owned_cell(g, lc, i, j, k);
     switch (blockIdx.y) {
-    case UU: jac_row<UU>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
-    case VV: jac_row<VV>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
-    case WW: jac_row<WW>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
-    case PP: jac_row<PP>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
-    case TT: jac_row<TT>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
-    default: jac_row<SS>(g, x, i, j, k, cell, ncell, rowintcon, val); break;
+    case UU: jac_row<UU>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
+    case VV: jac_row<VV>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
+    case WW: jac_row<WW>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
+    case PP: jac_row<PP>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
+    case TT: jac_row<TT>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
+    default: jac_row<SS>(g, x, i, j, k, lc, nloc, rowintcon, val); break;
     }
 }
 
 /* fillcolB times Mass (THCM.C:1150-1153), B = 0 at rowintcon */
-__global__ void k_diagB(Geo g, double* __restrict__ B, int64_t ncell, int64_t rowintcon)
+__global__ void k_diagB(Geo g, double* __restrict__ B, int64_t nloc, int64_t rowintcon)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
     int i, j, k;
-    cell_ijk(g, cell, i, j, k);
+    owned_cell(g, lc, i, j, k);
     double b[NUN];
     diagB_cell(g, i, j, k, b);
+    const int64_t cell = own0(g) + lc;
     for (int v = 0; v < NUN; v++) {
         const int64_t row = NUN * cell + v;
         B[row] = (row == rowintcon) ? 0.0 : b[v];
@@ -70,12 +66,13 @@ __global__ void k_diagB(Geo g, double* __restrict__ B, int64_t ncell, int64_t ro
 
 __global__ void __launch_bounds__(128) k_rhs(Geo g, const double* __restrict__ x,
                                              const double* __restrict__ frc,
-                                             double* __restrict__ F, int64_t ncell)
+                                             double* __restrict__ F, int64_t nloc)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
     int i, j, k;
-    cell_ijk(g, cell, i, j, k);
+    owned_cell(g, lc, i, j, k);
+    const int64_t cell = own0(g) + lc;
     double f;
     switch (blockIdx.y) {
     case UU: f = rhs_row_value<UU>(g, x, frc, i, j, k, cell); break;
@@ -105,15 +102,20 @@ __global__ void k_dot_partial(const double* __restrict__ a, const double* __rest
     }
     if (threadIdx.x == 0) part[blockIdx.x] = sm[0];
 }
-/* F[rowintcon] = intSign*(coeff . x - intCorrection)  (THCM.C:1005-1018) */
-__global__ void k_intcond_finish(const double* __restrict__ part, int nb, double* __restrict__ F,
-                                 int64_t row, int sign)
+/* out = sum of the block partials (fixed order) */
+__global__ void k_sum_partials(const double* __restrict__ part, int nb, double* __restrict__ out)
 {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         double s = 0.0;
         for (int q = 0; q < nb; q++) s += part[q];
-        F[row] = sign * (s - 0.0);
+        *out = s;
     }
+}
+/* F[rowintcon] = intSign*(coeff . x - intCorrection)  (THCM.C:1005-1018) */
+__global__ void k_intcond_set(const double* __restrict__ dotv, double* __restrict__ F, int64_t row,
+                              int sign)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) F[row] = sign * (*dotv - 0.0);
 }
 
 __global__ void k_qint(Geo g, const double* __restrict__ ftab, double* __restrict__ qcor,
@@ -124,12 +126,13 @@ __global__ void k_qint(Geo g, const double* __restrict__ ftab, double* __restric
 }
 
 __global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* __restrict__ qcor,
-                          double* __restrict__ frc, int64_t ncell)
+                          double* __restrict__ frc, int64_t nloc)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
     int i, j, k;
-    cell_ijk(g, cell, i, j, k);
+    owned_cell(g, lc, i, j, k);
+    const int64_t cell = own0(g) + lc;
     double f[NUN];
     forcing_cell(g, ftab, qcor, i, j, k, f);
     for (int v = 0; v < NUN; v++) frc[NUN * cell + v] = f[v];
@@ -139,11 +142,11 @@ __global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* 
 int assemble_jacobian(iemic_ctx* c, const double* x_dev)
 {
     Geo g = c->geo();
-    dim3 blk(128), grd((unsigned)((c->ncell + 127) / 128), NUN);
-    hipLaunchKernelGGL(k_jacobian, grd, blk, 0, c->stream, g, x_dev, c->d_val.p, c->ncell,
+    dim3 blk(128), grd((unsigned)((c->nloc + 127) / 128), NUN);
+    hipLaunchKernelGGL(k_jacobian, grd, blk, 0, c->stream, g, x_dev, c->d_val.p, c->nloc,
                        (int64_t)c->rowintcon);
-    hipLaunchKernelGGL(k_diagB, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0, c->stream,
-                       g, c->d_B.p, c->ncell, (int64_t)c->rowintcon);
+    hipLaunchKernelGGL(k_diagB, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, c->stream,
+                       g, c->d_B.p, c->nloc, (int64_t)c->rowintcon);
     HIP_OK(hipGetLastError());
     c->jac_valid = 1;
     return 0;
@@ -152,14 +155,22 @@ int assemble_jacobian(iemic_ctx* c, const double* x_dev)
 int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev)
 {
     Geo g = c->geo();
-    dim3 blk(128), grd((unsigned)((c->ncell + 127) / 128), NUN);
-    hipLaunchKernelGGL(k_rhs, grd, blk, 0, c->stream, g, x_dev, c->d_frc.p, F_dev, c->ncell);
-    if (c->rowintcon >= 0) {
+    dim3 blk(128), grd((unsigned)((c->nloc + 127) / 128), NUN);
+    hipLaunchKernelGGL(k_rhs, grd, blk, 0, c->stream, g, x_dev, c->d_frc.p, F_dev, c->nloc);
+    if (c->su.rowintcon_ref >= 0) {
+        /* the integral condition couples every S unknown: owned partial dot, a sum over the
+         * ranks, and the owning rank writes the entry */
         const int nb = 256;
-        hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(256), 0, c->stream, c->d_intc.p, x_dev,
-                           c->nrows, c->d_red.p);
-        hipLaunchKernelGGL(k_intcond_finish, dim3(1), dim3(64), 0, c->stream, c->d_red.p, nb, F_dev,
-                           (int64_t)c->rowintcon, c->cfg.int_sign);
+        const int64_t o = NUN * c->own0;
+        hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(256), 0, c->stream, c->d_intc.p + o,
+                           x_dev + o, c->nlrows, c->d_red.p);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, c->stream, c->d_red.p, nb,
+                           c->d_red.p + nb);
+        int rc = allreduce_sum(c, c->d_red.p + nb, 1);
+        if (rc) return rc;
+        if (c->rowintcon >= 0)
+            hipLaunchKernelGGL(k_intcond_set, dim3(1), dim3(64), 0, c->stream, c->d_red.p + nb, F_dev,
+                               (int64_t)c->rowintcon, c->cfg.int_sign);
     }
     HIP_OK(hipGetLastError());
     return 0;
@@ -170,8 +181,8 @@ int compute_forcing(iemic_ctx* c)
     Geo g = c->geo();
     hipLaunchKernelGGL(k_qint, dim3(1), dim3(64), 0, c->stream, g, c->d_ftab.p, c->d_qcor.p,
                        c->cfg.tres == 0 ? 1 : 0, c->cfg.sres == 0 ? 1 : 0);
-    hipLaunchKernelGGL(k_forcing, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0,
-                       c->stream, g, c->d_ftab.p, c->d_qcor.p, c->d_frc.p, c->ncell);
+    hipLaunchKernelGGL(k_forcing, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0,
+                       c->stream, g, c->d_ftab.p, c->d_qcor.p, c->d_frc.p, c->nloc);
     HIP_OK(hipGetLastError());
     return 0;
 }

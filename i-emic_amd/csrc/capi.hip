@@ -66,35 +66,50 @@ int upload_landm(iemic_ctx* c)
 }
 
 /* Ocean::analyzeJacobian1 (Ocean.C:273-340) + THCM::getLandMask(fix) (THCM.C:1298-1330):
- * P rows with at most 2 entries |v| > 1e-10 (and not a land identity row) become land. */
+ * P rows with at most 2 entries |v| > 1e-10 (and not a land identity row) become land.
+ * Each rank inspects its band; the fixes are summed over the ranks so every rank applies
+ * the same mask. */
 int mask_fix(iemic_ctx* c)
 {
     const int n = c->n, m = c->m;
-    HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nrows, c->stream));
+    HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, c->stream));
     const int pb = ROW_BEGIN[PP], pn = ROW_BEGIN[PP + 1] - ROW_BEGIN[PP];
-    std::vector<double> pv((size_t)pn * c->ncell);
+    std::vector<double> pv((size_t)pn * c->nloc);
+    DevBuf<double> dflag;
+    if (c->nranks > 1 && dflag.alloc(c->ncell)) return IEMIC_ENOMEM;
+    std::vector<double> flag;
     for (int cyc = 0; cyc < std::max(1, c->cfg.max_mask_fixes); cyc++) {
         int rc = assemble_jacobian(c, c->d_tmp1.p);
         if (rc) return rc;
-        if ((rc = d2h(c, pv.data(), c->d_val.p + (size_t)pb * c->ncell, sizeof(double) * pv.size())))
+        if ((rc = d2h(c, pv.data(), c->d_val.p + (size_t)pb * c->nloc, sizeof(double) * pv.size())))
             return rc;
-        int nfix = 0;
-        for (int64_t cell = 0; cell < c->ncell; cell++) {
-            if (NUN * cell + PP == c->rowintcon) continue;
+        flag.assign(c->ncell, 0.0);
+        for (int64_t lc = 0; lc < c->nloc; lc++) {
+            int i, j, k;
+            c->su.owned_ijk(lc, i, j, k);
+            if (NUN * c->su.ref_cell(i, j, k) + PP == c->su.rowintcon_ref) continue;
             double sum = 0.0;
             int el = 0;
             for (int s = 0; s < pn; s++) {
-                double v = pv[(size_t)s * c->ncell + cell];
+                double v = pv[(size_t)s * c->nloc + lc];
                 sum += v;
                 if (std::fabs(v) > 1e-10) el++;
             }
             if (sum == 1) continue;
-            if (el <= 2) {
-                int i = (int)(cell % n) + 1, j = (int)((cell / n) % m) + 1, k = (int)(cell / ((int64_t)n * m)) + 1;
+            if (el <= 2) flag[c->su.ref_cell(i, j, k)] = 1.0;
+        }
+        if (c->nranks > 1) {
+            if ((rc = h2d(c, dflag.p, flag.data(), sizeof(double) * c->ncell))) return rc;
+            if ((rc = allreduce_sum(c, dflag.p, (int)c->ncell))) return rc;
+            if ((rc = d2h(c, flag.data(), dflag.p, sizeof(double) * c->ncell))) return rc;
+        }
+        int nfix = 0;
+        for (int64_t q = 0; q < c->ncell; q++)
+            if (flag[q] != 0.0) {
+                const int i = (int)(q % n) + 1, j = (int)((q / n) % m) + 1, k = (int)(q / ((int64_t)n * m)) + 1;
                 c->su.landm[((size_t)k * (m + 2) + j) * (n + 2) + i] = LAND;
                 nfix++;
             }
-        }
         if (nfix == 0) break;
         int rc2 = upload_landm(c);
         if (rc2) return rc2;
@@ -107,7 +122,14 @@ int mask_fix(iemic_ctx* c)
 
 }  // namespace
 
-extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* landm)
+extern "C" int iemic_comm_unique_id(unsigned char* id128)
+{
+    if (!id128) return IEMIC_EINVAL;
+    return comm_unique_id(id128);
+}
+
+extern "C" int iemic_create_dist(iemic_ctx** out, const iemic_grid* grid, const int* landm,
+                                 const iemic_dist* dist)
 {
     if (!out || !grid || !landm) return IEMIC_EINVAL;
     *out = nullptr;
@@ -124,6 +146,17 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
         set_error("iemic_create: grid too small");
         return IEMIC_EINVAL;
     }
+    const int rank = dist ? dist->rank : 0, nranks = dist ? dist->nranks : 1;
+    if (nranks < 1 || rank < 0 || rank >= nranks) {
+        set_error("iemic_create: bad rank / nranks");
+        return IEMIC_EINVAL;
+    }
+    /* latitude bands: rows split evenly; each band must cover the halo depth */
+    const int jb0 = (int)((int64_t)rank * grid->m / nranks), jb1 = (int)((int64_t)(rank + 1) * grid->m / nranks);
+    if (jb1 - jb0 < HALO) {
+        set_error("iemic_create: too many ranks for the latitude rows (need >= 2 rows per rank)");
+        return IEMIC_EINVAL;
+    }
     iemic_ctx* c = new iemic_ctx();
     c->cfg = *grid;
     c->device = std::min(std::max(grid->device, 0), ndev - 1);
@@ -135,22 +168,36 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
     c->n = grid->n; c->m = grid->m; c->l = grid->l;
     c->ncell = (int64_t)c->n * c->m * c->l;
     c->nrows = NUN * c->ncell;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->jb0 = jb0;
+    c->jb1 = jb1;
     const int n = c->n, m = c->m, l = c->l;
     const size_t nl = (size_t)(n + 2) * (m + 2) * (l + 2);
-    c->su.init(*grid, landm);
+    c->su.init(*grid, landm, jb0, jb1);
+    c->nloc = c->su.nloc;
+    c->nlrows = NUN * c->nloc;
+    c->next = c->su.next;
+    c->nerows = NUN * c->next;
+    c->own0 = c->su.own0();
     c->rowintcon = c->su.rowintcon;
     int rc = 0;
+    if (nranks > 1 && (rc = comm_init(c, dist->id, rank, nranks))) {
+        delete c;
+        return rc;
+    }
+    const int64_t NE = c->nerows;
     rc |= c->d_landm.alloc(nl);
     rc |= c->d_ftab.alloc((size_t)3 * (m + 2) + (size_t)n * m);
-    rc |= c->d_frc.alloc(c->nrows);
+    rc |= c->d_frc.alloc(NE);
     rc |= c->d_qcor.alloc(8);
-    rc |= c->d_intc.alloc(c->nrows);
-    rc |= c->d_x.alloc(c->nrows);
-    rc |= c->d_F.alloc(c->nrows);
-    rc |= c->d_B.alloc(c->nrows);
-    rc |= c->d_val.alloc((size_t)NSLOT * c->ncell);
-    rc |= c->d_tmp1.alloc(c->nrows);
-    rc |= c->d_tmp2.alloc(c->nrows);
+    rc |= c->d_intc.alloc(NE);
+    rc |= c->d_x.alloc(NE);
+    rc |= c->d_F.alloc(NE);
+    rc |= c->d_B.alloc(NE);
+    rc |= c->d_val.alloc((size_t)NSLOT * c->nloc);
+    rc |= c->d_tmp1.alloc(NE);
+    rc |= c->d_tmp2.alloc(NE);
     rc |= c->d_red.alloc(2048);
     rc |= c->d_part.alloc((size_t)RED_BLOCKS * RED_ROWS);
     rc |= c->d_hbuf.alloc((size_t)2 * RED_ROWS);
@@ -160,7 +207,8 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
         delete c;
         return IEMIC_ENOMEM;
     }
-    (void)hipMemsetAsync(c->d_x.p, 0, sizeof(double) * c->nrows, c->stream);
+    for (DevBuf<double>* b : {&c->d_x, &c->d_F, &c->d_B, &c->d_frc, &c->d_tmp1, &c->d_tmp2})
+        (void)hipMemsetAsync(b->p, 0, sizeof(double) * b->n, c->stream);
     if (c->d_tab.alloc(c->su.tab.size()) ||
         h2d(c, c->d_tab.p, c->su.tab.data(), sizeof(double) * c->su.tab.size()) != 0) {
         set_error("iemic_create: cannot upload metric tables");
@@ -190,10 +238,16 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
     return 0;
 }
 
+extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* landm)
+{
+    return iemic_create_dist(out, grid, landm, nullptr);
+}
+
 extern "C" void iemic_destroy(iemic_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    comm_destroy(c);
     delete c; /* ~iemic_ctx drains the stream before any buffer is released */
 }
 
@@ -204,6 +258,38 @@ extern "C" void iemic_destroy(iemic_ctx* c)
         return IEMIC_EDEVICE;                          \
     }                                                  \
     StreamGuard stream_guard_{(c)}
+
+namespace {
+/* host reference-ordered global vector -> ext layout on the device (owned rows; halo 0) */
+int put_ref(iemic_ctx* c, const double* ref, double* dev)
+{
+    std::vector<double> e((size_t)c->nerows, 0.0);
+    c->su.ref_to_ext(ref, e.data());
+    return h2d(c, dev, e.data(), sizeof(double) * e.size());
+}
+/* ext layout on the device -> owned rows of a host reference-ordered global vector */
+int get_ref(iemic_ctx* c, const double* dev, double* ref)
+{
+    std::vector<double> e((size_t)c->nerows);
+    int rc = d2h(c, e.data(), dev, sizeof(double) * e.size());
+    if (rc) return rc;
+    c->su.ext_to_ref(e.data(), ref);
+    return 0;
+}
+}  // namespace
+
+namespace iemic {
+/* reference-ordered global device vector -> ext layout (owned rows) */
+__global__ void k_ref_to_ext(const double* __restrict__ ref, double* __restrict__ ext, int n, int m,
+                             int l, int jb0, int64_t nloc)
+{
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    const int64_t e = NUN * ((int64_t)HALO * l * n + lc), r = NUN * (((int64_t)k * m + j) * n + i);
+    for (int v = 0; v < NUN; v++) ext[e + v] = ref[r + v];
+}
+}  // namespace iemic
 
 extern "C" int iemic_set_par(iemic_ctx* c, int idx, double value)
 {
@@ -228,26 +314,38 @@ extern "C" int iemic_get_par(iemic_ctx* c, int idx, double* value)
 }
 
 extern "C" int iemic_nrows(const iemic_ctx* c) { return c ? (int)c->nrows : IEMIC_EINVAL; }
-extern "C" int iemic_rowintcon(const iemic_ctx* c) { return c ? c->rowintcon : IEMIC_EINVAL; }
+extern "C" int iemic_rowintcon(const iemic_ctx* c) { return c ? c->su.rowintcon_ref : IEMIC_EINVAL; }
 extern "C" int iemic_landm(const iemic_ctx* c, int* out)
 {
     if (!c || !out) return IEMIC_EINVAL;
     std::memcpy(out, c->su.landm.data(), sizeof(int) * c->su.landm.size());
     return 0;
 }
+extern "C" int iemic_layout(const iemic_ctx* c, int64_t* out)
+{
+    if (!c || !out) return IEMIC_EINVAL;
+    out[0] = c->nerows;
+    out[1] = NUN * c->own0;
+    out[2] = c->nlrows;
+    out[3] = c->jb0;
+    out[4] = c->jb1;
+    out[5] = c->rank;
+    out[6] = c->nranks;
+    return 0;
+}
 
-/* Maximal-graph rows (THCM.C:2288-2521): sorted, de-duplicated columns */
+/* Maximal-graph rows owned by this context (THCM.C:2288-2521) */
 extern "C" int64_t iemic_graph_nnz(const iemic_ctx* c)
 {
     if (!c) return IEMIC_EINVAL;
-    return c->su.to_csr(nullptr, nullptr, nullptr, nullptr, nullptr);
+    return c->su.to_csr(nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int iemic_set_state(iemic_ctx* c, const double* x)
 {
     CTX_CHECK(c);
     if (!x) return IEMIC_EINVAL;
-    int rc = h2d(c, c->d_x.p, x, sizeof(double) * c->nrows);
+    int rc = put_ref(c, x, c->d_x.p);
     if (rc) return rc;
     c->jac_valid = 0;
     return 0;
@@ -256,23 +354,24 @@ extern "C" int iemic_set_state_dev(iemic_ctx* c, const double* x_dev)
 {
     CTX_CHECK(c);
     if (!x_dev) return IEMIC_EINVAL;
-    HIP_OK(hipMemcpyAsync(c->d_x.p, x_dev, sizeof(double) * c->nrows, hipMemcpyDeviceToDevice,
-                          c->stream));
+    hipLaunchKernelGGL(k_ref_to_ext, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, c->stream,
+                       x_dev, c->d_x.p, c->n, c->m, c->l, c->jb0, c->nloc);
+    HIP_OK(hipGetLastError());
     c->jac_valid = 0;
     return 0;
 }
 extern "C" int iemic_get_state(iemic_ctx* c, double* x)
 {
     CTX_CHECK(c);
-    return d2h(c, x, c->d_x.p, sizeof(double) * c->nrows);
-    return 0;
+    return get_ref(c, c->d_x.p, x);
 }
 
 extern "C" int iemic_jacobian(iemic_ctx* c)
 {
     CTX_CHECK(c);
-    int rc = assemble_jacobian(c, c->d_x.p);
+    int rc = halo_exchange(c, c->d_x.p, HALO);
     if (rc) return rc;
+    if ((rc = assemble_jacobian(c, c->d_x.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -280,9 +379,10 @@ extern "C" int iemic_jacobian(iemic_ctx* c)
 extern "C" int iemic_rhs(iemic_ctx* c, double* F)
 {
     CTX_CHECK(c);
-    int rc = assemble_rhs(c, c->d_x.p, c->d_F.p);
+    int rc = halo_exchange(c, c->d_x.p, HALO);
     if (rc) return rc;
-    if (F) HIP_OK(hipMemcpyAsync(F, c->d_F.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
+    if (F) return get_ref(c, c->d_F.p, F);
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -291,9 +391,7 @@ extern "C" int iemic_diag_b(iemic_ctx* c, double* B)
 {
     CTX_CHECK(c);
     if (!c->jac_valid) return IEMIC_ESTATE;
-    int rc = d2h(c, B, c->d_B.p, sizeof(double) * c->nrows);
-    if (rc) return rc;
-    return 0;
+    return get_ref(c, c->d_B.p, B);
 }
 
 extern "C" int iemic_export_csr(iemic_ctx* c, int64_t* rowptr, int* col, double* val)
@@ -303,34 +401,26 @@ extern "C" int iemic_export_csr(iemic_ctx* c, int64_t* rowptr, int* col, double*
         set_error("iemic_export_csr: no Jacobian assembled");
         return IEMIC_ESTATE;
     }
-    std::vector<double> v((size_t)NSLOT * c->ncell);
+    std::vector<double> v((size_t)NSLOT * c->nloc);
     int rc = d2h(c, v.data(), c->d_val.p, sizeof(double) * v.size());
     if (rc) return rc;
-    std::vector<double> ic;
-    if (c->rowintcon >= 0) {
-        ic.resize(c->nrows);
-        if ((rc = d2h(c, ic.data(), c->d_intc.p, sizeof(double) * c->nrows))) return rc;
-    }
-    c->su.to_csr(v.data(), ic.data(), rowptr, col, val);
+    c->su.to_csr(v.data(), rowptr, col, val);
     return 0;
 }
 
 extern "C" int iemic_spmv(iemic_ctx* c, const double* x, double* y)
 {
     CTX_CHECK(c);
-    int rc = h2d(c, c->d_tmp1.p, x, sizeof(double) * c->nrows);
+    int rc = put_ref(c, x, c->d_tmp1.p);
     if (rc) return rc;
-    rc = spmv(c, c->d_tmp1.p, c->d_tmp2.p, c->stream);
-    if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(y, c->d_tmp2.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    return 0;
+    if ((rc = spmv(c, c->d_tmp1.p, c->d_tmp2.p, c->stream))) return rc;
+    return get_ref(c, c->d_tmp2.p, y);
 }
 
-extern "C" int iemic_spmv_dev(iemic_ctx* c, const double* x, double* y, void* stream)
+extern "C" int iemic_spmv_dev(iemic_ctx* c, double* x, double* y, void*)
 {
     CTX_CHECK(c);
-    return spmv(c, x, y, stream ? (hipStream_t)stream : c->stream);
+    return spmv(c, x, y, c->stream);
 }
 
 extern "C" int iemic_prec_compute(iemic_ctx* c, const iemic_krylov* opt)
@@ -345,13 +435,10 @@ extern "C" int iemic_prec_compute(iemic_ctx* c, const iemic_krylov* opt)
 extern "C" int iemic_prec_apply(iemic_ctx* c, const double* r, double* z)
 {
     CTX_CHECK(c);
-    int rc = h2d(c, c->d_tmp1.p, r, sizeof(double) * c->nrows);
+    int rc = put_ref(c, r, c->d_tmp1.p);
     if (rc) return rc;
-    rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);
-    if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(z, c->d_tmp2.p, sizeof(double) * c->nrows, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    return 0;
+    if ((rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p))) return rc;
+    return get_ref(c, c->d_tmp2.p, z);
 }
 
 extern "C" int iemic_solve_dev(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
@@ -368,12 +455,11 @@ extern "C" int iemic_solve(iemic_ctx* c, const double* b, double* x, const iemic
     CTX_CHECK(c);
     if (!opt || !b || !x) return IEMIC_EINVAL;
     DevBuf<double> db, dx;
-    if (db.alloc(c->nrows) || dx.alloc(c->nrows)) return IEMIC_ENOMEM;
-    int rc = h2d(c, db.p, b, sizeof(double) * c->nrows);
+    if (db.alloc(c->nerows) || dx.alloc(c->nerows)) return IEMIC_ENOMEM;
+    int rc = put_ref(c, b, db.p);
     if (rc) return rc;
-    rc = fgmres(c, db.p, dx.p, opt, info);
-    if (rc) return rc;
-    return d2h(c, x, dx.p, sizeof(double) * c->nrows);
+    if ((rc = fgmres(c, db.p, dx.p, opt, info))) return rc;
+    return get_ref(c, dx.p, x);
 }
 
 namespace iemic {
@@ -400,14 +486,15 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     auto T0 = clk::now();
-    const int64_t N = c->nrows;
-    const unsigned G = (unsigned)std::min<int64_t>((N + 255) / 256, 2048);
+    const int64_t o = NUN * c->own0, NL = c->nlrows;
+    const unsigned G = (unsigned)std::min<int64_t>((NL + 255) / 256, 2048);
     auto t = clk::now();
-    int rc = assemble_rhs(c, c->d_x.p, c->d_F.p);
+    int rc = halo_exchange(c, c->d_x.p, HALO);
     if (rc) return rc;
+    if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_rhs_ms += ms(t);
-    inf.norm_f0 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, N)));
+    inf.norm_f0 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, 0)));
     t = clk::now();
     if ((rc = assemble_jacobian(c, c->d_x.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -418,23 +505,25 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
         HIP_OK(hipStreamSynchronize(c->stream));
     }
     inf.t_prec_ms = ms(t);
-    hipLaunchKernelGGL(k_neg, dim3(G), dim3(256), 0, c->stream, c->d_F.p, c->d_tmp1.p, N);
+    hipLaunchKernelGGL(k_neg, dim3(G), dim3(256), 0, c->stream, c->d_F.p + o, c->d_tmp1.p + o, NL);
     t = clk::now();
     if ((rc = fgmres(c, c->d_tmp1.p, c->d_tmp2.p, opt, &inf.solve))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_solve_ms = ms(t);
-    hipLaunchKernelGGL(k_newton_update, dim3(G), dim3(256), 0, c->stream, c->d_x.p, c->d_tmp2.p, N);
+    hipLaunchKernelGGL(k_newton_update, dim3(G), dim3(256), 0, c->stream, c->d_x.p + o, c->d_tmp2.p + o, NL);
     t = clk::now();
+    if ((rc = halo_exchange(c, c->d_x.p, HALO))) return rc;
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_rhs_ms += ms(t);
-    inf.norm_f1 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, N)));
+    inf.norm_f1 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, 0)));
     c->jac_valid = 1;
     inf.t_total_ms = ms(T0);
     if (info) *info = inf;
     return 0;
 }
 
+/* mean duration of the SpMV kernel alone (no halo exchange), HIP events on its stream */
 extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
 {
     CTX_CHECK(c);
@@ -442,11 +531,11 @@ extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
-    int rc = spmv(c, c->d_x.p, c->d_tmp2.p, c->stream); /* warm */
+    int rc = spmv(c, c->d_x.p, c->d_tmp2.p, c->stream); /* warm, fills the halo */
     if (rc) return rc;
     HIP_OK(hipEventRecord(e0, c->stream));
     for (int r = 0; r < nrep; r++) {
-        rc = spmv(c, c->d_x.p, c->d_tmp2.p, c->stream);
+        rc = spmv_kernel(c, c->d_x.p, c->d_tmp2.p);
         if (rc) return rc;
     }
     HIP_OK(hipEventRecord(e1, c->stream));

@@ -96,8 +96,15 @@ struct iemic_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int n = 0, m = 0, l = 0;
-    int64_t ncell = 0, nrows = 0;
-    int rowintcon = -1;
+    int64_t ncell = 0, nrows = 0;    /* global cells / rows                               */
+    /* latitude-band decomposition (stencil.h ext layout): owned band [jb0, jb1) */
+    int rank = 0, nranks = 1;
+    int jb0 = 0, jb1 = 0;
+    int64_t nloc = 0, nlrows = 0;    /* owned cells / rows                                */
+    int64_t next = 0, nerows = 0;    /* cells / rows of an ext vector (band + 2 HALO)     */
+    int64_t own0 = 0;                /* ext cell of the first owned cell                  */
+    int64_t rowintcon = -1;          /* ext row of the integral condition if owned        */
+    void* comm = nullptr;            /* ncclComm_t when nranks > 1                        */
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
     iemic::DevBuf<int> d_landm;
@@ -147,12 +154,21 @@ struct StreamGuard {
     ~StreamGuard() { if (c && c->stream) (void)hipStreamSynchronize(c->stream); }
 };
 
+/* comm.hip: sums over the ranks (no-op for one rank) and halo exchange of the ext layout */
+int allreduce_sum(iemic_ctx* c, double* dev, int count);
+int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
+int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
+int comm_unique_id(unsigned char* id128);
+void comm_destroy(iemic_ctx* c);
+
 /* assembly.hip */
 int assemble_jacobian(iemic_ctx* c, const double* x_dev);
 int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev);
 int compute_forcing(iemic_ctx* c);
 /* krylov.hip */
-int spmv(iemic_ctx* c, const double* x, double* y, hipStream_t s);
+/* y = J x on the owned rows; x (ext layout) gets its halo rows exchanged first */
+int spmv(iemic_ctx* c, double* x, double* y, hipStream_t s);
+int spmv_kernel(iemic_ctx* c, const double* x, double* y);
 double dot(iemic_ctx* c, const double* a, const double* b, int64_t n);
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
            iemic_solve_info* info);

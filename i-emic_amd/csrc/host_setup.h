@@ -64,12 +64,44 @@ struct Setup {
     std::vector<double> tab;         /* Geo table block (see geo())            */
     double par[31] = {0};
     double qtnd = 0, qsnd = 0;
-    int rowintcon = -1;
+    int rowintcon_ref = -1;          /* reference (global) row of the integral condition */
+    int64_t rowintcon = -1;          /* its ext row when this band owns it, else -1       */
+    int jb0 = 0, jb1 = 0;            /* owned latitude band [jb0, jb1)                    */
+    int64_t nloc = 0, next = 0;      /* owned cells, cells incl. HALO rows each side      */
 
-    void init(const iemic_grid& g, const int* landm_in)
+    /* ---- layout helpers (see the ext layout in stencil.h) ------------------------- */
+    int64_t ext_cell(int i, int j, int k) const { return (((int64_t)j - jb0 + HALO) * l + k) * n + i; }
+    int64_t ref_cell(int i, int j, int k) const { return ((int64_t)k * m + j) * n + i; }
+    int64_t own0() const { return (int64_t)HALO * l * n; }        /* first owned ext cell  */
+    /* owned-local index lc -> 0-based (i, j, k) */
+    void owned_ijk(int64_t lc, int& i, int& j, int& k) const
+    {
+        i = (int)(lc % n);
+        k = (int)((lc / n) % l);
+        j = jb0 + (int)(lc / ((int64_t)n * l));
+    }
+    void ext_ijk(int64_t ec, int& i, int& j, int& k) const
+    {
+        i = (int)(ec % n);
+        k = (int)((ec / n) % l);
+        j = jb0 - HALO + (int)(ec / ((int64_t)n * l));
+    }
+    int64_t ext_to_ref_row(int64_t er) const
+    {
+        int i, j, k;
+        ext_ijk(er / NUN, i, j, k);
+        return NUN * ref_cell(i, j, k) + er % NUN;
+    }
+    bool owns_j(int j) const { return j >= jb0 && j < jb1; }
+
+    void init(const iemic_grid& g, const int* landm_in, int band0 = 0, int band1 = -1)
     {
         cfg = g;
         n = g.n; m = g.m; l = g.l;
+        jb0 = band0;
+        jb1 = band1 < 0 ? m : band1;
+        nloc = (int64_t)n * l * (jb1 - jb0);
+        next = (int64_t)n * l * (jb1 - jb0 + 2 * HALO);
         xmin = g.xmin * pi_ / 180.0;
         xmax = g.xmax * pi_ / 180.0;
         ymin = g.ymin * pi_ / 180.0;
@@ -85,10 +117,12 @@ struct Setup {
                     if (j == 0 || j == m + 1 || k == 0 || k == l + 1) v = LAND;
                 }
         rowintcon = -1;
+        rowintcon_ref = -1;
         if (g.sres == 0) {
             int Nic = g.int_i == -1 ? n - 1 : g.int_i;
             int Mic = g.int_j == -1 ? m - 1 : g.int_j;
-            rowintcon = NUN * ((l - 1) * n * m + n * Mic + Nic) + SS;
+            rowintcon_ref = (int)(NUN * ref_cell(Nic, Mic, l - 1) + SS);
+            if (owns_j(Mic)) rowintcon = NUN * ext_cell(Nic, Mic, l - 1) + SS;
         }
         grid();
         stpnt();
@@ -205,40 +239,43 @@ struct Setup {
         return t;
     }
 
+    /* integral-condition coefficient of the S unknown of (i,j,k), 0-based (thcm_utils.F90:285-312) */
+    double intcond_at(int i, int j, int k) const
+    {
+        return landm[((size_t)(k + 1) * (m + 2) + (j + 1)) * (n + 2) + (i + 1)] == OCEAN
+                   ? std::cos(y[j + 1]) * dfzT[k + 1] : 0.0;
+    }
+    /* coefficients in the ext layout (owned S rows), for the device */
     std::vector<double> intcond_coeff() const
     {
-        std::vector<double> ic((size_t)NUN * n * m * l, 0.0);
-        for (int k = 1; k <= l; k++)
-            for (int j = 1; j <= m; j++)
-                for (int i = 1; i <= n; i++)
-                    if (landm[((size_t)k * (m + 2) + j) * (n + 2) + i] == OCEAN)
-                        ic[(size_t)NUN * (((size_t)(k - 1) * m + (j - 1)) * n + (i - 1)) + SS] =
-                            std::cos(y[j]) * dfzT[k];
+        std::vector<double> ic((size_t)NUN * next, 0.0);
+        for (int64_t lc = 0; lc < nloc; lc++) {
+            int i, j, k;
+            owned_ijk(lc, i, j, k);
+            ic[(size_t)NUN * ext_cell(i, j, k) + SS] = intcond_at(i, j, k);
+        }
         return ic;
     }
 
-    /* Row `row` of the maximal graph (THCM::CreateMaximalGraph, THCM.C:2288-2491, columns
-     * sorted as Epetra stores them): columns and the stencil slot feeding each.  Several
-     * slots can name the same column (tiny periodic grids); `slot` keeps all of them, in
-     * `first` the position of the column they add into.  The intcond row (SRES = 0) is
-     * dense over all S unknowns (THCM.C:2475-2486); its slots are -1. */
-    void graph_row(int64_t row, std::vector<int64_t>& cols, std::vector<std::pair<int, int>>& slot) const
+    /* Owned rows of the maximal graph (THCM::CreateMaximalGraph, THCM.C:2288-2491) in the
+     * reference's numbering: columns sorted as Epetra stores them, plus the stencil slot
+     * feeding each (several slots can name one column on tiny periodic grids; `first` is
+     * the column position they add into).  The intcond row (SRES = 0) is dense over all S
+     * unknowns (THCM.C:2475-2486); its slots are -1. */
+    void graph_row(int i, int j, int k, int var, std::vector<int64_t>& cols,
+                   std::vector<std::pair<int, int>>& slot) const
     {
         cols.clear();
         slot.clear();
-        const int64_t ncell = (int64_t)n * m * l;
-        if (row == rowintcon) {
-            for (int64_t q = 0; q < ncell; q++) cols.push_back(NUN * q + SS);
+        if (NUN * ref_cell(i, j, k) + var == rowintcon_ref) {
+            for (int64_t q = 0; q < (int64_t)n * m * l; q++) cols.push_back(NUN * q + SS);
             return;
         }
         Geo g = geo(nullptr, tab.data());
-        const int64_t cell = row / NUN;
-        const int var = (int)(row % NUN);
-        const int i = (int)(cell % n) + 1, j = (int)((cell / n) % m) + 1, k = (int)(cell / ((int64_t)n * m)) + 1;
         std::vector<std::pair<int64_t, int>> e;
         for (int s = ROW_BEGIN[var]; s < ROW_BEGIN[var + 1]; s++) {
-            int64_t col = slot_col(g, s, i, j, k);
-            if (col >= 0) e.push_back({col, s});
+            int64_t col = slot_col(g, s, i + 1, j + 1, k + 1);
+            if (col >= 0) e.push_back({ext_to_ref_row(col), s});
         }
         std::sort(e.begin(), e.end());
         for (size_t a = 0; a < e.size(); a++) {
@@ -247,32 +284,59 @@ struct Setup {
         }
     }
 
-    /* Epetra-identical CSR of the Jacobian from slot-major stencil values (+ dense
-     * intcond row with coefficients intSign*ic).  rowptr/col/val may be null (count). */
-    int64_t to_csr(const double* v, const double* ic, int64_t* rowptr, int* col, double* val) const
+    /* Epetra-identical CSR of the owned rows (reference order: k-major) from slot-major
+     * values v[s*nloc + lc]; the dense intcond row gets intSign*coefficient.  rowptr/col/val
+     * may be null (count). */
+    int64_t to_csr(const double* v, int64_t* rowptr, int* col, double* val) const
     {
-        const int64_t ncell = (int64_t)n * m * l, nrows = NUN * ncell;
         std::vector<int64_t> cols;
         std::vector<std::pair<int, int>> slot;
-        int64_t pos = 0;
-        for (int64_t r = 0; r < nrows; r++) {
-            if (rowptr) rowptr[r] = pos;
-            graph_row(r, cols, slot);
-            if (col)
-                for (size_t a = 0; a < cols.size(); a++) col[pos + a] = (int)cols[a];
-            if (val) {
-                const int64_t cell = r / NUN;
-                if (r == rowintcon)
-                    for (size_t a = 0; a < cols.size(); a++) val[pos + a] = cfg.int_sign * ic[cols[a]];
-                else {
-                    for (size_t a = 0; a < cols.size(); a++) val[pos + a] = 0.0;
-                    for (auto& ps : slot) val[pos + ps.first] += v[(size_t)ps.second * ncell + cell];
-                }
-            }
-            pos += (int64_t)cols.size();
-        }
-        if (rowptr) rowptr[nrows] = pos;
+        int64_t pos = 0, r = 0;
+        for (int k = 0; k < l; k++)
+            for (int j = jb0; j < jb1; j++)
+                for (int i = 0; i < n; i++)
+                    for (int var = 0; var < NUN; var++, r++) {
+                        if (rowptr) rowptr[r] = pos;
+                        graph_row(i, j, k, var, cols, slot);
+                        if (col)
+                            for (size_t a = 0; a < cols.size(); a++) col[pos + a] = (int)cols[a];
+                        if (val) {
+                            const int64_t lc = (((int64_t)j - jb0) * l + k) * n + i;
+                            if (NUN * ref_cell(i, j, k) + var == rowintcon_ref)
+                                for (size_t a = 0; a < cols.size(); a++) {
+                                    const int64_t q = cols[a] / NUN;
+                                    val[pos + a] = cfg.int_sign *
+                                                   intcond_at((int)(q % n), (int)((q / n) % m), (int)(q / ((int64_t)n * m)));
+                                }
+                            else {
+                                for (size_t a = 0; a < cols.size(); a++) val[pos + a] = 0.0;
+                                for (auto& ps : slot) val[pos + ps.first] += v[(size_t)ps.second * nloc + lc];
+                            }
+                        }
+                        pos += (int64_t)cols.size();
+                    }
+        if (rowptr) rowptr[r] = pos;
         return pos;
+    }
+
+    /* reference-ordered global vector <-> ext-layout local vector (owned rows only) */
+    void ref_to_ext(const double* ref, double* ext) const
+    {
+        for (int64_t lc = 0; lc < nloc; lc++) {
+            int i, j, k;
+            owned_ijk(lc, i, j, k);
+            const int64_t e = NUN * ext_cell(i, j, k), r = NUN * ref_cell(i, j, k);
+            for (int v = 0; v < NUN; v++) ext[e + v] = ref[r + v];
+        }
+    }
+    void ext_to_ref(const double* ext, double* ref) const
+    {
+        for (int64_t lc = 0; lc < nloc; lc++) {
+            int i, j, k;
+            owned_ijk(lc, i, j, k);
+            const int64_t e = NUN * ext_cell(i, j, k), r = NUN * ref_cell(i, j, k);
+            for (int v = 0; v < NUN; v++) ref[r + v] = ext[e + v];
+        }
     }
 
     /* Geo over externally owned copies of landm / tab */
@@ -280,6 +344,7 @@ struct Setup {
     {
         Geo g{};
         g.n = n; g.m = m; g.l = l;
+        g.jb0 = jb0;
         g.periodic = cfg.periodic;
         g.tres = cfg.tres; g.sres = cfg.sres; g.coriolis_on = cfg.coriolis_on;
         g.dx = dx; g.dy = dy; g.dz = dz;

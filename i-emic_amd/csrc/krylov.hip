@@ -23,7 +23,7 @@ namespace iemic {
 /* ---- SpMV ------------------------------------------------------------------------ */
 template <int R>
 __device__ __forceinline__ double row_dot(const double* __restrict__ val, const double* __restrict__ x,
-                                          int64_t cell, int64_t ncell, const int64_t* nb)
+                                          int64_t lc, int64_t nloc, const int64_t* nb)
 {
     constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
     double acc = 0.0;
@@ -31,16 +31,17 @@ __device__ __forceinline__ double row_dot(const double* __restrict__ val, const 
     for (int s = 0; s < NS; s++) {
         const Slot sl = SLOTS[B + s];
         const int o = (sl.dk + 1) * 9 + (sl.dj + 1) * 3 + (sl.di + 1);
-        acc += val[(int64_t)(B + s) * ncell + cell] * x[NUN * nb[o] + sl.var];
+        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * nb[o] + sl.var];
     }
     return acc;
 }
 
-/* neighbour cell index for the 27 offsets; out-of-domain -> own cell (value slot is 0) */
-__device__ __forceinline__ void neighbours(int n, int m, int l, int periodic, int64_t cell,
-                                           int64_t* nb)
+/* ext cell of the 27 neighbours of owned cell (i, j, k) (0-based, j global); outside the
+ * domain -> the cell itself (those slots hold 0).  The j +- 1 rows of a band edge are
+ * halo rows, filled by halo_exchange before the launch. */
+__device__ __forceinline__ void neighbours(int n, int m, int l, int periodic, int jb0, int i, int j,
+                                           int k, int64_t* nb)
 {
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
     int ii[3], jj[3], kk[3];
     ii[0] = i - 1; ii[1] = i; ii[2] = i + 1;
     if (periodic) {
@@ -58,25 +59,26 @@ __device__ __forceinline__ void neighbours(int n, int m, int l, int periodic, in
         for (int b = 0; b < 3; b++)
 #pragma unroll
             for (int d = 0; d < 3; d++)
-                nb[a * 9 + b * 3 + d] = ((int64_t)kk[a] * m + jj[b]) * n + ii[d];
+                nb[a * 9 + b * 3 + d] = (((int64_t)jj[b] - jb0 + HALO) * l + kk[a]) * n + ii[d];
 }
 
-__global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic,
+__global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic, int jb0,
                                               const double* __restrict__ val,
                                               const double* __restrict__ x,
-                                              double* __restrict__ y, int64_t ncell)
+                                              double* __restrict__ y, int64_t nloc)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lc >= nloc) return;
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
     int64_t nb[27];
-    neighbours(n, m, l, periodic, cell, nb);
-    double r0 = row_dot<UU>(val, x, cell, ncell, nb);
-    double r1 = row_dot<VV>(val, x, cell, ncell, nb);
-    double r2 = row_dot<WW>(val, x, cell, ncell, nb);
-    double r3 = row_dot<PP>(val, x, cell, ncell, nb);
-    double r4 = row_dot<TT>(val, x, cell, ncell, nb);
-    double r5 = row_dot<SS>(val, x, cell, ncell, nb);
-    double* yc = y + NUN * cell;
+    neighbours(n, m, l, periodic, jb0, i, j, k, nb);
+    double r0 = row_dot<UU>(val, x, lc, nloc, nb);
+    double r1 = row_dot<VV>(val, x, lc, nloc, nb);
+    double r2 = row_dot<WW>(val, x, lc, nloc, nb);
+    double r3 = row_dot<PP>(val, x, lc, nloc, nb);
+    double r4 = row_dot<TT>(val, x, lc, nloc, nb);
+    double r5 = row_dot<SS>(val, x, lc, nloc, nb);
+    double* yc = y + NUN * ((int64_t)HALO * l * n + lc);
     yc[0] = r0; yc[1] = r1; yc[2] = r2; yc[3] = r3; yc[4] = r4; yc[5] = r5;
 }
 
@@ -315,36 +317,52 @@ static inline unsigned grid_for(int64_t N)
     return (unsigned)std::min<int64_t>(b, 2048);
 }
 
-int spmv(iemic_ctx* c, const double* x, double* y, hipStream_t s)
+/* the SpMV kernel(s) alone: x's halo rows must be current */
+int spmv_kernel(iemic_ctx* c, const double* x, double* y)
 {
     if (!c->jac_valid) {
         set_error("spmv: no Jacobian assembled");
         return IEMIC_ESTATE;
     }
-    hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0, s, c->n,
-                       c->m, c->l, c->cfg.periodic, c->d_val.p, x, y, c->ncell);
-    if (c->rowintcon >= 0) {
-        /* dense intcond row: y[rowintcon] = intSign * coeff . x */
-        hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, 1), dim3(256), 0, s, c->d_intc.p, (int64_t)0, 1,
-                           x, c->nrows, c->d_red.p);
+    hipStream_t s = c->stream;
+    hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, s, c->n,
+                       c->m, c->l, c->cfg.periodic, c->jb0, c->d_val.p, x, y, c->nloc);
+    if (c->su.rowintcon_ref >= 0) {
+        /* dense intcond row: y[rowintcon] = intSign * coeff . x (summed over the ranks) */
+        const int64_t o = NUN * c->own0;
+        hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, 1), dim3(256), 0, s, c->d_intc.p + o, (int64_t)0, 1,
+                           x + o, c->nlrows, c->d_red.p);
         hipLaunchKernelGGL(k_mdot_final, dim3(1), dim3(256), 0, s, c->d_red.p, RED_BLOCKS, 1,
                            c->d_red.p + RED_BLOCKS);
-        hipLaunchKernelGGL(k_scale_copy, dim3(1), dim3(1), 0, s, c->d_red.p + RED_BLOCKS,
-                           (double)c->cfg.int_sign, y + c->rowintcon, (int64_t)1);
+        int rc = allreduce_sum(c, c->d_red.p + RED_BLOCKS, 1);
+        if (rc) return rc;
+        if (c->rowintcon >= 0)
+            hipLaunchKernelGGL(k_scale_copy, dim3(1), dim3(1), 0, s, c->d_red.p + RED_BLOCKS,
+                               (double)c->cfg.int_sign, y + c->rowintcon, (int64_t)1);
     }
     HIP_OK(hipGetLastError());
     return 0;
 }
 
+int spmv(iemic_ctx* c, double* x, double* y, hipStream_t)
+{
+    int rc = halo_exchange(c, x, 1);
+    if (rc) return rc;
+    return spmv_kernel(c, x, y);
+}
+
 /* dot products of nvec vectors V_i (stride ldv) with w; result on host in out[] */
+/* V, w point at the first owned row; length nlrows; sums over the ranks */
 static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const double* w,
                      double* out)
 {
-    const int64_t N = c->nrows;
+    const int64_t N = c->nlrows;
     hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec), dim3(256), 0, c->stream, V, ldv, nvec, w, N,
                        c->d_part.p);
     hipLaunchKernelGGL(k_mdot_final, dim3(nvec), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS,
                        nvec, c->d_hbuf.p);
+    int rc = allreduce_sum(c, c->d_hbuf.p, nvec);
+    if (rc) return rc;
     HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * nvec, hipMemcpyDeviceToHost,
                           c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -352,11 +370,12 @@ static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const
     return 0;
 }
 
-double dot(iemic_ctx* c, const double* a, const double* b, int64_t n)
+/* a . b over the owned rows of two ext vectors, summed over the ranks */
+double dot(iemic_ctx* c, const double* a, const double* b, int64_t)
 {
-    (void)n;
+    const int64_t o = NUN * c->own0;
     double r = 0.0;
-    if (mdot_host(c, a, 0, 1, b, &r)) return NAN;
+    if (mdot_host(c, a + o, 0, 1, b + o, &r)) return NAN;
     return r;
 }
 
@@ -366,15 +385,18 @@ double dot(iemic_ctx* c, const double* a, const double* b, int64_t n)
 static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, double* w, double* h,
                      double* ww0, double* ww1)
 {
-    const int64_t N = c->nrows;
+    const int64_t N = c->nlrows;
     hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec + 1), dim3(256), 0, c->stream, V, ldv, nvec,
                        w, N, c->d_part.p, (const double*)w);
     hipLaunchKernelGGL(k_mdot_final, dim3(nvec + 1), dim3(256), 0, c->stream, c->d_part.p,
                        RED_BLOCKS, nvec + 1, c->d_hbuf.p);
+    int rc = allreduce_sum(c, c->d_hbuf.p, nvec + 1);   /* coefficients summed before use */
+    if (rc) return rc;
     hipLaunchKernelGGL(k_mupdate_norm, dim3(RED_BLOCKS), dim3(256), 0, c->stream, V, ldv, nvec,
                        c->d_hbuf.p, w, N, c->d_part.p);
     hipLaunchKernelGGL(k_mdot_final, dim3(1), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS, 1,
                        c->d_hbuf.p + nvec + 1);
+    if ((rc = allreduce_sum(c, c->d_hbuf.p + nvec + 1, 1))) return rc;
     HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (nvec + 2), hipMemcpyDeviceToHost,
                           c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -387,7 +409,7 @@ static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, doubl
 static int ensure_krylov(iemic_ctx* c, int m)
 {
     if (c->kr.m >= m && c->kr.V.p) return 0;
-    const int64_t N = c->nrows;
+    const int64_t N = c->nerows;
     int rc = 0;
     rc |= c->kr.V.alloc((size_t)(m + 1) * N);
     rc |= c->kr.Z.alloc((size_t)m * N);
@@ -423,8 +445,9 @@ static double ms_since(std::chrono::steady_clock::time_point t0)
 
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
 {
+    /* vectors are ext-layout (stride NE); kernels touch the owned rows [o, o + NL) */
     const int m = std::max(1, std::min(opt->krylov_dim, MAX_KRYLOV));
-    const int64_t N = c->nrows;
+    const int64_t NE = c->nerows, o = NUN * c->own0, NL = c->nlrows;
     int rc = ensure_krylov(c, m);
     if (rc) return rc;
     iemic_solve_info inf{};
@@ -433,7 +456,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     double* Z = c->kr.Z.p;
     double* w = c->kr.w.p;
     double* r = c->kr.r.p;
-    const unsigned G = grid_for(N);
+    const unsigned G = grid_for(NL);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
     if (2 * m + 3 > RED_ROWS) {
         set_error("fgmres: Krylov dimension too large");
@@ -447,35 +470,34 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     hipEvent_t* ev = evs.e;
     for (int q = 0; q < 3; q++) HIP_OK(hipEventCreate(&ev[q]));
 
-    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * N, c->stream));
-    double bnorm = std::sqrt(std::max(0.0, dot(c, b, b, N)));
+    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
+    double bnorm = std::sqrt(std::max(0.0, dot(c, b, b, 0)));
     if (!(bnorm > 0)) {
         inf.converged = 1;
         if (info) *info = inf;
         return 0;
     }
     /* r = b (x0 = 0) */
-    HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
     double beta = bnorm, res = 1.0;
     int it = 0;
     for (int cycle = 0; cycle <= opt->max_restarts; cycle++) {
-        hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r, 1.0 / beta, V, N);
+        hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r + o, 1.0 / beta, V + o, NL);
         std::fill(g.begin(), g.end(), 0.0);
         g[0] = beta;
         int j = 0;
-        bool conv = false;
         if (opt->orth == 1) {
             for (; j < m; j++) {
-                double* vj = V + (int64_t)j * N;
-                double* zj = Z + (int64_t)j * N;
-                double* vn = V + (int64_t)(j + 1) * N;
+                double* vj = V + (int64_t)j * NE;
+                double* zj = Z + (int64_t)j * NE;
+                double* vn = V + (int64_t)(j + 1) * NE;
                 /* prec and SpMV are timed with events (no extra host synchronisation) */
                 HIP_OK(hipEventRecord(ev[0], c->stream));
                 if (opt->prec > 0) {
                     rc = prec_apply(c, vj, zj);
                     if (rc) return rc;
                 } else {
-                    HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+                    HIP_OK(hipMemcpyAsync(zj, vj, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
                 }
                 HIP_OK(hipEventRecord(ev[1], c->stream));
                 rc = spmv(c, zj, vn, c->stream);
@@ -489,11 +511,11 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 double hn2 = 0.0;
                 {
                     double ww0 = 0.0;
-                    rc = orth_pass(c, V, N, j + 1, vn, h.data(), &ww0, &hn2);
+                    rc = orth_pass(c, V + o, NE, j + 1, vn + o, h.data(), &ww0, &hn2);
                     if (rc) return rc;
                     if (hn2 < 0.5 * ww0) {
                         double dummy = 0.0;
-                        rc = orth_pass(c, V, N, j + 1, vn, h2.data(), &dummy, &hn2);
+                        rc = orth_pass(c, V + o, NE, j + 1, vn + o, h2.data(), &dummy, &hn2);
                         if (rc) return rc;
                         for (int i = 0; i <= j; i++) h[i] += h2[i];
                         inf_reorth++;
@@ -501,14 +523,14 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 }
                 double hn = std::sqrt(std::max(0.0, hn2));
                 if (hn > 0)
-                    hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn, 1.0 / hn, vn, N);
+                    hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn + o, 1.0 / hn,
+                                       vn + o, NL);
                 {
                     float a1 = 0.f, a2 = 0.f;
                     (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
                     (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
                     inf.t_prec_ms += a1;
                     inf.t_spmv_ms += a2;
-                    /* host time of the orthogonalisation includes waiting for prec + SpMV */
                     inf.t_orth_ms += ms_since(tp) - a1 - a2;
                 }
                 for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
@@ -530,11 +552,9 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 it++;
                 if (res <= opt->tol || hn == 0.0) {
                     j++;
-                    conv = true;
                     break;
                 }
             }
-
         } else {
             /* DCGS2 (delayed classical Gram-Schmidt with reorthogonalisation): the new
              * vector u_j is orthogonalised once when produced and re-orthogonalised one step
@@ -545,17 +565,17 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             std::vector<double> htent(m + 1), col(m + 1), coef(2 * (size_t)m + 2);
             int ncolf = 0;                 /* finalised columns */
             for (int jj = 0; jj <= m; jj++) {
-                double* u = V + (int64_t)jj * N;
-                double* wv = jj < m ? V + (int64_t)(jj + 1) * N : nullptr;
+                double* u = V + (int64_t)jj * NE;
+                double* wv = jj < m ? V + (int64_t)(jj + 1) * NE : nullptr;
                 float a1 = 0.f, a2 = 0.f;
                 if (jj < m) {
-                    double* zj = Z + (int64_t)jj * N;
+                    double* zj = Z + (int64_t)jj * NE;
                     HIP_OK(hipEventRecord(ev[0], c->stream));
                     if (opt->prec > 0) {
                         rc = prec_apply(c, u, zj);
                         if (rc) return rc;
                     } else {
-                        HIP_OK(hipMemcpyAsync(zj, u, sizeof(double) * N, hipMemcpyDeviceToDevice,
+                        HIP_OK(hipMemcpyAsync(zj, u, sizeof(double) * NE, hipMemcpyDeviceToDevice,
                                               c->stream));
                     }
                     HIP_OK(hipEventRecord(ev[1], c->stream));
@@ -564,13 +584,14 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     HIP_OK(hipEventRecord(ev[2], c->stream));
                 }
                 auto tp = std::chrono::steady_clock::now();
-                /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1) */
+                /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
                 hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, (nv + 3) / 4 + 1), dim3(256), 0,
-                                   c->stream, V, N, nv, u, wd, N, c->d_part.p);
+                                   c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
+                if ((rc = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc;
                 HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (2 * nv + 3),
                                       hipMemcpyDeviceToHost, c->stream));
                 HIP_OK(hipStreamSynchronize(c->stream));
@@ -589,6 +610,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 const double uu = hr[2 * nv], uw = hr[2 * nv + 1];
                 const double beta2 = uu - aa;
                 const double bt = beta2 > 0.0 ? std::sqrt(beta2) : 0.0;
+                bool stop = false;
                 if (jj >= 1) {
                     /* finalise column jj-1: tentative + reorthogonalisation coefficients */
                     const int q = jj - 1;
@@ -611,13 +633,9 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     res = std::fabs(g[q + 1]) / bnorm;
                     ncolf = jj;
                     it++;
-                    if (res <= opt->tol || !(bt > 0.0)) {
-                        conv = true;
-                        inf.t_orth_ms += ms_since(tp) - a1 - a2;
-                        break;
-                    }
+                    stop = res <= opt->tol || !(bt > 0.0);
                 }
-                if (jj == m || !(bt > 0.0)) {
+                if (stop || jj == m || !(bt > 0.0)) {
                     inf.t_orth_ms += ms_since(tp) - a1 - a2;
                     break;
                 }
@@ -631,8 +649,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 }
                 htent[nv] = hjj;
                 if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
-                hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V, N, nv,
-                                   c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u, wv, N);
+                hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V + o, NE, nv,
+                                   c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u + o, wv + o, NL);
                 inf.t_orth_ms += ms_since(tp) - a1 - a2;
             }
             j = ncolf;
@@ -646,25 +664,24 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         }
         if (k > 0) {
             if ((rc = upload_coeffs(c, y.data(), k))) return rc;
-            hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z, N, k,
-                               c->d_hbuf.p + RED_ROWS, x, N);
+            hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z + o, NE, k,
+                               c->d_hbuf.p + RED_ROWS, x + o, NL);
         }
         if (cycle == opt->max_restarts) break;
         /* r = b - J x; a cycle that converged on the implicit (Givens) estimate restarts
          * only if the true residual has not reached the tolerance */
         rc = spmv(c, x, r, c->stream);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, r, r, N);
-        beta = std::sqrt(std::max(0.0, dot(c, r, r, N)));
+        hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b + o, -1.0, r + o, r + o, NL);
+        beta = std::sqrt(std::max(0.0, dot(c, r, r, 0)));
         res = beta / bnorm;
         if (res <= opt->tol) break;
-        (void)conv;
     }
     /* explicit residual (Ocean.C:1140-1150) */
     rc = spmv(c, x, w, c->stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b, -1.0, w, w, N);
-    double e2 = dot(c, w, w, N);
+    hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b + o, -1.0, w + o, w + o, NL);
+    double e2 = dot(c, w, w, 0);
     inf.iters = it;
     inf.reorth = inf_reorth;
     inf.implicit_rel_res = res;

@@ -86,6 +86,7 @@ __global__ void __launch_bounds__(128) k_bj_compute(const double* __restrict__ v
         for (int j = 0; j < 6; j++) dinv[(int64_t)(i * 6 + j) * ncell + cell] = inv[i][j];
 }
 
+/* r, z: ext vectors already offset to the first owned row; dinv per owned cell */
 __global__ void __launch_bounds__(256) k_bj_apply(const double* __restrict__ dinv, int64_t ncell,
                                                   const double* __restrict__ r, double* __restrict__ z)
 {
@@ -111,15 +112,15 @@ int prec_compute(iemic_ctx* c, const iemic_krylov* opt)
     }
     c->gs.kind = opt ? opt->prec : 1;
     if (c->gs.kind == 2) return gs_compute(c, opt);
-    if (c->gs.dinv.n < (size_t)36 * c->ncell) {
-        if (c->gs.dinv.alloc((size_t)36 * c->ncell)) {
+    if (c->gs.dinv.n < (size_t)36 * c->nloc) {
+        if (c->gs.dinv.alloc((size_t)36 * c->nloc)) {
             set_error("prec_compute: out of memory");
             return IEMIC_ENOMEM;
         }
     }
     HIP_OK(hipMemsetAsync(c->d_red.p, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_bj_compute, dim3((unsigned)((c->ncell + 127) / 128)), dim3(128), 0, c->stream,
-                       c->d_val.p, c->ncell, c->gs.dinv.p, (int*)c->d_red.p);
+    hipLaunchKernelGGL(k_bj_compute, dim3((unsigned)((c->nloc + 127) / 128)), dim3(128), 0, c->stream,
+                       c->d_val.p, c->nloc, c->gs.dinv.p, (int*)c->d_red.p);
     HIP_OK(hipGetLastError());
     c->gs.ready = 1;
     return 0;
@@ -132,8 +133,9 @@ int prec_apply(iemic_ctx* c, const double* r, double* z)
         return IEMIC_ESTATE;
     }
     if (c->gs.kind == 2) return gs_apply(c, r, z);
-    hipLaunchKernelGGL(k_bj_apply, dim3((unsigned)((c->ncell + 255) / 256)), dim3(256), 0, c->stream,
-                       c->gs.dinv.p, c->ncell, r, z);
+    const int64_t o = NUN * c->own0;
+    hipLaunchKernelGGL(k_bj_apply, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, c->stream,
+                       c->gs.dinv.p, c->nloc, r + o, z + o);
     HIP_OK(hipGetLastError());
     return 0;
 }

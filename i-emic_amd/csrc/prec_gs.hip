@@ -44,10 +44,32 @@ constexpr int S_PW0 = 62, S_PWM = 63;               /* P row: W(k), W(k-1)      
 constexpr int S_TT0 = 64, S_TS0 = 81;               /* T row: T self, S self            */
 constexpr int S_SS0 = 84, S_ST0 = 101;              /* S row: S self, T self            */
 
-__device__ __forceinline__ int64_t cidx(int i, int j, int k, int n, int m)
+/* band layout seen by the kernels (stencil.h ext layout); per-cell arrays are indexed by
+ * ext cell, the Jacobian by owned cell (ext cell - own0) */
+struct Lay {
+    int n, m, l, periodic, jb0;
+    int64_t nloc, own0;
+};
+__device__ __forceinline__ int64_t ecell(const Lay& L, int i, int j, int k)
 {
-    return ((int64_t)k * m + j) * n + i;
+    return (((int64_t)j - L.jb0 + HALO) * L.l + k) * L.n + i;
 }
+__device__ __forceinline__ void lc_ijk(const Lay& L, int64_t lc, int& i, int& j, int& k)
+{
+    i = (int)(lc % L.n);
+    k = (int)((lc / L.n) % L.l);
+    j = L.jb0 + (int)(lc / ((int64_t)L.n * L.l));
+}
+#define LAY_ALIASES const int n = L.n, m = L.m, l = L.l, periodic = L.periodic; (void)n; (void)m; (void)l; (void)periodic
+/* thread -> owned cell: lc (Jacobian column), cell (ext), (i, j, k) */
+#define OWNED_CELL                                                                       \
+    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;                   \
+    if (lc >= L.nloc) return;                                                            \
+    const int64_t cell = L.own0 + lc;                                                    \
+    const int64_t ncell = L.nloc;                                                        \
+    int i, j, k;                                                                         \
+    lc_ijk(L, lc, i, j, k);                                                              \
+    (void)i; (void)j; (void)k; (void)ncell
 /* wrap / reject a horizontal neighbour; returns false when outside the domain */
 __device__ __forceinline__ bool hnb(int& i, int& j, int n, int m, int periodic)
 {
@@ -62,15 +84,14 @@ __device__ __forceinline__ bool hnb(int& i, int& j, int n, int m, int periodic)
 /* ---- structure ------------------------------------------------------------------- */
 
 /* identity rows: diagonal slot exactly 1, every other slot exactly 0 */
-__global__ void k_known(const double* __restrict__ val, int64_t ncell, int64_t rowintcon,
+__global__ void k_known(const double* __restrict__ val, Lay L, int64_t rowintcon,
                         uint8_t* __restrict__ known)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    OWNED_CELL;
     for (int r = 0; r < NUN; r++) {
-        bool id = val[(int64_t)ROW_BEGIN[r] * ncell + cell] == 1.0;
+        bool id = val[(int64_t)ROW_BEGIN[r] * ncell + lc] == 1.0;
         for (int s = ROW_BEGIN[r] + 1; id && s < ROW_BEGIN[r + 1]; s++)
-            id = val[(int64_t)s * ncell + cell] == 0.0;
+            id = val[(int64_t)s * ncell + lc] == 0.0;
         known[NUN * cell + r] = (id && NUN * cell + r != rowintcon) ? 1 : 0;
     }
 }
@@ -95,13 +116,12 @@ __device__ __forceinline__ void inv2(double a, double b, double c, double d, boo
 
 /* per-cell factors: U/V and T/S 2x2 inverses, depth-integration weight of the P row */
 __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                               int64_t ncell, int64_t rowintcon, int int_sign,
+                               Lay L, int64_t rowintcon, int int_sign,
                                const double* __restrict__ intc, double* __restrict__ uvinv,
-                               double* __restrict__ tsinv, double* __restrict__ pw, int n, int m)
+                               double* __restrict__ tsinv, double* __restrict__ pw)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    auto V = [&](int s) { return val[(int64_t)s * ncell + cell]; };
+    OWNED_CELL;
+    auto V = [&](int s) { return val[(int64_t)s * ncell + lc]; };
     const uint8_t* kn = known + NUN * cell;
     inv2(V(S_UU0), V(S_UV0), V(S_VU0), V(S_VV0), !kn[UU], !kn[VV], uvinv + 4 * cell);
     double sdiag = V(S_SS0), sofft = V(S_ST0);
@@ -114,8 +134,7 @@ __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __
      * the row's own W (or -1/b_k with b_k that of W(k-1) when the own W is an identity) */
     double w = 0.0;
     if (!kn[PP]) {
-        const int64_t nm = (int64_t)n * m;
-        const int k = (int)(cell / nm);
+        const int64_t nm = L.n;                 /* k - 1 is one row of n cells back */
         const bool w_own = !kn[WW];
         const bool w_below = k > 0 && !known[NUN * (cell - nm) + WW];
         if (w_own && V(S_PW0) != 0.0) w = 1.0 / V(S_PW0);
@@ -130,8 +149,9 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
                               const double* __restrict__ uvinv, const double* __restrict__ pw,
                               const int* __restrict__ col_of_ij, const int* __restrict__ ij_of_col,
                               const uint8_t* __restrict__ pinned, int ncol, int bl, int bu,
-                              int n, int m, int l, int periodic, double* __restrict__ band)
+                              Lay L, double* __restrict__ band)
 {
+    LAY_ALIASES;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)ncol * 9) return;
     const int c = (int)(t / 9), o = (int)(t % 9);
@@ -149,12 +169,12 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
         return;
     }
     if (pinned[c2]) return;
-    const int64_t ncell = (int64_t)n * m * l;
+    const int64_t ncell = L.nloc;
     double s = 0.0;
     for (int k = 0; k < l; k++) {
-        const int64_t pc = cidx(i, j, k, n, m);
+        const int64_t pc = ecell(L, i, j, k);
         if (known[NUN * pc + PP]) continue;
-        const int64_t tc = cidx(ti, tj, k, n, m);
+        const int64_t tc = ecell(L, ti, tj, k);
         if (known[NUN * tc + PP]) continue;
         double acc = 0.0;
         /* corners q = (i+a, j+b), a,b in {0,-1}; P row slot index q4 = (0,0),(-1,0),(0,-1),(-1,-1) */
@@ -164,17 +184,17 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
             if (e < 0 || e > 1 || f < 0 || f > 1) continue;
             int qi = i + a, qj = j + b;
             if (!hnb(qi, qj, n, m, periodic)) continue;
-            const int64_t qc = cidx(qi, qj, k, n, m);
+            const int64_t qc = ecell(L, qi, qj, k);
             const bool ua = !known[NUN * qc + UU], va = !known[NUN * qc + VV];
             if (!ua && !va) continue;
-            const double du = ua ? val[(int64_t)(S_PU + q4) * ncell + pc] : 0.0;
-            const double dv = va ? val[(int64_t)(S_PV + q4) * ncell + pc] : 0.0;
+            const double du = ua ? val[(int64_t)(S_PU + q4) * ncell + (pc - L.own0)] : 0.0;
+            const double dv = va ? val[(int64_t)(S_PV + q4) * ncell + (pc - L.own0)] : 0.0;
             const double* Di = uvinv + 4 * qc;
             const double yu = du * Di[0] + dv * Di[2];
             const double yv = du * Di[1] + dv * Di[3];
             const int g4 = e + 2 * f;                      /* (0,0),(1,0),(0,1),(1,1) */
-            const double gu = ua ? val[(int64_t)(S_UP + g4) * ncell + qc] : 0.0;
-            const double gv = va ? val[(int64_t)(S_VP + g4) * ncell + qc] : 0.0;
+            const double gu = ua ? val[(int64_t)(S_UP + g4) * ncell + (qc - L.own0)] : 0.0;
+            const double gv = va ? val[(int64_t)(S_VP + g4) * ncell + (qc - L.own0)] : 0.0;
             acc += yu * gu + yv * gv;
         }
         s += pw[pc] * acc;
@@ -400,12 +420,10 @@ __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__
 /* z = r on identity rows; rr = r - A(:, known) r(known) on the others (slot bitmask) */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const uint64_t* __restrict__ kmask, const double* __restrict__ r,
-                        double* __restrict__ z, double* __restrict__ rr, int n, int m, int l,
-                        int periodic)
+                        double* __restrict__ z, double* __restrict__ rr, Lay L)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    LAY_ALIASES;
+    OWNED_CELL;
     double acc[NUN];
 #pragma unroll
     for (int R = 0; R < NUN; R++) {
@@ -415,7 +433,6 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     }
     uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
     if (b[0] | b[1]) {
-        const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
         for (int h = 0; h < 2; h++)
             while (b[h]) {
                 const int s = 64 * h + __builtin_ctzll(b[h]);
@@ -425,8 +442,8 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
                 int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
                 const int kk = k + SLOTS[s].dk;
                 hnb(ii, jj, n, m, periodic);
-                const int64_t col = NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var;
-                acc[R] -= val[(int64_t)s * ncell + cell] * r[col];
+                const int64_t col = NUN * ecell(L, ii, jj, kk) + SLOTS[s].var;
+                acc[R] -= val[(int64_t)s * ncell + lc] * r[col];
             }
     }
 #pragma unroll
@@ -439,21 +456,20 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
 /* per cell: bitmask of the slots (104 bits) through which an active row couples to an
  * identity-row column (coast, sea floor, rigid lid); empty for most interior cells */
 __global__ void k_knownmask(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                            uint64_t* __restrict__ kmask, int n, int m, int l, int periodic)
+                            uint64_t* __restrict__ kmask, Lay L, int jb1)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    LAY_ALIASES;
+    OWNED_CELL;
     uint64_t b0 = 0, b1 = 0;
     int R = 0;
     for (int s = 0; s < NSLOT; s++) {
         while (s >= ROW_BEGIN[R + 1]) R++;
-        if (known[NUN * cell + R] || val[(int64_t)s * ncell + cell] == 0.0) continue;
+        if (known[NUN * cell + R] || val[(int64_t)s * ncell + lc] == 0.0) continue;
         int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
         const int kk = k + SLOTS[s].dk;
         if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-        if (known[NUN * cidx(ii, jj, kk, n, m) + SLOTS[s].var]) {
+        if (jj < L.jb0 || jj >= jb1) continue;   /* other rank's unknown: dropped (block Jacobi) */
+        if (known[NUN * ecell(L, ii, jj, kk) + SLOTS[s].var]) {
             if (s < 64) b0 |= (uint64_t)1 << s;
             else b1 |= (uint64_t)1 << (s - 64);
         }
@@ -467,13 +483,10 @@ __global__ void k_knownmask(const double* __restrict__ val, const uint8_t* __res
  * k-1, k+1; zero where the column is an identity row, outside, or the row is inactive. */
 constexpr int TS_NC = 16;
 __global__ void k_ts_compact(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                             double* __restrict__ tsoff, int n, int m, int l, int periodic,
-                             int64_t rowintcon)
+                             double* __restrict__ tsoff, Lay L, int64_t next, int64_t rowintcon)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    LAY_ALIASES;
+    OWNED_CELL;
     for (int R = TT; R <= SS; R++) {
         const int base = ROW_BEGIN[R];
         const int other = R == TT ? SS : TT;
@@ -487,32 +500,38 @@ __global__ void k_ts_compact(const double* __restrict__ val, const uint8_t* __re
                 int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
                 const int kk = k + SLOTS[s].dk;
                 if (kk >= 0 && kk < l && hnb(ii, jj, n, m, periodic) &&
-                    !known[NUN * cidx(ii, jj, kk, n, m) + (q < 6 ? R : other)])
-                    v = val[(int64_t)s * ncell + cell];
+                    !known[NUN * ecell(L, ii, jj, kk) + (q < 6 ? R : other)])
+                    v = val[(int64_t)s * ncell + lc];
             }
-            tsoff[(int64_t)((R - TT) * 8 + q) * ncell + cell] = v;
+            tsoff[(int64_t)((R - TT) * 8 + q) * next + cell] = v;
         }
     }
 }
 
 /* 1. hydrostatic rows top-down: ptil (stored in z at the P rows) */
+/* column kernels: one thread per (i, j) of the band, i fastest (lanes read adjacent cells) */
+#define BAND_COLUMN                                                                      \
+    const int t_ = blockIdx.x * blockDim.x + threadIdx.x;                                \
+    if (t_ >= (int)(L.nloc / L.l)) return;                                               \
+    const int ij = L.jb0 * L.n + t_;                                                     \
+    const int i = ij % L.n, j = ij / L.n;                                                \
+    const int64_t ncell = L.nloc
+
 __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restrict__ known,
                           const int* __restrict__ col_of_ij, const double* __restrict__ rr,
-                          double* __restrict__ z, int n, int m, int l)
+                          double* __restrict__ z, Lay L)
 {
-    /* one thread per water column, (i,j) in memory order so that lanes read adjacent cells */
-    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ij >= n * m || col_of_ij[ij] < 0) return;
-    const int64_t ncell = (int64_t)n * m * l;
-    const int i = ij % n, j = ij / n;
+    LAY_ALIASES;
+    BAND_COLUMN;
+    if (col_of_ij[ij] < 0) return;
     double pabove = 0.0;
     for (int k = l - 1; k >= 0; k--) {
-        const int64_t cell = cidx(i, j, k, n, m);
+        const int64_t cell = ecell(L, i, j, k);
         const bool pa = !known[NUN * cell + PP];
         double p = 0.0;
         if (pa && k < l - 1 && !known[NUN * cell + WW]) {
-            const double g0 = val[(int64_t)S_WP0 * ncell + cell];
-            const double g1 = val[(int64_t)S_WP1 * ncell + cell];
+            const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
+            const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
             if (g0 != 0.0) p = (rr[NUN * cell + WW] - g1 * pabove) / g0;
         }
         if (pa) z[NUN * cell + PP] = p;
@@ -523,15 +542,17 @@ __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restr
 /* sum over the 4 P corners of a U/V point of G * p(P)  (U row slots 20..23 / V 42..45) */
 __device__ __forceinline__ void guv_p(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                       const double* __restrict__ pv, int64_t pstride, int i, int j,
-                                      int k, int64_t cell, int n, int m, int periodic,
-                                      int64_t ncell, double& gu, double& gv,
+                                      int k, int64_t lc, const Lay& L, double& gu, double& gv,
                                       const int* __restrict__ col_of_ij)
 {
+    const int n = L.n, m = L.m, periodic = L.periodic;
+    const int64_t ncell = L.nloc;
+    const int64_t cell = lc;
     gu = gv = 0.0;
     for (int g4 = 0; g4 < 4; g4++) {
         int pi = i + (g4 & 1), pj = j + ((g4 >> 1) & 1);
         if (!hnb(pi, pj, n, m, periodic)) continue;
-        const int64_t pc = cidx(pi, pj, k, n, m);
+        const int64_t pc = ecell(L, pi, pj, k);
         if (known[NUN * pc + PP]) continue;
         double p;
         if (col_of_ij) {            /* column value (pbar) */
@@ -549,16 +570,13 @@ __device__ __forceinline__ void guv_p(const double* __restrict__ val, const uint
 /* 2. uv* = D^-1 (rr_uv - Guv ptil)  (stored in z at the U/V rows) */
 __global__ void k_gs_uvs(const double* __restrict__ val, const uint8_t* __restrict__ known,
                          const double* __restrict__ uvinv, const double* __restrict__ rr,
-                         double* __restrict__ z, int n, int m, int l, int periodic)
+                         double* __restrict__ z, Lay L)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    OWNED_CELL;
     const bool ua = !known[NUN * cell + UU], va = !known[NUN * cell + VV];
     if (!ua && !va) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
     double gu, gv;
-    guv_p(val, known, z, NUN, i, j, k, cell, n, m, periodic, ncell, gu, gv, nullptr);
+    guv_p(val, known, z, NUN, i, j, k, lc, L, gu, gv, nullptr);
     const double ru = ua ? rr[NUN * cell + UU] - gu : 0.0;
     const double rv = va ? rr[NUN * cell + VV] - gv : 0.0;
     const double* D = uvinv + 4 * cell;
@@ -567,15 +585,18 @@ __global__ void k_gs_uvs(const double* __restrict__ val, const uint8_t* __restri
 }
 
 /* Duv uv at a P cell: sum over the 4 U/V corners (P row slots 54..61) */
+/* pl: owned index (Jacobian column) of the P cell */
 __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                          const double* __restrict__ z, int i, int j, int k,
-                                         int64_t pc, int n, int m, int periodic, int64_t ncell)
+                                         int64_t pl, const Lay& L)
 {
+    const int n = L.n, m = L.m, periodic = L.periodic;
+    const int64_t ncell = L.nloc, pc = pl;
     double acc = 0.0;
     for (int q4 = 0; q4 < 4; q4++) {
         int qi = i - (q4 & 1), qj = j - ((q4 >> 1) & 1);
         if (!hnb(qi, qj, n, m, periodic)) continue;
-        const int64_t qc = cidx(qi, qj, k, n, m);
+        const int64_t qc = ecell(L, qi, qj, k);
         if (!known[NUN * qc + UU]) acc += val[(int64_t)(S_PU + q4) * ncell + pc] * z[NUN * qc + UU];
         if (!known[NUN * qc + VV]) acc += val[(int64_t)(S_PV + q4) * ncell + pc] * z[NUN * qc + VV];
     }
@@ -587,26 +608,22 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
  * gives the continuity right-hand side rr_p - Duv uv used by the W sweep. */
 __global__ void k_gs_pcell(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ pw, const double* __restrict__ rr,
-                           const double* __restrict__ z, double* __restrict__ t, int n, int m,
-                           int l, int periodic, int mode)
+                           const double* __restrict__ z, double* __restrict__ t, Lay L, int mode)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    OWNED_CELL;
     if (known[NUN * cell + PP]) { t[cell] = 0.0; return; }
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
-    const double d = duv_uv(val, known, z, i, j, k, cell, n, m, periodic, ncell);
+    const double d = duv_uv(val, known, z, i, j, k, lc, L);
     t[cell] = mode == 0 ? pw[cell] * (d - rr[NUN * cell + PP]) : rr[NUN * cell + PP] - d;
 }
 __global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ col_of_ij,
-                          const uint8_t* __restrict__ pinned, double* __restrict__ rhs, int nm, int l)
+                          const uint8_t* __restrict__ pinned, double* __restrict__ rhs, Lay L)
 {
-    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ij >= nm) return;
+    BAND_COLUMN;
+    (void)ncell;
     const int c = col_of_ij[ij];
     if (c < 0) return;
     double s = 0.0;
-    for (int k = 0; k < l; k++) s += t[(int64_t)k * nm + ij];
+    for (int k = 0; k < L.l; k++) s += t[ecell(L, i, j, k)];
     rhs[c] = pinned[c] ? 0.0 : s;
 }
 
@@ -635,17 +652,13 @@ __global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int 
 /* 4. uv = uv* - D^-1 Guv Mz1^T pbar */
 __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ uvinv, const int* __restrict__ col_of_ij,
-                           const double* __restrict__ pbar, double* __restrict__ z, int n, int m,
-                           int l, int periodic)
+                           const double* __restrict__ pbar, double* __restrict__ z, Lay L)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    OWNED_CELL;
     const bool ua = !known[NUN * cell + UU], va = !known[NUN * cell + VV];
     if (!ua && !va) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
     double gu, gv;
-    guv_p(val, known, pbar, 0, i, j, k, cell, n, m, periodic, ncell, gu, gv, col_of_ij);
+    guv_p(val, known, pbar, 0, i, j, k, lc, L, gu, gv, col_of_ij);
     if (!ua) gu = 0.0;
     if (!va) gv = 0.0;
     const double* D = uvinv + 4 * cell;
@@ -656,25 +669,22 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
 /* 4b/5. p = ptil + pbar; continuity rows bottom-up for w (top P row excluded) */
 __global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const int* __restrict__ col_of_ij, const double* __restrict__ pbar,
-                        const double* __restrict__ crhs, double* __restrict__ z, int n, int m,
-                        int l)
+                        const double* __restrict__ crhs, double* __restrict__ z, Lay L)
 {
-    const int ij = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ij >= n * m) return;
+    LAY_ALIASES;
+    BAND_COLUMN;
     const int c = col_of_ij[ij];
     if (c < 0) return;
-    const int64_t ncell = (int64_t)n * m * l;
-    const int i = ij % n, j = ij / n;
     const double pb = pbar[c];
     double wbelow = 0.0;
     for (int k = 0; k < l; k++) {
-        const int64_t cell = cidx(i, j, k, n, m);
+        const int64_t cell = ecell(L, i, j, k);
         const bool pa = !known[NUN * cell + PP], wa = !known[NUN * cell + WW];
         if (pa) z[NUN * cell + PP] += pb;
         double w = 0.0;
         if (pa && wa) {
-            const double a = val[(int64_t)S_PW0 * ncell + cell];
-            const double b = val[(int64_t)S_PWM * ncell + cell];
+            const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
+            const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
             const double rhs = crhs[cell];
             if (a != 0.0) w = (rhs - b * wbelow) / a;
             z[NUN * cell + WW] = w;
@@ -688,12 +698,10 @@ __global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restric
 /* 6a. T/S right-hand side: rr_ts - B_ts,(u,v,w) z;  z_ts = 0 */
 __global__ void k_gs_bts(const double* __restrict__ val, const uint8_t* __restrict__ known,
                          const double* __restrict__ rr, double* __restrict__ z, double* __restrict__ bts,
-                         int n, int m, int l, int periodic)
+                         Lay L)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    LAY_ALIASES;
+    OWNED_CELL;
     for (int R = TT; R <= SS; R++) {
         const int64_t row = NUN * cell + R;
         if (known[row]) continue;
@@ -701,12 +709,12 @@ __global__ void k_gs_bts(const double* __restrict__ val, const uint8_t* __restri
         for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
             const int var = SLOTS[s].var;
             if (var == TT || var == SS) continue;
-            const double v = val[(int64_t)s * ncell + cell];
+            const double v = val[(int64_t)s * ncell + lc];
             if (v == 0.0) continue;
             int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
             const int kk = k + SLOTS[s].dk;
             if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-            const int64_t col = NUN * cidx(ii, jj, kk, n, m) + var;
+            const int64_t col = NUN * ecell(L, ii, jj, kk) + var;
             if (!known[col]) acc -= v * z[col];
         }
         bts[row] = acc;
@@ -714,26 +722,25 @@ __global__ void k_gs_bts(const double* __restrict__ val, const uint8_t* __restri
     }
 }
 
-/* colour of a cell for the T/S sweeps: parity of i+j+k; on a periodic grid with odd n
- * the wrap pairs (n-1, 0) would share a colour, so column i = n-1 gets colours 2/3 */
+/* colour of a cell for the T/S sweeps: parity of i+j+k (global j); on a periodic grid with
+ * odd n the wrap pairs (n-1, 0) would share a colour, so column i = n-1 gets colours 2/3 */
 __device__ __forceinline__ int ts_color(int i, int j, int k, int n, int periodic)
 {
     if (periodic && (n & 1) && i == n - 1) return 2 + ((j + k) & 1);
     return (i + j + k) & 1;
 }
 
-/* 6b. one red-black half sweep on the T/S block with 2x2 cell blocks (compact couplings) */
+/* 6b. one red-black half sweep on the T/S block with 2x2 cell blocks (compact couplings;
+ * generic layout, used for odd n) */
 __global__ void __launch_bounds__(256) k_gs_ts_half(const double* __restrict__ tsoff,
                                                     const uint8_t* __restrict__ known,
                                                     const double* __restrict__ tsinv,
                                                     const double* __restrict__ bts,
-                                                    double* __restrict__ z, int n, int m, int l,
-                                                    int periodic, int color)
+                                                    double* __restrict__ z, Lay L, int64_t next,
+                                                    int color)
 {
-    const int64_t ncell = (int64_t)n * m * l;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    LAY_ALIASES;
+    OWNED_CELL;
     if (ts_color(i, j, k, n, periodic) != color) return;
     const bool ta = !known[NUN * cell + TT], sa = !known[NUN * cell + SS];
     if (!ta && !sa) return;
@@ -743,18 +750,18 @@ __global__ void __launch_bounds__(256) k_gs_ts_half(const double* __restrict__ t
     else { if (im < 0) im = i; if (ip >= n) ip = i; }
     const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
     const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
-    const int64_t nb[6] = {cidx(im, j, k, n, m), cidx(ip, j, k, n, m), cidx(i, jm, k, n, m),
-                           cidx(i, jp, k, n, m), cidx(i, j, km, n, m), cidx(i, j, kp, n, m)};
+    const int64_t nb[6] = {ecell(L, im, j, k), ecell(L, ip, j, k), ecell(L, i, jm, k),
+                           ecell(L, i, jp, k), ecell(L, i, j, km), ecell(L, i, j, kp)};
     double res[2];
 #pragma unroll
     for (int R = 0; R < 2; R++) {
         const int var = TT + R, oth = SS - R;
-        const double* a = tsoff + (int64_t)(R * 8) * ncell + cell;
+        const double* a = tsoff + (int64_t)(R * 8) * next + cell;
         double acc = bts[NUN * cell + var];
 #pragma unroll
-        for (int q = 0; q < 6; q++) acc -= a[(int64_t)q * ncell] * z[NUN * nb[q] + var];
-        acc -= a[(int64_t)6 * ncell] * z[NUN * nb[4] + oth];
-        acc -= a[(int64_t)7 * ncell] * z[NUN * nb[5] + oth];
+        for (int q = 0; q < 6; q++) acc -= a[(int64_t)q * next] * z[NUN * nb[q] + var];
+        acc -= a[(int64_t)6 * next] * z[NUN * nb[4] + oth];
+        acc -= a[(int64_t)7 * next] * z[NUN * nb[5] + oth];
         res[R] = acc;
     }
     const double* D = tsinv + 4 * cell;
@@ -762,20 +769,19 @@ __global__ void __launch_bounds__(256) k_gs_ts_half(const double* __restrict__ t
     if (sa) z[NUN * cell + SS] = D[2] * res[0] + D[3] * res[1];
 }
 
-/* Even n: the cells of one colour are cell = 2q + ((j+k+c)&1), q = cell >> 1, so every
- * per-cell T/S array can be stored per colour and read contiguously by a half sweep.
- * tsc[(c*16 + e)*half + q] couplings, tic[(c*4 + e)*half + q] 2x2 inverses,
- * bc[(c*2 + v)*half + q] right-hand sides; zt / zs: T and S iterates, natural order. */
+/* Even n: the owned cells of one colour are lc = 2q + ((j+k+c)&1) (lc = (row)*n + i with
+ * row = (j-jb0)*l + k), so every per-cell T/S array can be stored per colour and read
+ * contiguously by a half sweep:  tsc[(c*16 + e)*half + q] couplings,
+ * tic[(c*4 + e)*half + q] 2x2 inverses, bc[(c*2 + v)*half + q] right-hand sides;
+ * zt / zs: T and S iterates by ext cell (halo entries stay 0). */
 __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __restrict__ tsinv,
-                          double* __restrict__ tsc, double* __restrict__ tic, int n, int m, int l)
+                          double* __restrict__ tsc, double* __restrict__ tic, Lay L, int64_t next)
 {
-    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    OWNED_CELL;
+    const int64_t half = ncell / 2;
     const int c = (i + j + k) & 1;
-    const int64_t q = cell >> 1;
-    for (int e = 0; e < TS_NC; e++) tsc[(int64_t)(c * TS_NC + e) * half + q] = tsoff[(int64_t)e * ncell + cell];
+    const int64_t q = lc >> 1;
+    for (int e = 0; e < TS_NC; e++) tsc[(int64_t)(c * TS_NC + e) * half + q] = tsoff[(int64_t)e * next + cell];
     for (int e = 0; e < 4; e++) tic[(int64_t)(c * 4 + e) * half + q] = tsinv[4 * cell + e];
 }
 
@@ -783,12 +789,11 @@ __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __rest
 __global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ rr, const double* __restrict__ z,
                            double* __restrict__ bc, double* __restrict__ zt, double* __restrict__ zs,
-                           int n, int m, int l, int periodic)
+                           Lay L)
 {
-    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
-    const int i = (int)(cell % n), j = (int)((cell / n) % m), k = (int)(cell / ((int64_t)n * m));
+    LAY_ALIASES;
+    OWNED_CELL;
+    const int64_t half = ncell / 2;
     const int c = (i + j + k) & 1;
     for (int R = TT; R <= SS; R++) {
         const int64_t row = NUN * cell + R;
@@ -798,16 +803,16 @@ __global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __rest
             for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
                 const int var = SLOTS[s].var;
                 if (var == TT || var == SS) continue;
-                const double v = val[(int64_t)s * ncell + cell];
+                const double v = val[(int64_t)s * ncell + lc];
                 if (v == 0.0) continue;
                 int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
                 const int kk = k + SLOTS[s].dk;
                 if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-                const int64_t col = NUN * cidx(ii, jj, kk, n, m) + var;
+                const int64_t col = NUN * ecell(L, ii, jj, kk) + var;
                 if (!known[col]) acc -= v * z[col];
             }
         }
-        bc[(int64_t)(c * 2 + (R - TT)) * half + (cell >> 1)] = acc;
+        bc[(int64_t)(c * 2 + (R - TT)) * half + (lc >> 1)] = acc;
     }
     zt[cell] = 0.0;
     zs[cell] = 0.0;
@@ -817,22 +822,24 @@ __global__ void __launch_bounds__(256) k_gs_ts_half_c(const double* __restrict__
                                                       const double* __restrict__ tic,
                                                       const double* __restrict__ bc,
                                                       double* __restrict__ zt, double* __restrict__ zs,
-                                                      int n, int m, int l, int periodic, int c)
+                                                      Lay L, int c)
 {
-    const int64_t ncell = (int64_t)n * m * l, half = ncell / 2;
+    LAY_ALIASES;
+    const int64_t half = L.nloc / 2;
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= half) return;
-    const int64_t row = (2 * q) / n;
-    const int j = (int)(row % m), k = (int)(row / m);
-    const int64_t cell = 2 * q + ((j + k + c) & 1);
-    const int i = (int)(cell - row * n);
+    const int64_t row = (2 * q) / n;                 /* (j - jb0) * l + k */
+    const int k = (int)(row % l), j = L.jb0 + (int)(row / l);
+    const int64_t lc = 2 * q + ((j + k + c) & 1);
+    const int i = (int)(lc - row * n);
+    const int64_t cell = L.own0 + lc;
     int im = i - 1, ip = i + 1;
     if (periodic) { if (im < 0) im = n - 1; if (ip >= n) ip = 0; }
     else { if (im < 0) im = i; if (ip >= n) ip = i; }
-    const int64_t nm = (int64_t)n * m;
+    const int64_t ln = (int64_t)l * n;
     const int64_t base = cell - i;
-    const int64_t nb[6] = {base + im, base + ip, j > 0 ? cell - n : cell, j < m - 1 ? cell + n : cell,
-                           k > 0 ? cell - nm : cell, k < l - 1 ? cell + nm : cell};
+    const int64_t nb[6] = {base + im, base + ip, j > 0 ? cell - ln : cell, j < m - 1 ? cell + ln : cell,
+                           k > 0 ? cell - n : cell, k < l - 1 ? cell + n : cell};
     const double* a = tsc + (int64_t)(c * TS_NC) * half + q;
     double rt = bc[(int64_t)(c * 2) * half + q], rs = bc[(int64_t)(c * 2 + 1) * half + q];
 #pragma unroll
@@ -849,10 +856,9 @@ __global__ void __launch_bounds__(256) k_gs_ts_half_c(const double* __restrict__
 
 /* z(T,S) = zt, zs on the active rows */
 __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __restrict__ zt,
-                             const double* __restrict__ zs, double* __restrict__ z, int64_t ncell)
+                             const double* __restrict__ zs, double* __restrict__ z, Lay L)
 {
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= ncell) return;
+    OWNED_CELL;
     if (!known[NUN * cell + TT]) z[NUN * cell + TT] = zt[cell];
     if (!known[NUN * cell + SS]) z[NUN * cell + SS] = zs[cell];
 }
@@ -864,17 +870,18 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
     BlockGS& gs = c->gs;
     const int n = c->n, m = c->m, l = c->l;
     const int periodic = c->cfg.periodic;
-    auto cellof = [&](int i, int j, int k) { return ((int64_t)k * m + j) * n + i; };
-    /* water columns: any active P */
+    auto cellof = [&](int i, int j, int k) { return c->su.ext_cell(i, j, k); };
+    /* water columns of the band: any active P (the Schur complement is rank-local:
+     * block Jacobi across latitude bands) */
     std::vector<int> colid((size_t)n * m, -1);
     std::vector<uint8_t> act((size_t)n * m, 0);
-    for (int j = 0; j < m; j++)
+    for (int j = c->jb0; j < c->jb1; j++)
         for (int i = 0; i < n; i++)
             for (int k = 0; k < l; k++)
                 if (!kn[NUN * cellof(i, j, k) + PP]) { act[(size_t)j * n + i] = 1; break; }
     /* U/V point (i,j) active at any level */
     std::vector<uint8_t> uva((size_t)n * m, 0);
-    for (int j = 0; j < m; j++)
+    for (int j = c->jb0; j < c->jb1; j++)
         for (int i = 0; i < n; i++)
             for (int k = 0; k < l; k++) {
                 const int64_t cc = cellof(i, j, k);
@@ -901,7 +908,7 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
         for (int i = 0; i < n; i++) ipos[i] = i;
     }
     std::vector<std::pair<int64_t, int>> ord;
-    for (int j = 0; j < m; j++)
+    for (int j = c->jb0; j < c->jb1; j++)
         for (int i = 0; i < n; i++)
             if (act[(size_t)j * n + i]) ord.push_back({(int64_t)ipos[i] * m + j, j * n + i});
     std::sort(ord.begin(), ord.end());
@@ -992,59 +999,74 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
 
 }  // namespace
 
+static Lay lay_of(const iemic_ctx* c)
+{
+    Lay L;
+    L.n = c->n; L.m = c->m; L.l = c->l; L.periodic = c->cfg.periodic; L.jb0 = c->jb0;
+    L.nloc = c->nloc; L.own0 = c->own0;
+    return L;
+}
+
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
 {
     BlockGS& gs = c->gs;
     gs.ready = 0;
     gs.ts_sweeps = opt ? std::max(0, opt->ts_sweeps) : 3;
-    const int64_t N = c->nrows, ncell = c->ncell;
+    const int64_t NE = c->nerows, next = c->next;
+    const Lay L = lay_of(c);
     int rc = 0;
-    if (gs.known.n < (size_t)N) {
-        rc |= gs.known.alloc(N);
-        rc |= gs.uvinv.alloc((size_t)4 * ncell);
-        rc |= gs.tsinv.alloc((size_t)4 * ncell);
-        rc |= gs.pw.alloc(ncell);
-        rc |= gs.rr.alloc(N);
-        rc |= gs.bts.alloc(N);
-        rc |= gs.kmask.alloc((size_t)2 * ncell);
-        rc |= gs.tsoff.alloc((size_t)TS_NC * ncell);
-        rc |= gs.tsc.alloc((size_t)TS_NC * ncell);
-        rc |= gs.tic.alloc((size_t)4 * ncell);
-        rc |= gs.bc.alloc((size_t)2 * ncell);
-        rc |= gs.zt.alloc(ncell);
-        rc |= gs.zs.alloc(ncell);
-        rc |= gs.tcell.alloc(ncell);
+    if (gs.known.n < (size_t)NE) {
+        /* per-cell arrays span the ext layout; the halo entries stay 0 (and the halo rows
+         * are identity rows), which is what makes the bands block-Jacobi coupled */
+        rc |= gs.known.alloc(NE);
+        rc |= gs.uvinv.alloc((size_t)4 * next);
+        rc |= gs.tsinv.alloc((size_t)4 * next);
+        rc |= gs.pw.alloc(next);
+        rc |= gs.rr.alloc(NE);
+        rc |= gs.bts.alloc(NE);
+        rc |= gs.kmask.alloc((size_t)2 * next);
+        rc |= gs.tsoff.alloc((size_t)TS_NC * next);
+        rc |= gs.tsc.alloc((size_t)TS_NC * c->nloc);
+        rc |= gs.tic.alloc((size_t)4 * c->nloc);
+        rc |= gs.bc.alloc((size_t)2 * c->nloc);
+        rc |= gs.zt.alloc(next);
+        rc |= gs.zs.alloc(next);
+        rc |= gs.tcell.alloc(next);
         if (rc) {
             set_error("block GS: out of device memory");
             return IEMIC_ENOMEM;
         }
+        for (DevBuf<double>* bptr : {&gs.uvinv, &gs.tsinv, &gs.pw, &gs.rr, &gs.bts, &gs.tsoff, &gs.zt,
+                                     &gs.zs, &gs.tcell})
+            HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
+        HIP_OK(hipMemsetAsync(gs.kmask.p, 0, sizeof(uint64_t) * gs.kmask.n, c->stream));
         gs.known_h.clear();
     }
-    const unsigned gc = (unsigned)((ncell + 255) / 256);
-    hipLaunchKernelGGL(k_known, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, ncell,
+    const unsigned gc = (unsigned)((c->nloc + 255) / 256);
+    HIP_OK(hipMemsetAsync(gs.known.p, 1, NE, c->stream));     /* halo rows: identity */
+    hipLaunchKernelGGL(k_known, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L,
                        (int64_t)c->rowintcon, gs.known.p);
     HIP_OK(hipGetLastError());
-    std::vector<uint8_t> kn(N);
-    if ((rc = d2h(c, kn.data(), gs.known.p, N))) return rc;
+    std::vector<uint8_t> kn(NE);
+    if ((rc = d2h(c, kn.data(), gs.known.p, NE))) return rc;
     if (kn != gs.known_h)
         if ((rc = build_structure(c, kn))) return rc;
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
-                       ncell, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
-                       gs.tsinv.p, gs.pw.p, c->n, c->m);
+                       L, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
+                       gs.tsinv.p, gs.pw.p);
     hipLaunchKernelGGL(k_knownmask, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
-                       gs.kmask.p, c->n, c->m, c->l, c->cfg.periodic);
+                       gs.kmask.p, L, c->jb1);
     hipLaunchKernelGGL(k_ts_compact, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
-                       gs.tsoff.p, c->n, c->m, c->l, c->cfg.periodic, (int64_t)c->rowintcon);
+                       gs.tsoff.p, L, next, (int64_t)c->rowintcon);
     if ((c->n & 1) == 0)
         hipLaunchKernelGGL(k_ts_pack, dim3(gc), dim3(256), 0, c->stream, gs.tsoff.p, gs.tsinv.p,
-                           gs.tsc.p, gs.tic.p, c->n, c->m, c->l);
+                           gs.tsc.p, gs.tic.p, L, next);
     const int W = 2 * gs.bl + gs.bu + 1;
     HIP_OK(hipMemsetAsync(gs.band.p, 0, sizeof(double) * (size_t)gs.ncol * W, c->stream));
     const int64_t nt = (int64_t)gs.ncol * 9;
     hipLaunchKernelGGL(k_schur_build, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream,
                        c->d_val.p, gs.known.p, gs.uvinv.p, gs.pw.p, gs.col_of_ij.p, gs.ij_of_col.p,
-                       gs.pinned.p, gs.ncol, gs.bl, gs.bu, c->n, c->m, c->l, c->cfg.periodic,
-                       gs.band.p);
+                       gs.pinned.p, gs.ncol, gs.bl, gs.bu, L, gs.band.p);
     {
         const size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * NBP + (size_t)NBP * (gs.bl + gs.bu));
         if (lb > 150 * 1024) {
@@ -1099,55 +1121,54 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
 int gs_apply(iemic_ctx* c, const double* r, double* z)
 {
     BlockGS& gs = c->gs;
-    const int n = c->n, m = c->m, l = c->l, per = c->cfg.periodic;
-    const int64_t ncell = c->ncell;
-    const unsigned gc = (unsigned)((ncell + 255) / 256);
-    const unsigned gij = (unsigned)((n * m + 255) / 256);
+    const Lay L = lay_of(c);
+    const int n = c->n;
+    const unsigned gc = (unsigned)((c->nloc + 255) / 256);
+    const unsigned gij = (unsigned)((c->nloc / c->l + 255) / 256);
     hipStream_t s = c->stream;
-    HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nrows, s));
+    HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
-                       r, z, gs.rr.p, n, m, l, per);
+                       r, z, gs.rr.p, L);
     hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.rr.p, z, n, m, l);
+                       gs.rr.p, z, L);
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.rr.p, z, n, m, l, per);
+                       gs.rr.p, z, L);
     hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.rr.p, z, gs.tcell.p, n, m, l, per, 0);
+                       gs.rr.p, z, gs.tcell.p, L, 0);
     hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                       gs.pinned.p, gs.colv.p, n * m, l);
+                       gs.pinned.p, gs.colv.p, L);
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
                        gs.ncol, gs.colv.p, gs.colv2.p);
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.col_of_ij.p, gs.colv2.p, z, n, m, l, per);
+                       gs.col_of_ij.p, gs.colv2.p, z, L);
     hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.rr.p, z, gs.tcell.p, n, m, l, per, 1);
+                       gs.rr.p, z, gs.tcell.p, L, 1);
     hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.colv2.p, gs.tcell.p, z, n, m, l);
+                       gs.colv2.p, gs.tcell.p, z, L);
     const int nsw = std::max(1, gs.ts_sweeps);
     if ((n & 1) == 0) {
         /* colour-compacted symmetric red-black sweeps */
-        const unsigned gh = (unsigned)((ncell / 2 + 255) / 256);
+        const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
         hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                           gs.bc.p, gs.zt.p, gs.zs.p, n, m, l, per);
+                           gs.bc.p, gs.zt.p, gs.zs.p, L);
         const int seq[4] = {0, 1, 1, 0};
         for (int sw = 0; sw < nsw; sw++)
             for (int h = 0; h < 4; h++)
                 hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
-                                   gs.zt.p, gs.zs.p, n, m, l, per, seq[h]);
-        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z,
-                           ncell);
+                                   gs.zt.p, gs.zs.p, L, seq[h]);
+        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
     } else {
         hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                           gs.bts.p, n, m, l, per);
+                           gs.bts.p, L);
         /* symmetric sweeps: colours forward then backward */
-        const bool four = per && (n & 1);
+        const bool four = c->cfg.periodic && (n & 1);
         const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
         const int* seq = four ? seq4 : seq2;
         const int ns = four ? 8 : 4;
         for (int sw = 0; sw < nsw; sw++)
             for (int h = 0; h < ns; h++)
                 hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
-                                   gs.tsinv.p, gs.bts.p, z, n, m, l, per, seq[h]);
+                                   gs.tsinv.p, gs.bts.p, z, L, c->next, seq[h]);
     }
     HIP_OK(hipGetLastError());
     return 0;

@@ -100,8 +100,17 @@ HD constexpr int fortran_rank(int s)
 }
 
 /* ---- per-context geometry (grid.F90, usrc.F90 stpnt/init) ------------------------- */
+/* Internal vector layout ("ext"): cells ordered j-major, (j, k, i) with i fastest, over the
+ * owned latitude band [jb0, jb1) plus HALO rows on each side:
+ *     cell = ((j - jb0 + HALO) * l + k) * n + i,   row = 6 * cell + var   (0-based i,j,k).
+ * A band of j rows is then one contiguous slab, so halo exchanges need no packing, and
+ * the reference's row order (k-major, THCMdefs.H:21) is restored only at the C ABI.
+ * With one GPU the band is the whole grid. */
+constexpr int HALO = 2;
+
 struct Geo {
-    int n, m, l;                    /* local (sub)domain                                */
+    int n, m, l;                    /* global grid                                      */
+    int jb0;                        /* first owned j (0-based)                          */
     int periodic;
     int tres, sres, coriolis_on;
     double dx, dy, dz;
@@ -126,11 +135,21 @@ HD int LM(const Geo& g, int i, int j, int k)
 {
     return g.landm[((int64_t)k * (g.m + 2) + j) * (g.n + 2) + i];
 }
-/* 0-based row of variable v at 1-based (i,j,k) (find_row2, matetc.F90:123) */
+/* internal (ext) row of variable v at 1-based global (i,j,k) */
 HD int64_t frow(const Geo& g, int i, int j, int k, int v)
 {
-    return (int64_t)NUN * (((int64_t)(k - 1) * g.m + (j - 1)) * g.n + (i - 1)) + v;
+    return (int64_t)NUN * ((((int64_t)(j - 1) - g.jb0 + HALO) * g.l + (k - 1)) * g.n + (i - 1)) + v;
 }
+
+/* owned-local cell lc (0 .. n*l*(jb1-jb0)-1) -> 1-based global (i,j,k); its ext cell is
+ * HALO*l*n + lc */
+HD void owned_cell(const Geo& g, int64_t lc, int& i, int& j, int& k)
+{
+    i = (int)(lc % g.n) + 1;
+    k = (int)((lc / g.n) % g.l) + 1;
+    j = g.jb0 + (int)(lc / ((int64_t)g.n * g.l)) + 1;
+}
+HD int64_t own0(const Geo& g) { return (int64_t)HALO * g.l * g.n; }
 
 /* ---- usol (usrc.F90:997-1104): padded staggered state, closed forms ---------------- */
 HD bool land_in(const Geo& g, int i, int j, int k)

@@ -29,6 +29,11 @@ class Grid(C.Structure):
                 ("device", C.c_int)]
 
 
+class Dist(C.Structure):
+    """iemic_dist: latitude-band decomposition over nranks GPUs (RCCL unique id)."""
+    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("id", C.c_ubyte * 128)]
+
+
 class Krylov(C.Structure):
     _fields_ = [("tol", C.c_double), ("krylov_dim", C.c_int), ("max_restarts", C.c_int),
                 ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int)]
@@ -75,6 +80,9 @@ def lib():
     vp = C.c_void_p
     sig = {
         "iemic_create": (C.c_int, [P(vp), P(Grid), PI]),
+        "iemic_create_dist": (C.c_int, [P(vp), P(Grid), PI, P(Dist)]),
+        "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
+        "iemic_layout": (C.c_int, [vp, P64]),
         "iemic_destroy": (None, [vp]),
         "iemic_device_count": (C.c_int, []),
         "iemic_last_error": (C.c_char_p, []),
@@ -108,7 +116,8 @@ def lib():
     return L
 
 
-EXPORTED = ("iemic_create", "iemic_destroy", "iemic_device_count", "iemic_last_error",
+EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
+            "iemic_destroy", "iemic_device_count", "iemic_last_error",
             "iemic_set_par", "iemic_get_par", "iemic_nrows", "iemic_graph_nnz",
             "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",
             "iemic_set_state_dev",

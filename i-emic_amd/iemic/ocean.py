@@ -29,13 +29,22 @@ class Ocean:
     """One THCM ocean model instance on one GPU (Ocean.C:63-213)."""
 
     def __init__(self, cfg: THCMConfig, landm: Optional[np.ndarray] = None, device: int = 0,
-                 analyze_jacobian: bool = True, solver_params: Optional[dict] = None):
+                 analyze_jacobian: bool = True, solver_params: Optional[dict] = None,
+                 rank: int = 0, nranks: int = 1, comm_id: Optional[bytes] = None):
+        """rank/nranks/comm_id: latitude-band decomposition (one Ocean per GPU); comm_id is
+        the RCCL unique id of rank 0 (Ocean.unique_id()), shared by the caller."""
         self.cfg = cfg
         L = landmask(cfg) if landm is None else landm
         L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
         self._grid = _lib.grid_from_config(cfg, device=device, analyze_jacobian=analyze_jacobian)
         h = C.c_void_p()
-        rc = lib().iemic_create(C.byref(h), C.byref(self._grid), ptr(L, C.c_int))
+        if nranks > 1:
+            d = _lib.Dist(rank, nranks)
+            C.memmove(d.id, comm_id, 128)
+            rc = lib().iemic_create_dist(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
+                                         C.byref(d))
+        else:
+            rc = lib().iemic_create(C.byref(h), C.byref(self._grid), ptr(L, C.c_int))
         check(rc, "iemic_create")
         self._h = h
         self.N = lib().iemic_nrows(h)
@@ -52,6 +61,19 @@ class Ocean:
         self._F = np.zeros(self.N)
         self._sol = np.zeros(self.N)
         self.last_solve = None
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """RCCL unique id for a multi-GPU Ocean (call on rank 0, broadcast the bytes)."""
+        buf = (C.c_ubyte * 128)()
+        check(lib().iemic_comm_unique_id(buf), "iemic_comm_unique_id")
+        return bytes(buf)
+
+    def layout(self) -> dict:
+        out = np.zeros(7, dtype=np.int64)
+        check(lib().iemic_layout(self._h, ptr(out, C.c_int64)), "iemic_layout")
+        return dict(ext_rows=int(out[0]), own_first=int(out[1]), own_rows=int(out[2]),
+                    jb0=int(out[3]), jb1=int(out[4]), rank=int(out[5]), nranks=int(out[6]))
 
     # ---- lifecycle -----------------------------------------------------------------
     def close(self):

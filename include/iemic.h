@@ -80,12 +80,26 @@ typedef struct {
     int reorth;                  /* DGKS second passes taken                         */
 } iemic_solve_info;
 
+/* Latitude-band decomposition over several GPUs (one process and one context per GPU,
+ * RCCL over xGMI).  `id` is an RCCL unique id from iemic_comm_unique_id on
+ * rank 0, broadcast by the caller (e.g. torch.distributed).  Rank r owns latitude rows
+ * [r*m/P, (r+1)*m/P) with all columns and levels; vectors passed to the host-pointer entry
+ * points are full reference-ordered global vectors of which each rank reads / writes its
+ * owned rows. */
+typedef struct {
+    int rank, nranks;
+    unsigned char id[128];
+} iemic_dist;
+
 /* ---- lifecycle ---------------------------------------------------------------------- */
 /* landm: (n+2)(m+2)(l+2) ints, i fastest, the global mask m_global::get_landm returns
  * (THCM.C:391).  The context applies init_'s border handling (usrc.F90:83-107), builds
  * grid metrics, stpnt parameters, forcing and the maximal graph, and (if requested)
  * runs the Ocean mask-fix cycle (Ocean.C:496-569, analyzeJacobian1). */
 int  iemic_create(iemic_ctx** ctx, const iemic_grid* grid, const int* landm);
+int  iemic_create_dist(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
+                       const iemic_dist* dist);
+int  iemic_comm_unique_id(unsigned char* id128);
 void iemic_destroy(iemic_ctx* ctx);
 int  iemic_device_count(void);
 const char* iemic_last_error(void);
@@ -99,11 +113,16 @@ int     iemic_nrows(const iemic_ctx* ctx);
 int64_t iemic_graph_nnz(const iemic_ctx* ctx);       /* Epetra maximal-graph nnz       */
 int     iemic_rowintcon(const iemic_ctx* ctx);       /* -1 when SRES != 0              */
 int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local mask   */
+/* internal vector layout of the _dev entry points: out[0] ext length (rows), out[1] first
+ * owned row, out[2] owned rows, out[3..4] owned latitude band [jb0, jb1), out[5] rank,
+ * out[6] nranks.  Internally cells are ordered (j, k, i), i fastest, with 2 halo rows. */
+int     iemic_layout(const iemic_ctx* ctx, int64_t* out);
 
 /* ---- state ------------------------------------------------------------------------ */
 int iemic_set_state(iemic_ctx* ctx, const double* x);     /* host -> device state     */
 int iemic_get_state(iemic_ctx* ctx, double* x);
-/* device -> device state copy on the library stream (x_dev: N doubles in HBM) */
+/* device -> device state copy on the library stream (x_dev: N doubles in HBM, reference
+ * order, the global vector) */
 int iemic_set_state_dev(iemic_ctx* ctx, const double* x_dev);
 
 /* ---- assembly (THCM::evaluate, THCM.C:949-1192) --------------------------------- */
@@ -115,14 +134,15 @@ int iemic_export_csr(iemic_ctx* ctx, int64_t* rowptr, int* col, double* val);
 
 /* ---- operators (Epetra_Operator Apply / ApplyInverse) --------------------------- */
 int iemic_spmv(iemic_ctx* ctx, const double* x, double* y);          /* y = J x     */
-int iemic_spmv_dev(iemic_ctx* ctx, const double* x, double* y, void* stream);
+/* x, y: device vectors in the internal layout (iemic_layout); x's halo rows are updated */
+int iemic_spmv_dev(iemic_ctx* ctx, double* x, double* y, void* stream);
 int iemic_prec_compute(iemic_ctx* ctx, const iemic_krylov* opt);    /* factor once */
 int iemic_prec_apply(iemic_ctx* ctx, const double* r, double* z);
 
 /* ---- linear solve J x = b (Ocean::solve) ---------------------------------------- */
 int iemic_solve(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* opt,
                 iemic_solve_info* info);
-/* device-resident variant: b, x are device pointers of length nrows */
+/* device-resident variant: b, x are device vectors in the internal layout (iemic_layout) */
 int iemic_solve_dev(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* opt,
                     iemic_solve_info* info);
 

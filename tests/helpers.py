@@ -64,26 +64,33 @@ def mask_fix(orc, cfg, L, max_fix: int = 5):
 
 
 class Emul:
-    """ctypes wrapper of tests/emul/stencil_emul.cpp."""
+    """ctypes wrapper of tests/emul/stencil_emul.cpp (one latitude band, default: all)."""
 
-    def __init__(self, cfg, landm):
+    def __init__(self, cfg, landm, jb0: int = 0, jb1: int = -1):
         lib = C.CDLL(EMUL_LIB)
-        lib.emul_create.restype = C.c_void_p
-        lib.emul_create.argtypes = [P(_lib.Grid), P(C.c_int)]
-        lib.emul_destroy.argtypes = [C.c_void_p]
-        lib.emul_set_par.argtypes = [C.c_void_p, C.c_int, C.c_double]
-        lib.emul_jacobian.argtypes = [C.c_void_p] + [P(C.c_double)] * 3
-        lib.emul_rhs.argtypes = [C.c_void_p] + [P(C.c_double)] * 2
+        vp = C.c_void_p
+        lib.emul_create_band.restype = vp
+        lib.emul_create_band.argtypes = [P(_lib.Grid), P(C.c_int), C.c_int, C.c_int]
+        lib.emul_destroy.argtypes = [vp]
+        lib.emul_set_par.argtypes = [vp, C.c_int, C.c_double]
+        lib.emul_ext_rows.restype = C.c_int64
+        lib.emul_ext_rows.argtypes = [vp]
+        lib.emul_jacobian_ext.argtypes = [vp, P(C.c_double), P(C.c_double)]
+        lib.emul_rhs_ext.argtypes = [vp, P(C.c_double), P(C.c_double), P(C.c_double)]
         lib.emul_to_csr.restype = C.c_int64
-        lib.emul_to_csr.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int64), P(C.c_int),
-                                    P(C.c_double)]
+        lib.emul_to_csr.argtypes = [vp, P(C.c_int64), P(C.c_int), P(C.c_double)]
+        lib.emul_ref_to_ext.argtypes = [vp, P(C.c_double), P(C.c_double)]
+        lib.emul_ext_to_ref.argtypes = [vp, P(C.c_double), P(C.c_double)]
         self.lib = lib
         self.cfg = cfg
         g = _lib.grid_from_config(cfg, analyze_jacobian=False)
         L = np.ascontiguousarray(landm.reshape(-1), dtype=np.int32)
-        self.h = lib.emul_create(C.byref(g), _lib.ptr(L, C.c_int))
+        self.h = lib.emul_create_band(C.byref(g), _lib.ptr(L, C.c_int), jb0, jb1)
         for idx, v in cfg.par_list():
             lib.emul_set_par(self.h, idx, v)
+        self.ext_rows = lib.emul_ext_rows(self.h)
+        self.jb0 = jb0
+        self.jb1 = cfg.m if jb1 < 0 else jb1
 
     def __del__(self):
         try:
@@ -91,22 +98,47 @@ class Emul:
         except Exception:
             pass
 
-    def jacobian_csr(self, x):
-        c = self.cfg
-        slots = np.zeros(104 * c.ncell)
-        B = np.zeros(c.nrows)
-        x = np.ascontiguousarray(x, dtype=np.float64)
-        self.lib.emul_jacobian(self.h, _lib.ptr(x), _lib.ptr(slots), _lib.ptr(B))
-        nnz = self.lib.emul_to_csr(self.h, _lib.ptr(slots), None, None, None)
-        rowptr = np.zeros(c.nrows + 1, dtype=np.int64)
+    # layout -------------------------------------------------------------------------
+    def to_ext(self, x_ref, ext=None):
+        ext = np.zeros(self.ext_rows) if ext is None else ext
+        self.lib.emul_ref_to_ext(self.h, _lib.ptr(np.ascontiguousarray(x_ref, dtype=np.float64)),
+                                 _lib.ptr(ext))
+        return ext
+
+    def to_ref(self, ext, ref=None):
+        ref = np.zeros(self.cfg.nrows) if ref is None else ref
+        self.lib.emul_ext_to_ref(self.h, _lib.ptr(ext), _lib.ptr(ref))
+        return ref
+
+    # band-level (ext) calls -----------------------------------------------------------
+    def jacobian_ext(self, xe):
+        Be = np.zeros(self.ext_rows)
+        self.lib.emul_jacobian_ext(self.h, _lib.ptr(xe), _lib.ptr(Be))
+        return Be
+
+    def csr(self):
+        nnz = self.lib.emul_to_csr(self.h, None, None, None)
+        nrow = 6 * self.cfg.n * self.cfg.l * (self.jb1 - self.jb0)
+        rowptr = np.zeros(nrow + 1, dtype=np.int64)
         col = np.zeros(nnz, dtype=np.int32)
         val = np.zeros(nnz)
-        self.lib.emul_to_csr(self.h, _lib.ptr(slots), _lib.ptr(rowptr, C.c_int64),
-                             _lib.ptr(col, C.c_int), _lib.ptr(val))
-        return rowptr, col, val, B
+        self.lib.emul_to_csr(self.h, _lib.ptr(rowptr, C.c_int64), _lib.ptr(col, C.c_int),
+                             _lib.ptr(val))
+        return rowptr, col, val
+
+    def rhs_ext(self, xe):
+        Fe = np.zeros(self.ext_rows)
+        part = C.c_double()
+        self.lib.emul_rhs_ext(self.h, _lib.ptr(xe), _lib.ptr(Fe), C.byref(part))
+        return Fe, part.value
+
+    # whole-grid convenience (reference order in and out) -------------------------------
+    def jacobian_csr(self, x):
+        xe = self.to_ext(x)
+        Be = self.jacobian_ext(xe)
+        rowptr, col, val = self.csr()
+        return rowptr, col, val, self.to_ref(Be)
 
     def rhs(self, x):
-        F = np.zeros(self.cfg.nrows)
-        x = np.ascontiguousarray(x, dtype=np.float64)
-        self.lib.emul_rhs(self.h, _lib.ptr(x), _lib.ptr(F))
-        return F
+        Fe, _ = self.rhs_ext(self.to_ext(x))
+        return self.to_ref(Fe)
