@@ -128,8 +128,26 @@ extern "C" int iemic_comm_unique_id(unsigned char* id128)
     return comm_unique_id(id128);
 }
 
+static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm,
+                       const iemic_dist* dist, void* group, int grank, int granks);
+
 extern "C" int iemic_create_dist(iemic_ctx** out, const iemic_grid* grid, const int* landm,
                                  const iemic_dist* dist)
+{
+    return create_impl(out, grid, landm, dist, nullptr, 0, 1);
+}
+
+extern "C" void* iemic_local_group_new(int nranks) { return local_group_new(nranks); }
+extern "C" void iemic_local_group_free(void* group) { local_group_free(group); }
+extern "C" int iemic_create_local(iemic_ctx** out, const iemic_grid* grid, const int* landm,
+                                  void* group, int rank, int nranks)
+{
+    if (!group) return IEMIC_EINVAL;
+    return create_impl(out, grid, landm, nullptr, group, rank, nranks);
+}
+
+static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm,
+                       const iemic_dist* dist, void* group, int grank, int granks)
 {
     if (!out || !grid || !landm) return IEMIC_EINVAL;
     *out = nullptr;
@@ -146,7 +164,8 @@ extern "C" int iemic_create_dist(iemic_ctx** out, const iemic_grid* grid, const 
         set_error("iemic_create: grid too small");
         return IEMIC_EINVAL;
     }
-    const int rank = dist ? dist->rank : 0, nranks = dist ? dist->nranks : 1;
+    const int rank = group ? grank : dist ? dist->rank : 0;
+    const int nranks = group ? granks : dist ? dist->nranks : 1;
     if (nranks < 1 || rank < 0 || rank >= nranks) {
         set_error("iemic_create: bad rank / nranks");
         return IEMIC_EINVAL;
@@ -182,7 +201,8 @@ extern "C" int iemic_create_dist(iemic_ctx** out, const iemic_grid* grid, const 
     c->own0 = c->su.own0();
     c->rowintcon = c->su.rowintcon;
     int rc = 0;
-    if (nranks > 1 && (rc = comm_init(c, dist->id, rank, nranks))) {
+    if (group) local_group_join(c, group);
+    else if (nranks > 1 && (rc = comm_init(c, dist->id, rank, nranks))) {
         delete c;
         return rc;
     }

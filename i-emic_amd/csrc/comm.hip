@@ -10,7 +10,10 @@
  */
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "common.h"
 
@@ -24,6 +27,82 @@ namespace iemic {
             return IEMIC_EDEVICE;                                                        \
         }                                                                                \
     } while (0)
+
+/* ---- in-process group (test facility) ------------------------------------------------
+ * Several band contexts of one problem in one process (one host thread each, e.g. on one
+ * GPU, where RCCL refuses duplicate devices): collectives are host-staged through a shared
+ * object with a reusable barrier.  Sums are taken in rank order, so results do not depend
+ * on thread timing. */
+struct LocalGroup {
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, generation = 0;
+    std::vector<std::vector<double>> slot;
+    std::vector<double*> vec;
+    std::vector<iemic_ctx*> ctxs;
+    explicit LocalGroup(int p) : P(p), slot(p), vec(p, nullptr), ctxs(p, nullptr) {}
+    void barrier()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        const int gen = generation;
+        if (++arrived == P) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+    }
+};
+
+static int local_allreduce(iemic_ctx* c, double* dev, int count)
+{
+    LocalGroup* g = (LocalGroup*)c->group;
+    auto& mine = g->slot[c->rank];
+    mine.resize(count);
+    int rc = d2h(c, mine.data(), dev, sizeof(double) * count);
+    if (rc) return rc;
+    g->barrier();
+    std::vector<double> sum(count, 0.0);
+    for (int r = 0; r < g->P; r++)
+        for (int q = 0; q < count; q++) sum[q] += g->slot[r][q];
+    g->barrier();
+    return h2d(c, dev, sum.data(), sizeof(double) * count);
+}
+
+static int local_halo(iemic_ctx* c, double* v, int rows_j)
+{
+    LocalGroup* g = (LocalGroup*)c->group;
+    const int64_t slab = (int64_t)NUN * c->l * c->n, cnt = slab * rows_j;
+    const int64_t own_first = (int64_t)NUN * c->own0, own_end = own_first + c->nlrows;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    g->vec[c->rank] = v;
+    g->barrier();
+    /* neighbours' ext vectors have the same halo depth; their owned rows start at HALO */
+    if (c->rank > 0) {
+        /* lower halo <- last rows of rank-1's band; rank-1 owns the band below: its owned end */
+        iemic_ctx* nb = g->ctxs[c->rank - 1];
+        const double* src = g->vec[c->rank - 1] + (int64_t)NUN * nb->own0 + nb->nlrows - cnt;
+        HIP_OK(hipMemcpyAsync(v + own_first - cnt, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (c->rank < g->P - 1) {
+        iemic_ctx* nb = g->ctxs[c->rank + 1];
+        const double* src = g->vec[c->rank + 1] + (int64_t)NUN * nb->own0;
+        HIP_OK(hipMemcpyAsync(v + own_end, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    g->barrier();
+    return 0;
+}
+
+void* local_group_new(int nranks) { return nranks > 0 ? new LocalGroup(nranks) : nullptr; }
+void local_group_free(void* g) { delete (LocalGroup*)g; }
+void local_group_join(iemic_ctx* c, void* g)
+{
+    c->group = g;
+    ((LocalGroup*)g)->ctxs[c->rank] = c;
+}
 
 int comm_unique_id(unsigned char* id128)
 {
@@ -54,6 +133,7 @@ void comm_destroy(iemic_ctx* c)
 int allreduce_sum(iemic_ctx* c, double* dev, int count)
 {
     if (c->nranks <= 1 || count <= 0) return 0;
+    if (c->group) return local_allreduce(c, dev, count);
     NCCL_OK(ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)c->comm,
                           c->stream));
     return 0;
@@ -63,6 +143,7 @@ int allreduce_sum(iemic_ctx* c, double* dev, int count)
 int halo_exchange(iemic_ctx* c, double* v, int rows_j)
 {
     if (c->nranks <= 1) return 0;
+    if (c->group) return local_halo(c, v, rows_j);
     const int64_t slab = (int64_t)NUN * c->l * c->n;          /* doubles per latitude row */
     const int64_t cnt = slab * rows_j;
     const int64_t own_first = (int64_t)NUN * c->own0;          /* first owned row          */

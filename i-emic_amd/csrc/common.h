@@ -105,6 +105,7 @@ struct iemic_ctx {
     int64_t own0 = 0;                /* ext cell of the first owned cell                  */
     int64_t rowintcon = -1;          /* ext row of the integral condition if owned        */
     void* comm = nullptr;            /* ncclComm_t when nranks > 1                        */
+    void* group = nullptr;           /* in-process band group (test facility), else null  */
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
     iemic::DevBuf<int> d_landm;
@@ -159,6 +160,9 @@ int allreduce_sum(iemic_ctx* c, double* dev, int count);
 int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
 int comm_unique_id(unsigned char* id128);
+void* local_group_new(int nranks);
+void local_group_free(void* g);
+void local_group_join(iemic_ctx* c, void* g);
 void comm_destroy(iemic_ctx* c);
 
 /* assembly.hip */

@@ -83,6 +83,9 @@ def lib():
         "iemic_create_dist": (C.c_int, [P(vp), P(Grid), PI, P(Dist)]),
         "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
         "iemic_layout": (C.c_int, [vp, P64]),
+        "iemic_local_group_new": (vp, [C.c_int]),
+        "iemic_local_group_free": (None, [vp]),
+        "iemic_create_local": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int]),
         "iemic_destroy": (None, [vp]),
         "iemic_device_count": (C.c_int, []),
         "iemic_last_error": (C.c_char_p, []),
@@ -117,6 +120,7 @@ def lib():
 
 
 EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
+            "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",
             "iemic_set_par", "iemic_get_par", "iemic_nrows", "iemic_graph_nnz",
             "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",

@@ -30,7 +30,8 @@ class Ocean:
 
     def __init__(self, cfg: THCMConfig, landm: Optional[np.ndarray] = None, device: int = 0,
                  analyze_jacobian: bool = True, solver_params: Optional[dict] = None,
-                 rank: int = 0, nranks: int = 1, comm_id: Optional[bytes] = None):
+                 rank: int = 0, nranks: int = 1, comm_id: Optional[bytes] = None,
+                 local_group=None):
         """rank/nranks/comm_id: latitude-band decomposition (one Ocean per GPU); comm_id is
         the RCCL unique id of rank 0 (Ocean.unique_id()), shared by the caller."""
         self.cfg = cfg
@@ -38,7 +39,10 @@ class Ocean:
         L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
         self._grid = _lib.grid_from_config(cfg, device=device, analyze_jacobian=analyze_jacobian)
         h = C.c_void_p()
-        if nranks > 1:
+        if local_group is not None:
+            rc = lib().iemic_create_local(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
+                                          local_group, rank, nranks)
+        elif nranks > 1:
             d = _lib.Dist(rank, nranks)
             C.memmove(d.id, comm_id, 128)
             rc = lib().iemic_create_dist(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),

@@ -100,6 +100,13 @@ int  iemic_create(iemic_ctx** ctx, const iemic_grid* grid, const int* landm);
 int  iemic_create_dist(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
                        const iemic_dist* dist);
 int  iemic_comm_unique_id(unsigned char* id128);
+/* Test facility: the bands of one problem as contexts of one process (one host thread
+ * each, all on `grid->device`), collectives host-staged through `group`.  Used to check
+ * the band decomposition on a single GPU, where RCCL refuses duplicate devices. */
+void* iemic_local_group_new(int nranks);
+void  iemic_local_group_free(void* group);
+int   iemic_create_local(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
+                         void* group, int rank, int nranks);
 void iemic_destroy(iemic_ctx* ctx);
 int  iemic_device_count(void);
 const char* iemic_last_error(void);
