@@ -71,11 +71,11 @@ static int local_allreduce(iemic_ctx* c, double* dev, int count)
     return h2d(c, dev, sum.data(), sizeof(double) * count);
 }
 
-static int local_halo(iemic_ctx* c, double* v, int rows_j)
+static int local_halo(iemic_ctx* c, double* v, int width, int rows_j)
 {
     LocalGroup* g = (LocalGroup*)c->group;
-    const int64_t slab = (int64_t)NUN * c->l * c->n, cnt = slab * rows_j;
-    const int64_t own_first = (int64_t)NUN * c->own0, own_end = own_first + c->nlrows;
+    const int64_t slab = (int64_t)width * c->l * c->n, cnt = slab * rows_j;
+    const int64_t own_first = (int64_t)width * c->own0, own_end = own_first + (int64_t)width * c->nloc;
     HIP_OK(hipStreamSynchronize(c->stream));
     g->vec[c->rank] = v;
     g->barrier();
@@ -83,12 +83,12 @@ static int local_halo(iemic_ctx* c, double* v, int rows_j)
     if (c->rank > 0) {
         /* lower halo <- last rows of rank-1's band; rank-1 owns the band below: its owned end */
         iemic_ctx* nb = g->ctxs[c->rank - 1];
-        const double* src = g->vec[c->rank - 1] + (int64_t)NUN * nb->own0 + nb->nlrows - cnt;
+        const double* src = g->vec[c->rank - 1] + (int64_t)width * (nb->own0 + nb->nloc) - cnt;
         HIP_OK(hipMemcpyAsync(v + own_first - cnt, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
     }
     if (c->rank < g->P - 1) {
         iemic_ctx* nb = g->ctxs[c->rank + 1];
-        const double* src = g->vec[c->rank + 1] + (int64_t)NUN * nb->own0;
+        const double* src = g->vec[c->rank + 1] + (int64_t)width * nb->own0;
         HIP_OK(hipMemcpyAsync(v + own_end, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
     }
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -139,15 +139,16 @@ int allreduce_sum(iemic_ctx* c, double* dev, int count)
     return 0;
 }
 
-/* exchange rows_j (<= HALO) latitude rows with the neighbouring bands */
-int halo_exchange(iemic_ctx* c, double* v, int rows_j)
+/* exchange rows_j (<= HALO) latitude rows of a per-cell array (width doubles per ext
+ * cell) with the neighbouring bands */
+int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
 {
     if (c->nranks <= 1) return 0;
-    if (c->group) return local_halo(c, v, rows_j);
-    const int64_t slab = (int64_t)NUN * c->l * c->n;          /* doubles per latitude row */
+    if (c->group) return local_halo(c, v, width, rows_j);
+    const int64_t slab = (int64_t)width * c->l * c->n;        /* doubles per latitude row */
     const int64_t cnt = slab * rows_j;
-    const int64_t own_first = (int64_t)NUN * c->own0;          /* first owned row          */
-    const int64_t own_end = own_first + c->nlrows;             /* one past the last owned  */
+    const int64_t own_first = (int64_t)width * c->own0;        /* first owned cell         */
+    const int64_t own_end = own_first + (int64_t)width * c->nloc; /* one past the last     */
     ncclComm_t comm = (ncclComm_t)c->comm;
     NCCL_OK(ncclGroupStart());
     if (c->rank > 0) {
@@ -161,5 +162,8 @@ int halo_exchange(iemic_ctx* c, double* v, int rows_j)
     NCCL_OK(ncclGroupEnd());
     return 0;
 }
+
+/* state-vector halo (NUN doubles per cell) */
+int halo_exchange(iemic_ctx* c, double* v, int rows_j) { return halo_exchange_w(c, v, NUN, rows_j); }
 
 }  // namespace iemic

@@ -59,8 +59,12 @@ struct BlockGS {
     int ts_sweeps = 3;               /* symmetric red-black sweeps on the T/S block     */
     DevBuf<double> dinv;             /* block-Jacobi: 6x6 inverses, slot-major          */
     /* structure (rebuilt when the identity-row pattern changes) */
-    std::vector<uint8_t> known_h;    /* identity rows the structure was built for       */
+    std::vector<double> flags_h;     /* global (active column, U/V point) flags the      */
+                                     /* structure was built for                         */
     int ncol = 0, bl = 0, bu = 0;    /* active water columns, Schur band widths          */
+    int ncol_own = 0;                /* columns of this band (inverse slab width)       */
+    DevBuf<int> own_cols;            /* their Schur indices, ascending                  */
+    DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8), halo-filled */
     DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
     DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index (band order) or -1       */
     DevBuf<int> ij_of_col;           /* Schur index -> j*n+i                            */
@@ -75,8 +79,8 @@ struct BlockGS {
     DevBuf<double> band;             /* Schur band, row-wise, width 2*bl+bu+1           */
     DevBuf<int> piv, info;
     DevBuf<double> lpan;             /* band-LU panel multipliers                       */
-    DevBuf<double> sinv;             /* dense Schur inverse, ncol x ncol row-major      */
-    DevBuf<double> rr, bts, colv, colv2; /* work                                         */
+    DevBuf<double> sinv;             /* Schur inverse columns of this band, ncol x ncol_own */
+    DevBuf<double> rr, bts, colv, colv2, colv_own; /* work                               */
 };
 
 struct Krylov {
@@ -158,6 +162,7 @@ struct StreamGuard {
 /* comm.hip: sums over the ranks (no-op for one rank) and halo exchange of the ext layout */
 int allreduce_sum(iemic_ctx* c, double* dev, int count);
 int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
+int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int rows_j);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
 int comm_unique_id(unsigned char* id128);
 void* local_group_new(int nranks);

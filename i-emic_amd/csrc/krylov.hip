@@ -686,7 +686,9 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     inf.reorth = inf_reorth;
     inf.implicit_rel_res = res;
     inf.explicit_rel_res = std::sqrt(std::max(0.0, e2)) / bnorm;
-    inf.converged = res <= opt->tol;
+    /* converged: the Givens estimate reached the tolerance and the true residual agrees
+     * with it (a loss of orthogonality shows up as a gap between the two) */
+    inf.converged = res <= opt->tol && inf.explicit_rel_res <= 2.0 * opt->tol;
     inf.t_total_ms = ms_since(T0);
     HIP_OK(hipGetLastError());
     if (info) *info = inf;

@@ -144,12 +144,16 @@ __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __
     pw[cell] = w;
 }
 
-/* Schur entry S[c][c'] for c' = column (i+di, j+dj), written into the band (row-wise) */
+/* Schur entry S[c][c'] for c' = column (i+di, j+dj), written into the band (row-wise).
+ * Only the rows of this band's columns are built (the bands' rows are summed over the
+ * ranks afterwards); corner U/V points one latitude row below the band are read from the
+ * halo-filled per-cell arrays (known, uvinv, gslot). */
 __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                              const double* __restrict__ uvinv, const double* __restrict__ pw,
+                              const double* __restrict__ uvinv, const double* __restrict__ gslot,
+                              const double* __restrict__ pw,
                               const int* __restrict__ col_of_ij, const int* __restrict__ ij_of_col,
                               const uint8_t* __restrict__ pinned, int ncol, int bl, int bu,
-                              Lay L, double* __restrict__ band)
+                              Lay L, int jb1, double* __restrict__ band)
 {
     LAY_ALIASES;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -158,6 +162,7 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
     const int di = o % 3 - 1, dj = o / 3 - 1;
     const int ij = ij_of_col[c];
     const int i = ij % n, j = ij / n;
+    if (j < L.jb0 || j >= jb1) return;
     int ti = i + di, tj = j + dj;
     if (!hnb(ti, tj, n, m, periodic)) return;
     const int c2 = col_of_ij[tj * n + ti];
@@ -193,13 +198,37 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
             const double yu = du * Di[0] + dv * Di[2];
             const double yv = du * Di[1] + dv * Di[3];
             const int g4 = e + 2 * f;                      /* (0,0),(1,0),(0,1),(1,1) */
-            const double gu = ua ? val[(int64_t)(S_UP + g4) * ncell + (qc - L.own0)] : 0.0;
-            const double gv = va ? val[(int64_t)(S_VP + g4) * ncell + (qc - L.own0)] : 0.0;
+            const double gu = ua ? gslot[8 * qc + g4] : 0.0;
+            const double gv = va ? gslot[8 * qc + 4 + g4] : 0.0;
             acc += yu * gu + yv * gv;
         }
         s += pw[pc] * acc;
     }
     row[c2 - c + bl] += s;
+}
+
+/* per owned cell: the U and V rows' couplings to the 4 P corners (slots 20..23, 42..45) */
+__global__ void k_gslot_pack(const double* __restrict__ val, Lay L, double* __restrict__ gslot)
+{
+    OWNED_CELL;
+    for (int g = 0; g < 4; g++) {
+        gslot[8 * cell + g] = val[(int64_t)(S_UP + g) * ncell + lc];
+        gslot[8 * cell + 4 + g] = val[(int64_t)(S_VP + g) * ncell + lc];
+    }
+}
+
+/* identity-row flags <-> doubles (for the halo exchange of the flags) */
+__global__ void k_u8_to_d(const uint8_t* __restrict__ a, double* __restrict__ b, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x)
+        b[q] = a[q];
+}
+__global__ void k_d_to_u8(const double* __restrict__ b, uint8_t* __restrict__ a, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x)
+        a[q] = b[q] != 0.0 ? 1 : 0;
 }
 
 /* Band LU with partial pivoting (LAPACK gbtrf semantics), one workgroup of 1024 threads,
@@ -334,25 +363,29 @@ __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int n
     if (tid == 0) *info = s_info;
 }
 
-/* Columns [c0, c0+NB) of the inverse, X = U^-1 L^-1 P, one workgroup of 256 threads per
- * block of NB right-hand sides (unit vectors).  Thread t owns column t % NB and every
- * 256/NB-th row of the active window; the window lives in LDS as a ring buffer:
- *   forward  (P, L^-1): rows k..k+bl      y is written to X (row-major, ncol x ncol)
+/* Columns cols[q0 .. q0+NB) of the inverse, X = U^-1 L^-1 P, one workgroup of 256
+ * threads per block of NB right-hand sides (unit vectors); cols ascending.  Column q of
+ * the slab is X[row * nq + q] (row-major ncol x nq).  Thread t owns slab column t % NB
+ * and every 256/NB-th row of the active window; the window lives in LDS as a ring buffer:
+ *   forward  (P, L^-1): rows k..k+bl      y is written to X
  *   backward (U^-1)   : rows i+1..i+bl+bu x overwrites y in X
  * Two barriers per elimination step; the factors are read from L2. */
 template <int NB>
 __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__ ab,
                                                       const double* __restrict__ lpan,
                                                       const int* __restrict__ piv, int ncol,
-                                                      int bl, int bu, double* __restrict__ X)
+                                                      int bl, int bu, const int* __restrict__ cols,
+                                                      int nq, double* __restrict__ Xs)
 {
     extern __shared__ double lds[];
     constexpr int G = 256 / NB;              /* row groups */
     const int W = 2 * bl + bu + 1;
     const int col = threadIdx.x % NB, grp = threadIdx.x / NB;
-    const int c0 = blockIdx.x * NB;
-    const int c = c0 + col;
-    const bool on = c < ncol;
+    const int q0 = blockIdx.x * NB;
+    const int q = q0 + col;
+    const bool on = q < nq;
+    const int c0 = cols[q0];
+    const int c = on ? cols[q] : -1;
     double* red = lds;                       /* G x NB partial sums */
     double* win = lds + G * NB;              /* ring buffer         */
     /* ---- forward, panel by panel: ring of R1 = bl + NBP + 1 rows ---- */
@@ -385,14 +418,14 @@ __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__
         }
         /* rows k0 .. k0+nbk-1 are final: y -> X; bring in the rows of the next panel */
         for (int t = grp; t < nbk; t += G)
-            if (on) X[(int64_t)(k0 + t) * ncol + c] = win[((k0 + t) % R1) * NB + col];
+            if (on) Xs[(int64_t)(k0 + t) * nq + q] = win[((k0 + t) % R1) * NB + col];
         __syncthreads();
         for (int r = pend + 1 + grp; r <= min(k0 + 2 * NBP - 1 + bl, ncol - 1); r += G)
             win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
     }
     /* rows above the first panel are zero in y */
     if (grp == 0 && on)
-        for (int r = 0; r < kst; r++) X[(int64_t)r * ncol + c] = 0.0;
+        for (int r = 0; r < kst; r++) Xs[(int64_t)r * nq + q] = 0.0;
     /* ---- backward: ring of R2 = bl + bu + 1 rows holding x(i+1 .. i+bl+bu) ---- */
     const int R2 = bl + bu + 1;
     __syncthreads();
@@ -406,10 +439,10 @@ __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__
         if (grp == 0) {
             double t = 0.0;
             for (int g2 = 0; g2 < G; g2++) t += red[g2 * NB + col];
-            const double y = on ? X[(int64_t)i * ncol + c] : 0.0;
+            const double y = on ? Xs[(int64_t)i * nq + q] : 0.0;
             const double x = (y - t) / ar[i];
             win[(i % R2) * NB + col] = x;
-            if (on) X[(int64_t)i * ncol + c] = x;
+            if (on) Xs[(int64_t)i * nq + q] = x;
         }
         __syncthreads();
     }
@@ -468,7 +501,7 @@ __global__ void k_knownmask(const double* __restrict__ val, const uint8_t* __res
         int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
         const int kk = k + SLOTS[s].dk;
         if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-        if (jj < L.jb0 || jj >= jb1) continue;   /* other rank's unknown: dropped (block Jacobi) */
+        if (jj < L.jb0 - 1 || jj > jb1) continue;   /* beyond the exchanged halo row */
         if (known[NUN * ecell(L, ii, jj, kk) + SLOTS[s].var]) {
             if (s < 64) b0 |= (uint64_t)1 << s;
             else b1 |= (uint64_t)1 << (s - 64);
@@ -627,26 +660,34 @@ __global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ 
     rhs[c] = pinned[c] ? 0.0 : s;
 }
 
-/* 3b. y = X b, one wavefront per row */
-__global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int nr,
+/* 3b. y = X b (X row-major nr x nc), one wavefront per row */
+__global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int nr, int nc,
                                               const double* __restrict__ b, double* __restrict__ y)
 {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= nr) return;
-    const double* xr = X + (int64_t)row * nr;
+    const double* xr = X + (int64_t)row * nc;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     int c = lane;
-    for (; c + 192 < nr; c += 256) {
+    for (; c + 192 < nc; c += 256) {
         s0 += xr[c] * b[c];
         s1 += xr[c + 64] * b[c + 64];
         s2 += xr[c + 128] * b[c + 128];
         s3 += xr[c + 192] * b[c + 192];
     }
-    for (; c < nr; c += 64) s0 += xr[c] * b[c];
+    for (; c < nc; c += 64) s0 += xr[c] * b[c];
     double s = (s0 + s1) + (s2 + s3);
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     if (lane == 0) y[row] = s;
+}
+
+/* b_own[q] = b[cols[q]] */
+__global__ void k_gather(const double* __restrict__ b, const int* __restrict__ cols, int nq,
+                         double* __restrict__ bo)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) bo[q] = b[cols[q]];
 }
 
 /* 4. uv = uv* - D^-1 Guv Mz1^T pbar */
@@ -865,28 +906,33 @@ __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __
 
 /* ---- host: structure from the identity-row pattern ------------------------------ */
 
-int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
+/* flags[j*n+i] = 1 for an active water column (any active P), flags[n*m + j*n+i] = 1
+ * for an active U/V point, over the band's latitude rows */
+static void band_flags(const iemic_ctx* c, const std::vector<uint8_t>& kn, std::vector<double>& flags)
 {
-    BlockGS& gs = c->gs;
     const int n = c->n, m = c->m, l = c->l;
-    const int periodic = c->cfg.periodic;
-    auto cellof = [&](int i, int j, int k) { return c->su.ext_cell(i, j, k); };
-    /* water columns of the band: any active P (the Schur complement is rank-local:
-     * block Jacobi across latitude bands) */
-    std::vector<int> colid((size_t)n * m, -1);
-    std::vector<uint8_t> act((size_t)n * m, 0);
-    for (int j = c->jb0; j < c->jb1; j++)
-        for (int i = 0; i < n; i++)
-            for (int k = 0; k < l; k++)
-                if (!kn[NUN * cellof(i, j, k) + PP]) { act[(size_t)j * n + i] = 1; break; }
-    /* U/V point (i,j) active at any level */
-    std::vector<uint8_t> uva((size_t)n * m, 0);
+    flags.assign((size_t)2 * n * m, 0.0);
     for (int j = c->jb0; j < c->jb1; j++)
         for (int i = 0; i < n; i++)
             for (int k = 0; k < l; k++) {
-                const int64_t cc = cellof(i, j, k);
-                if (!kn[NUN * cc + UU] || !kn[NUN * cc + VV]) { uva[(size_t)j * n + i] = 1; break; }
+                const int64_t cc = c->su.ext_cell(i, j, k);
+                if (!kn[NUN * cc + PP]) flags[(size_t)j * n + i] = 1.0;
+                if (!kn[NUN * cc + UU] || !kn[NUN * cc + VV]) flags[(size_t)n * m + j * n + i] = 1.0;
             }
+}
+
+/* Schur structure of the whole grid from the global flags (identical on every rank) */
+int build_structure(iemic_ctx* c, const std::vector<double>& flags)
+{
+    BlockGS& gs = c->gs;
+    const int n = c->n, m = c->m;
+    const int periodic = c->cfg.periodic;
+    std::vector<int> colid((size_t)n * m, -1);
+    std::vector<uint8_t> act((size_t)n * m, 0), uva((size_t)n * m, 0);
+    for (size_t q = 0; q < (size_t)n * m; q++) {
+        act[q] = flags[q] != 0.0;
+        uva[q] = flags[(size_t)n * m + q] != 0.0;
+    }
     auto wrap = [&](int& i, int& j) {
         if (j < 0 || j >= m) return false;
         if (i < 0 || i >= n) {
@@ -908,7 +954,7 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
         for (int i = 0; i < n; i++) ipos[i] = i;
     }
     std::vector<std::pair<int64_t, int>> ord;
-    for (int j = c->jb0; j < c->jb1; j++)
+    for (int j = 0; j < m; j++)
         for (int i = 0; i < n; i++)
             if (act[(size_t)j * n + i]) ord.push_back({(int64_t)ipos[i] * m + j, j * n + i});
     std::sort(ord.begin(), ord.end());
@@ -968,11 +1014,19 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
             }
         }
     }
-    if ((int64_t)ncol * ncol > (int64_t)4 << 30) {
+    if ((int64_t)ncol * std::max<int64_t>(1, ncol / std::max(1, c->nranks)) > (int64_t)4 << 30) {
         set_error("block GS: too many water columns for the dense Schur inverse");
         return IEMIC_EINVAL;
     }
+    std::vector<int> own;
+    for (int q = 0; q < ncol; q++) {
+        const int j = ij_of_col[q] / n;
+        if (j >= c->jb0 && j < c->jb1) own.push_back(q);
+    }
+    const int nq = std::max(1, (int)own.size());
+    if (own.empty()) own.push_back(0);     /* keeps the kernels' shapes valid; b_own = 0 */
     gs.ncol = ncol;
+    gs.ncol_own = (int)own.size();
     gs.bl = gs.bu = std::max(bw, 1);
     const int W = 2 * gs.bl + gs.bu + 1;
     int rc = 0;
@@ -983,9 +1037,11 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
     rc |= gs.piv.alloc(ncol);
     rc |= gs.lpan.alloc((size_t)((ncol + NBP - 1) / NBP) * (NBP + gs.bl) * NBP);
     rc |= gs.info.alloc(1);
-    rc |= gs.sinv.alloc((size_t)ncol * ncol);
+    rc |= gs.sinv.alloc((size_t)ncol * nq);
     rc |= gs.colv.alloc(ncol);
     rc |= gs.colv2.alloc(ncol);
+    rc |= gs.colv_own.alloc(nq);
+    rc |= gs.own_cols.alloc(nq);
     if (rc) {
         set_error("block GS: out of device memory");
         return IEMIC_ENOMEM;
@@ -993,7 +1049,8 @@ int build_structure(iemic_ctx* c, const std::vector<uint8_t>& kn)
     if ((rc = h2d(c, gs.col_of_ij.p, colid.data(), sizeof(int) * colid.size()))) return rc;
     if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * ncol))) return rc;
     if ((rc = h2d(c, gs.pinned.p, pin.data(), ncol))) return rc;
-    gs.known_h = kn;
+    if ((rc = h2d(c, gs.own_cols.p, own.data(), sizeof(int) * own.size()))) return rc;
+    gs.flags_h = flags;
     return 0;
 }
 
@@ -1040,20 +1097,48 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                                      &gs.zs, &gs.tcell})
             HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         HIP_OK(hipMemsetAsync(gs.kmask.p, 0, sizeof(uint64_t) * gs.kmask.n, c->stream));
-        gs.known_h.clear();
+        gs.flags_h.clear();
     }
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
-    HIP_OK(hipMemsetAsync(gs.known.p, 1, NE, c->stream));     /* halo rows: identity */
+    const unsigned gN = (unsigned)std::min<int64_t>((NE + 255) / 256, 4096);
+    HIP_OK(hipMemsetAsync(gs.known.p, 1, NE, c->stream));     /* outer halo rows: identity */
     hipLaunchKernelGGL(k_known, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L,
                        (int64_t)c->rowintcon, gs.known.p);
     HIP_OK(hipGetLastError());
+    if (c->nranks > 1) {
+        /* the neighbours' flags of the adjacent latitude rows */
+        hipLaunchKernelGGL(k_u8_to_d, dim3(gN), dim3(256), 0, c->stream, gs.known.p, gs.rr.p, NE);
+        if ((rc = halo_exchange_w(c, gs.rr.p, NUN, 1))) return rc;
+        hipLaunchKernelGGL(k_d_to_u8, dim3(gN), dim3(256), 0, c->stream, gs.rr.p, gs.known.p, NE);
+    }
     std::vector<uint8_t> kn(NE);
     if ((rc = d2h(c, kn.data(), gs.known.p, NE))) return rc;
-    if (kn != gs.known_h)
-        if ((rc = build_structure(c, kn))) return rc;
+    {
+        /* global column / U/V-point flags: the Schur structure is that of the whole grid */
+        std::vector<double> flags;
+        band_flags(c, kn, flags);
+        if (c->nranks > 1) {
+            DevBuf<double> fb;
+            if (fb.alloc(flags.size())) return IEMIC_ENOMEM;
+            if ((rc = h2d(c, fb.p, flags.data(), sizeof(double) * flags.size()))) return rc;
+            if ((rc = allreduce_sum(c, fb.p, (int)flags.size()))) return rc;
+            if ((rc = d2h(c, flags.data(), fb.p, sizeof(double) * flags.size()))) return rc;
+        }
+        if (flags != gs.flags_h)
+            if ((rc = build_structure(c, flags))) return rc;
+    }
+    if (gs.gslot.n < (size_t)8 * next) {
+        if (gs.gslot.alloc((size_t)8 * next)) return IEMIC_ENOMEM;
+        HIP_OK(hipMemsetAsync(gs.gslot.p, 0, sizeof(double) * gs.gslot.n, c->stream));
+    }
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        L, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
                        gs.tsinv.p, gs.pw.p);
+    hipLaunchKernelGGL(k_gslot_pack, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L, gs.gslot.p);
+    if (c->nranks > 1) {
+        if ((rc = halo_exchange_w(c, gs.uvinv.p, 4, 1))) return rc;
+        if ((rc = halo_exchange_w(c, gs.gslot.p, 8, 1))) return rc;
+    }
     hipLaunchKernelGGL(k_knownmask, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        gs.kmask.p, L, c->jb1);
     hipLaunchKernelGGL(k_ts_compact, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
@@ -1065,8 +1150,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     HIP_OK(hipMemsetAsync(gs.band.p, 0, sizeof(double) * (size_t)gs.ncol * W, c->stream));
     const int64_t nt = (int64_t)gs.ncol * 9;
     hipLaunchKernelGGL(k_schur_build, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream,
-                       c->d_val.p, gs.known.p, gs.uvinv.p, gs.pw.p, gs.col_of_ij.p, gs.ij_of_col.p,
-                       gs.pinned.p, gs.ncol, gs.bl, gs.bu, L, gs.band.p);
+                       c->d_val.p, gs.known.p, gs.uvinv.p, gs.gslot.p, gs.pw.p, gs.col_of_ij.p,
+                       gs.ij_of_col.p, gs.pinned.p, gs.ncol, gs.bl, gs.bu, L, c->jb1, gs.band.p);
+    /* every band built the rows of its own columns: the sum is the whole Schur band */
+    if ((rc = allreduce_sum(c, gs.band.p, gs.ncol * W))) return rc;
     {
         const size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * NBP + (size_t)NBP * (gs.bl + gs.bu));
         if (lb > 150 * 1024) {
@@ -1093,21 +1180,21 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         if (bytes(32) <= lmax) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(32)));
-            hipLaunchKernelGGL(k_band_inv_blk<32>, dim3((unsigned)((gs.ncol + 31) / 32)), dim3(256),
-                               bytes(32), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
-                               gs.sinv.p);
+            hipLaunchKernelGGL(k_band_inv_blk<32>, dim3((unsigned)((gs.ncol_own + 31) / 32)),
+                               dim3(256), bytes(32), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
+                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
         } else if (bytes(16) <= lmax) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(16)));
-            hipLaunchKernelGGL(k_band_inv_blk<16>, dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256),
-                               bytes(16), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
-                               gs.sinv.p);
+            hipLaunchKernelGGL(k_band_inv_blk<16>, dim3((unsigned)((gs.ncol_own + 15) / 16)),
+                               dim3(256), bytes(16), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
+                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
         } else if (bytes(8) <= lmax) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(8)));
-            hipLaunchKernelGGL(k_band_inv_blk<8>, dim3((unsigned)((gs.ncol + 7) / 8)), dim3(256),
-                               bytes(8), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu,
-                               gs.sinv.p);
+            hipLaunchKernelGGL(k_band_inv_blk<8>, dim3((unsigned)((gs.ncol_own + 7) / 8)),
+                               dim3(256), bytes(8), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
+                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
         } else {
             set_error("block GS: Schur band too wide for the LDS inverse");
             return IEMIC_EINVAL;
@@ -1126,21 +1213,32 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
     const unsigned gij = (unsigned)((c->nloc / c->l + 255) / 256);
     hipStream_t s = c->stream;
+    const bool band = c->nranks > 1;
+    int rc = 0;
+    /* the halo rows of r hold the neighbours' identity-row values the couplings need */
+    if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
     hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
                        gs.rr.p, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.rr.p, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
     hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
                        gs.rr.p, z, gs.tcell.p, L, 0);
     hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
                        gs.pinned.p, gs.colv.p, L);
+    /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
+                       gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
-                       gs.ncol, gs.colv.p, gs.colv2.p);
+                       gs.ncol, gs.ncol_own, gs.colv_own.p, gs.colv2.p);
+    if ((rc = allreduce_sum(c, gs.colv2.p, gs.ncol))) return rc;
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.col_of_ij.p, gs.colv2.p, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
     hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
                        gs.rr.p, z, gs.tcell.p, L, 1);
     hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,

@@ -92,6 +92,73 @@ def test_bands_in_one_process(oracle_lib, name, nranks):
     assert abs(res[0]["info"].norm_f1 - f1) <= 1e-9 * f1 + 1e-14 * f0
 
 
+def _run_bands(nranks, fn):
+    """Run fn(rank, group) on nranks host threads sharing one in-process group."""
+    from iemic import _lib
+    group = _lib.lib().iemic_local_group_new(nranks)
+    res = [None] * nranks
+
+    def work(r):
+        try:
+            res[r] = fn(r, group)
+        except Exception as e:  # noqa: BLE001
+            res[r] = dict(err=repr(e))
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    _lib.lib().iemic_local_group_free(group)
+    errs = [r["err"] for r in res if isinstance(r, dict) and "err" in r]
+    assert not errs, errs
+    return res
+
+
+@pytest.mark.parametrize("name,nranks,prec", [("natl8", 2, 1), ("natl8", 2, 2),
+                                              ("gateway16", 3, 2), ("global4", 4, 2)])
+def test_bands_spmv_and_solve(oracle_lib, name, nranks, prec):
+    """Band SpMV equals the oracle's J v on the owned rows; a band FGMRES solve (no
+    preconditioner, block Jacobi, block GS) gives ||b - J x|| <= 1e-8 ||b|| globally."""
+    from iemic import _lib
+    from iemic.ocean import Ocean
+    c = cf.preset(name, mixing=0)
+    L0 = golden_landm(name)
+    L = mask_fix(oracle_lib, c, L0)
+    o = oracle_lib.Oracle(c.ref_dict(), L, c.par_list())
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    ov, _ = o.jacobian(x)
+    v = cf.synthetic_vector(c)
+    yref = o.spmv(ov, v)
+    b = -o.rhs(x)
+    y = np.zeros(c.nrows)
+    xs = np.zeros(c.nrows)
+
+    def fn(r, group):
+        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks,
+                   solver_params={"Preconditioner": prec, "FGMRES tolerance": 1e-10,
+                                  "FGMRES iterations": 1000})
+        oc.setState(x)
+        oc.computeJacobian()
+        lay = oc.layout()
+        yy = oc.applyMatrix(v)
+        sol = oc.solve(b)
+        oc.close()
+        return dict(lay=lay, y=yy, sol=sol)
+
+    res = _run_bands(nranks, fn)
+    for r in res:
+        jb0, jb1 = r["lay"]["jb0"], r["lay"]["jb1"]
+        rows = np.array([6 * ((k * c.m + j) * c.n + i) + q for k in range(c.l)
+                         for j in range(jb0, jb1) for i in range(c.n) for q in range(6)])
+        y[rows] = r["y"][rows]
+        xs[rows] = r["sol"][rows]
+    scale = np.abs(ov).max() * np.abs(v).max()
+    assert np.max(np.abs(y - yref)) <= 1e-13 * scale
+    lin = np.linalg.norm(b - o.spmv(ov, xs)) / np.linalg.norm(b)
+    assert lin <= 1e-8, lin
+
+
 def _rccl_worker(rank, nranks, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
