@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PMC_TAG = "r01"         # profiles/<tag>_spmv_pmc.json: PMC HBM bytes per k_spmv launch
 
 
 def spmv_bytes(nnz: int, n: int) -> int:
@@ -52,11 +53,20 @@ def parse():
     p.add_argument("--amp-ts", type=float, default=1e-3,
                    help="T/S amplitude of the synthetic state (DESIGN.md: benchmark state)")
     p.add_argument("--tol", type=float, default=1e-8)
-    p.add_argument("--krylov", type=int, default=1000)
-    p.add_argument("--restarts", type=int, default=2)
+    p.add_argument("--krylov", type=int, default=100)
+    p.add_argument("--restarts", type=int, default=20)
     p.add_argument("--ts-sweeps", type=int, default=12)
     p.add_argument("--orth", default="DCGS2", choices=["DCGS2", "DGKS"])
-    p.add_argument("--spmv-reps", type=int, default=100)
+    p.add_argument("--dyn-iters", type=int, default=2,
+                   help="defect-correction passes on the dynamics block of the block GS")
+    p.add_argument("--schur-fp64", action="store_true", help="Schur inverse in fp64 (default fp32)")
+    p.add_argument("--ts-mg", type=int, default=1,
+                   help="T/S aggregation-multigrid V-cycles (0: --ts-sweeps plain sweeps)")
+    p.add_argument("--mg-sweeps", type=int, default=1, help="sweeps per multigrid level")
+    p.add_argument("--spmv-reps", type=int, default=0,
+                   help="extra back-to-back (hot Infinity Cache) SpMV launches, reported apart")
+    p.add_argument("--cold-reps", type=int, default=0,
+                   help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=48)
     return p.parse_args()
@@ -157,7 +167,9 @@ def main():
     cfg = cf.preset(args.config, mixing=0)
     sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
           "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
-          "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth}
+          "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth,
+          "Dyn iterations": args.dyn_iters, "Schur fp32": not args.schur_fp64,
+          "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps}
     comm_id = None
     if world > 1:
         idt = torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -195,16 +207,36 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms = float(tt.item())
 
-    # SpMV roofline on the Jacobian of the last step (HIP events on the library stream)
-    oc.setState(x0h)
-    oc.computeJacobian()
-    spmv_ms = oc.time_spmv(args.spmv_reps)
+    # SpMV roofline: the k_spmv launches of the timed Newton steps themselves (HIP events
+    # on the library stream around every SpMV inside FGMRES; at N > 1 the span includes
+    # the halo exchange), so the rocprofv3 average of the same command agrees.
+    n_sp = sum(i.solve.n_spmv for i in infos)
+    spmv_ms = sum(i.solve.t_spmv_ms for i in infos) / max(1, n_sp)
     nnz = int(L_.iemic_graph_nnz(oc._h))          # rows owned by this GPU
     lay = oc.layout()
     nown = lay["own_rows"]
     bsp = spmv_bytes(nnz, nown)
     achieved = bsp / (spmv_ms * 1e-3) / 1e9
     ell = stencil_ell_bytes(nown // 6, 104, nown)
+    extra = {}
+    if args.spmv_reps > 0 or args.cold_reps > 0:
+        oc.setState(x0h)
+        oc.computeJacobian()
+        if args.spmv_reps > 0:
+            extra["hot_us"] = round(oc.time_spmv(args.spmv_reps) * 1e3, 2)
+        if args.cold_reps > 0:
+            fl = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            extra["cold_us"] = round(oc.time_spmv_cold(fl.data_ptr(), fl.numel(),
+                                                       args.cold_reps) * 1e3, 2)
+            del fl
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"{PMC_TAG}_spmv_pmc.json")
+    if os.path.exists(pmc) and world == 1:
+        with open(pmc) as f:
+            pm = json.load(f)
+        if pm.get("config") == args.config:
+            traffic = pm.get("hbm_bytes_per_launch")
 
     last = infos[-1]
     s = last.solve
@@ -219,7 +251,9 @@ def main():
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
-                   "ts_sweeps": args.ts_sweeps,
+                   "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters,
+                   "schur": "fp64" if args.schur_fp64 else "fp32",
+                   "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps,
                    "parallelism": f"latitude-bands x{world}" if world > 1 else "single",
                    "band_rows": [lay["jb0"], lay["jb1"]]},
         "newton": {"iters": s.iters, "converged": s.converged,
@@ -230,13 +264,13 @@ def main():
                    "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms,
                    "dgks_reorth": s.reorth},
         "spmv_gbps": round(achieved, 1),
-        "roofline": {"kernel": "k_spmv (per GPU, rank 0)", "bound": "hbm",
+        "roofline": {"kernel": "k_spmv (per GPU, rank 0; in-solve launches)", "bound": "hbm",
                      "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes": bsp, "stencil_ell_bytes": ell,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
-                     "launch_us": round(spmv_ms * 1e3, 2)},
+                     "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp, **extra},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -80,6 +80,19 @@ struct BlockGS {
     DevBuf<int> piv, info;
     DevBuf<double> lpan;             /* band-LU panel multipliers                       */
     DevBuf<double> sinv;             /* Schur inverse columns of this band, ncol x ncol_own */
+    DevBuf<float> sinvf;             /* the same in fp32, rows padded to ldf (16-B rows)  */
+    int ldf = 0, fp32 = 1;           /* fp32: the apply's GEMV reads sinvf               */
+    int dyn_iters = 1;               /* defect-correction passes on the dynamics block   */
+    DevBuf<double> dres, zc;         /* dynamics defect and correction (ext rows)        */
+    /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local):
+     * level 0 is the fine T/S block (tsoff/tsdiag/tsinv, ext cells); coarse level q has
+     * mg_n[q] x mg_m[q] x l cells with 16 couplings, 2x2 block and inverse, rhs, iterate */
+    static constexpr int MG_MAX = 12;
+    int ts_mg = 1, mg_sweeps = 1, mg_nlev = 0;
+    int mg_n[MG_MAX] = {}, mg_m[MG_MAX] = {};
+    DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
+    DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_dinv[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
+    DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work                               */
 };
 

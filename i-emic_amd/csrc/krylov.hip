@@ -13,6 +13,7 @@
  *    Ocean::solve (Ocean.C:1140-1150).
  */
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 
@@ -80,6 +81,169 @@ __global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic,
     double r5 = row_dot<SS>(val, x, lc, nloc, nb);
     double* yc = y + NUN * ((int64_t)HALO * l * n + lc);
     yc[0] = r0; yc[1] = r1; yc[2] = r2; yc[3] = r3; yc[4] = r4; yc[5] = r5;
+}
+
+/* Two cells per thread (even n): the pair (lc, lc+1) shares its (j, k) row, so the slot
+ * values load as one 16-B double2 per slot and the 27-point neighbourhoods overlap in
+ * four i columns (i-1 .. i+2).  Blocks are dealt to the 8 XCDs in contiguous runs
+ * (blockIdx b runs on XCD b % 8), so each XCD's L2 serves the x neighbourhood of one
+ * contiguous slab of latitude rows instead of every XCD fetching all of x. */
+template <int R>
+__device__ __forceinline__ void row_dot2(const double* __restrict__ val, const double* __restrict__ x,
+                                         int64_t lc, int64_t nloc, const int* rb, const int* iu,
+                                         double& a0, double& a1)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const Slot sl = SLOTS[B + s];
+        const int r = rb[(sl.dk + 1) * 3 + (sl.dj + 1)];
+        const double2 v = *reinterpret_cast<const double2*>(val + (int64_t)(B + s) * nloc + lc);
+        s0 += v.x * x[NUN * (int64_t)(r + iu[sl.di + 1]) + sl.var];
+        s1 += v.y * x[NUN * (int64_t)(r + iu[sl.di + 2]) + sl.var];
+    }
+    a0 = s0;
+    a1 = s1;
+}
+
+__global__ void __launch_bounds__(256) k_spmv2(int n, int m, int l, int periodic, int jb0,
+                                               const double* __restrict__ val,
+                                               const double* __restrict__ x,
+                                               double* __restrict__ y, int64_t nloc, int nblk)
+{
+    const int per = (nblk + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= nblk) return;
+    const int64_t lc = 2 * ((int64_t)tile * blockDim.x + threadIdx.x);
+    if (lc >= nloc) return;
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    int iu[4] = {i - 1, i, i + 1, i + 2};
+    if (iu[0] < 0) iu[0] = periodic ? n - 1 : 0;
+    if (iu[3] >= n) iu[3] = periodic ? 0 : n - 1;
+    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
+    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
+    int rb[9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
+    double r[12];
+    row_dot2<UU>(val, x, lc, nloc, rb, iu, r[0], r[6]);
+    row_dot2<VV>(val, x, lc, nloc, rb, iu, r[1], r[7]);
+    row_dot2<WW>(val, x, lc, nloc, rb, iu, r[2], r[8]);
+    row_dot2<PP>(val, x, lc, nloc, rb, iu, r[3], r[9]);
+    row_dot2<TT>(val, x, lc, nloc, rb, iu, r[4], r[10]);
+    row_dot2<SS>(val, x, lc, nloc, rb, iu, r[5], r[11]);
+    double2* yc = reinterpret_cast<double2*>(y + NUN * ((int64_t)HALO * l * n + lc));
+#pragma unroll
+    for (int q = 0; q < 6; q++) yc[q] = make_double2(r[2 * q], r[2 * q + 1]);
+}
+
+/* One wavefront per (64 cells, equation): a 384-thread block covers 64 consecutive cells
+ * and wave R computes their row R (U, V, W, P, T, S).  Loads stay coalesced (lanes read
+ * adjacent cells of one slot), the per-lane work is one row (7-24 slots), and the grid
+ * has 6x more wavefronts than a thread-per-cell launch, enough to keep HBM busy at the
+ * 2-degree size (233k cells per GPU).  Blocks are dealt to the XCDs in contiguous runs. */
+template <int R>
+__device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, const double* __restrict__ x,
+                                             int64_t lc, int64_t nloc, const int* rb, const int* ii)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const Slot sl = SLOTS[B + s];
+        const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
+        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * (int64_t)cidx + sl.var];
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(384) k_spmv6(int n, int m, int l, int periodic, int jb0,
+                                               const double* __restrict__ val,
+                                               const double* __restrict__ x,
+                                               double* __restrict__ y, int64_t nloc, int nblk)
+{
+    const int per = (nblk + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= nblk) return;
+    const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
+    if (lc >= nloc) return;
+    const int R = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    int ii[3] = {i - 1, i, i + 1};
+    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
+    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
+    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
+    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
+    int rb[9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
+    double acc;
+    switch (R) {
+    case UU: acc = row_dot_rb<UU>(val, x, lc, nloc, rb, ii); break;
+    case VV: acc = row_dot_rb<VV>(val, x, lc, nloc, rb, ii); break;
+    case WW: acc = row_dot_rb<WW>(val, x, lc, nloc, rb, ii); break;
+    case PP: acc = row_dot_rb<PP>(val, x, lc, nloc, rb, ii); break;
+    case TT: acc = row_dot_rb<TT>(val, x, lc, nloc, rb, ii); break;
+    default: acc = row_dot_rb<SS>(val, x, lc, nloc, rb, ii); break;
+    }
+    y[NUN * ((int64_t)HALO * l * n + lc) + R] = acc;
+}
+
+/* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
+ * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
+ * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
+ * full rows of the SpMV are used: one wavefront per (64 cells, dynamics equation). */
+__global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int periodic, int jb0,
+                                                  const double* __restrict__ val,
+                                                  const double* __restrict__ z,
+                                                  const double* __restrict__ r,
+                                                  const uint8_t* __restrict__ known,
+                                                  double* __restrict__ d, int64_t nloc, int nblk)
+{
+    const int per = (nblk + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= nblk) return;
+    const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
+    if (lc >= nloc) return;
+    const int R = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    int ii[3] = {i - 1, i, i + 1};
+    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
+    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
+    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
+    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
+    int rb[9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
+    const int64_t row = NUN * ((int64_t)HALO * l * n + lc) + R;
+    if (known[row]) {
+        d[row] = 0.0;
+        return;
+    }
+    double acc;
+    switch (R) {
+    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, rb, ii); break;
+    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, rb, ii); break;
+    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, rb, ii); break;
+    default: acc = row_dot_rb<PP>(val, z, lc, nloc, rb, ii); break;
+    }
+    d[row] = r[row] - acc;
+}
+
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d)
+{
+    const int nblk = (int)((c->nloc + 63) / 64);
+    const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
+    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
+                       c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
+    return 0;
 }
 
 /* ---- reductions / BLAS-1 ------------------------------------------------------------ */
@@ -325,8 +489,24 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
         return IEMIC_ESTATE;
     }
     hipStream_t s = c->stream;
-    hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, s, c->n,
-                       c->m, c->l, c->cfg.periodic, c->jb0, c->d_val.p, x, y, c->nloc);
+    static const int variant = [] {
+        const char* e = getenv("IEMIC_SPMV");
+        return e ? atoi(e) : 6;
+    }();
+    if (variant == 6) {
+        const int nblk = (int)((c->nloc + 63) / 64);
+        const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
+        hipLaunchKernelGGL(k_spmv6, dim3(grid), dim3(384), 0, s, c->n, c->m, c->l, c->cfg.periodic,
+                           c->jb0, c->d_val.p, x, y, c->nloc, nblk);
+    } else if (variant == 2 && (c->n & 1) == 0 && c->n >= 4) {
+        const int nblk = (int)((c->nloc / 2 + 255) / 256);
+        const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
+        hipLaunchKernelGGL(k_spmv2, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
+                           c->jb0, c->d_val.p, x, y, c->nloc, nblk);
+    } else {
+        hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, s, c->n,
+                           c->m, c->l, c->cfg.periodic, c->jb0, c->d_val.p, x, y, c->nloc);
+    }
     if (c->su.rowintcon_ref >= 0) {
         /* dense intcond row: y[rowintcon] = intSign * coeff . x (summed over the ranks) */
         const int64_t o = NUN * c->own0;
@@ -503,7 +683,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 rc = spmv(c, zj, vn, c->stream);
                 if (rc) return rc;
                 HIP_OK(hipEventRecord(ev[2], c->stream));
-                auto tp = std::chrono::steady_clock::now();
+
                 /* DGKS (Belos' default orthogonalisation): one classical Gram-Schmidt pass
                  * h = V^T w (with ||w||^2 in the same launch), w -= V h (with ||w||^2 fused),
                  * and a second pass only when the norm dropped below 1/sqrt(2) of its value
@@ -531,7 +711,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
                     inf.t_prec_ms += a1;
                     inf.t_spmv_ms += a2;
-                    inf.t_orth_ms += ms_since(tp) - a1 - a2;
+                    inf.n_spmv++;
                 }
                 for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
                 H[(size_t)(j + 1) * m + j] = hn;
@@ -583,7 +763,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     if (rc) return rc;
                     HIP_OK(hipEventRecord(ev[2], c->stream));
                 }
-                auto tp = std::chrono::steady_clock::now();
+
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
@@ -600,6 +780,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
                     inf.t_prec_ms += a1;
                     inf.t_spmv_ms += a2;
+                    inf.n_spmv++;
                 }
                 const double* hr = c->h_red;
                 double aa = 0.0, ab = 0.0;
@@ -636,7 +817,6 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     stop = res <= opt->tol || !(bt > 0.0);
                 }
                 if (stop || jj == m || !(bt > 0.0)) {
-                    inf.t_orth_ms += ms_since(tp) - a1 - a2;
                     break;
                 }
                 /* update pass: q_jj = (u - Q a)/bt,  w -= Q c + gamma u */
@@ -651,7 +831,6 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
                 hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V + o, NE, nv,
                                    c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u + o, wv + o, NL);
-                inf.t_orth_ms += ms_since(tp) - a1 - a2;
             }
             j = ncolf;
         }
@@ -690,6 +869,9 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
      * with it (a loss of orthogonality shows up as a gap between the two) */
     inf.converged = res <= opt->tol && inf.explicit_rel_res <= 2.0 * opt->tol;
     inf.t_total_ms = ms_since(T0);
+    /* everything that is not the (event-timed) preconditioner or SpMV: Gram-Schmidt
+     * passes, reductions, host synchronisation and the Hessenberg work */
+    inf.t_orth_ms = std::max(0.0, inf.t_total_ms - inf.t_prec_ms - inf.t_spmv_ms);
     HIP_OK(hipGetLastError());
     if (info) *info = inf;
     return 0;

@@ -24,6 +24,7 @@
  * (ncol^2 doubles, 0.7 GB at 2 degrees).
  */
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -118,7 +119,8 @@ __device__ __forceinline__ void inv2(double a, double b, double c, double d, boo
 __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                Lay L, int64_t rowintcon, int int_sign,
                                const double* __restrict__ intc, double* __restrict__ uvinv,
-                               double* __restrict__ tsinv, double* __restrict__ pw)
+                               double* __restrict__ tsinv, double* __restrict__ pw,
+                               double* __restrict__ tsdiag, int64_t next)
 {
     OWNED_CELL;
     auto V = [&](int s) { return val[(int64_t)s * ncell + lc]; };
@@ -130,6 +132,14 @@ __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __
         sofft = 0.0;
     }
     inv2(V(S_TT0), V(S_TS0), sofft, sdiag, !kn[TT], !kn[SS], tsinv + 4 * cell);
+    {
+        /* the 2x2 T/S block the sweeps invert, restricted to the active unknowns */
+        const bool ta = !kn[TT], sa = !kn[SS];
+        tsdiag[cell] = ta ? V(S_TT0) : 0.0;
+        tsdiag[next + cell] = ta && sa ? V(S_TS0) : 0.0;
+        tsdiag[2 * next + cell] = ta && sa ? sofft : 0.0;
+        tsdiag[3 * next + cell] = sa ? sdiag : 0.0;
+    }
     /* depth integral of the continuity rows: weight 1/a_k with a_k the coefficient of
      * the row's own W (or -1/b_k with b_k that of W(k-1) when the own W is an identity) */
     double w = 0.0;
@@ -690,6 +700,89 @@ __global__ void k_gather(const double* __restrict__ b, const int* __restrict__ c
     if (q < nq) bo[q] = b[cols[q]];
 }
 
+/* fp32 copy of the Schur inverse slab, rows padded to ld floats (16-B aligned rows) */
+__global__ void k_to_f32(const double* __restrict__ X, int nr, int nc, float* __restrict__ Y, int ld)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)nr * ld) return;
+    const int r = (int)(t / ld), c = (int)(t % ld);
+    Y[t] = c < nc ? (float)X[(int64_t)r * nc + c] : 0.0f;
+}
+
+/* 3b'. y = X b with X fp32 (row-major, ld floats per row, ld % 4 == 0), fp64 accumulation:
+ * one wavefront per 4 rows, 16-B loads of X, each b element loaded once per 4 rows */
+__global__ void __launch_bounds__(256) k_gemv_f(const float* __restrict__ X, int nr, int nc, int ld,
+                                                const double* __restrict__ b, double* __restrict__ y)
+{
+    const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+    const int lane = threadIdx.x & 63;
+    if (r0 >= nr) return;
+    const int nrow = min(4, nr - r0);
+    const float4* xr[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        xr[q] = reinterpret_cast<const float4*>(X + (int64_t)(r0 + min(q, nrow - 1)) * ld);
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    const int n4 = ld >> 2;
+    for (int c4 = lane; c4 < n4; c4 += 64) {
+        const int c = 4 * c4;
+        const double b0 = c < nc ? b[c] : 0.0, b1 = c + 1 < nc ? b[c + 1] : 0.0;
+        const double b2 = c + 2 < nc ? b[c + 2] : 0.0, b3 = c + 3 < nc ? b[c + 3] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 v = xr[q][c4];
+            s[q] += (double)v.x * b0 + (double)v.y * b1 + (double)v.z * b2 + (double)v.w * b3;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        double t = s[q];
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+        if (lane == 0 && q < nrow) y[r0 + q] = t;
+    }
+}
+
+/* dynamics defect: d = rr - A_DD z on the active U/V/W/P rows (couplings to active
+ * U/V/W/P columns only: the block the dynamics solve approximates), 0 elsewhere */
+__global__ void k_dyn_resid(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                            const double* __restrict__ rr, const double* __restrict__ z,
+                            double* __restrict__ d, Lay L)
+{
+    LAY_ALIASES;
+    OWNED_CELL;
+    for (int R = UU; R <= PP; R++) {
+        const int64_t row = NUN * cell + R;
+        if (known[row]) { d[row] = 0.0; continue; }
+        double acc = rr[row];
+        for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
+            const int var = SLOTS[s].var;
+            if (var > PP) continue;
+            const double v = val[(int64_t)s * ncell + lc];
+            if (v == 0.0) continue;
+            int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
+            const int kk = k + SLOTS[s].dk;
+            if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
+            const int64_t col = NUN * ecell(L, ii, jj, kk) + var;
+            if (!known[col]) acc -= v * z[col];
+        }
+        d[row] = acc;
+    }
+    d[NUN * cell + TT] = 0.0;
+    d[NUN * cell + SS] = 0.0;
+}
+
+/* z += zc on the active U/V/W/P rows */
+__global__ void k_dyn_add(const uint8_t* __restrict__ known, const double* __restrict__ zc,
+                          double* __restrict__ z, Lay L)
+{
+    OWNED_CELL;
+#pragma unroll
+    for (int R = UU; R <= PP; R++) {
+        const int64_t row = NUN * cell + R;
+        if (!known[row]) z[row] += zc[row];
+    }
+}
+
 /* 4. uv = uv* - D^-1 Guv Mz1^T pbar */
 __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ uvinv, const int* __restrict__ col_of_ij,
@@ -830,7 +923,7 @@ __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __rest
 __global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ rr, const double* __restrict__ z,
                            double* __restrict__ bc, double* __restrict__ zt, double* __restrict__ zs,
-                           Lay L)
+                           Lay L, double* __restrict__ bts)
 {
     LAY_ALIASES;
     OWNED_CELL;
@@ -854,6 +947,7 @@ __global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __rest
             }
         }
         bc[(int64_t)(c * 2 + (R - TT)) * half + (lc >> 1)] = acc;
+        bts[row] = acc;
     }
     zt[cell] = 0.0;
     zs[cell] = 0.0;
@@ -902,6 +996,201 @@ __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __
     OWNED_CELL;
     if (!known[NUN * cell + TT]) z[NUN * cell + TT] = zt[cell];
     if (!known[NUN * cell + SS]) z[NUN * cell + SS] = zs[cell];
+}
+
+/* ---- T/S aggregation multigrid ----------------------------------------------------
+ * The T/S block is an advection-diffusion operator whose smooth error modes Gauss-Seidel
+ * sweeps barely touch.  Its coarse spaces aggregate 2x2 horizontal neighbours over the
+ * full depth (each level is again an n x m x l grid with the fine coupling pattern:
+ * 6 same-variable face couplings, T<->S at k-1/k+1, a 2x2 cell block), built by Galerkin
+ * summation with piecewise-constant transfers.  Aggregates stay inside a latitude band
+ * (block-Jacobi across GPUs, like the fine T/S sweeps).  One V-cycle: symmetric red-black
+ * smoothing on every level, a one-workgroup solve on the coarsest. */
+struct TsLev {
+    int n, mb, l, periodic;
+    int64_t base, cstr;              /* cell index = base + (jl*l + k)*n + i; array stride */
+    const double* off;               /* 16 x cstr: T row q 0..7, S row q 8..15          */
+    const double* diag;              /* 4 x cstr: 2x2 block (TT, TS, ST, SS)           */
+    const double* dinv;              /* 4 x cstr (level 0: packed per cell, 4*cell)     */
+    int dinv_aos;                    /* 1: dinv[4*cell + e] (level 0: tsinv)            */
+    const double* bt; const double* bs; int bstr;
+    double* zt; double* zs;
+};
+__device__ __forceinline__ int64_t mg_cell(const TsLev& V, int i, int jl, int k)
+{
+    return V.base + ((int64_t)jl * V.l + k) * V.n + i;
+}
+/* neighbour q (-i,+i,-j,+j,-k,+k) of (i,jl,k): false outside the level's band */
+__device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, int& k)
+{
+    switch (q) {
+    case 0: i--; break;
+    case 1: i++; break;
+    case 2: jl--; break;
+    case 3: jl++; break;
+    case 4: k--; break;
+    default: k++; break;
+    }
+    if (jl < 0 || jl >= V.mb || k < 0 || k >= V.l) return false;
+    if (i < 0 || i >= V.n) {
+        if (!V.periodic) return false;
+        i = (i + V.n) % V.n;
+    }
+    return true;
+}
+/* off-diagonal part of row (T, S) of cell (i,jl,k) applied to the iterate */
+__device__ __forceinline__ void mg_offmul(const TsLev& V, int i, int jl, int k, int64_t c,
+                                          double& at, double& as)
+{
+    at = as = 0.0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        int ii = i, jj = jl, kk = k;
+        if (!mg_nb(V, q, ii, jj, kk)) continue;
+        const int64_t nc = mg_cell(V, ii, jj, kk);
+        at += V.off[(int64_t)q * V.cstr + c] * V.zt[nc];
+        as += V.off[(int64_t)(8 + q) * V.cstr + c] * V.zs[nc];
+        if (q == 4) {
+            at += V.off[(int64_t)6 * V.cstr + c] * V.zs[nc];
+            as += V.off[(int64_t)14 * V.cstr + c] * V.zt[nc];
+        } else if (q == 5) {
+            at += V.off[(int64_t)7 * V.cstr + c] * V.zs[nc];
+            as += V.off[(int64_t)15 * V.cstr + c] * V.zt[nc];
+        }
+    }
+}
+__device__ __forceinline__ int mg_colour(const TsLev& V, int i, int jl, int k)
+{
+    if (V.periodic && (V.n & 1) && i == V.n - 1) return 2 + ((jl + k) & 1);
+    return (i + jl + k) & 1;
+}
+__device__ __forceinline__ void mg_relax(const TsLev& V, int i, int jl, int k)
+{
+    const int64_t c = mg_cell(V, i, jl, k);
+    double at, as;
+    mg_offmul(V, i, jl, k, c, at, as);
+    const double rt = V.bt[c * V.bstr] - at, rs = V.bs[c * V.bstr] - as;
+    double d0, d1, d2, d3;
+    if (V.dinv_aos) {
+        d0 = V.dinv[4 * c]; d1 = V.dinv[4 * c + 1]; d2 = V.dinv[4 * c + 2]; d3 = V.dinv[4 * c + 3];
+    } else {
+        d0 = V.dinv[c]; d1 = V.dinv[V.cstr + c]; d2 = V.dinv[2 * V.cstr + c]; d3 = V.dinv[3 * V.cstr + c];
+    }
+    V.zt[c] = d0 * rt + d1 * rs;
+    V.zs[c] = d2 * rt + d3 * rs;
+}
+/* one colour of a red-black sweep on a coarse level (all cells launched, one colour acts) */
+__global__ void k_mg_half(TsLev V, int colour)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ncl = (int64_t)V.n * V.mb * V.l;
+    if (t >= ncl) return;
+    const int i = (int)(t % V.n), k = (int)((t / V.n) % V.l), jl = (int)(t / ((int64_t)V.n * V.l));
+    if (mg_colour(V, i, jl, k) != colour) return;
+    mg_relax(V, i, jl, k);
+}
+/* coarse rhs = sum of the children's residuals b - A z; coarse iterate = 0 */
+__global__ void k_mg_restrict(TsLev F, TsLev C, double* __restrict__ bc, double* __restrict__ zc)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ncl = (int64_t)C.n * C.mb * C.l;
+    if (t >= ncl) return;
+    const int I = (int)(t % C.n), k = (int)((t / C.n) % C.l), J = (int)(t / ((int64_t)C.n * C.l));
+    double st = 0.0, ss = 0.0;
+    for (int b = 0; b < 2; b++)
+        for (int a = 0; a < 2; a++) {
+            const int i = 2 * I + a, jl = 2 * J + b;
+            if (i >= F.n || jl >= F.mb) continue;
+            const int64_t c = mg_cell(F, i, jl, k);
+            double at, as;
+            mg_offmul(F, i, jl, k, c, at, as);
+            const double zt = F.zt[c], zs = F.zs[c];
+            at += F.diag[c] * zt + F.diag[F.cstr + c] * zs;
+            as += F.diag[2 * F.cstr + c] * zt + F.diag[3 * F.cstr + c] * zs;
+            st += F.bt[c * F.bstr] - at;
+            ss += F.bs[c * F.bstr] - as;
+        }
+    bc[t] = st;
+    bc[ncl + t] = ss;
+    zc[t] = 0.0;
+    zc[ncl + t] = 0.0;
+}
+/* fine iterate += coarse correction of its aggregate (active unknowns only) */
+__global__ void k_mg_prolong(TsLev F, TsLev C)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nfl = (int64_t)F.n * F.mb * F.l;
+    if (t >= nfl) return;
+    const int i = (int)(t % F.n), k = (int)((t / F.n) % F.l), jl = (int)(t / ((int64_t)F.n * F.l));
+    const int64_t c = mg_cell(F, i, jl, k);
+    const int64_t p = mg_cell(C, i >> 1, jl >> 1, k);
+    if (F.diag[c] != 0.0) F.zt[c] += C.zt[p];
+    if (F.diag[3 * F.cstr + c] != 0.0) F.zs[c] += C.zs[p];
+}
+/* Galerkin coarse operator: sum of the children's blocks and couplings; couplings inside
+ * the aggregate go to the coarse 2x2 block */
+__global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double* __restrict__ diag,
+                              double* __restrict__ dinv)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ncl = (int64_t)C.n * C.mb * C.l;
+    if (t >= ncl) return;
+    const int I = (int)(t % C.n), k = (int)((t / C.n) % C.l), J = (int)(t / ((int64_t)C.n * C.l));
+    double o[16], d[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int e = 0; e < 16; e++) o[e] = 0.0;
+    for (int b = 0; b < 2; b++)
+        for (int a = 0; a < 2; a++) {
+            const int i = 2 * I + a, jl = 2 * J + b;
+            if (i >= F.n || jl >= F.mb) continue;
+            const int64_t c = mg_cell(F, i, jl, k);
+            for (int e = 0; e < 4; e++) d[e] += F.diag[(int64_t)e * F.cstr + c];
+            for (int R = 0; R < 2; R++)
+                for (int q = 0; q < 8; q++) {
+                    const double v = F.off[(int64_t)(8 * R + q) * F.cstr + c];
+                    if (v == 0.0) continue;
+                    int ii = i, jj = jl, kk = k;
+                    if (!mg_nb(F, q < 6 ? q : q - 2, ii, jj, kk)) continue;
+                    if (q < 6 && (ii >> 1) == I && (jj >> 1) == J && kk == k)
+                        d[3 * R] += v;                    /* same variable, same aggregate */
+                    else
+                        o[8 * R + q] += v;
+                }
+        }
+    const bool at = d[0] != 0.0, as = d[3] != 0.0;
+    if (!at) { d[1] = d[2] = 0.0; for (int q = 0; q < 8; q++) o[q] = 0.0; }
+    if (!as) { d[1] = d[2] = 0.0; for (int q = 8; q < 16; q++) o[q] = 0.0; }
+    for (int e = 0; e < 16; e++) off[(int64_t)e * ncl + t] = o[e];
+    for (int e = 0; e < 4; e++) diag[(int64_t)e * ncl + t] = d[e];
+    double inv[4];
+    inv2(d[0], d[1], d[2], d[3], at, as, inv);
+    for (int e = 0; e < 4; e++) dinv[(int64_t)e * ncl + t] = inv[e];
+}
+/* coarsest level: `sweeps` symmetric red-black sweeps in one workgroup, iterate in LDS */
+constexpr int MG_COARSE_MAX = 2048;
+__global__ void __launch_bounds__(1024) k_mg_coarsest(TsLev V, int sweeps)
+{
+    __shared__ double zl[2 * MG_COARSE_MAX];
+    const int ncl = V.n * V.mb * V.l;
+    TsLev W = V;
+    W.zt = zl;
+    W.zs = zl + ncl;
+    W.base = 0;
+    for (int t = threadIdx.x; t < 2 * ncl; t += blockDim.x) zl[t] = 0.0;
+    __syncthreads();
+    const int ncol = (V.periodic && (V.n & 1)) ? 4 : 2;
+    for (int sw = 0; sw < sweeps; sw++)
+        for (int h = 0; h < 2 * ncol; h++) {
+            const int colour = h < ncol ? h : 2 * ncol - 1 - h;
+            for (int t = threadIdx.x; t < ncl; t += blockDim.x) {
+                const int i = t % V.n, k = (t / V.n) % V.l, jl = t / (V.n * V.l);
+                if (mg_colour(W, i, jl, k) == colour) mg_relax(W, i, jl, k);
+            }
+            __syncthreads();
+        }
+    for (int t = threadIdx.x; t < ncl; t += blockDim.x) {
+        V.zt[t] = zl[t];
+        V.zs[t] = zl[ncl + t];
+    }
 }
 
 /* ---- host: structure from the identity-row pattern ------------------------------ */
@@ -1064,6 +1353,218 @@ static Lay lay_of(const iemic_ctx* c)
     return L;
 }
 
+
+/* ---- T/S multigrid: host side ------------------------------------------------------ */
+static TsLev mg_view(iemic_ctx* c, int q)
+{
+    BlockGS& gs = c->gs;
+    TsLev V{};
+    V.l = c->l;
+    V.periodic = c->cfg.periodic;
+    if (q == 0) {
+        V.n = c->n;
+        V.mb = c->jb1 - c->jb0;
+        V.base = c->own0;
+        V.cstr = c->next;
+        V.off = gs.tsoff.p;
+        V.diag = gs.tsdiag.p;
+        V.dinv = gs.tsinv.p;
+        V.dinv_aos = 1;
+        V.bt = gs.bts.p + TT;
+        V.bs = gs.bts.p + SS;
+        V.bstr = NUN;
+        V.zt = gs.zt.p;
+        V.zs = gs.zs.p;
+    } else {
+        V.n = gs.mg_n[q];
+        V.mb = gs.mg_m[q];
+        const int64_t ncl = (int64_t)V.n * V.mb * V.l;
+        V.base = 0;
+        V.cstr = ncl;
+        V.off = gs.mg_off[q].p;
+        V.diag = gs.mg_diag[q].p;
+        V.dinv = gs.mg_dinv[q].p;
+        V.dinv_aos = 0;
+        V.bt = gs.mg_b[q].p;
+        V.bs = gs.mg_b[q].p + ncl;
+        V.bstr = 1;
+        V.zt = gs.mg_z[q].p;
+        V.zs = gs.mg_z[q].p + ncl;
+    }
+    return V;
+}
+
+static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+/* Gauss-Jordan inverse with partial pivoting (host, the coarsest level: <= 256 unknowns);
+ * unknowns without any coupling (inactive) get an identity row */
+static void dense_inverse(std::vector<double>& A, int N, std::vector<double>& X)
+{
+    X.assign((size_t)N * N, 0.0);
+    for (int i = 0; i < N; i++) {
+        X[(size_t)i * N + i] = 1.0;
+        bool any = false;
+        for (int j = 0; j < N; j++) any |= A[(size_t)i * N + j] != 0.0;
+        if (!any) A[(size_t)i * N + i] = 1.0;
+    }
+    for (int k = 0; k < N; k++) {
+        int p = k;
+        for (int i = k + 1; i < N; i++)
+            if (std::fabs(A[(size_t)i * N + k]) > std::fabs(A[(size_t)p * N + k])) p = i;
+        if (p != k)
+            for (int j = 0; j < N; j++) {
+                std::swap(A[(size_t)p * N + j], A[(size_t)k * N + j]);
+                std::swap(X[(size_t)p * N + j], X[(size_t)k * N + j]);
+            }
+        const double d = A[(size_t)k * N + k];
+        const double q = d != 0.0 ? 1.0 / d : 0.0;
+        for (int j = 0; j < N; j++) {
+            A[(size_t)k * N + j] *= q;
+            X[(size_t)k * N + j] *= q;
+        }
+        for (int i = 0; i < N; i++) {
+            if (i == k) continue;
+            const double f = A[(size_t)i * N + k];
+            if (f == 0.0) continue;
+            for (int j = 0; j < N; j++) {
+                A[(size_t)i * N + j] -= f * A[(size_t)k * N + j];
+                X[(size_t)i * N + j] -= f * X[(size_t)k * N + j];
+            }
+        }
+    }
+}
+
+/* coarse levels, Galerkin operators and the coarsest inverse (once per Jacobian) */
+static int mg_setup(iemic_ctx* c)
+{
+    BlockGS& gs = c->gs;
+    const int l = c->l;
+    int n = c->n, m = c->jb1 - c->jb0, q = 0;
+    if (gs.mg_nlev == 0) {
+        /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns) */
+        while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)n * m * l > 128) && (n > 1 || m > 1)) {
+            n = (n + 1) / 2;
+            m = (m + 1) / 2;
+            q++;
+            gs.mg_n[q] = n;
+            gs.mg_m[q] = m;
+            const size_t ncl = (size_t)n * m * l;
+            if (gs.mg_off[q].alloc(16 * ncl) || gs.mg_diag[q].alloc(4 * ncl) ||
+                gs.mg_dinv[q].alloc(4 * ncl) || gs.mg_b[q].alloc(2 * ncl) || gs.mg_z[q].alloc(2 * ncl))
+                return IEMIC_ENOMEM;
+        }
+        if (q == 0) {
+            gs.ts_mg = 0;            /* a single water column per band: plain sweeps */
+            return 0;
+        }
+        if ((int64_t)n * m * l > 1024) {
+            set_error("block GS: T/S multigrid coarsest level too large");
+            return IEMIC_EINVAL;
+        }
+        gs.mg_nlev = q + 1;
+        const size_t N = (size_t)2 * n * m * l;
+        if (gs.mg_cinv.alloc(N * N)) return IEMIC_ENOMEM;
+    }
+    if (gs.mg_nlev < 2) {
+        gs.ts_mg = 0;
+        return 0;
+    }
+    hipStream_t s = c->stream;
+    for (q = 1; q < gs.mg_nlev; q++) {
+        const TsLev F = mg_view(c, q - 1), C = mg_view(c, q);
+        hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C,
+                           gs.mg_off[q].p, gs.mg_diag[q].p, gs.mg_dinv[q].p);
+    }
+    HIP_OK(hipGetLastError());
+    /* coarsest level: dense operator on the host, inverted, back to the device */
+    const int qc = gs.mg_nlev - 1;
+    const int64_t ncl = (int64_t)gs.mg_n[qc] * gs.mg_m[qc] * l;
+    const int N = (int)(2 * ncl);
+    std::vector<double> off(16 * ncl), dg(4 * ncl);
+    int rc;
+    if ((rc = d2h(c, off.data(), gs.mg_off[qc].p, sizeof(double) * off.size()))) return rc;
+    if ((rc = d2h(c, dg.data(), gs.mg_diag[qc].p, sizeof(double) * dg.size()))) return rc;
+    std::vector<double> A((size_t)N * N, 0.0), X;
+    const int cn = gs.mg_n[qc], cm = gs.mg_m[qc];
+    for (int64_t t = 0; t < ncl; t++) {
+        const int i = (int)(t % cn), k = (int)((t / cn) % l), jl = (int)(t / ((int64_t)cn * l));
+        for (int R = 0; R < 2; R++) {
+            const int64_t row = R * ncl + t;
+            A[row * N + R * ncl + t] += dg[(3 * R) * ncl + t];
+            A[row * N + (1 - R) * ncl + t] += dg[(1 + R) * ncl + t];
+            for (int qq = 0; qq < 8; qq++) {
+                const double v = off[(8 * R + qq) * ncl + t];
+                if (v == 0.0) continue;
+                int ii = i, jj = jl, kk = k;
+                const int dir = qq < 6 ? qq : qq - 2;
+                switch (dir) {
+                case 0: ii--; break;
+                case 1: ii++; break;
+                case 2: jj--; break;
+                case 3: jj++; break;
+                case 4: kk--; break;
+                default: kk++; break;
+                }
+                if (jj < 0 || jj >= cm || kk < 0 || kk >= l) continue;
+                if (ii < 0 || ii >= cn) {
+                    if (!c->cfg.periodic) continue;
+                    ii = (ii + cn) % cn;
+                }
+                const int64_t nb = ((int64_t)jj * l + kk) * cn + ii;
+                const int var = qq < 6 ? R : 1 - R;
+                A[row * N + var * ncl + nb] += v;
+            }
+        }
+    }
+    dense_inverse(A, N, X);
+    return h2d(c, gs.mg_cinv.p, X.data(), sizeof(double) * X.size());
+}
+
+static void mg_smooth(iemic_ctx* c, int q, int nu)
+{
+    BlockGS& gs = c->gs;
+    hipStream_t s = c->stream;
+    const Lay L = lay_of(c);
+    if (q == 0 && (c->n & 1) == 0) {
+        const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
+        const int seq[4] = {0, 1, 1, 0};
+        for (int sw = 0; sw < nu; sw++)
+            for (int h = 0; h < 4; h++)
+                hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
+                                   gs.zt.p, gs.zs.p, L, seq[h]);
+        return;
+    }
+    const TsLev V = mg_view(c, q);
+    const int64_t ncl = (int64_t)V.n * V.mb * V.l;
+    const bool four = V.periodic && (V.n & 1);
+    const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
+    const int* seq = four ? seq4 : seq2;
+    const int ns = four ? 8 : 4;
+    for (int sw = 0; sw < nu; sw++)
+        for (int h = 0; h < ns; h++)
+            hipLaunchKernelGGL(k_mg_half, dim3(blocks_for(ncl)), dim3(256), 0, s, V, seq[h]);
+}
+
+static void mg_vcycle(iemic_ctx* c, int q)
+{
+    BlockGS& gs = c->gs;
+    hipStream_t s = c->stream;
+    if (q == gs.mg_nlev - 1) {
+        const int N = 2 * gs.mg_n[q] * gs.mg_m[q] * c->l;
+        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
+                           gs.mg_b[q].p, gs.mg_z[q].p);
+        return;
+    }
+    const int nu = std::max(1, gs.mg_sweeps);
+    mg_smooth(c, q, nu);
+    const TsLev F = mg_view(c, q), C = mg_view(c, q + 1);
+    hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
+                       gs.mg_z[q + 1].p);
+    mg_vcycle(c, q + 1);
+    hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)F.n * F.mb * F.l)), dim3(256), 0, s, F, C);
+    mg_smooth(c, q, nu);
+}
+
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
 {
     BlockGS& gs = c->gs;
@@ -1089,12 +1590,13 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         rc |= gs.zt.alloc(next);
         rc |= gs.zs.alloc(next);
         rc |= gs.tcell.alloc(next);
+        rc |= gs.tsdiag.alloc((size_t)4 * next);
         if (rc) {
             set_error("block GS: out of device memory");
             return IEMIC_ENOMEM;
         }
         for (DevBuf<double>* bptr : {&gs.uvinv, &gs.tsinv, &gs.pw, &gs.rr, &gs.bts, &gs.tsoff, &gs.zt,
-                                     &gs.zs, &gs.tcell})
+                                     &gs.zs, &gs.tcell, &gs.tsdiag})
             HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         HIP_OK(hipMemsetAsync(gs.kmask.p, 0, sizeof(uint64_t) * gs.kmask.n, c->stream));
         gs.flags_h.clear();
@@ -1133,7 +1635,7 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     }
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        L, (int64_t)c->rowintcon, c->cfg.int_sign, c->d_intc.p, gs.uvinv.p,
-                       gs.tsinv.p, gs.pw.p);
+                       gs.tsinv.p, gs.pw.p, gs.tsdiag.p, next);
     hipLaunchKernelGGL(k_gslot_pack, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L, gs.gslot.p);
     if (c->nranks > 1) {
         if ((rc = halo_exchange_w(c, gs.uvinv.p, 4, 1))) return rc;
@@ -1177,13 +1679,17 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         const int rows = std::max(gs.bl + NBP + 1, gs.bl + gs.bu + 1);
         auto bytes = [&](int nb) { return (size_t)(rows + 256 / nb) * nb * sizeof(double); };
         const size_t lmax = 150 * 1024;
-        if (bytes(32) <= lmax) {
+        static const int force_nb = [] {
+            const char* e = getenv("IEMIC_INV_NB");
+            return e ? atoi(e) : 0;
+        }();
+        if (bytes(32) <= lmax && (force_nb == 0 || force_nb == 32)) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(32)));
             hipLaunchKernelGGL(k_band_inv_blk<32>, dim3((unsigned)((gs.ncol_own + 31) / 32)),
                                dim3(256), bytes(32), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
                                gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-        } else if (bytes(16) <= lmax) {
+        } else if (bytes(16) <= lmax && (force_nb == 0 || force_nb == 16)) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(16)));
             hipLaunchKernelGGL(k_band_inv_blk<16>, dim3((unsigned)((gs.ncol_own + 15) / 16)),
@@ -1200,10 +1706,70 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
             return IEMIC_EINVAL;
         }
     }
+    gs.ts_mg = opt ? std::max(0, opt->ts_mg) : 0;
+    gs.mg_sweeps = opt ? std::max(1, opt->mg_sweeps) : 1;
+    if (gs.ts_mg > 0 && (rc = mg_setup(c))) return rc;
+    gs.fp32 = opt ? (opt->schur_fp32 != 0) : 1;
+    gs.dyn_iters = opt ? std::max(1, opt->dyn_iters) : 1;
+    if (gs.fp32) {
+        gs.ldf = (gs.ncol_own + 3) & ~3;
+        const size_t nf = (size_t)gs.ncol * gs.ldf;
+        if (gs.sinvf.n < nf && gs.sinvf.alloc(nf)) return IEMIC_ENOMEM;
+        const int64_t tot = (int64_t)nf;
+        hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                           gs.sinv.p, gs.ncol, gs.ncol_own, gs.sinvf.p, gs.ldf);
+    }
+    if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
+        if (gs.dres.alloc(NE) || gs.zc.alloc(NE)) return IEMIC_ENOMEM;
+        HIP_OK(hipMemsetAsync(gs.dres.p, 0, sizeof(double) * NE, c->stream));
+        HIP_OK(hipMemsetAsync(gs.zc.p, 0, sizeof(double) * NE, c->stream));
+    }
     HIP_OK(hipGetLastError());
     gs.ready = 1;
     return 0;
 }
+
+/* dynamics block: z(U/V/W/P) from the right-hand side rr (steps 1-5 of the header) */
+static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
+{
+    BlockGS& gs = c->gs;
+    const Lay L = lay_of(c);
+    const unsigned gc = (unsigned)((c->nloc + 255) / 256);
+    const unsigned gij = (unsigned)((c->nloc / c->l + 255) / 256);
+    hipStream_t s = c->stream;
+    const bool band = c->nranks > 1;
+    int rc = 0;
+    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       rr, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
+    hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
+                       rr, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       rr, z, gs.tcell.p, L, 0);
+    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
+                       gs.pinned.p, gs.colv.p, L);
+    /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
+                       gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
+    if (gs.fp32)
+        hipLaunchKernelGGL(k_gemv_f, dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256), 0, s, gs.sinvf.p,
+                           gs.ncol, gs.ncol_own, gs.ldf, gs.colv_own.p, gs.colv2.p);
+    else
+        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
+                           gs.ncol, gs.ncol_own, gs.colv_own.p, gs.colv2.p);
+    if ((rc = allreduce_sum(c, gs.colv2.p, gs.ncol))) return rc;
+    hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
+                       gs.col_of_ij.p, gs.colv2.p, z, L);
+    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       rr, z, gs.tcell.p, L, 1);
+    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       gs.colv2.p, gs.tcell.p, z, L);
+    return 0;
+}
+
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d);
 
 int gs_apply(iemic_ctx* c, const double* r, double* z)
 {
@@ -1211,7 +1777,6 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     const Lay L = lay_of(c);
     const int n = c->n;
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
-    const unsigned gij = (unsigned)((c->nloc / c->l + 255) / 256);
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
     int rc = 0;
@@ -1220,35 +1785,37 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
-    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.rr.p, z, L);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
-    hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.rr.p, z, L);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.rr.p, z, gs.tcell.p, L, 0);
-    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                       gs.pinned.p, gs.colv.p, L);
-    /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
-                       gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
-    hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
-                       gs.ncol, gs.ncol_own, gs.colv_own.p, gs.colv2.p);
-    if ((rc = allreduce_sum(c, gs.colv2.p, gs.ncol))) return rc;
-    hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.col_of_ij.p, gs.colv2.p, z, L);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       gs.rr.p, z, gs.tcell.p, L, 1);
-    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.colv2.p, gs.tcell.p, z, L);
+    if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;
+    /* defect correction on the dynamics block: z_D += M_D^-1 (rr_D - A_DD z_D) */
+    for (int it = 1; it < gs.dyn_iters; it++) {
+        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* w, p of the neighbours */
+        if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
+        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
+        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zc.p, z, L);
+    }
+    if (band && gs.dyn_iters > 1 && (rc = halo_exchange(c, z, 1))) return rc;
+    if (gs.ts_mg > 0) {
+        /* T/S by aggregation-multigrid V-cycles on (zt, zs) with rhs bts */
+        if ((n & 1) == 0) {
+            hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                               gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
+        } else {
+            hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                               gs.bts.p, L);
+            HIP_OK(hipMemsetAsync(gs.zt.p, 0, sizeof(double) * c->next, s));
+            HIP_OK(hipMemsetAsync(gs.zs.p, 0, sizeof(double) * c->next, s));
+        }
+        for (int cyc = 0; cyc < gs.ts_mg; cyc++) mg_vcycle(c, 0);
+        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     const int nsw = std::max(1, gs.ts_sweeps);
     if ((n & 1) == 0) {
         /* colour-compacted symmetric red-black sweeps */
         const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
         hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                           gs.bc.p, gs.zt.p, gs.zs.p, L);
+                           gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
         const int seq[4] = {0, 1, 1, 0};
         for (int sw = 0; sw < nsw; sw++)
             for (int h = 0; h < 4; h++)

@@ -36,14 +36,17 @@ class Dist(C.Structure):
 
 class Krylov(C.Structure):
     _fields_ = [("tol", C.c_double), ("krylov_dim", C.c_int), ("max_restarts", C.c_int),
-                ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int)]
+                ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int),
+                ("dyn_iters", C.c_int), ("schur_fp32", C.c_int), ("ts_mg", C.c_int),
+                ("mg_sweeps", C.c_int)]
 
 
 class SolveInfo(C.Structure):
     _fields_ = [("iters", C.c_int), ("converged", C.c_int),
                 ("implicit_rel_res", C.c_double), ("explicit_rel_res", C.c_double),
                 ("t_prec_ms", C.c_double), ("t_spmv_ms", C.c_double),
-                ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double), ("reorth", C.c_int)]
+                ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double), ("reorth", C.c_int),
+                ("n_spmv", C.c_int)]
 
 
 class NewtonInfo(C.Structure):
@@ -110,6 +113,7 @@ def lib():
         "iemic_solve_dev": (C.c_int, [vp, vp, vp, P(Krylov), P(SolveInfo)]),
         "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
         "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
+        "iemic_time_spmv_cold": (C.c_int, [vp, C.c_int, vp, C.c_int64, PD]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -127,7 +131,7 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
-            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv")
+            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold")
 
 
 class IemicError(RuntimeError):

@@ -54,7 +54,9 @@ class Ocean:
         self.N = lib().iemic_nrows(h)
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
-              "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2"}
+              "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
+              "Dyn iterations": 2, "Schur fp32": True, "TS multigrid cycles": 1,
+              "Multigrid sweeps": 1}
         if solver_params:
             sp.update(solver_params)
         self.solver_params = sp
@@ -145,7 +147,9 @@ class Ocean:
         sp = self.solver_params
         return _lib.Krylov(float(sp["FGMRES tolerance"]), int(sp["FGMRES iterations"]),
                            int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
-                           int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0)
+                           int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0,
+                           int(sp["Dyn iterations"]), int(bool(sp["Schur fp32"])),
+                           int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]))
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""
@@ -209,4 +213,12 @@ class Ocean:
     def time_spmv(self, nrep: int = 20) -> float:
         ms = C.c_double()
         check(lib().iemic_time_spmv(self._h, int(nrep), C.byref(ms)), "iemic_time_spmv")
+        return ms.value
+
+    def time_spmv_cold(self, flush_ptr: int, flush_bytes: int, nrep: int = 10) -> float:
+        """Mean SpMV kernel ms with the Infinity Cache flushed (device memset of a caller
+        buffer) before each launch -- the in-solve, cold-cache rate."""
+        ms = C.c_double()
+        check(lib().iemic_time_spmv_cold(self._h, int(nrep), C.c_void_p(flush_ptr),
+                                         int(flush_bytes), C.byref(ms)), "iemic_time_spmv_cold")
         return ms.value

@@ -69,6 +69,14 @@ typedef struct {
     int prec;                    /* 0: none, 1: cell block-Jacobi, 2: block Gauss-Seidel */
     int ts_sweeps;               /* symmetric red-black sweeps on the T/S block      */
     int orth;                    /* 0: DCGS2 (default), 1: DGKS (Belos' default)     */
+    int dyn_iters;               /* block GS: defect-correction passes on the U/V/W/P */
+                                 /* block (<= 1: one pass, the plain block GS)        */
+    int schur_fp32;              /* block GS: Schur inverse stored in fp32 (GEMV bytes */
+                                 /* halved; accumulation in fp64)                     */
+    int ts_mg;                   /* block GS: T/S solve by this many aggregation-      */
+                                 /* multigrid V-cycles (0: ts_sweeps plain sweeps)    */
+    int mg_sweeps;               /* symmetric red-black sweeps before/after the coarse */
+                                 /* correction on every multigrid level               */
 } iemic_krylov;
 
 typedef struct {
@@ -78,6 +86,7 @@ typedef struct {
     double explicit_rel_res;     /* ||b - J x|| / ||b||  (Ocean.C:1140-1150)         */
     double t_prec_ms, t_spmv_ms, t_orth_ms, t_total_ms;
     int reorth;                  /* DGKS second passes taken                         */
+    int n_spmv;                  /* SpMV launches inside the Arnoldi loop (t_spmv_ms) */
 } iemic_solve_info;
 
 /* Latitude-band decomposition over several GPUs (one process and one context per GPU,
@@ -166,6 +175,10 @@ int iemic_newton_step(iemic_ctx* ctx, const iemic_krylov* opt, iemic_newton_info
 /* ---- profiling helpers (bench): time n launches of the SpMV kernel with HIP events
  * on the stream it runs on; returns mean kernel milliseconds. */
 int iemic_time_spmv(iemic_ctx* ctx, int nrep, double* ms_per_launch);
+/* Same, with the Infinity Cache flushed before every launch (a streaming read of
+ * flush_bytes of flush_dev on the library stream, outside the timed span): the cold rate. */
+int iemic_time_spmv_cold(iemic_ctx* ctx, int nrep, void* flush_dev, int64_t flush_bytes,
+                         double* ms_per_launch);
 
 #ifdef __cplusplus
 }

@@ -94,8 +94,11 @@ def test_global2_full_size(oracle_lib, Ocean):
 @pytest.mark.parametrize("name", ["test6x6x4", "natl8", "2dmoc", "2dmoc_run", "gateway16",
                                   "global4"])
 def test_block_gs_apply_matches_cpu(oracle_lib, Ocean, name):
-    """GPU block Gauss-Seidel apply (dense Schur inverse) == CPU twin (band solve)."""
-    c, oc, o, L = make(Ocean, oracle_lib, name, solver_params={"Preconditioner": 2, "TS sweeps": 3})
+    """GPU block Gauss-Seidel apply (dense fp64 Schur inverse) == CPU twin (band solve)."""
+    c, oc, o, L = make(Ocean, oracle_lib, name, solver_params={"Preconditioner": 2, "TS sweeps": 3,
+                                                               "Schur fp32": False,
+                                                               "Dyn iterations": 1,
+                                                               "TS multigrid cycles": 0})
     x = cf.synthetic_state(c, L, amp_ts=1e-3)
     oc.setState(x)
     oc.computeJacobian()
@@ -107,6 +110,79 @@ def test_block_gs_apply_matches_cpu(oracle_lib, Ocean, name):
     zc = P.apply(r)
     assert np.all(np.isfinite(z))
     assert np.max(np.abs(z - zc)) <= 1e-8 * np.max(np.abs(zc))
+
+
+@pytest.mark.parametrize("name", ["natl8", "gateway16", "global4"])
+def test_block_gs_fp32_schur(oracle_lib, Ocean, name):
+    """The fp32-stored Schur inverse (fp64 accumulation) changes the apply only at the
+    single-precision level of the depth-integrated pressure correction."""
+    c, oc, o, L = make(Ocean, oracle_lib, name, solver_params={"Preconditioner": 2, "TS sweeps": 3,
+                                                               "Schur fp32": True,
+                                                               "Dyn iterations": 1,
+                                                               "TS multigrid cycles": 0})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    oc.buildPreconditioner(force=True)
+    ov, _ = o.jacobian(x)
+    zc = oracle_lib.BlockGS(o, ov, 3).apply(cf.synthetic_vector(c, seed=3))
+    z = oc.applyPrecon(cf.synthetic_vector(c, seed=3))
+    assert np.all(np.isfinite(z))
+    assert np.max(np.abs(z - zc)) <= 1e-4 * np.max(np.abs(zc))
+
+
+@pytest.mark.parametrize("name,dyn", [("natl8", 2), ("gateway16", 3), ("global4", 2)])
+def test_dyn_defect_correction(oracle_lib, Ocean, name, dyn):
+    """Block GS with defect-correction passes on the dynamics block: a linear operator
+    (apply(a r1 + r2) = a apply(r1) + apply(r2)) that converges FGMRES in fewer steps."""
+    its = {}
+    for d in (1, dyn):
+        c, oc, o, L = make(Ocean, oracle_lib, name,
+                           solver_params={"Preconditioner": 2, "FGMRES iterations": 500,
+                                          "FGMRES tolerance": 1e-8, "Dyn iterations": d})
+        x = cf.synthetic_state(c, L, amp_ts=1e-3)
+        oc.setState(x)
+        oc.computeJacobian()
+        ov, _ = o.jacobian(x)
+        b = o.spmv(ov, cf.synthetic_vector(c, seed=5))
+        sol = oc.solve(b)
+        res = np.linalg.norm(b - o.spmv(ov, sol)) / np.linalg.norm(b)
+        assert oc.last_solve.converged == 1 and res <= 1e-7
+        its[d] = oc.last_solve.iters
+        if d > 1:
+            r1, r2 = cf.synthetic_vector(c, seed=3), cf.synthetic_vector(c, seed=4)
+            z = oc.applyPrecon(2.5 * r1 + r2)
+            zl = 2.5 * oc.applyPrecon(r1) + oc.applyPrecon(r2)
+            assert np.max(np.abs(z - zl)) <= 1e-9 * np.max(np.abs(zl))
+    assert its[dyn] <= its[1], its
+
+
+@pytest.mark.parametrize("name", ["natl8", "2dmoc", "gateway16", "global4"])
+def test_ts_multigrid(oracle_lib, Ocean, name):
+    """T/S solve by one aggregation-multigrid V-cycle instead of 12 plain sweeps: still a
+    linear preconditioner, FGMRES converges to 1e-8 in no more iterations."""
+    its = {}
+    for mg in (0, 1):
+        c, oc, o, L = make(Ocean, oracle_lib, name,
+                           solver_params={"Preconditioner": 2, "FGMRES iterations": 500,
+                                          "FGMRES tolerance": 1e-8, "TS multigrid cycles": mg,
+                                          "TS sweeps": 12})
+        x = cf.synthetic_state(c, L, amp_ts=1e-3)
+        oc.setState(x)
+        oc.computeJacobian()
+        ov, _ = o.jacobian(x)
+        b = o.spmv(ov, cf.synthetic_vector(c, seed=5))
+        sol = oc.solve(b)
+        res = np.linalg.norm(b - o.spmv(ov, sol)) / np.linalg.norm(b)
+        assert oc.last_solve.converged == 1 and res <= 1e-7, (mg, res)
+        its[mg] = oc.last_solve.iters
+        if mg:
+            r1, r2 = cf.synthetic_vector(c, seed=3), cf.synthetic_vector(c, seed=4)
+            z = oc.applyPrecon(2.5 * r1 + r2)
+            zl = 2.5 * oc.applyPrecon(r1) + oc.applyPrecon(r2)
+            assert np.max(np.abs(z - zl)) <= 1e-9 * np.max(np.abs(zl))
+            assert np.array_equal(oc.applyPrecon(r1), oc.applyPrecon(r1))   # deterministic
+    assert its[1] <= its[0] + 2, its
 
 
 @pytest.mark.parametrize("name,prec", [("test6x6x4", 1), ("test6x6x4", 2), ("natl8", 2), ("2dmoc", 2),
