@@ -252,16 +252,18 @@ constexpr int NBP = 16;
 
 __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int ncol, int bl, int bu,
                                                   int* __restrict__ piv, int* __restrict__ info,
-                                                  double* __restrict__ lpan)
+                                                  double* __restrict__ lpan, int stage_o)
 {
     extern __shared__ double lds[];
     const int W = 2 * bl + bu + 1;
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wave = tid >> 6, nwave = nthr >> 6;
-    double* P = lds;                              /* (NBP + bl) x NBP panel          */
-    double* U = lds + (NBP + bl) * NBP;           /* NBP x (bl + bu) block row U12   */
-    __shared__ int s_lp[NBP];
-    __shared__ int s_p;
+    /* panel rows padded to PS = NBP + 1 doubles: lanes walking a column hit distinct banks */
+    constexpr int PS = NBP + 1;
+    double* P = lds;                              /* (NBP + bl) x PS panel           */
+    double* U = lds + (NBP + bl) * PS;            /* NBP x (bl + bu) block row U12   */
+    double* Uo = U + NBP * (bl + bu);             /* NBP x (bl + bu) pivot rows below */
+    __shared__ int s_lp[NBP], s_slot[NBP];
     __shared__ double s_best;
     __shared__ int s_info;
     if (tid == 0) s_info = 0;
@@ -273,17 +275,19 @@ __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int n
         /* load the panel */
         for (int e = tid; e < nprow * NBP; e += nthr) {
             const int r = e / NBP, t = e % NBP;
-            P[e] = (t < nbk && r <= t + bl) ? A(k0 + r, k0 + t) : 0.0;
+            P[r * PS + t] = (t < nbk && r <= t + bl) ? A(k0 + r, k0 + t) : 0.0;
         }
         __syncthreads();
-        /* factorise the panel */
+        /* factorise the panel: wavefront 0 finds the pivot and interchanges the panel
+         * rows; then one thread per row below scales its multiplier and updates the rest
+         * of its row (two workgroup barriers per column) */
         for (int t = 0; t < nbk; t++) {
             const int rlast = min(t + bl, nprow - 1);
             if (wave == 0) {
                 double best = -1.0;
                 int bi = t;
                 for (int r = t + lane; r <= rlast; r += 64) {
-                    const double v = fabs(P[r * NBP + t]);
+                    const double v = fabs(P[r * PS + t]);
                     if (v > best) { best = v; bi = r; }
                 }
                 for (int off = 32; off > 0; off >>= 1) {
@@ -291,33 +295,34 @@ __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int n
                     const int oi = __shfl_down(bi, off, 64);
                     if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
                 }
-                if (lane == 0) { s_p = bi; s_best = best; }
+                best = __shfl(best, 0, 64);
+                const int rp = __shfl(bi, 0, 64);
+                if (best == 0.0) {
+                    if (lane == 0) {
+                        s_lp[t] = t;
+                        piv[k0 + t] = k0 + t;
+                        s_best = 0.0;
+                        if (s_info == 0) s_info = k0 + t + 1;
+                    }
+                } else {
+                    if (rp != t && lane < nbk) {
+                        const double x = P[t * PS + lane];
+                        P[t * PS + lane] = P[rp * PS + lane];
+                        P[rp * PS + lane] = x;
+                    }
+                    if (lane == 0) { s_lp[t] = rp; piv[k0 + t] = k0 + rp; s_best = best; }
+                }
             }
             __syncthreads();
-            const int rp = s_p;
             if (s_best == 0.0) {
-                if (tid == 0) {
-                    s_lp[t] = t;
-                    piv[k0 + t] = k0 + t;
-                    if (s_info == 0) s_info = k0 + t + 1;
-                }
                 __syncthreads();
                 continue;
             }
-            if (rp != t && tid < nbk) {
-                const double x = P[t * NBP + tid];
-                P[t * NBP + tid] = P[rp * NBP + tid];
-                P[rp * NBP + tid] = x;
-            }
-            if (tid == 0) { s_lp[t] = rp; piv[k0 + t] = k0 + rp; }
-            __syncthreads();
-            const double pivot = P[t * NBP + t];
-            for (int r = t + 1 + tid; r <= rlast; r += nthr) P[r * NBP + t] /= pivot;
-            __syncthreads();
-            const int ncl = nbk - t - 1;
-            for (int e = tid; e < (rlast - t) * ncl; e += nthr) {
-                const int r = t + 1 + e / ncl, cc = t + 1 + e % ncl;
-                P[r * NBP + cc] -= P[r * NBP + t] * P[t * NBP + cc];
+            const double pivot = P[t * PS + t];
+            for (int r = t + 1 + tid; r <= rlast; r += nthr) {
+                const double l = P[r * PS + t] / pivot;
+                P[r * PS + t] = l;
+                for (int cc = t + 1; cc < nbk; cc++) P[r * PS + cc] -= l * P[t * PS + cc];
             }
             __syncthreads();
         }
@@ -327,45 +332,94 @@ __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int n
         for (int e = tid; e < (NBP + bl) * NBP; e += nthr) {
             const int r = e / NBP, t = e % NBP;
             const bool in = r < nprow && t < nbk;
-            if (in && r <= t) A(k0 + r, k0 + t) = P[e];
-            Lp[e] = (in && r > t) ? P[e] : 0.0;
+            if (in && r <= t) A(k0 + r, k0 + t) = P[r * PS + t];
+            Lp[e] = (in && r > t) ? P[r * PS + t] : 0.0;
         }
-        /* row swaps of the trailing columns, in pivot order, one thread per column */
+        /* A12 (the panel rows right of the panel) and the rows below the panel that were
+         * chosen as pivots (distinct ones, slot s_slot[t]) are staged in LDS with coalesced
+         * loads; per column (one thread each) the interchanges in pivot order and
+         * U12 = L11^-1 A12 then run on LDS only, and the pivot rows are written back */
         const int jlo = k0 + nbk, jhi = min(k0 + nbk - 1 + bl + bu, ncol - 1);
-        for (int j = jlo + tid; j <= jhi; j += nthr)
+        const int ncu = jhi - jlo + 1;
+        const int LW = bl + bu;
+        if (tid == 0)
+            for (int t = 0; t < nbk; t++) {
+                int sl = -1;
+                if (s_lp[t] >= nbk) {
+                    sl = t;
+                    for (int u = 0; u < t; u++)
+                        if (s_lp[u] == s_lp[t]) { sl = s_slot[u]; break; }
+                }
+                s_slot[t] = sl;
+            }
+        for (int e = tid; e < nbk * ncu; e += nthr) {
+            const int t = e / ncu, jj = e % ncu, j = jlo + jj;
+            U[t * LW + jj] = (j <= k0 + t + bl + bu) ? A(k0 + t, j) : 0.0;
+        }
+        __syncthreads();
+        for (int e = tid; e < nbk * ncu; e += nthr) {
+            const int t = e / ncu, jj = e % ncu;
+            if (stage_o && s_slot[t] == t) Uo[t * LW + jj] = A(k0 + s_lp[t], jlo + jj);
+        }
+        __syncthreads();
+        for (int jj = tid; jj < ncu; jj += nthr) {
+            const int j = jlo + jj;
             for (int t = 0; t < nbk; t++) {
                 const int rp = s_lp[t];
                 if (rp == t || j > k0 + t + bl + bu) continue;
-                double& x = A(k0 + t, j);
-                double& y = A(k0 + rp, j);
+                double& x = U[t * LW + jj];
+                double& y = rp < nbk ? U[rp * LW + jj] : (stage_o ? Uo[s_slot[t] * LW + jj] : A(k0 + rp, j));
                 const double tmp = x; x = y; y = tmp;
             }
-        __syncthreads();
-        /* U12 = L11^-1 A12, one thread per column */
-        const int ncu = jhi - jlo + 1;
-        for (int jj = tid; jj < ncu; jj += nthr) {
-            const int j = jlo + jj;
             double u[NBP];
             for (int t = 0; t < nbk; t++) {
-                double v = (j <= k0 + t + bl + bu) ? A(k0 + t, j) : 0.0;
-                for (int q = 0; q < t; q++) v -= P[t * NBP + q] * u[q];
+                double v = U[t * LW + jj];
+                for (int q = 0; q < t; q++) v -= P[t * PS + q] * u[q];
                 u[t] = v;
-                U[t * (bl + bu) + jj] = v;
+                U[t * LW + jj] = v;
                 if (j <= k0 + t + bl + bu) A(k0 + t, j) = v;
             }
         }
         __syncthreads();
-        /* A22 -= L21 U12 over rows k0+nbk .. pend */
-        for (int r = nbk + wave; r < nprow; r += nwave) {
-            const int i = k0 + r;
-            double l[NBP];
-            bool any = false;
-            for (int t = 0; t < nbk; t++) { l[t] = P[r * NBP + t]; any |= l[t] != 0.0; }
-            if (!any) continue;
-            for (int jj = lane; jj < ncu; jj += 64) {
-                double acc = 0.0;
-                for (int t = 0; t < nbk; t++) acc += l[t] * U[t * (bl + bu) + jj];
-                A(i, jlo + jj) -= acc;
+        for (int e = tid; e < nbk * ncu; e += nthr) {
+            const int t = e / ncu, jj = e % ncu;
+            if (stage_o && s_slot[t] == t) A(k0 + s_lp[t], jlo + jj) = Uo[t * LW + jj];
+        }
+        __syncthreads();
+        /* A22 -= L21 U12 over rows k0+nbk .. pend: 4x4 register tiles (lanes along the
+         * columns, so the 16 global loads of a tile are coalesced across the wavefront and
+         * issued together before the rank-NBP update) */
+        {
+            const int nr2 = nprow - nbk;
+            const int tr = (nr2 + 3) / 4, tc = (ncu + 3) / 4;
+            for (int e = tid; e < tr * tc; e += nthr) {
+                const int r0 = nbk + 4 * (e / tc), j0 = 4 * (e % tc);
+                double a[4][4];
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const int r = r0 + x, jj = j0 + y;
+                        a[x][y] = (r < nprow && jj < ncu) ? A(k0 + r, jlo + jj) : 0.0;
+                    }
+                for (int t = 0; t < nbk; t++) {
+                    double lv[4], uv[4];
+#pragma unroll
+                    for (int x = 0; x < 4; x++) lv[x] = r0 + x < nprow ? P[(r0 + x) * PS + t] : 0.0;
+#pragma unroll
+                    for (int y = 0; y < 4; y++) uv[y] = j0 + y < ncu ? U[t * (bl + bu) + j0 + y] : 0.0;
+#pragma unroll
+                    for (int x = 0; x < 4; x++)
+#pragma unroll
+                        for (int y = 0; y < 4; y++) a[x][y] -= lv[x] * uv[y];
+                }
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const int r = r0 + x, jj = j0 + y;
+                        if (r < nprow && jj < ncu) A(k0 + r, jlo + jj) = a[x][y];
+                    }
             }
         }
         __syncthreads();
@@ -453,6 +507,155 @@ __global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__
             const double x = (y - t) / ar[i];
             win[(i % R2) * NB + col] = x;
             if (on) Xs[(int64_t)i * nq + q] = x;
+        }
+        __syncthreads();
+    }
+}
+
+/* Panel-blocked variant of k_band_inv_blk (same inputs, same output): per panel of NBP
+ * rows the triangular part is solved by the NB lanes of wavefront 0 (one right-hand side
+ * per lane, no workgroup barrier inside the panel) and the coupling to the rest of the
+ * window is one parallel block update, so a panel costs ~3 barriers instead of 2 per row.
+ *   forward : swaps, L11 solve (wave 0), rows below -= L21 y_panel (all threads)
+ *   backward: t = U(panel, right of panel) x (all threads), U11 solve (wave 0)          */
+template <int NB, bool STAGE>
+__global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__ ab,
+                                                      const double* __restrict__ lpan,
+                                                      const int* __restrict__ piv, int ncol,
+                                                      int bl, int bu, const int* __restrict__ cols,
+                                                      int nq, double* __restrict__ Xs)
+{
+    extern __shared__ double lds[];
+    constexpr int G = 256 / NB;              /* row groups */
+    const int W = 2 * bl + bu + 1;
+    const int col = threadIdx.x % NB, grp = threadIdx.x / NB;
+    const int q0 = blockIdx.x * NB;
+    const int q = q0 + col;
+    const bool on = q < nq;
+    const int c0 = cols[q0];
+    const int c = on ? cols[q] : -1;
+    const int R1 = bl + NBP + 1, R2 = bl + bu + 1;
+    double* red = lds;                       /* NBP x NB panel sums                     */
+    double* win = lds + NBP * NB;            /* ring buffer                             */
+    /* STAGE: the panel's multipliers (forward) / U rows (backward) are copied to LDS with
+     * coalesced loads once per panel, so the inner loops read LDS instead of chains of
+     * dependent global loads */
+    double* ysh = win + (size_t)max(R1, R2) * NB;   /* NBP x NB forward results of a panel */
+    double* stg = ysh + NBP * NB;
+    /* ---- forward ---- */
+    const int kst = (max(0, c0 - bl - NBP + 1) / NBP) * NBP;
+    for (int r = kst + grp; r <= min(kst + NBP - 1 + bl, ncol - 1); r += G)
+        win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
+    for (int k0 = kst; k0 < ncol; k0 += NBP) {
+        const int nbk = min(NBP, ncol - k0);
+        const int pend = min(k0 + nbk - 1 + bl, ncol - 1);
+        const int nprow = pend - k0 + 1;
+        const double* Lg = lpan + (int64_t)(k0 / NBP) * (NBP + bl) * NBP;
+        if (STAGE)
+            for (int e = threadIdx.x; e < nprow * NBP; e += 256) stg[e] = Lg[e];
+        const double* Lp = STAGE ? stg : Lg;
+        const int kb = k0 % R1;                  /* ring slot of row k0 */
+        auto slot = [&](int r) { const int v = kb + r; return v >= R1 ? v - R1 : v; };  /* r < R1 */
+        __syncthreads();
+        if (grp == 0) {
+            /* interchanges, then the unit-lower L11 solve, one column per lane */
+            for (int t = 0; t < nbk; t++) {
+                const int rp = piv[k0 + t] - k0;
+                if (rp != t) {
+                    double* a = win + slot(t) * NB + col;
+                    double* b = win + slot(rp) * NB + col;
+                    const double x = *a; *a = *b; *b = x;
+                }
+            }
+            double y[NBP];
+#pragma unroll
+            for (int t = 0; t < NBP; t++) {
+                if (t < nbk) {
+                    double v = win[slot(t) * NB + col];
+#pragma unroll
+                    for (int u = 0; u < t; u++) v -= Lp[t * NBP + u] * y[u];
+                    y[t] = v;
+                    win[slot(t) * NB + col] = v;
+                }
+            }
+        }
+        __syncthreads();
+        /* rows below the panel: -= L21 y (panel values held in registers) */
+        {
+            double y[NBP];
+#pragma unroll
+            for (int t = 0; t < NBP; t++) y[t] = t < nbk ? win[slot(t) * NB + col] : 0.0;
+            for (int r = nbk + grp; r < nprow; r += G) {
+                const double* lr = Lp + r * NBP;
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int t = 0; t < NBP; t += 2) {
+                    a0 += lr[t] * y[t];
+                    a1 += lr[t + 1] * y[t + 1];
+                }
+                win[slot(r) * NB + col] -= a0 + a1;
+            }
+        }
+        /* panel rows are final: y -> X */
+        for (int t = grp; t < nbk; t += G)
+            if (on) Xs[(int64_t)(k0 + t) * nq + q] = win[slot(t) * NB + col];
+        __syncthreads();
+        for (int r = pend + 1 + grp; r <= min(k0 + 2 * NBP - 1 + bl, ncol - 1); r += G)
+            win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
+    }
+    if (grp == 0 && on)
+        for (int r = 0; r < kst; r++) Xs[(int64_t)r * nq + q] = 0.0;
+    /* ---- backward, panels from the bottom: ring of R2 = bl + bu + 1 rows ---- */
+    __syncthreads();
+    const int npan = (ncol + NBP - 1) / NBP;
+    const int WU = bl + bu + 1;              /* staged U row: columns i .. i+bl+bu */
+    for (int pn = npan - 1; pn >= 0; pn--) {
+        const int i0 = pn * NBP, i1 = min(ncol, i0 + NBP);
+        const int nr = i1 - i0;
+        if (STAGE) {
+            for (int e = threadIdx.x; e < nr * WU; e += 256) {
+                const int rr = e / WU, jj = e % WU;
+                const int i = i0 + rr;
+                stg[e] = (i + jj < ncol) ? ab[(int64_t)i * W + bl + jj] : 0.0;
+            }
+            __syncthreads();
+        }
+        /* t_i = sum_{j >= i1} U_ij x_j for the panel rows (rows x column per thread);
+         * the forward results y_i of the panel rows are fetched alongside */
+        for (int e = grp; e < nr; e += G) {
+            ysh[e * NB + col] = on ? Xs[(int64_t)(i0 + e) * nq + q] : 0.0;
+            const int i = i0 + e;
+            const int jend = min(i + bl + bu, ncol - 1);
+            double s0 = 0.0, s1 = 0.0;
+            const double* ur = STAGE ? stg + e * WU - i : ab + (int64_t)i * W + (bl - i);
+            /* x_j sits at ring slot j % R2: walk the slots with a wrap instead of a modulo */
+            int js = i1 % R2;
+            int j = i1;
+            for (; j + 1 <= jend; j += 2) {
+                const int js1 = js + 1 == R2 ? 0 : js + 1;
+                s0 += ur[j] * win[js * NB + col];
+                s1 += ur[j + 1] * win[js1 * NB + col];
+                js = js1 + 1 == R2 ? 0 : js1 + 1;
+            }
+            if (j <= jend) s0 += ur[j] * win[js * NB + col];
+            red[e * NB + col] = s0 + s1;
+        }
+        __syncthreads();
+        if (grp == 0) {
+            for (int i = i1 - 1; i >= i0; i--) {
+                const double* ar = STAGE ? stg + (i - i0) * WU - i : ab + (int64_t)i * W + (bl - i);
+                double t = red[(i - i0) * NB + col];
+                const int jend = min(i1 - 1, i + bl + bu);
+                int js = (i + 1) % R2;
+                for (int j = i + 1; j <= jend; j++) {
+                    t += ar[j] * win[js * NB + col];
+                    js = js + 1 == R2 ? 0 : js + 1;
+                }
+                const double yv = ysh[(i - i0) * NB + col];
+                const double x = (yv - t) / ar[i];
+                win[(i % R2) * NB + col] = x;
+                if (on) Xs[(int64_t)i * nq + q] = x;
+            }
         }
         __syncthreads();
     }
@@ -579,6 +782,98 @@ __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restr
         }
         if (pa) z[NUN * cell + PP] = p;
         pabove = pa ? p : 0.0;
+    }
+}
+
+/* Column recurrences as parallel scans: P lanes (P = power of two >= l) per water column,
+ * lane = level k.  Each level is an affine map x_k = A_k + B_k x_{k+-1}; a Hillis-Steele
+ * scan over the lanes composes them, so the l-step dependency chain becomes log2(P)
+ * shuffle steps and every load is issued at once. */
+template <int P>
+__global__ void __launch_bounds__(256) k_gs_ptil_scan(const double* __restrict__ val,
+                                                      const uint8_t* __restrict__ known,
+                                                      const int* __restrict__ col_of_ij,
+                                                      const double* __restrict__ rr,
+                                                      double* __restrict__ z, Lay L)
+{
+    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int k = threadIdx.x % P;
+    if (t_ >= (int)(L.nloc / L.l)) return;                  /* whole column groups exit */
+    const int ij = L.jb0 * L.n + t_;
+    if (col_of_ij[ij] < 0) return;
+    const int i = ij % L.n, j = ij / L.n;
+    const int64_t ncell = L.nloc;
+    double A = 0.0, B = 0.0;
+    bool pa = false;
+    int64_t cell = 0;
+    if (k < L.l) {
+        cell = ecell(L, i, j, k);
+        pa = !known[NUN * cell + PP];
+        if (pa && k < L.l - 1 && !known[NUN * cell + WW]) {
+            const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
+            const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
+            if (g0 != 0.0) {
+                A = rr[NUN * cell + WW] / g0;
+                B = -g1 / g0;
+            }
+        }
+    }
+    /* suffix composition from the top: p_k = A_k + B_k p_{k+1}, p_l = 0 */
+#pragma unroll
+    for (int d = 1; d < P; d <<= 1) {
+        const double A2 = __shfl_down(A, d, P), B2 = __shfl_down(B, d, P);
+        if (k + d < P) {
+            A = A + B * A2;
+            B = B * B2;
+        }
+    }
+    if (pa) z[NUN * cell + PP] = A;
+}
+
+template <int P>
+__global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ val,
+                                                    const uint8_t* __restrict__ known,
+                                                    const int* __restrict__ col_of_ij,
+                                                    const double* __restrict__ pbar,
+                                                    const double* __restrict__ crhs,
+                                                    double* __restrict__ z, Lay L)
+{
+    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int k = threadIdx.x % P;
+    if (t_ >= (int)(L.nloc / L.l)) return;
+    const int ij = L.jb0 * L.n + t_;
+    const int c = col_of_ij[ij];
+    if (c < 0) return;
+    const int i = ij % L.n, j = ij / L.n;
+    const int64_t ncell = L.nloc;
+    double A = 0.0, B = 0.0;
+    bool pa = false, wa = false;
+    int64_t cell = 0;
+    if (k < L.l) {
+        cell = ecell(L, i, j, k);
+        pa = !known[NUN * cell + PP];
+        wa = !known[NUN * cell + WW];
+        if (pa && wa) {
+            const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
+            const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
+            if (a != 0.0) {
+                A = crhs[cell] / a;
+                B = -b / a;
+            }
+        }
+    }
+    /* prefix composition from the bottom: w_k = A_k + B_k w_{k-1}, w_{-1} = 0 */
+#pragma unroll
+    for (int d = 1; d < P; d <<= 1) {
+        const double A2 = __shfl_up(A, d, P), B2 = __shfl_up(B, d, P);
+        if (k >= d) {
+            A = A + B * A2;
+            B = B * B2;
+        }
+    }
+    if (k < L.l) {
+        if (pa) z[NUN * cell + PP] += pbar[c];
+        if (wa) z[NUN * cell + WW] = pa ? A : 0.0;
     }
 }
 
@@ -1520,7 +1815,7 @@ static int mg_setup(iemic_ctx* c)
     return h2d(c, gs.mg_cinv.p, X.data(), sizeof(double) * X.size());
 }
 
-static void mg_smooth(iemic_ctx* c, int q, int nu)
+static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
 {
     BlockGS& gs = c->gs;
     hipStream_t s = c->stream;
@@ -1539,10 +1834,16 @@ static void mg_smooth(iemic_ctx* c, int q, int nu)
     const bool four = V.periodic && (V.n & 1);
     const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
     const int* seq = four ? seq4 : seq2;
-    const int ns = four ? 8 : 4;
+    int ns = four ? 8 : 4, h0 = 0;
+    /* coarse levels: forward colour order before the coarse correction, backward after
+     * it (the V-cycle as a whole stays symmetric; half the launches of full sweeps) */
+    if (q > 0) {
+        ns /= 2;
+        h0 = post ? ns : 0;
+    }
     for (int sw = 0; sw < nu; sw++)
         for (int h = 0; h < ns; h++)
-            hipLaunchKernelGGL(k_mg_half, dim3(blocks_for(ncl)), dim3(256), 0, s, V, seq[h]);
+            hipLaunchKernelGGL(k_mg_half, dim3(blocks_for(ncl)), dim3(256), 0, s, V, seq[h0 + h]);
 }
 
 static void mg_vcycle(iemic_ctx* c, int q)
@@ -1556,13 +1857,13 @@ static void mg_vcycle(iemic_ctx* c, int q)
         return;
     }
     const int nu = std::max(1, gs.mg_sweeps);
-    mg_smooth(c, q, nu);
+    mg_smooth(c, q, nu, false);
     const TsLev F = mg_view(c, q), C = mg_view(c, q + 1);
     hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
                        gs.mg_z[q + 1].p);
     mg_vcycle(c, q + 1);
     hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)F.n * F.mb * F.l)), dim3(256), 0, s, F, C);
-    mg_smooth(c, q, nu);
+    mg_smooth(c, q, nu, true);
 }
 
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
@@ -1657,7 +1958,12 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     /* every band built the rows of its own columns: the sum is the whole Schur band */
     if ((rc = allreduce_sum(c, gs.band.p, gs.ncol * W))) return rc;
     {
-        const size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * NBP + (size_t)NBP * (gs.bl + gs.bu));
+        size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * (NBP + 1) + (size_t)2 * NBP * (gs.bl + gs.bu));
+        int stage_o = 1;                        /* pivot rows below the panel staged in LDS */
+        if (lb > 150 * 1024) {
+            lb -= sizeof(double) * (size_t)NBP * (gs.bl + gs.bu);
+            stage_o = 0;
+        }
         if (lb > 150 * 1024) {
             set_error("block GS: Schur band too wide for the LDS band LU");
             return IEMIC_EINVAL;
@@ -1665,7 +1971,7 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         HIP_OK(hipFuncSetAttribute((const void*)k_band_lu, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lb));
         hipLaunchKernelGGL(k_band_lu, dim3(1), dim3(1024), lb, c->stream, gs.band.p, gs.ncol, gs.bl,
-                           gs.bu, gs.piv.p, gs.info.p, gs.lpan.p);
+                           gs.bu, gs.piv.p, gs.info.p, gs.lpan.p, stage_o);
     }
     int info = 0;
     HIP_OK(hipGetLastError());
@@ -1683,6 +1989,45 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
             const char* e = getenv("IEMIC_INV_NB");
             return e ? atoi(e) : 0;
         }();
+        static const bool old_inv = getenv("IEMIC_INV_OLD") != nullptr;
+        if (!old_inv) {
+            /* panel-blocked inverse: LDS = panel sums + ring of max(bl+NBP+1, bl+bu+1) rows
+             * (+ the staged panel multipliers / U rows when they fit) */
+            const int ring = std::max(gs.bl + NBP + 1, gs.bl + gs.bu + 1);
+            const size_t stg = (size_t)std::max((NBP + gs.bl) * NBP, NBP * (gs.bl + gs.bu + 1));
+            auto pbytes = [&](int nb, bool st) {
+                return ((size_t)(ring + 2 * NBP) * nb + (st ? stg : 0)) * sizeof(double);
+            };
+            int nb = 0;
+            bool st = false;
+            for (int cand : {32, 16})
+                for (bool sv : {true, false})
+                    if (!nb && pbytes(cand, sv) <= lmax && (force_nb == 0 || force_nb == cand)) {
+                        nb = cand;
+                        st = sv;
+                    }
+            if (!nb) {
+                set_error("block GS: Schur band too wide for the LDS inverse");
+                return IEMIC_EINVAL;
+            }
+            const unsigned nblk = (unsigned)((gs.ncol_own + nb - 1) / nb);
+            const size_t lb = pbytes(nb, st);
+            const void* fn = nb == 32 ? (st ? (const void*)k_band_inv_pan<32, true> : (const void*)k_band_inv_pan<32, false>)
+                                      : (st ? (const void*)k_band_inv_pan<16, true> : (const void*)k_band_inv_pan<16, false>);
+            HIP_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
+            if (nb == 32 && st)
+                hipLaunchKernelGGL((k_band_inv_pan<32, true>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
+                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
+            else if (nb == 32)
+                hipLaunchKernelGGL((k_band_inv_pan<32, false>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
+                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
+            else if (st)
+                hipLaunchKernelGGL((k_band_inv_pan<16, true>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
+                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
+            else
+                hipLaunchKernelGGL((k_band_inv_pan<16, false>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
+                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
+        } else
         if (bytes(32) <= lmax && (force_nb == 0 || force_nb == 32)) {
             HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(32)));
@@ -1739,8 +2084,21 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
     int rc = 0;
-    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       rr, z, L);
+    const int64_t ncolb = c->nloc / c->l;                        /* water columns of the band */
+    const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : (c->l <= 64 ? 64 : 0));
+    const unsigned gsc = (unsigned)((ncolb * std::max(Pl, 1) + 255) / 256);
+    if (Pl == 0)
+        hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                           rr, z, L);
+    else if (Pl == 16)
+        hipLaunchKernelGGL(k_gs_ptil_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, rr, z, L);
+    else if (Pl == 32)
+        hipLaunchKernelGGL(k_gs_ptil_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, rr, z, L);
+    else
+        hipLaunchKernelGGL(k_gs_ptil_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, rr, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        rr, z, L);
@@ -1764,8 +2122,18 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
     hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
                        rr, z, gs.tcell.p, L, 1);
-    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.colv2.p, gs.tcell.p, z, L);
+    if (Pl == 0)
+        hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                           gs.colv2.p, gs.tcell.p, z, L);
+    else if (Pl == 16)
+        hipLaunchKernelGGL(k_gs_pw_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
+    else if (Pl == 32)
+        hipLaunchKernelGGL(k_gs_pw_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
+    else
+        hipLaunchKernelGGL(k_gs_pw_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
     return 0;
 }
 
