@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="global2")
+    p.add_argument("--mixing", type=int, default=1,
+                   help="THCM 'Mixing' (vmix): 1 as in run/ocean/global/ocean_params.xml")
     p.add_argument("--prec", type=int, default=2, help="0 none, 1 block Jacobi, 2 block GS")
     p.add_argument("--amp-ts", type=float, default=1e-3,
                    help="T/S amplitude of the synthetic state (DESIGN.md: benchmark state)")
@@ -164,7 +166,7 @@ def main():
     from iemic import config as cf
     from iemic.ocean import Ocean
 
-    cfg = cf.preset(args.config, mixing=0)
+    cfg = cf.preset(args.config, mixing=args.mixing)
     sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
           "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth,
@@ -247,7 +249,7 @@ def main():
         "higher_is_better": False, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": (f"synthetic (splitmix64 seed 20261015 state, u,v,w,p ~ U(+-1e-3), T,S ~ "
                  f"U(+-{args.amp_ts:g}); Combined Forcing 0.5)"),
-        "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing=0, one Newton "
+        "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing={args.mixing}, one Newton "
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,

@@ -10,6 +10,9 @@
  *   forcing (forcing.F90:4-218) -> k_forcing (+ k_qint for the flux corrections).
  * Compiled with -ffp-contract=off: values are bit-identical to the reference.
  */
+#include <cmath>
+#include <vector>
+
 #include "common.h"
 
 namespace iemic {
@@ -139,8 +142,51 @@ __global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* 
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* vmix_control (mix_imp.f:131-166) for Mixing = 2: the first evaluation fixes whether T
+ * and S mix (L2 norm of the field > 1e-12, summed over the bands); and the restated
+ * subset of vmix_fun must cover the current parameters */
+static int mix_control(iemic_ctx* c, const double* x_dev)
+{
+    host::Setup& su = c->su;
+    if (su.cfg.vmix == 0) return 0;
+    if (su.cfg.vmix == 2 && !su.vmix_fix) {
+        std::vector<double> h((size_t)c->nerows);
+        int rc = d2h(c, h.data(), x_dev, sizeof(double) * h.size());
+        if (rc) return rc;
+        double sq[2] = {0.0, 0.0};
+        for (int64_t lc = 0; lc < c->nloc; lc++) {
+            const double t = h[NUN * (c->own0 + lc) + TT], sv = h[NUN * (c->own0 + lc) + SS];
+            sq[0] += t * t;
+            sq[1] += sv * sv;
+        }
+        if (c->nranks > 1) {
+            if ((rc = h2d(c, c->d_red.p, sq, sizeof(sq)))) return rc;
+            if ((rc = allreduce_sum(c, c->d_red.p, 2))) return rc;
+            if ((rc = d2h(c, sq, c->d_red.p, sizeof(sq)))) return rc;
+        }
+        su.vmix_t = std::sqrt(sq[0]) > 1.0e-12;
+        su.vmix_s = std::sqrt(sq[1]) > 1.0e-12;
+        /* vmix_control partitions only when T mixes (mix_imp.f:158): salinity-only mixing
+         * stays off; temperature-only mixing (zero salinity field) is not restated */
+        if (!su.vmix_t) su.vmix_s = 0;
+        su.vmix_fix = 1;
+        if (su.vmix_t && !su.vmix_s) {
+            set_error("Mixing = 2 with a zero salinity field is not supported");
+            return IEMIC_EINVAL;
+        }
+    }
+    if ((su.vmix_t || su.vmix_s) && !su.vmix_supported()) {
+        set_error("vertical mixing: neutral physics / Gent-McWilliams / energetically consistent "
+                  "mixing (MIXP, MKAP != 0 or ALPC != 1) are not restated");
+        return IEMIC_EINVAL;
+    }
+    return 0;
+}
+
 int assemble_jacobian(iemic_ctx* c, const double* x_dev)
 {
+    int rc = mix_control(c, x_dev);
+    if (rc) return rc;
     Geo g = c->geo();
     dim3 blk(128), grd((unsigned)((c->nloc + 127) / 128), NUN);
     hipLaunchKernelGGL(k_jacobian, grd, blk, 0, c->stream, g, x_dev, c->d_val.p, c->nloc,
@@ -154,6 +200,8 @@ int assemble_jacobian(iemic_ctx* c, const double* x_dev)
 
 int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev)
 {
+    int rc0 = mix_control(c, x_dev);
+    if (rc0) return rc0;
     Geo g = c->geo();
     dim3 blk(128), grd((unsigned)((c->nloc + 127) / 128), NUN);
     hipLaunchKernelGGL(k_rhs, grd, blk, 0, c->stream, g, x_dev, c->d_frc.p, F_dev, c->nloc);

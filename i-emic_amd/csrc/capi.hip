@@ -156,8 +156,8 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
         set_error("iemic_create: no HIP device available (the library never runs on the CPU)");
         return IEMIC_ENODEV;
     }
-    if (grid->vmix != 0) {
-        set_error("iemic_create: Mixing != 0 not implemented yet (SURVEY.md §8f row 1)");
+    if (grid->vmix < 0 || grid->vmix > 2) {
+        set_error("iemic_create: Mixing must be 0, 1 or 2");
         return IEMIC_EINVAL;
     }
     if (grid->n < 3 || grid->m < 2 || grid->l < 2) {
@@ -194,6 +194,7 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     const int n = c->n, m = c->m, l = c->l;
     const size_t nl = (size_t)(n + 2) * (m + 2) * (l + 2);
     c->su.init(*grid, landm, jb0, jb1);
+    c->su.vmix_init();
     c->nloc = c->su.nloc;
     c->nlrows = NUN * c->nloc;
     c->next = c->su.next;

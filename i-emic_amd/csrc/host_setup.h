@@ -57,6 +57,21 @@ inline double wfun(double yy)
 
 struct Setup {
     iemic_grid cfg;
+    /* m_mix flags (mix_imp.f vmix_init 58-109): Mixing 1 mixes T and S from the start;
+     * Mixing 2 decides at the first evaluation (vmix_control, 131-166) */
+    int vmix_t = 0, vmix_s = 0, vmix_fix = 1;
+    void vmix_init()
+    {
+        vmix_t = vmix_s = cfg.vmix == 1;
+        vmix_fix = cfg.vmix != 2;
+    }
+    /* MIXP = MKAP = 0 and ALPC = 1 (usrc.F90:1169-1176 defaults): only the implicit
+     * vertical mixing term of vmix_fun is restated */
+    bool vmix_supported() const
+    {
+        return par[P_MIXP] == 0.0 && par[P_MKAP] == 0.0 &&
+               (1.0 - par[P_ALPC]) * par[P_ENER] * par[P_PE_V] == 0.0;
+    }
     int n = 0, m = 0, l = 0;
     double xmin = 0, xmax = 0, ymin = 0, ymax = 0, dx = 0, dy = 0, dz = 0;
     std::vector<double> y, yv, dfzT, dfzW;
@@ -362,6 +377,10 @@ struct Setup {
         g.dfzT = tab_p + 9 * M2;
         g.dfzW = tab_p + 9 * M2 + (l + 2);
         for (int i = 0; i < 31; i++) g.par[i] = par[i];
+        g.vmix_t = cfg.vmix != 0 && vmix_t;
+        g.vmix_s = cfg.vmix != 0 && vmix_s;
+        g.rho_mixing = cfg.rho_mixing;
+        g.alphaT = cfg.alpha_t;
         return g;
     }
 };

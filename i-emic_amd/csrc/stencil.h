@@ -129,6 +129,10 @@ struct Geo {
     const double* dfzT;             /* dfzT(k), k = 1..l (index 0 unused)               */
     const double* dfzW;             /* dfzW(k), k = 0..l                                */
     double par[31];                 /* par(1..30)                                       */
+    /* vertical mixing (mix_imp.f): T/S mixing flags (vmix_temp/vmix_salt after
+     * vmix_init/vmix_control), "Rho mixing", alphaT of the taper */
+    int vmix_t, vmix_s, rho_mixing;
+    double alphaT;
 };
 
 HD int LM(const Geo& g, int i, int j, int k)
@@ -845,6 +849,91 @@ HD void boundaries_row(const Geo& g, const CellCtx& c, double* A, bool& frc_zero
     }
 }
 
+
+/* ---- vertical mixing (mix_imp.f vmix_fun 231-562, vmix_jac 729-815) --------------
+ * Default mixing parameters (usrc.F90:1169-1176: MIXP = MKAP = 0, ALPC = 1; the host
+ * rejects others) leave the implicit convective vertical mixing of T and S:
+ *   Ftimp(k) = -tprstb(-drhodzt(k), SPL1) * P_VC * dtdzt(k)   (top face of cell k)
+ *   mix(T)   = (Ftimp(k) - Ftimp(k-1)) / (dz dfzT(k))
+ * and its Jacobian by forward differences (eps 1e-8) w.r.t. the T/S unknowns of the
+ * column neighbours k-1, k, k+1 (the only nonzero entries of the 27-point FD pattern). */
+HD double mix_isoc(const Geo& g, int i, int j, int k)
+{
+    const int lm = LM(g, i, j, k);
+    return (lm == OCEAN || lm == 3) ? 1.0 : 0.0;       /* OCEAN or PERIO */
+}
+HD void mix_face(const Geo& g, int i, int j, int k, double t0, double t1, double s0, double s1,
+                 double& ft, double& fs)
+{
+    const double lambda = g.par[P_LAMB], xes = g.par[P_NLES], kvc = g.par[P_P_VC];
+    const double sp1 = g.par[P_SPL1];
+    if (kvc == 0.0) { ft = fs = 0.0; return; }
+    const double r0 = lambda * s0 - t0 - xes * (ALPT1 * t0 + ALPT2 * t0 * t0 - ALPT3 * t0 * t0 * t0);
+    const double r1 = lambda * s1 - t1 - xes * (ALPT1 * t1 + ALPT2 * t1 * t1 - ALPT3 * t1 * t1 * t1);
+    const double iso = mix_isoc(g, i, j, k + 1) * mix_isoc(g, i, j, k);
+    const double dzw = g.dz * g.dfzW[k];
+    const double dtdz = iso * (t1 - t0) / dzw, dsdz = iso * (s1 - s0) / dzw;
+    const double drdz = iso * (r1 - r0) / dzw;
+    /* tprstb(-drhodzt, SPL1) (mix_imp.f:836-856) */
+    const double fac = g.alphaT * sp1;
+    const double xx = -(-drdz) * fac;
+    const double th = tanh(xx * xx * xx);
+    const double tpr = th > 0.0 ? th : 0.0;
+    ft = -tpr * kvc * dtdz;
+    fs = -tpr * kvc * dsdz;
+}
+template <int R>
+HD double mix_row(const Geo& g, int i, int j, int k, const double* t3, const double* s3)
+{
+    if ((R == TT && !g.vmix_t) || (R == SS && !g.vmix_s)) return 0.0;
+    const double lambda = g.par[P_LAMB], xes = g.par[P_NLES];
+    double ftk, fsk, ftm = 0.0, fsm = 0.0;
+    mix_face(g, i, j, k, t3[1], t3[2], s3[1], s3[2], ftk, fsk);
+    if (k >= 2) mix_face(g, i, j, k - 1, t3[0], t3[1], s3[0], s3[1], ftm, fsm);
+    if (g.rho_mixing && xes == 0.0) {
+        if (R == TT) return ((ftk - ftm) - (fsk - fsm) * lambda) / (2.0 * g.dz * g.dfzT[k]) + 0.0;
+        return ((fsk - fsm) - (ftk - ftm) / lambda) / (2.0 * g.dz * g.dfzT[k]) + 0.0;
+    }
+    if (R == TT) return (ftk - ftm) / (g.dz * g.dfzT[k]) + 0.0;
+    return (fsk - fsm) / (g.dz * g.dfzT[k]) + 0.0;
+}
+HD void mix_col(const Geo& g, const double* x, int i, int j, int k, double* t3, double* s3)
+{
+    for (int d = 0; d < 3; d++) {
+        t3[d] = ts_arr(g, x, TT, i, j, k - 1 + d);
+        s3[d] = ts_arr(g, x, SS, i, j, k - 1 + d);
+    }
+}
+/* vmix_jac contributions of row R of an OCEAN cell, added to the slots after nlin_jac */
+template <int R>
+HD void mix_jac_row(const Geo& g, const double* x, int i, int j, int k, double* A)
+{
+    const double eps = 1.0e-08;
+    double t3[3], s3[3];
+    mix_col(g, x, i, j, k, t3, s3);
+    const double m0 = mix_row<R>(g, i, j, k, t3, s3);
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+    for (int d = 0; d < 3; d++) {
+        const int lm = LM(g, i, j, k - 1 + d);
+        if (lm != OCEAN && lm != 3) continue;
+        const int pos = d == 0 ? 14 : (d == 1 ? 5 : 23);
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+        for (int cv = TT; cv <= SS; cv++) {
+            if ((cv == TT && !g.vmix_t) || (cv == SS && !g.vmix_s)) continue;
+            double tp[3] = {t3[0], t3[1], t3[2]}, sp[3] = {s3[0], s3[1], s3[2]};
+            if (cv == TT) tp[d] = tp[d] + eps;
+            else sp[d] = sp[d] + eps;
+            const double m1 = mix_row<R>(g, i, j, k, tp, sp);
+            const int q = cv == TT ? ls<R>(pos, TT) : ls<R>(pos, SS);
+            A[q] = A[q] + (m1 - m0) / eps;
+        }
+    }
+}
+
 /* Full row: lin + nonlinear + boundaries + fillcolA threshold.  Returns slots in A. */
 template <int R, bool JAC>
 HD void assemble_row(const Geo& g, const double* x, int i, int j, int k, double* A, bool& frc_zero)
@@ -863,6 +952,9 @@ HD void assemble_row(const Geo& g, const double* x, int i, int j, int k, double*
         const int pos = pos_of(sl.di, sl.dj, sl.dk);
         double a = lin_val<R>(g, c, pos, sl.var);
         A[s] = nlin_add<R, JAC>(g, f, c, pos, sl.var, a);
+    }
+    if constexpr (JAC && (R == TT || R == SS)) {
+        if ((R == TT ? g.vmix_t : g.vmix_s) && LM(g, i, j, k) == OCEAN) mix_jac_row<R>(g, x, i, j, k, A);
     }
     frc_zero = false;
     boundaries_row<R>(g, c, A, frc_zero);
@@ -913,8 +1005,16 @@ HD double rhs_row_value(const Geo& g, const double* x, const double* frc, int i,
     }
     const int64_t row = NUN * cell + R;
     const double f = fz ? 0.0 : frc[row];
+    double mx = 0.0;
+    if constexpr (R == TT || R == SS) {
+        if (R == TT ? g.vmix_t : g.vmix_s) {
+            double t3[3], s3[3];
+            mix_col(g, x, i, j, k, t3, s3);
+            mx = mix_row<R>(g, i, j, k, t3, s3);
+        }
+    }
     /* B = -Au - mix + Frc - p0*(1-par(RESC))*ures; B *= (1-landm); F = -B */
-    const double b = -au - 0.0 + f - 0.0 * (1 - g.par[P_RESC]) * 0.0;
+    const double b = -au - mx + f - 0.0 * (1 - g.par[P_RESC]) * 0.0;
     return -(b * (1 - LM(g, i, j, k)));
 }
 

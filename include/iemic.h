@@ -59,6 +59,7 @@ typedef struct {
     int analyze_jacobian;        /* Ocean "Analyze Jacobian" mask fix (Ocean.C:505)  */
     int max_mask_fixes;          /* Ocean "Max mask fixes" (default 5)               */
     int device;                  /* HIP device ordinal                               */
+    int rho_mixing;              /* "Rho mixing" (vmix_fun: mix T and S as density)  */
 } iemic_grid;
 
 /* Krylov settings (Ocean.C:961-1020, getDefaultInitParameters 2232-2237). */

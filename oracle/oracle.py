@@ -39,7 +39,7 @@ class _Cfg(C.Structure):
                 ("iza", C.c_int), ("forcing_type", C.c_int), ("ih", C.c_int),
                 ("vmix", C.c_int), ("coriolis_on", C.c_int), ("alphaT", C.c_double),
                 ("alphaS", C.c_double), ("int_sign", C.c_int), ("nic", C.c_int),
-                ("mic", C.c_int)]
+                ("mic", C.c_int), ("rho_mixing", C.c_int)]
 
 
 def _p(a, t):
@@ -86,7 +86,8 @@ def cfg_struct(d: dict) -> _Cfg:
     return _Cfg(d["n"], d["m"], d["l"], d["xmin_deg"], d["xmax_deg"], d["ymin_deg"],
                 d["ymax_deg"], d["periodic"], d["hdim"], d["qz"], d["tres"], d["sres"],
                 d["ite"], d["its"], d["iza"], d["forcing_type"], d["ih"], d["vmix"],
-                d["coriolis_on"], d["alphaT"], d["alphaS"], d["int_sign"], d["nic"], d["mic"])
+                d["coriolis_on"], d["alphaT"], d["alphaS"], d["int_sign"], d["nic"], d["mic"],
+                d["rho_mixing"])
 
 
 class Oracle:

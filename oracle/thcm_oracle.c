@@ -53,6 +53,7 @@ struct orc {
     double *taux, *tauy, *tatm, *emip, *spert;
     double* Frc;                       /* forcing.F90 (before boundaries zeroing) */
     int rowintcon;                     /* 0-based, -1 if SRES != 0 */
+    int vmix_temp, vmix_salt, vmix_fix; /* m_mix flags (mix_imp.f vmix_init/control)   */
     /* maximal graph */
     int64_t* gptr;
     int* gcol;
@@ -1117,14 +1118,127 @@ static inline void shiftkk(const orc_t* o, int i, int j, int k, int kk, int* i2,
     }
 }
 
+
+/* ---- vertical mixing (mix_imp.f vmix_fun 231-562, vmix_jac 729-815) ---------------
+ * Restricted to the default mixing parameters of stpnt (usrc.F90:1169-1176): MIXP =
+ * MKAP = 0 (no neutral physics / Gent-McWilliams) and ALPC = 1 (no energetically
+ * consistent mixing), which leaves the implicit convective vertical mixing of T and S:
+ *   Ftimp(k) = -tprstb(-drhodzt(k), SPL1) * P_VC * dtdzt(k)   (top face of cell k)
+ *   mix(T)   = (Ftimp(k) - Ftimp(k-1)) / (dz dfzT(k))          (rho_mixing off)      */
+static int mix_supported(const orc_t* o)
+{
+    const double* par = o->par;
+    return par[MIXP] == 0.0 && par[MKAP] == 0.0 && (1.0 - par[ALPC]) * par[ENER] * par[PE_V] == 0.0;
+}
+static inline double isoc_(const orc_t* o, int i, int j, int k)
+{
+    const int lm = LM(o, i, j, k);
+    return (lm == OCEAN || lm == 3) ? 1.0 : 0.0;      /* OCEAN or PERIO (par.F90:78-81) */
+}
+/* tprstb (mix_imp.f:836-856) */
+static inline double tprstb_(const orc_t* o, double grad, double spl)
+{
+    const double fac = o->c.alphaT * spl;
+    const double x = -grad * fac;
+    const double t = tanh(x * x * x);
+    return t > 0.0 ? t : 0.0;
+}
+/* Ftimp, Fsimp on the top face of cell (i,j,k) from t, s at k and k+1 (dCdzt, drhodC) */
+static void mix_face(const orc_t* o, int i, int j, int k, double t0, double t1, double s0,
+                     double s1, double* ft, double* fs)
+{
+    const double* par = o->par;
+    const double lambda = par[LAMB], xes = par[NLES], kvc = par[P_VC], sp1 = par[SPL1];
+    if (kvc == 0.0) { *ft = *fs = 0.0; return; }
+    const double r0 = lambda * s0 - t0 - xes * (alpt1 * t0 + alpt2 * t0 * t0 - alpt3 * t0 * t0 * t0);
+    const double r1 = lambda * s1 - t1 - xes * (alpt1 * t1 + alpt2 * t1 * t1 - alpt3 * t1 * t1 * t1);
+    const double iso = isoc_(o, i, j, k + 1) * isoc_(o, i, j, k);
+    const double dzw = o->dz * DFZW(k);
+    const double dtdz = iso * (t1 - t0) / dzw, dsdz = iso * (s1 - s0) / dzw;
+    const double drdz = iso * (r1 - r0) / dzw;
+    const double tpr = tprstb_(o, -drdz, sp1);
+    *ft = -tpr * kvc * dtdz;
+    *fs = -tpr * kvc * dsdz;
+}
+/* mix of row var (TT or SS) of cell (i,j,k) from t, s at k-1, k, k+1 (index 0..2) */
+static double mix_row(const orc_t* o, int var, int i, int j, int k, const double* t3, const double* s3)
+{
+    const double* par = o->par;
+    const double lambda = par[LAMB], xes = par[NLES];
+    if ((var == TT && !o->vmix_temp) || (var == SS && !o->vmix_salt)) return 0.0;
+    double ftk, fsk, ftm = 0.0, fsm = 0.0;
+    mix_face(o, i, j, k, t3[1], t3[2], s3[1], s3[2], &ftk, &fsk);
+    if (k >= 2) mix_face(o, i, j, k - 1, t3[0], t3[1], s3[0], s3[1], &ftm, &fsm);
+    if (o->c.rho_mixing && xes == 0.0) {
+        if (var == TT) return ((ftk - ftm) - (fsk - fsm) * lambda) / (2.0 * o->dz * DFZT(k)) + 0.0;
+        return ((fsk - fsm) - (ftk - ftm) / lambda) / (2.0 * o->dz * DFZT(k)) + 0.0;
+    }
+    if (var == TT) return (ftk - ftm) / (o->dz * DFZT(k)) + 0.0;
+    return (fsk - fsm) / (o->dz * DFZT(k)) + 0.0;
+}
+static void mix_col(const fields_t* f, int i, int j, int k, double* t3, double* s3)
+{
+    for (int d = 0; d < 3; d++) {
+        t3[d] = FT(f, i, j, k - 1 + d);
+        s3[d] = FS(f, i, j, k - 1 + d);
+    }
+}
+static int mix_active(const orc_t* o) { return o->c.vmix != 0 && (o->vmix_temp || o->vmix_salt); }
+/* vmix_control (mix_imp.f:131-166): flag 2 fixes T/S mixing at the first evaluation */
+static void mix_control(orc_t* o, const double* x)
+{
+    if (o->c.vmix != 2 || o->vmix_fix) return;
+    double st = 0.0, ss = 0.0;
+    for (int r = 0; r < o->ndim; r += NUN) {
+        st += x[r + TT - 1] * x[r + TT - 1];
+        ss += x[r + SS - 1] * x[r + SS - 1];
+    }
+    o->vmix_temp = sqrt(st) > 1.0e-12;
+    o->vmix_salt = sqrt(ss) > 1.0e-12;
+    /* vmix_control partitions only when T mixes (mix_imp.f:158): salt-only mixing is off */
+    if (!o->vmix_temp) o->vmix_salt = 0;
+    o->vmix_fix = 1;
+}
+/* vmix_jac: forward differences (eps 1e-8) of mix w.r.t. the T/S unknowns of the
+ * column neighbours k-1, k, k+1, added to An before boundaries */
+static void mix_jac_cell(const orc_t* o, const fields_t* f, int i, int j, int k, aloc_t A)
+{
+    if (!mix_active(o) || LM(o, i, j, k) != OCEAN) return;
+    const double eps = 1.0e-08;
+    double t3[3], s3[3];
+    mix_col(f, i, j, k, t3, s3);
+    for (int var = TT; var <= SS; var++) {
+        if ((var == TT && !o->vmix_temp) || (var == SS && !o->vmix_salt)) continue;
+        const double m0 = mix_row(o, var, i, j, k, t3, s3);
+        for (int d = 0; d < 3; d++) {
+            const int kk = k - 1 + d;
+            const int lm = LM(o, i, j, kk);
+            if (lm != OCEAN && lm != 3) continue;
+            const int pos = d == 0 ? 14 : (d == 1 ? 5 : 23);
+            for (int cv = TT; cv <= SS; cv++) {
+                if ((cv == TT && !o->vmix_temp) || (cv == SS && !o->vmix_salt)) continue;
+                double tp[3] = {t3[0], t3[1], t3[2]}, sp[3] = {s3[0], s3[1], s3[2]};
+                if (cv == TT) tp[d] = tp[d] + eps;
+                else sp[d] = sp[d] + eps;
+                const double m1 = mix_row(o, var, i, j, k, tp, sp);
+                A[pos][var][cv] = A[pos][var][cv] + (m1 - m0) / eps;
+            }
+        }
+    }
+}
+
 /* Build the final local block An(27,6,6) of cell (i,j,k) as matrix() (jac=1) or
  * rhs() (jac=0) would, before fillcolA. */
 static void cell_block(const orc_t* o, const fields_t* f, int i, int j, int k, int jac, aloc_t A,
                        int frc_zero[NUN + 1])
 {
     lin_cell(o, i, j, k, A);
-    if (jac) nlin_jac_cell(o, f, i, j, k, A);
-    else nlin_rhs_cell(o, f, i, j, k, A);
+    if (jac) {
+        nlin_jac_cell(o, f, i, j, k, A);
+        mix_jac_cell(o, f, i, j, k, A);
+    } else {
+        nlin_rhs_cell(o, f, i, j, k, A);
+    }
     for (int q = 0; q <= NUN; q++) frc_zero[q] = 0;
     boundaries_cell(o, i, j, k, A, frc_zero);
 }
@@ -1144,12 +1258,16 @@ static void fillcolB_cell(const orc_t* o, int i, int j, int k, double* coB)
 /* ================================================================================ */
 orc_t* orc_create(const orc_cfg* cfg, const int* landm, const double* spert)
 {
-    if (cfg->ite != 1 || cfg->its != 1 || cfg->iza != 2 || cfg->vmix != 0) {
-        fprintf(stderr, "orc_create: only idealized ocean-only forcing, vmix=0 supported\n");
+    if (cfg->ite != 1 || cfg->its != 1 || cfg->iza != 2 || cfg->vmix < 0 || cfg->vmix > 2) {
+        fprintf(stderr, "orc_create: only idealized ocean-only forcing, vmix 0..2 supported\n");
         return NULL;
     }
     orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
     o->c = *cfg;
+    /* mix_imp.f vmix_init (58-109): flag 1 mixes T and S from the start, flag 2 decides
+     * at the first matrix/rhs evaluation (vmix_control) */
+    o->vmix_temp = o->vmix_salt = cfg->vmix == 1;
+    o->vmix_fix = cfg->vmix != 2;
     int n = cfg->n, m = cfg->m, l = cfg->l;
     o->n = n; o->m = m; o->l = l;
     o->ncell = n * m * l;
@@ -1309,6 +1427,11 @@ void orc_graph(const orc_t* o, int64_t* rowptr, int* col)
 /* matrix() + assemble/fillcolA (assemble.F90:57-139): Fortran CSR, 1-based */
 int64_t orc_fortran_matrix(orc_t* o, const double* x, int* beg, int* jco, double* co, double* coB)
 {
+    mix_control(o, x);
+    if (mix_active(o) && !mix_supported(o)) {
+        fprintf(stderr, "oracle: neutral physics / GM / consistent mixing not restated\n");
+        abort();
+    }
     fields_t f;
     usol(o, x, &f);
     int64_t v = 1;
@@ -1342,9 +1465,14 @@ int64_t orc_fortran_matrix(orc_t* o, const double* x, int* beg, int* jco, double
     return v - 1;
 }
 
-/* rhs() (usrc.F90:506-586) with vmix = 0, ires = 0: B = (-Au + Frc_eff)*(1-landm) */
+/* rhs() (usrc.F90:506-586) with ires = 0: B = (-Au - mix + Frc_eff)*(1-landm) */
 void orc_fortran_rhs(orc_t* o, const double* x, double* B)
 {
+    mix_control(o, x);
+    if (mix_active(o) && !mix_supported(o)) {
+        fprintf(stderr, "oracle: neutral physics / GM / consistent mixing not restated\n");
+        abort();
+    }
     fields_t f;
     usol(o, x, &f);
     int n = o->n, m = o->m, l = o->l;
@@ -1369,7 +1497,13 @@ void orc_fortran_rhs(orc_t* o, const double* x, double* B)
                         }
                     }
                 double frc = fz_[ii] ? 0.0 : o->Frc[row];
-                double b = -au - 0.0 + frc - 0.0 * (1 - o->par[RESC]) * 0.0;
+                double mx = 0.0;
+                if ((ii == TT || ii == SS) && mix_active(o)) {
+                    double t3[3], s3[3];
+                    mix_col(&f, i, j, k, t3, s3);
+                    mx = mix_row(o, ii, i, j, k, t3, s3);
+                }
+                double b = -au - mx + frc - 0.0 * (1 - o->par[RESC]) * 0.0;
                 B[row] = b * (1 - LM(o, i, j, k));
             }
         }
@@ -1392,6 +1526,11 @@ void orc_intcond_coeff(const orc_t* o, double* coeff)
  * maximal graph, intcond_S row (2121-2198), B = coB*Mass (Mass = 1). */
 void orc_jacobian(orc_t* o, const double* x, double* val, double* diagB)
 {
+    mix_control(o, x);
+    if (mix_active(o) && !mix_supported(o)) {
+        fprintf(stderr, "oracle: neutral physics / GM / consistent mixing not restated\n");
+        abort();
+    }
     fields_t f;
     usol(o, x, &f);
     int n = o->n, m = o->m;

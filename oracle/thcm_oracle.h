@@ -28,6 +28,7 @@ typedef struct {
     double alphaT, alphaS;
     int int_sign;                      /* "Salinity Integral Sign" (THCM.C:235)     */
     int nic, mic;                      /* integral row coordinates (-1 = default)   */
+    int rho_mixing;                    /* "Rho mixing" (mix_imp.f vmix_fun)         */
 } orc_cfg;
 
 typedef struct orc orc_t;

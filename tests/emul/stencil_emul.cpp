@@ -1,3 +1,4 @@
+#include <cmath>
 /*
  * stencil_emul.cpp -- TEST HARNESS: runs the device library's per-row assembly code
  * (i-emic_amd/csrc/stencil.h, host_setup.h) on the CPU, loop for loop like the kernels
@@ -49,6 +50,7 @@ void* emul_create_band(const iemic_grid* grid, const int* landm, int jb0, int jb
 {
     Emul* e = new Emul();
     e->su.init(*grid, landm, jb0, jb1);
+    e->su.vmix_init();
     return e;
 }
 void* emul_create(const iemic_grid* grid, const int* landm) { return emul_create_band(grid, landm, 0, -1); }
@@ -73,10 +75,28 @@ static void forcing(Emul* e)
     }
 }
 
+/* vmix_control for Mixing = 2 (as assembly.hip mix_control, one band) */
+static void mix_control(Emul* e, const double* x)
+{
+    host::Setup& su = e->su;
+    if (su.cfg.vmix != 2 || su.vmix_fix) return;
+    double st = 0.0, ss = 0.0;
+    for (int64_t lc = 0; lc < su.nloc; lc++) {
+        const int64_t r = NUN * ((int64_t)HALO * su.l * su.n + lc);
+        st += x[r + TT] * x[r + TT];
+        ss += x[r + SS] * x[r + SS];
+    }
+    su.vmix_t = std::sqrt(st) > 1.0e-12;
+    su.vmix_s = std::sqrt(ss) > 1.0e-12;
+    if (!su.vmix_t) su.vmix_s = 0;
+    su.vmix_fix = 1;
+}
+
 /* x: ext-layout state (owned + halo rows); fills the band's slot values and B (ext) */
 void emul_jacobian_ext(void* h, const double* x, double* B)
 {
     Emul* e = (Emul*)h;
+    mix_control(e, x);
     const host::Setup& su = e->su;
     Geo g = su.geo(su.landm.data(), su.tab.data());
     const int64_t nloc = su.nloc;
@@ -103,6 +123,7 @@ void emul_jacobian_ext(void* h, const double* x, double* B)
 void emul_rhs_ext(void* h, const double* x, double* F, double* intcond_partial)
 {
     Emul* e = (Emul*)h;
+    mix_control(e, x);
     forcing(e);
     const host::Setup& su = e->su;
     Geo g = su.geo(su.landm.data(), su.tab.data());
