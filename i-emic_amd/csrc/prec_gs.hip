@@ -1384,6 +1384,103 @@ __global__ void k_mg_half(TsLev V, int colour)
     if (mg_colour(V, i, jl, k) != colour) return;
     mg_relax(V, i, jl, k);
 }
+/* z-line relaxation: every water column (i, jl) of one horizontal colour solves its
+ * 2x2-block tridiagonal T/S system along k exactly (block Thomas), with the horizontal
+ * couplings to the neighbouring columns taken from the current iterate.  Strong vertical
+ * coupling (the convective mixing of Mixing = 1/2, vertical diffusion on stretched
+ * layers) is then handled by the smoother, the horizontal smooth modes by the coarse
+ * levels.  Inactive unknowns (zero diagonal) are identity rows with zero right-hand side.
+ * Colour of a column: (i + jl) & 1, with 2/3 for i = n-1 on an odd periodic level. */
+__device__ __forceinline__ int mg_lcolour(const TsLev& V, int i, int jl)
+{
+    if (V.periodic && (V.n & 1) && i == V.n - 1) return 2 + (jl & 1);
+    return (i + jl) & 1;
+}
+/* One column per P lanes (lane = level k, P >= l): every lane loads its level (right-hand side minus horizontal couplings, 2x2 diagonal block,
+ * couplings to k-1 and k+1) at once, and the block-tridiagonal system is solved by
+ * parallel cyclic reduction over the lanes (log2 P shuffle steps of 2x2 block algebra)
+ * instead of a serial block Thomas sweep. */
+struct B2 { double a, b, c, d; };            /* [[a b] [c d]] */
+__device__ __forceinline__ B2 b2mul(const B2& x, const B2& y)
+{
+    return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+}
+__device__ __forceinline__ B2 b2inv(const B2& x)
+{
+    const double det = x.a * x.d - x.b * x.c;
+    const double q = det != 0.0 ? 1.0 / det : 0.0;
+    return {x.d * q, -x.b * q, -x.c * q, x.a * q};
+}
+template <int P>
+__device__ __forceinline__ B2 shfl_b2(const B2& x, int src)
+{
+    return {__shfl(x.a, src, P), __shfl(x.b, src, P), __shfl(x.c, src, P), __shfl(x.d, src, P)};
+}
+template <int P>
+__global__ void __launch_bounds__(256) k_mg_zline_pcr(TsLev V, int colour)
+{
+    const int t = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int k = threadIdx.x % P;
+    if (t >= V.n * V.mb) return;                       /* whole column groups exit */
+    const int i = t % V.n, jl = t / V.n;
+    if (mg_lcolour(V, i, jl) != colour) return;
+    const int64_t cs = V.cstr;
+    B2 A{1.0, 0.0, 0.0, 1.0}, Bm{0.0, 0.0, 0.0, 0.0}, Cm{0.0, 0.0, 0.0, 0.0};
+    double d0 = 0.0, d1 = 0.0;
+    int64_t c = 0;
+    if (k < V.l) {
+        c = mg_cell(V, i, jl, k);
+        double rt = V.bt[c * V.bstr], rs = V.bs[c * V.bstr];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int ii = i, jj = jl, kk = k;
+            if (!mg_nb(V, q, ii, jj, kk)) continue;
+            const int64_t nc = mg_cell(V, ii, jj, kk);
+            rt -= V.off[(int64_t)q * cs + c] * V.zt[nc];
+            rs -= V.off[(int64_t)(8 + q) * cs + c] * V.zs[nc];
+        }
+        const bool at = V.diag[c] != 0.0, as = V.diag[3 * cs + c] != 0.0;
+        A = {V.diag[c], V.diag[cs + c], V.diag[2 * cs + c], V.diag[3 * cs + c]};
+        Bm = {V.off[4 * cs + c], V.off[6 * cs + c], V.off[14 * cs + c], V.off[12 * cs + c]};
+        Cm = {V.off[5 * cs + c], V.off[7 * cs + c], V.off[15 * cs + c], V.off[13 * cs + c]};
+        d0 = rt;
+        d1 = rs;
+        if (!at) { A.a = 1.0; A.b = A.c = 0.0; Bm.a = Bm.b = 0.0; Cm.a = Cm.b = 0.0; d0 = 0.0; }
+        if (!as) { A.d = 1.0; A.b = A.c = 0.0; Bm.c = Bm.d = 0.0; Cm.c = Cm.d = 0.0; d1 = 0.0; }
+    }
+#pragma unroll
+    for (int s = 1; s < P; s <<= 1) {
+        const int lo = k - s, hi = k + s;
+        const B2 Alo = shfl_b2<P>(A, lo < 0 ? k : lo), Ahi = shfl_b2<P>(A, hi >= P ? k : hi);
+        const B2 Blo = shfl_b2<P>(Bm, lo < 0 ? k : lo), Bhi = shfl_b2<P>(Bm, hi >= P ? k : hi);
+        const B2 Clo = shfl_b2<P>(Cm, lo < 0 ? k : lo), Chi = shfl_b2<P>(Cm, hi >= P ? k : hi);
+        const double dlo0 = __shfl(d0, lo < 0 ? k : lo, P), dlo1 = __shfl(d1, lo < 0 ? k : lo, P);
+        const double dhi0 = __shfl(d0, hi >= P ? k : hi, P), dhi1 = __shfl(d1, hi >= P ? k : hi, P);
+        B2 al{0.0, 0.0, 0.0, 0.0}, ga{0.0, 0.0, 0.0, 0.0};
+        if (lo >= 0) {
+            al = b2mul(Bm, b2inv(Alo));
+            al = {-al.a, -al.b, -al.c, -al.d};
+        }
+        if (hi < P) {
+            ga = b2mul(Cm, b2inv(Ahi));
+            ga = {-ga.a, -ga.b, -ga.c, -ga.d};
+        }
+        const B2 t1 = b2mul(al, Clo), t2 = b2mul(ga, Bhi);
+        A = {A.a + t1.a + t2.a, A.b + t1.b + t2.b, A.c + t1.c + t2.c, A.d + t1.d + t2.d};
+        const double nd0 = d0 + (al.a * dlo0 + al.b * dlo1) + (ga.a * dhi0 + ga.b * dhi1);
+        const double nd1 = d1 + (al.c * dlo0 + al.d * dlo1) + (ga.c * dhi0 + ga.d * dhi1);
+        Bm = lo >= 0 ? b2mul(al, Blo) : B2{0.0, 0.0, 0.0, 0.0};
+        Cm = hi < P ? b2mul(ga, Chi) : B2{0.0, 0.0, 0.0, 0.0};
+        d0 = nd0;
+        d1 = nd1;
+    }
+    if (k < V.l) {
+        const B2 Ai = b2inv(A);
+        V.zt[c] = Ai.a * d0 + Ai.b * d1;
+        V.zs[c] = Ai.c * d0 + Ai.d * d1;
+    }
+}
+
 /* coarse rhs = sum of the children's residuals b - A z; coarse iterate = 0 */
 __global__ void k_mg_restrict(TsLev F, TsLev C, double* __restrict__ bc, double* __restrict__ zc)
 {
@@ -1820,6 +1917,24 @@ static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
     BlockGS& gs = c->gs;
     hipStream_t s = c->stream;
     const Lay L = lay_of(c);
+    if (c->l <= 64) {
+        /* z-line relaxation: colours forward before the coarse correction, backward after */
+        const TsLev V = mg_view(c, q);
+        const int ncolour = (V.periodic && (V.n & 1)) ? 4 : 2;
+        const int P = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : 64);
+        const unsigned gp = (unsigned)(((int64_t)V.n * V.mb * P + 255) / 256);
+        for (int sw = 0; sw < nu; sw++)
+            for (int h = 0; h < ncolour; h++) {
+                const int col = post ? ncolour - 1 - h : h;
+                if (P == 16)
+                    hipLaunchKernelGGL(k_mg_zline_pcr<16>, dim3(gp), dim3(256), 0, s, V, col);
+                else if (P == 32)
+                    hipLaunchKernelGGL(k_mg_zline_pcr<32>, dim3(gp), dim3(256), 0, s, V, col);
+                else
+                    hipLaunchKernelGGL(k_mg_zline_pcr<64>, dim3(gp), dim3(256), 0, s, V, col);
+            }
+        return;
+    }
     if (q == 0 && (c->n & 1) == 0) {
         const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
         const int seq[4] = {0, 1, 1, 0};
