@@ -64,6 +64,7 @@ struct BlockGS {
     int ncol = 0, bl = 0, bu = 0;    /* active water columns, Schur band widths          */
     int ncol_own = 0;                /* columns of this band (inverse slab width)       */
     DevBuf<int> own_cols;            /* their Schur indices, ascending                  */
+    DevBuf<int> own_pos;             /* Schur index -> position in own_cols or -1       */
     DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8), halo-filled */
     DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
     DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index (band order) or -1       */

@@ -364,21 +364,26 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
                                                   const double* __restrict__ w, int64_t N,
                                                   double* __restrict__ partial)
 {
-    __shared__ double sm[8 * 4];
-    const int nq = (nvec + 3) / 4;
+    /* blockIdx.y < nq: a group of DG basis vectors against u and w (u, w re-read once per
+     * group, so larger groups cut their traffic); blockIdx.y == nq: u.u, u.w, w.w */
+    constexpr int DG = 8;
+    __shared__ double sm[8 * 2 * DG];
+    const int nq = (nvec + DG - 1) / DG;
     const int by = blockIdx.y;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (by < nq) {
-        const int i0 = 4 * by;
-        const int nv = min(4, nvec - i0);
-        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int i0 = DG * by;
+        const int nv = min(DG, nvec - i0);
+        double acc[2 * DG];
+#pragma unroll
+        for (int t = 0; t < 2 * DG; t++) acc[t] = 0.0;
         const double* q0 = V + (int64_t)i0 * ldv;
-        if (nv == 4) {
+        if (nv == DG) {
             for (int64_t e = e0; e < N; e += stride) {
                 const double ue = u[e], we = w[e];
 #pragma unroll
-                for (int t = 0; t < 4; t++) {
+                for (int t = 0; t < DG; t++) {
                     const double qe = q0[(int64_t)t * ldv + e];
                     acc[2 * t] += qe * ue;
                     acc[2 * t + 1] += qe * we;
@@ -394,7 +399,7 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
                 }
             }
         }
-        block_sum_n<8>(acc, sm);
+        block_sum_n<2 * DG>(acc, sm);
         if (threadIdx.x == 0)
             for (int t = 0; t < 2 * nv; t++)
                 partial[(int64_t)(2 * i0 + t) * gridDim.x + blockIdx.x] = acc[t];
@@ -767,7 +772,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
-                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, (nv + 3) / 4 + 1), dim3(256), 0,
+                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, (nv + 7) / 8 + 1), dim3(256), 0,
                                    c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);

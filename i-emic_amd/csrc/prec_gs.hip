@@ -785,6 +785,9 @@ __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restr
     }
 }
 
+__device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                                         const double* __restrict__ z, int i, int j, int k,
+                                         int64_t pl, const Lay& L);
 /* Column recurrences as parallel scans: P lanes (P = power of two >= l) per water column,
  * lane = level k.  Each level is an affine map x_k = A_k + B_k x_{k+-1}; a Hillis-Steele
  * scan over the lanes composes them, so the l-step dependency chain becomes log2(P)
@@ -836,7 +839,8 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
                                                     const int* __restrict__ col_of_ij,
                                                     const double* __restrict__ pbar,
                                                     const double* __restrict__ crhs,
-                                                    double* __restrict__ z, Lay L)
+                                                    double* __restrict__ z, Lay L,
+                                                    const double* __restrict__ rr)
 {
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
@@ -857,7 +861,10 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
             const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
             const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
             if (a != 0.0) {
-                A = crhs[cell] / a;
+                /* continuity right-hand side rr_p - Duv uv, evaluated in place */
+                const double rhs = crhs ? crhs[cell]
+                                        : rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
+                A = rhs / a;
                 B = -b / a;
             }
         }
@@ -877,6 +884,16 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
     }
 }
 
+template <int P>
+__global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__ val,
+                                                      const uint8_t* __restrict__ known,
+                                                      const double* __restrict__ pw,
+                                                      const double* __restrict__ rr,
+                                                      const double* __restrict__ z,
+                                                      const int* __restrict__ col_of_ij,
+                                                      const uint8_t* __restrict__ pinned,
+                                                      const int* __restrict__ own_pos,
+                                                      double* __restrict__ colv_own, Lay L);
 /* sum over the 4 P corners of a U/V point of G * p(P)  (U row slots 20..23 / V 42..45) */
 __device__ __forceinline__ void guv_p(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                       const double* __restrict__ pv, int64_t pstride, int i, int j,
@@ -963,6 +980,42 @@ __global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ 
     double s = 0.0;
     for (int k = 0; k < L.l; k++) s += t[ecell(L, i, j, k)];
     rhs[c] = pinned[c] ? 0.0 : s;
+}
+
+/* 3a'. the Schur right-hand side of a water column in one pass: P lanes per column
+ * (lane = level k) evaluate w_k (Duv uv - rr_p), a shuffle reduction sums them, and the
+ * entry goes straight to this band's slab of the right-hand side (no per-cell buffer, no
+ * gather) */
+template <int P>
+__global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__ val,
+                                                      const uint8_t* __restrict__ known,
+                                                      const double* __restrict__ pw,
+                                                      const double* __restrict__ rr,
+                                                      const double* __restrict__ z,
+                                                      const int* __restrict__ col_of_ij,
+                                                      const uint8_t* __restrict__ pinned,
+                                                      const int* __restrict__ own_pos,
+                                                      double* __restrict__ colv_own, Lay L)
+{
+    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int k = threadIdx.x % P;
+    if (t_ >= (int)(L.nloc / L.l)) return;
+    const int ij = L.jb0 * L.n + t_;
+    const int c = col_of_ij[ij];
+    if (c < 0) return;
+    const int i = ij % L.n, j = ij / L.n;
+    double v = 0.0;
+    if (k < L.l) {
+        const int64_t cell = ecell(L, i, j, k);
+        if (!known[NUN * cell + PP])
+            v = pw[cell] * (duv_uv(val, known, z, i, j, k, cell - L.own0, L) - rr[NUN * cell + PP]);
+    }
+#pragma unroll
+    for (int o = P / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, P);
+    if (k == 0) {
+        const int q = own_pos[c];
+        if (q >= 0) colv_own[q] = pinned[c] ? 0.0 : v;
+    }
 }
 
 /* 3b. y = X b (X row-major nr x nc), one wavefront per row */
@@ -1723,6 +1776,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     rc |= gs.colv2.alloc(ncol);
     rc |= gs.colv_own.alloc(nq);
     rc |= gs.own_cols.alloc(nq);
+    rc |= gs.own_pos.alloc(ncol);
     if (rc) {
         set_error("block GS: out of device memory");
         return IEMIC_ENOMEM;
@@ -1731,6 +1785,11 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * ncol))) return rc;
     if ((rc = h2d(c, gs.pinned.p, pin.data(), ncol))) return rc;
     if ((rc = h2d(c, gs.own_cols.p, own.data(), sizeof(int) * own.size()))) return rc;
+    {
+        std::vector<int> pos(ncol, -1);
+        for (size_t q = 0; q < own.size(); q++) pos[own[q]] = (int)q;
+        if ((rc = h2d(c, gs.own_pos.p, pos.data(), sizeof(int) * pos.size()))) return rc;
+    }
     gs.flags_h = flags;
     return 0;
 }
@@ -2218,13 +2277,24 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        rr, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       rr, z, gs.tcell.p, L, 0);
-    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                       gs.pinned.p, gs.colv.p, L);
+    if (Pl == 0) {
+        hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                           rr, z, gs.tcell.p, L, 0);
+        hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
+                           gs.pinned.p, gs.colv.p, L);
+        hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
+                           gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
+    } else if (Pl == 16) {
+        hipLaunchKernelGGL(k_gs_pcol_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+    } else if (Pl == 32) {
+        hipLaunchKernelGGL(k_gs_pcol_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+    } else {
+        hipLaunchKernelGGL(k_gs_pcol_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
+                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+    }
     /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
-                       gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
     if (gs.fp32)
         hipLaunchKernelGGL(k_gemv_f, dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256), 0, s, gs.sinvf.p,
                            gs.ncol, gs.ncol_own, gs.ldf, gs.colv_own.p, gs.colv2.p);
@@ -2235,20 +2305,22 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.col_of_ij.p, gs.colv2.p, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       rr, z, gs.tcell.p, L, 1);
+    if (Pl == 0) {
+        hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                           rr, z, gs.tcell.p, L, 1);
+    }
     if (Pl == 0)
         hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
                            gs.colv2.p, gs.tcell.p, z, L);
     else if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
     else if (Pl == 32)
         hipLaunchKernelGGL(k_gs_pw_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
     else
         hipLaunchKernelGGL(k_gs_pw_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, gs.tcell.p, z, L);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
     return 0;
 }
 
