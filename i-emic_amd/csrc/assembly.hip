@@ -149,7 +149,7 @@ static int mix_control(iemic_ctx* c, const double* x_dev)
 {
     host::Setup& su = c->su;
     if (su.cfg.vmix == 0) return 0;
-    if (su.cfg.vmix == 2 && !su.vmix_fix) {
+    if (su.cfg.vmix == 2) {   /* Ocean.C:1271/1292: fixMixing(0) before every evaluation */
         std::vector<double> h((size_t)c->nerows);
         int rc = d2h(c, h.data(), x_dev, sizeof(double) * h.size());
         if (rc) return rc;

@@ -357,8 +357,8 @@ __device__ __forceinline__ void block_sum_n(double* v, double* sm)
 }
 
 /* DCGS2 dot pass: rows 2i, 2i+1 = Q_i.u, Q_i.w (i < nvec); rows 2nvec..2nvec+2 = u.u, u.w,
- * w.w.  Block y < ceil(nvec/4) handles four basis vectors so that u and w are read once
- * per four; the last y handles the three self products.  partial[row*gridDim.x + blk]. */
+ * w.w.  Block y < ceil(nvec/8) handles eight basis vectors so that u and w are read once
+ * per eight; the last y handles the three self products.  partial[row*gridDim.x + blk]. */
 __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, int64_t ldv, int nvec,
                                                   const double* __restrict__ u,
                                                   const double* __restrict__ w, int64_t N,

@@ -1,0 +1,372 @@
+"""Pseudo-arclength continuation over the GPU ocean model.
+
+Restates ``Continuation<Model>`` (src/continuation/Continuation.H) on the Model surface
+the reference drives (``computeRHS``, ``computeJacobian``, ``solve``, ``applyMatrix``,
+``getState/getRHS/getSolution``, ``getPar/setPar``, ``preProcess/postProcess``): Euler
+predictor, Newton corrector on the bordered system with two solves against the same
+Jacobian (Continuation.H:587-813; the preconditioner is built once per Jacobian and reused
+by both solves), finite-difference dF/dpar (389-418), secant/Euler tangents and their
+normalisation (421-544), step-size control (952-982), reset/restore (1004-1050) and the
+secant landing on destinations (858-933).  Parameter names and defaults are the
+reference's (getDefaultInitParameters, Continuation.H:1330-1366).
+
+Vectors are host numpy arrays in the reference row order (the reference's Epetra vector
+algebra runs on the host too); F, J and the solves run on the GPU behind the model.
+Eigenvalue analysis (JDQZ), backtracking (off by default) and user monitors are not
+restated.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+DEFAULTS = {
+    "continuation parameter": "Combined Forcing",
+    "initial step size": 1.0e-2, "minimum step size": 1.0e-8, "maximum step size": 1.0e3,
+    "increase step size": 1.25, "decrease step size": 2.0, "epsilon increment": 1.0e-5,
+    "maximum number of steps": -1, "maximum Newton iterations": 7,
+    "minimum Newton iterations": 1, "optimal Newton iterations": 3.5,
+    "Newton tolerance": 1.0e-4, "destination tolerance": 1.0e-7,
+    "detection of special points": "D", "state tangent scaling": 1.0,
+    "normalize strategy": "N", "reject failed iteration": True,
+    "give up at minimum step size": True, "enable Newton Chord hybrid solve": False,
+    "tangent type": "S", "corrector residual test": "D", "initial tangent type": "E",
+    "post processing": "at every point", "predictor bound": 1e3,
+}
+
+
+def _sgn(x: float) -> int:
+    return (x > 0) - (x < 0)
+
+
+@dataclass
+class _Storage:
+    state0: Optional[np.ndarray] = None
+    state00: Optional[np.ndarray] = None
+    stateDot0: Optional[np.ndarray] = None
+    par0: float = 0.0
+    par00: float = 0.0
+    parDot0: float = 0.0
+    ds0: float = 0.0
+    ds00: float = 0.0
+
+
+@dataclass
+class StepRecord:
+    step: int
+    par: float
+    ds: float
+    norm_x: float
+    norm_f: float
+    newton_iters: int
+
+
+class Continuation:
+    """``Continuation<Model>`` (Continuation.H) for a Model with the Ocean surface."""
+
+    def __init__(self, model, params: Optional[dict] = None):
+        p = dict(DEFAULTS)
+        if params:
+            p.update(params)
+        self.model = model
+        self.p = p
+        self.parName = p["continuation parameter"]
+        self.dsInit = float(p["initial step size"])
+        self.dsMin = float(p["minimum step size"])
+        self.dsMax = float(p["maximum step size"])
+        self.scale2 = float(p["decrease step size"])
+        self.epsilon = float(p["epsilon increment"])
+        self.maxSteps = int(p["maximum number of steps"])
+        self.maxNewton = int(p["maximum Newton iterations"])
+        self.minNewton = int(p["minimum Newton iterations"])
+        self.optNewton = float(p["optimal Newton iterations"])
+        self.newtonTol = float(p["Newton tolerance"])
+        self.destTol = float(p["destination tolerance"])
+        self.detectMode = p["detection of special points"]
+        self.tanScaling = float(p["state tangent scaling"])
+        self.normalizeStrategy = p["normalize strategy"]
+        self.rejectFailed = bool(p["reject failed iteration"])
+        self.giveUpAtdsMin = bool(p["give up at minimum step size"])
+        self.chordHybrid = bool(p["enable Newton Chord hybrid solve"])
+        self.tangentType = p["tangent type"]
+        self.residualTest = p["corrector residual test"]
+        self.initialTangent = p["initial tangent type"]
+        self.postProcessMode = p["post processing"]
+        self.predictorBound = float(p["predictor bound"])
+        self.destinations = []
+        for i in range(999):
+            d = p.get(f"destination {i}")
+            if d is None or d == -999.0:
+                break
+            self.destinations.append(float(d))
+        self.destinationsBackup = list(self.destinations)
+        self.history: list[StepRecord] = []
+
+    # ---- helpers -------------------------------------------------------------------
+    @staticmethod
+    def _norm(v):
+        return float(np.linalg.norm(v))
+
+    def _set_state(self, x):
+        self.model.setState(x)
+
+    # ---- Continuation.H:1158-1230 initialize ----------------------------------------
+    def initialize(self):
+        self.ds = self.dsInit
+        self.model.computeRHS()
+        self.state = self.model.getState("C")
+        self.rhs = self.model.getRHS("C")
+        self.par = self.model.getPar(self.parName)
+        self.st = _Storage(ds0=self.ds, ds00=self.ds, par0=self.par, par00=self.par,
+                           parDot0=0.0, state0=self.state.copy())
+        self.destinations = list(self.destinationsBackup)
+        self.signMonitor = [0] * len(self.destinations)
+        self.secant = False
+        N = len(self.state)
+        if self.normalizeStrategy == "O":
+            self.zeta = 1.0 / N
+        else:
+            self.zeta = self.tanScaling / N
+        self.newtonIter = 0
+        self.sumNewtonIter = 0
+        self.parDot = 0.0
+        self.stateDot = None
+        self.step_ = 0
+        self.resetCounter = 0
+        self.reachedLastDest = False
+        self.abortFlag = False
+        self.fixStepSize = False
+        self.dsStart = self.ds
+
+    # ---- 389-418 ---------------------------------------------------------------------
+    def computeDFDPar(self, mode: str):
+        if mode == "F":
+            self.model.computeRHS()
+        self.rhsCopy = self.model.getRHS("C")
+        self.model.setPar(self.parName, self.par + self.epsilon)
+        self.model.computeRHS()
+        self.model.setPar(self.parName, self.par)
+        Fe = self.model.getRHS("C")
+        self.dFdPar = Fe * (1.0 / self.epsilon) + self.rhsCopy * (-1.0 / self.epsilon)
+
+    # ---- 300-384 ---------------------------------------------------------------------
+    def createInitialTangent(self):
+        self.computeDFDPar("F")
+        if self.initialTangent in ("E", "S"):
+            self.model.preProcess()
+            self.model.computeJacobian()
+            self.stateDot = self.model.solve(-self.dFdPar).copy()
+        else:
+            self.stateDot = -self.dFdPar
+        self.normalize()
+
+    # ---- 497-544 ---------------------------------------------------------------------
+    def normalize(self):
+        if self.normalizeStrategy == "O":
+            self.zeta = self.tanScaling / self._norm(self.stateDot)
+            self.stateDot = self.stateDot * self.zeta
+            nrm = self._norm(self.stateDot)
+            normComb = math.sqrt(nrm * nrm + 1)
+            self.stateDot = self.stateDot / normComb
+            self.parDot = 1.0 / normComb
+        else:
+            nrm = self._norm(self.stateDot)
+            normComb = math.sqrt(self.zeta * nrm * nrm + 1)
+            self.parDot = 1.0 / normComb
+            self.stateDot = self.stateDot * self.parDot
+
+    # ---- 421-494 ---------------------------------------------------------------------
+    def createTangent(self, mode: str):
+        if mode == "S":
+            state = self.model.getState("C")
+            self.stateDot = (state - self.st.state0) / self.st.ds0
+            self.par = self.model.getPar(self.parName)
+            self.parDot = (self.par - self.st.par0) / self.st.ds0
+        else:
+            if self.chordHybrid:
+                self.computeDFDPar("F")
+                self.model.computeJacobian()
+                self.stateDot = self.model.solve(-self.dFdPar).copy()
+            elif self.newtonIter != 0:
+                self.stateDot = -self.stateDot
+            self.normalize()
+
+    # ---- 547-583 ---------------------------------------------------------------------
+    def eulerPredictor(self) -> int:
+        self.state = self.state + self.ds * self.stateDot
+        self._set_state(self.state)
+        self.par = self.par + self.ds * self.parDot
+        self.model.setPar(self.parName, self.par)
+        self.model.computeRHS()
+        return 1 if self._norm(self.model.getRHS("V")) > self.predictorBound else 0
+
+    # ---- 587-813 ---------------------------------------------------------------------
+    def newtonCorrector(self) -> int:
+        res = 100.0
+        y = None
+        self.newtonIter = 0
+        while self.newtonIter < self.maxNewton:
+            mode = "F" if self.newtonIter == 0 else "A"
+            self.computeDFDPar(mode)
+            R = -self.rhsCopy
+            self.normRHS = self._norm(self.rhsCopy)
+            stateDiff = self.model.getState("C") - self.st.state0
+            parDiff = self.par - self.st.par0
+            if self.normalizeStrategy == "O":
+                rbp = self.ds - float(np.dot(self.stateDot, stateDiff)) * self.zeta - self.parDot * parDiff
+            else:
+                rbp = (self.ds * self.ds) - float(np.dot(stateDiff, stateDiff)) * self.zeta - parDiff * parDiff
+            self.model.computeJacobian()
+            # two solves with the same Jacobian (the preconditioner is computed once)
+            if not self.chordHybrid:
+                y = self.model.solve(self.dFdPar).copy()
+            z = self.model.solve(R).copy()
+            if self.normalizeStrategy == "O":
+                if self.chordHybrid:
+                    parDir = ((rbp - self.zeta * float(np.dot(self.stateDot, z))) /
+                              (self.parDot + self.zeta * float(np.dot(self.stateDot, self.stateDot))))
+                else:
+                    parDir = ((rbp - self.zeta * float(np.dot(self.stateDot, z))) /
+                              (self.parDot - self.zeta * float(np.dot(self.stateDot, y))))
+            else:
+                if self.chordHybrid:
+                    parDir = ((rbp - 2 * self.zeta * float(np.dot(stateDiff, z))) /
+                              (2 * parDiff + 2 * (self.zeta / parDiff) * float(np.dot(stateDiff, stateDiff))))
+                else:
+                    parDir = ((rbp - 2 * self.zeta * float(np.dot(stateDiff, z))) /
+                              (2 * parDiff - 2 * self.zeta * float(np.dot(stateDiff, y))))
+            stateDir = z + parDir * self.stateDot if self.chordHybrid else z - parDir * y
+            self.state = self.model.getState("C") + stateDir
+            self._set_state(self.state)
+            self.par = self.par + parDir
+            self.model.setPar(self.parName, self.par)
+            self.newtonIter += 1
+            self.sumNewtonIter += 1
+            self.model.computeRHS()
+            self.normRHStest = self._norm(self.model.getRHS("V"))
+            if self.normRHStest > self.predictorBound:
+                return 1
+            n0 = self._norm(self.st.state0)
+            if self._norm(stateDir) > 1e3 * n0 and n0 > 0:
+                return 1
+            if self.residualTest == "R":
+                res = self.normRHStest
+            else:
+                res = max(abs(parDir), float(np.max(np.abs(stateDir))))
+            if res < self.newtonTol and self.newtonIter >= self.minNewton:
+                break
+        if not self.chordHybrid and y is not None:
+            self.stateDot = y
+        if res > self.newtonTol and self.rejectFailed:
+            return 1
+        return 0
+
+    # ---- 1052-1090 store / restore ----------------------------------------------------
+    def store(self):
+        self.st.state00 = self.st.state0
+        self.st.state0 = self.model.getState("C")
+        self.st.stateDot0 = None if self.stateDot is None else self.stateDot.copy()
+        self.st.par00 = self.st.par0
+        self.st.par0 = self.model.getPar(self.parName)
+        self.st.ds00 = self.st.ds0
+        self.st.ds0 = self.ds
+        self.st.parDot0 = self.parDot
+
+    def restore(self):
+        self.state = self.st.state0.copy()
+        self._set_state(self.state)
+        self.stateDot = None if self.st.stateDot0 is None else self.st.stateDot0.copy()
+        self.par = self.st.par0
+        self.model.setPar(self.parName, self.par)
+        self.parDot = self.st.parDot0
+        self.ds = self.st.ds0
+
+    def reset(self):
+        self.step_ -= 1
+        self.restore()
+        s = _sgn(self.ds)
+        self.ds = s * max(abs(self.ds) / self.scale2, abs(self.dsMin))
+        self.resetCounter += 1
+        self.fixStepSize = True
+        if abs(self.ds) <= abs(self.dsMin) and (self.resetCounter >= 100 or self.giveUpAtdsMin):
+            self.abortFlag = True
+
+    # ---- 952-982 ---------------------------------------------------------------------
+    def adjustStep(self):
+        if self.secant or self.fixStepSize:
+            self.fixStepSize = False
+            return
+        factor = self.optNewton / float(self.newtonIter)
+        factor = min(max(factor, 0.5), 2.0)
+        self.ds *= factor
+        if abs(self.ds) > abs(self.dsMax):
+            self.ds = _sgn(self.ds) * abs(self.dsMax)
+        if abs(self.ds) < abs(self.dsMin):
+            self.ds = _sgn(self.ds) * abs(self.dsMin)
+
+    # ---- 858-933 ---------------------------------------------------------------------
+    def detect(self):
+        if not self.destinations:
+            return
+        dest = self.destinations[0]
+        self.par = self.model.getPar(self.parName)
+        if self.detectMode == "D":
+            f0, f1 = self.st.par0 - dest, self.par - dest
+        else:
+            f0, f1 = self.st.parDot0, self.parDot
+        if self.signMonitor[0] == 0:
+            self.signMonitor[0] = _sgn(f1)
+        if self.signMonitor[0] != _sgn(f1) and not self.secant:
+            self.secant = True
+            self.dsStart = self.ds
+        else:
+            self.signMonitor[0] = _sgn(f1)
+        if self.secant:
+            self.ds = -f1 * self.ds / (f1 - f0)
+            self.createTangent("S")
+        if self.secant and abs(f1) < self.destTol:
+            self.secant = False
+            self.ds = self.dsStart
+            self.fixStepSize = True
+            self.destinations.pop(0)
+            self.signMonitor.pop(0)
+            if not self.destinations:
+                self.reachedLastDest = True
+            else:
+                self.signMonitor[0] = _sgn(self.par - self.destinations[0])
+
+    # ---- 230-298 ---------------------------------------------------------------------
+    def step(self) -> int:
+        self.model.preProcess()
+        if self.eulerPredictor():
+            return 1
+        if self.newtonCorrector():
+            return 1
+        self.createTangent(self.tangentType)
+        if self.postProcessMode == "at every point":
+            self.model.postProcess()
+        return 0
+
+    # ---- 184-228 ---------------------------------------------------------------------
+    def run(self) -> int:
+        self.initialize()
+        self.createInitialTangent()
+        while not self.reachedLastDest and self.step_ != self.maxSteps and not self.abortFlag:
+            self.step_ += 1
+            self.store()
+            if self.step():
+                self.reset()
+                continue
+            self.history.append(StepRecord(self.step_, self.par, self.ds,
+                                           self._norm(self.model.getState("V")),
+                                           self.normRHStest, self.newtonIter))
+            self.detect()
+            self.adjustStep()
+        if self.abortFlag:
+            return 1
+        if self.postProcessMode != "at every point":
+            self.model.postProcess()
+        return 0
