@@ -142,8 +142,9 @@ __global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* 
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* vmix_control (mix_imp.f:131-166) for Mixing = 2: the first evaluation fixes whether T
- * and S mix (L2 norm of the field > 1e-12, summed over the bands); and the restated
+/* vmix_control (mix_imp.f:131-166) for Mixing = 2: the Ocean layer calls fixMixing(0)
+ * before every evaluation (Ocean.C:1271/1292), so whether T and S mix (L2 norm of the
+ * field > 1e-12, summed over the bands) is re-decided at each call; and the restated
  * subset of vmix_fun must cover the current parameters */
 static int mix_control(iemic_ctx* c, const double* x_dev)
 {
