@@ -515,7 +515,7 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_rhs_ms += ms(t);
-    inf.norm_f0 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, 0)));
+    inf.norm_f0 = std::sqrt(dot(c, c->d_F.p, c->d_F.p, 0));   /* NaN stays NaN */
     t = clk::now();
     if ((rc = assemble_jacobian(c, c->d_x.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -537,7 +537,7 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_rhs_ms += ms(t);
-    inf.norm_f1 = std::sqrt(std::max(0.0, dot(c, c->d_F.p, c->d_F.p, 0)));
+    inf.norm_f1 = std::sqrt(dot(c, c->d_F.p, c->d_F.p, 0));   /* NaN stays NaN */
     c->jac_valid = 1;
     inf.t_total_ms = ms(T0);
     if (info) *info = inf;

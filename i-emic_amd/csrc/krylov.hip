@@ -628,6 +628,16 @@ static double ms_since(std::chrono::steady_clock::time_point t0)
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+/* sqrt of a squared norm that rounding may have driven below zero; NaN stays NaN */
+static inline double sqrt0(double v) { return v > 0.0 ? std::sqrt(v) : (v == v ? 0.0 : v); }
+
+/* a NaN/Inf reaching the Hessenberg column would pass for a breakdown (res = 0): stop loudly */
+static int nonfinite()
+{
+    set_error("FGMRES: non-finite value in the Krylov basis (operator or preconditioner output)");
+    return IEMIC_ERANGE;
+}
+
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
 {
     /* vectors are ext-layout (stride NE); kernels touch the owned rows [o, o + NL) */
@@ -656,7 +666,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     for (int q = 0; q < 3; q++) HIP_OK(hipEventCreate(&ev[q]));
 
     HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
-    double bnorm = std::sqrt(std::max(0.0, dot(c, b, b, 0)));
+    double bnorm = sqrt0(dot(c, b, b, 0));
+    if (!std::isfinite(bnorm)) return nonfinite();
     if (!(bnorm > 0)) {
         inf.converged = 1;
         if (info) *info = inf;
@@ -706,7 +717,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                         inf_reorth++;
                     }
                 }
-                double hn = std::sqrt(std::max(0.0, hn2));
+                if (!std::isfinite(hn2)) return nonfinite();
+                double hn = sqrt0(hn2);
                 if (hn > 0)
                     hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, vn + o, 1.0 / hn,
                                        vn + o, NL);
@@ -794,6 +806,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     ab += hr[2 * i] * hr[2 * i + 1];
                 }
                 const double uu = hr[2 * nv], uw = hr[2 * nv + 1];
+                if (!std::isfinite(uu) || !std::isfinite(uw)) return nonfinite();
                 const double beta2 = uu - aa;
                 const double bt = beta2 > 0.0 ? std::sqrt(beta2) : 0.0;
                 bool stop = false;
@@ -857,7 +870,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         rc = spmv(c, x, r, c->stream);
         if (rc) return rc;
         hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b + o, -1.0, r + o, r + o, NL);
-        beta = std::sqrt(std::max(0.0, dot(c, r, r, 0)));
+        beta = sqrt0(dot(c, r, r, 0));
         res = beta / bnorm;
         if (res <= opt->tol) break;
     }
@@ -869,7 +882,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     inf.iters = it;
     inf.reorth = inf_reorth;
     inf.implicit_rel_res = res;
-    inf.explicit_rel_res = std::sqrt(std::max(0.0, e2)) / bnorm;
+    inf.explicit_rel_res = sqrt0(e2) / bnorm;
     /* converged: the Givens estimate reached the tolerance and the true residual agrees
      * with it (a loss of orthogonality shows up as a gap between the two) */
     inf.converged = res <= opt->tol && inf.explicit_rel_res <= 2.0 * opt->tol;

@@ -39,6 +39,7 @@ extern "C" {
 #define IEMIC_ENOMEM  (-12)
 #define IEMIC_EDEVICE (-5)
 #define IEMIC_ESTATE  (-71)
+#define IEMIC_ERANGE  (-34)   /* non-finite value in the operator / preconditioner output */
 
 typedef struct iemic_ctx iemic_ctx;
 

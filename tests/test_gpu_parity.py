@@ -26,8 +26,8 @@ def Ocean():
     return Ocean
 
 
-def make(Ocean, orc, name, **kw):
-    c = cf.preset(name, mixing=0)
+def make(Ocean, orc, name, mixing=0, **kw):
+    c = cf.preset(name, mixing=mixing)
     L0 = golden_landm(name) if name != "global2" else cf.init_landmask(c, cf.landmask(c))
     oc = Ocean(c, landm=L0, **kw)
     L = mask_fix(orc, c, L0)
@@ -202,6 +202,18 @@ def test_fgmres_solve(oracle_lib, Ocean, name, prec):
     assert oc.last_solve.converged == 1
     assert res <= 1e-7
     assert abs(oc.last_solve.explicit_rel_res - res) <= 1e-9
+
+
+def test_fgmres_nonfinite_is_an_error(oracle_lib, Ocean):
+    """A NaN reaching the Krylov basis raises instead of passing for a breakdown (res = 0)."""
+    from iemic._lib import IemicError
+    c, oc, o, L = make(Ocean, oracle_lib, "natl8", solver_params={"Preconditioner": 2})
+    oc.setState(cf.synthetic_state(c, L, amp_ts=1e-3))
+    oc.computeJacobian()
+    b = cf.synthetic_vector(c, seed=5)
+    b[len(b) // 2] = np.nan
+    with pytest.raises(IemicError, match="non-finite"):
+        oc.solve(b)
 
 
 def _land_rows(c, L):
