@@ -59,8 +59,10 @@ def parse():
     p.add_argument("--restarts", type=int, default=20)
     p.add_argument("--ts-sweeps", type=int, default=12)
     p.add_argument("--orth", default="DCGS2", choices=["DCGS2", "DGKS"])
-    p.add_argument("--dyn-iters", type=int, default=2,
+    p.add_argument("--dyn-iters", type=int, default=4,
                    help="defect-correction passes on the dynamics block of the block GS")
+    p.add_argument("--dyn-omega", type=float, default=0.95, help="step of the correction passes")
+    p.add_argument("--dyn-mr", action="store_true", help="minimal-residual step per pass")
     p.add_argument("--schur-fp64", action="store_true", help="Schur inverse in fp64 (default fp32)")
     p.add_argument("--ts-mg", type=int, default=1,
                    help="T/S aggregation-multigrid V-cycles (0: --ts-sweeps plain sweeps)")
@@ -170,7 +172,8 @@ def main():
     sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
           "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth,
-          "Dyn iterations": args.dyn_iters, "Schur fp32": not args.schur_fp64,
+          "Dyn iterations": args.dyn_iters,
+          "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr, "Schur fp32": not args.schur_fp64,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps}
     comm_id = None
     if world > 1:
@@ -253,7 +256,7 @@ def main():
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
-                   "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters,
+                   "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
                    "schur": "fp64" if args.schur_fp64 else "fp32",
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps,
                    "parallelism": f"latitude-bands x{world}" if world > 1 else "single",

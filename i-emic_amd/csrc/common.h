@@ -85,6 +85,9 @@ struct BlockGS {
     int ldf = 0, fp32 = 1;           /* fp32: the apply's GEMV reads sinvf               */
     int dyn_iters = 1;               /* defect-correction passes on the dynamics block   */
     DevBuf<double> dres, zc;         /* dynamics defect and correction (ext rows)        */
+    DevBuf<double> dq, dzero, dmr;   /* MR passes: -A_DD zc, a zero vector, dot partials  */
+    int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
+    double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
     /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local):
      * level 0 is the fine T/S block (tsoff/tsdiag/tsinv, ext cells); coarse level q has
      * mg_n[q] x mg_m[q] x l cells with 16 couplings, 2x2 block and inverse, rhs, iterate */

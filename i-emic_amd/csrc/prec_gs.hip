@@ -1121,13 +1121,70 @@ __global__ void k_dyn_resid(const double* __restrict__ val, const uint8_t* __res
 
 /* z += zc on the active U/V/W/P rows */
 __global__ void k_dyn_add(const uint8_t* __restrict__ known, const double* __restrict__ zc,
-                          double* __restrict__ z, Lay L)
+                          double* __restrict__ z, Lay L, double omega)
 {
     OWNED_CELL;
 #pragma unroll
     for (int R = UU; R <= PP; R++) {
         const int64_t row = NUN * cell + R;
-        if (!known[row]) z[row] += zc[row];
+        if (!known[row]) z[row] += omega * zc[row];
+    }
+}
+
+/* Minimal-residual defect correction: with d the defect and q = -A_DD zc the change a
+ * full correction zc would make to it, the step w = argmin ||d + w q|| = -(d.q)/(q.q).
+ * Block partials in a fixed order (deterministic), summed by one thread. */
+constexpr int MR_NB = 256;
+__global__ void __launch_bounds__(256) k_mr_dots(const double* __restrict__ d, const double* __restrict__ q,
+                                                 int64_t n, double* __restrict__ part)
+{
+    __shared__ double s0[256], s1[256];
+    double a = 0.0, b = 0.0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const double qv = q[t];
+        a += d[t] * qv;
+        b += qv * qv;
+    }
+    s0[threadIdx.x] = a;
+    s1[threadIdx.x] = b;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s0[threadIdx.x] += s0[threadIdx.x + w];
+            s1[threadIdx.x] += s1[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s0[0];
+        part[gridDim.x + blockIdx.x] = s1[0];
+    }
+}
+__global__ void k_mr_sum(double* __restrict__ part, int nb)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double a = 0.0, b = 0.0;
+    for (int e = 0; e < nb; e++) {
+        a += part[e];
+        b += part[nb + e];
+    }
+    part[2 * nb] = a;
+    part[2 * nb + 1] = b;
+}
+/* z += w zc, and (upd) d += w q, on the active U/V/W/P rows */
+__global__ void k_mr_update(const uint8_t* __restrict__ known, const double* __restrict__ sums,
+                            const double* __restrict__ zc, const double* __restrict__ q,
+                            double* __restrict__ z, double* __restrict__ d, Lay L, int upd)
+{
+    OWNED_CELL;
+    const double w = sums[1] > 0.0 ? -sums[0] / sums[1] : 0.0;
+#pragma unroll
+    for (int R = UU; R <= PP; R++) {
+        const int64_t row = NUN * cell + R;
+        if (known[row]) continue;
+        z[row] += w * zc[row];
+        if (upd) d[row] += w * q[row];
     }
 }
 
@@ -2174,8 +2231,11 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
             };
             int nb = 0;
             bool st = false;
-            for (int cand : {32, 16})
-                for (bool sv : {true, false})
+            /* measured at 2 deg (ncol_own 9024, 1 GPU): NB 16 without staging keeps 3 blocks per
+             * CU resident and fills the chip in one round (60.7 ms set-up vs 75.2 for NB 32
+             * staged, whose 282 blocks of 126 KB LDS need two rounds) */
+            for (int cand : {16, 32})
+                for (bool sv : {false, true})
                     if (!nb && pbytes(cand, sv) <= lmax && (force_nb == 0 || force_nb == cand)) {
                         nb = cand;
                         st = sv;
@@ -2238,10 +2298,14 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
                            gs.sinv.p, gs.ncol, gs.ncol_own, gs.sinvf.p, gs.ldf);
     }
+    gs.dyn_mr = opt ? (opt->dyn_mr != 0) : 0;
+    gs.dyn_omega = opt && opt->dyn_omega > 0.0 ? opt->dyn_omega : 1.0;
     if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
-        if (gs.dres.alloc(NE) || gs.zc.alloc(NE)) return IEMIC_ENOMEM;
-        HIP_OK(hipMemsetAsync(gs.dres.p, 0, sizeof(double) * NE, c->stream));
-        HIP_OK(hipMemsetAsync(gs.zc.p, 0, sizeof(double) * NE, c->stream));
+        if (gs.dres.alloc(NE) || gs.zc.alloc(NE) || gs.dq.alloc(NE) || gs.dzero.alloc(NE) ||
+            gs.dmr.alloc(2 * MR_NB + 2))
+            return IEMIC_ENOMEM;
+        for (DevBuf<double>* bptr : {&gs.dres, &gs.zc, &gs.dq, &gs.dzero})
+            HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * NE, c->stream));
     }
     HIP_OK(hipGetLastError());
     gs.ready = 1;
@@ -2341,12 +2405,29 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
     if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;
-    /* defect correction on the dynamics block: z_D += M_D^-1 (rr_D - A_DD z_D) */
-    for (int it = 1; it < gs.dyn_iters; it++) {
+    /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
+     * minimal-residual w (dyn_mr) or the fixed w = dyn_omega */
+    if (gs.dyn_mr && gs.dyn_iters > 1) {
+        const int64_t o = NUN * c->own0, NL = c->nlrows;
+        if (band && (rc = halo_exchange(c, z, 1))) return rc;
+        if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
+        for (int it = 1; it < gs.dyn_iters; it++) {
+            if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
+            if (band && (rc = halo_exchange(c, gs.zc.p, 1))) return rc;
+            if ((rc = spmv_dyn_defect(c, gs.zc.p, gs.dzero.p, gs.known.p, gs.dq.p))) return rc;
+            hipLaunchKernelGGL(k_mr_dots, dim3(MR_NB), dim3(256), 0, s, gs.dres.p + o, gs.dq.p + o, NL,
+                               gs.dmr.p);
+            hipLaunchKernelGGL(k_mr_sum, dim3(1), dim3(64), 0, s, gs.dmr.p, MR_NB);
+            if (band && (rc = allreduce_sum(c, gs.dmr.p + 2 * MR_NB, 2))) return rc;
+            hipLaunchKernelGGL(k_mr_update, dim3(gc), dim3(256), 0, s, gs.known.p, gs.dmr.p + 2 * MR_NB,
+                               gs.zc.p, gs.dq.p, z, gs.dres.p, L, it + 1 < gs.dyn_iters ? 1 : 0);
+        }
+    }
+    for (int it = 1; !gs.dyn_mr && it < gs.dyn_iters; it++) {
         if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* w, p of the neighbours */
         if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
         if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
-        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zc.p, z, L);
+        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zc.p, z, L, gs.dyn_omega);
     }
     if (band && gs.dyn_iters > 1 && (rc = halo_exchange(c, z, 1))) return rc;
     if (gs.ts_mg > 0) {

@@ -55,7 +55,7 @@ class Ocean:
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
-              "Dyn iterations": 2, "Schur fp32": True, "TS multigrid cycles": 1,
+              "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "Schur fp32": True, "TS multigrid cycles": 1,
               "Multigrid sweeps": 1}
         if solver_params:
             sp.update(solver_params)
@@ -149,7 +149,8 @@ class Ocean:
                            int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
                            int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0,
                            int(sp["Dyn iterations"]), int(bool(sp["Schur fp32"])),
-                           int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]))
+                           int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]),
+                           float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])))
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""

@@ -79,6 +79,9 @@ typedef struct {
                                  /* multigrid V-cycles (0: ts_sweeps plain sweeps)    */
     int mg_sweeps;               /* symmetric red-black sweeps before/after the coarse */
                                  /* correction on every multigrid level               */
+    double dyn_omega;            /* block GS: step of the defect-correction passes    */
+                                 /* (z_D += omega M_D^-1 d; 0 means 1)                */
+    int dyn_mr;                  /* 1: minimal-residual step per pass instead         */
 } iemic_krylov;
 
 typedef struct {
