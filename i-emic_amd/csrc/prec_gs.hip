@@ -1058,36 +1058,64 @@ __global__ void k_to_f32(const double* __restrict__ X, int nr, int nc, float* __
 }
 
 /* 3b'. y = X b with X fp32 (row-major, ld floats per row, ld % 4 == 0), fp64 accumulation:
- * one wavefront per 4 rows, 16-B loads of X, each b element loaded once per 4 rows */
+ * RPW rows per wavefront, 16-B loads of X, each b element loaded once per RPW rows; UNR
+ * column steps unrolled so RPW * UNR loads per lane are in flight */
+template <int RPW, int UNR>
 __global__ void __launch_bounds__(256) k_gemv_f(const float* __restrict__ X, int nr, int nc, int ld,
                                                 const double* __restrict__ b, double* __restrict__ y)
 {
-    const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+    const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
     const int lane = threadIdx.x & 63;
     if (r0 >= nr) return;
-    const int nrow = min(4, nr - r0);
-    const float4* xr[4];
+    const int nrow = min(RPW, nr - r0);
+    const float4* xr[RPW];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
+    for (int q = 0; q < RPW; q++)
         xr[q] = reinterpret_cast<const float4*>(X + (int64_t)(r0 + min(q, nrow - 1)) * ld);
-    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double s[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; q++) s[q] = 0.0;
     const int n4 = ld >> 2;
-    for (int c4 = lane; c4 < n4; c4 += 64) {
+    int c4 = lane;
+    for (; c4 + 64 * (UNR - 1) < n4; c4 += 64 * UNR) {
+        float4 v[UNR][RPW];
+#pragma unroll
+        for (int u = 0; u < UNR; u++)
+#pragma unroll
+            for (int q = 0; q < RPW; q++) v[u][q] = xr[q][c4 + 64 * u];
+#pragma unroll
+        for (int u = 0; u < UNR; u++) {
+            const int c = 4 * (c4 + 64 * u);
+            const double b0 = c < nc ? b[c] : 0.0, b1 = c + 1 < nc ? b[c + 1] : 0.0;
+            const double b2 = c + 2 < nc ? b[c + 2] : 0.0, b3 = c + 3 < nc ? b[c + 3] : 0.0;
+#pragma unroll
+            for (int q = 0; q < RPW; q++)
+                s[q] += (double)v[u][q].x * b0 + (double)v[u][q].y * b1 + (double)v[u][q].z * b2 +
+                        (double)v[u][q].w * b3;
+        }
+    }
+    for (; c4 < n4; c4 += 64) {
         const int c = 4 * c4;
         const double b0 = c < nc ? b[c] : 0.0, b1 = c + 1 < nc ? b[c + 1] : 0.0;
         const double b2 = c + 2 < nc ? b[c + 2] : 0.0, b3 = c + 3 < nc ? b[c + 3] : 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < RPW; q++) {
             const float4 v = xr[q][c4];
             s[q] += (double)v.x * b0 + (double)v.y * b1 + (double)v.z * b2 + (double)v.w * b3;
         }
     }
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < RPW; q++) {
         double t = s[q];
         for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
         if (lane == 0 && q < nrow) y[r0 + q] = t;
     }
+}
+/* measured at 2 deg (325 MB fp32 slab): <4, 2> 1-2 % faster than <4, 1>, <2, *>, <1, 4>, <8, 1> */
+static void gemv_f(const BlockGS& gs, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_gemv_f<4, 2>), dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256), 0, s,
+                       gs.sinvf.p, gs.ncol, gs.ncol_own, gs.ldf, gs.colv_own.p, gs.colv2.p);
 }
 
 /* dynamics defect: d = rr - A_DD z on the active U/V/W/P rows (couplings to active
@@ -2360,8 +2388,7 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
     }
     /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
     if (gs.fp32)
-        hipLaunchKernelGGL(k_gemv_f, dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256), 0, s, gs.sinvf.p,
-                           gs.ncol, gs.ncol_own, gs.ldf, gs.colv_own.p, gs.colv2.p);
+        gemv_f(gs, s);
     else
         hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
                            gs.ncol, gs.ncol_own, gs.colv_own.p, gs.colv2.p);
