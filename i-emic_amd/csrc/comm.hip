@@ -163,6 +163,31 @@ int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
     return 0;
 }
 
+int halo_exchange_pair(iemic_ctx* c, double* a, double* b)
+{
+    if (c->nranks <= 1) return 0;
+    if (c->group) {
+        int rc = local_halo(c, a, 1, 1);
+        return rc ? rc : local_halo(c, b, 1, 1);
+    }
+    const int64_t cnt = (int64_t)c->l * c->n;                   /* one latitude row */
+    const int64_t own_first = c->own0, own_end = own_first + c->nloc;
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    NCCL_OK(ncclGroupStart());
+    for (double* v : {a, b}) {
+        if (c->rank > 0) {
+            NCCL_OK(ncclSend(v + own_first, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
+            NCCL_OK(ncclRecv(v + own_first - cnt, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
+        }
+        if (c->rank < c->nranks - 1) {
+            NCCL_OK(ncclSend(v + own_end - cnt, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
+            NCCL_OK(ncclRecv(v + own_end, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
+        }
+    }
+    NCCL_OK(ncclGroupEnd());
+    return 0;
+}
+
 /* state-vector halo (NUN doubles per cell) */
 int halo_exchange(iemic_ctx* c, double* v, int rows_j) { return halo_exchange_w(c, v, NUN, rows_j); }
 

@@ -93,6 +93,7 @@ struct BlockGS {
      * mg_n[q] x mg_m[q] x l cells with 16 couplings, 2x2 block and inverse, rhs, iterate */
     static constexpr int MG_MAX = 12;
     int ts_mg = 1, mg_sweeps = 1, mg_nlev = 0;
+    int ts_halo = 1;                 /* bands: level-0 T/S smoothing across band edges  */
     int mg_n[MG_MAX] = {}, mg_m[MG_MAX] = {};
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
     DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_dinv[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
@@ -180,6 +181,8 @@ struct StreamGuard {
 int allreduce_sum(iemic_ctx* c, double* dev, int count);
 int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
 int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int rows_j);
+/* one row of two per-cell arrays (width 1) in one communication group */
+int halo_exchange_pair(iemic_ctx* c, double* a, double* b);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
 int comm_unique_id(unsigned char* id128);
 void* local_group_new(int nranks);

@@ -1448,6 +1448,8 @@ struct TsLev {
     int dinv_aos;                    /* 1: dinv[4*cell + e] (level 0: tsinv)            */
     const double* bt; const double* bs; int bstr;
     double* zt; double* zs;
+    int halo_j;                      /* 1: the latitude rows jl = -1 and mb (level 0 of a   */
+                                     /* band, refreshed by halo exchanges) are neighbours  */
 };
 __device__ __forceinline__ int64_t mg_cell(const TsLev& V, int i, int jl, int k)
 {
@@ -1464,7 +1466,7 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
     case 4: k--; break;
     default: k++; break;
     }
-    if (jl < 0 || jl >= V.mb || k < 0 || k >= V.l) return false;
+    if (jl < -V.halo_j || jl >= V.mb + V.halo_j || k < 0 || k >= V.l) return false;
     if (i < 0 || i >= V.n) {
         if (!V.periodic) return false;
         i = (i + V.n) % V.n;
@@ -1900,6 +1902,8 @@ static TsLev mg_view(iemic_ctx* c, int q)
     if (q == 0) {
         V.n = c->n;
         V.mb = c->jb1 - c->jb0;
+        /* bands: the level-0 z-line smoother and residual see the neighbour bands' rows */
+        V.halo_j = (c->nranks > 1 && c->l <= 64 && gs.ts_halo) ? 1 : 0;
         V.base = c->own0;
         V.cstr = c->next;
         V.off = gs.tsoff.p;
@@ -2007,7 +2011,9 @@ static int mg_setup(iemic_ctx* c)
     }
     hipStream_t s = c->stream;
     for (q = 1; q < gs.mg_nlev; q++) {
-        const TsLev F = mg_view(c, q - 1), C = mg_view(c, q);
+        TsLev F = mg_view(c, q - 1);
+        const TsLev C = mg_view(c, q);
+        F.halo_j = 0;                /* aggregates and coarse operators stay band-local */
         hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C,
                            gs.mg_off[q].p, gs.mg_diag[q].p, gs.mg_dinv[q].p);
     }
@@ -2056,11 +2062,19 @@ static int mg_setup(iemic_ctx* c)
     return h2d(c, gs.mg_cinv.p, X.data(), sizeof(double) * X.size());
 }
 
-static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
+/* refresh the level-0 iterate's latitude halo rows (bands coupled in the T/S smoother) */
+static int mg_halo(iemic_ctx* c, const TsLev& V)
+{
+    if (!V.halo_j) return 0;
+    return halo_exchange_pair(c, V.zt, V.zs);
+}
+
+static int mg_smooth(iemic_ctx* c, int q, int nu, bool post)
 {
     BlockGS& gs = c->gs;
     hipStream_t s = c->stream;
     const Lay L = lay_of(c);
+    int rc;
     if (c->l <= 64) {
         /* z-line relaxation: colours forward before the coarse correction, backward after */
         const TsLev V = mg_view(c, q);
@@ -2070,6 +2084,7 @@ static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
         for (int sw = 0; sw < nu; sw++)
             for (int h = 0; h < ncolour; h++) {
                 const int col = post ? ncolour - 1 - h : h;
+                if ((rc = mg_halo(c, V))) return rc;
                 if (P == 16)
                     hipLaunchKernelGGL(k_mg_zline_pcr<16>, dim3(gp), dim3(256), 0, s, V, col);
                 else if (P == 32)
@@ -2077,7 +2092,7 @@ static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
                 else
                     hipLaunchKernelGGL(k_mg_zline_pcr<64>, dim3(gp), dim3(256), 0, s, V, col);
             }
-        return;
+        return 0;
     }
     if (q == 0 && (c->n & 1) == 0) {
         const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
@@ -2086,7 +2101,7 @@ static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
             for (int h = 0; h < 4; h++)
                 hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
                                    gs.zt.p, gs.zs.p, L, seq[h]);
-        return;
+        return 0;
     }
     const TsLev V = mg_view(c, q);
     const int64_t ncl = (int64_t)V.n * V.mb * V.l;
@@ -2101,28 +2116,33 @@ static void mg_smooth(iemic_ctx* c, int q, int nu, bool post)
         h0 = post ? ns : 0;
     }
     for (int sw = 0; sw < nu; sw++)
-        for (int h = 0; h < ns; h++)
+        for (int h = 0; h < ns; h++) {
+            if ((rc = mg_halo(c, V))) return rc;
             hipLaunchKernelGGL(k_mg_half, dim3(blocks_for(ncl)), dim3(256), 0, s, V, seq[h0 + h]);
+        }
+    return 0;
 }
 
-static void mg_vcycle(iemic_ctx* c, int q)
+static int mg_vcycle(iemic_ctx* c, int q)
 {
     BlockGS& gs = c->gs;
     hipStream_t s = c->stream;
+    int rc;
     if (q == gs.mg_nlev - 1) {
         const int N = 2 * gs.mg_n[q] * gs.mg_m[q] * c->l;
         hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
                            gs.mg_b[q].p, gs.mg_z[q].p);
-        return;
+        return 0;
     }
     const int nu = std::max(1, gs.mg_sweeps);
-    mg_smooth(c, q, nu, false);
+    if ((rc = mg_smooth(c, q, nu, false))) return rc;
     const TsLev F = mg_view(c, q), C = mg_view(c, q + 1);
+    if ((rc = mg_halo(c, F))) return rc;
     hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
                        gs.mg_z[q + 1].p);
-    mg_vcycle(c, q + 1);
+    if ((rc = mg_vcycle(c, q + 1))) return rc;
     hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)F.n * F.mb * F.l)), dim3(256), 0, s, F, C);
-    mg_smooth(c, q, nu, true);
+    return mg_smooth(c, q, nu, true);
 }
 
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
@@ -2313,6 +2333,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
             return IEMIC_EINVAL;
         }
     }
+    {
+        const char* e = getenv("IEMIC_TS_HALO");
+        gs.ts_halo = e ? atoi(e) : 1;
+    }
     gs.ts_mg = opt ? std::max(0, opt->ts_mg) : 0;
     gs.mg_sweeps = opt ? std::max(1, opt->mg_sweeps) : 1;
     if (gs.ts_mg > 0 && (rc = mg_setup(c))) return rc;
@@ -2468,7 +2492,8 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
             HIP_OK(hipMemsetAsync(gs.zt.p, 0, sizeof(double) * c->next, s));
             HIP_OK(hipMemsetAsync(gs.zs.p, 0, sizeof(double) * c->next, s));
         }
-        for (int cyc = 0; cyc < gs.ts_mg; cyc++) mg_vcycle(c, 0);
+        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
+            if ((rc = mg_vcycle(c, 0))) return rc;
         hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
         HIP_OK(hipGetLastError());
         return 0;

@@ -92,6 +92,44 @@ def test_bands_in_one_process(oracle_lib, name, nranks):
     assert abs(res[0]["info"].norm_f1 - f1) <= 1e-9 * f1 + 1e-14 * f0
 
 
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_bands_global2_newton_mixing(oracle_lib, nranks):
+    """The bench workload split as the multi-GPU bench splits it (global 2 deg, Mixing = 1,
+    default solver: block GS with 4 damped defect passes, T/S multigrid per band): the
+    banded Newton step converges and solves the linearised system of the whole problem."""
+    from iemic.ocean import Ocean
+    c = cf.preset("global2", mixing=1)
+    L0 = cf.init_landmask(c, cf.landmask(c))
+    L = mask_fix(oracle_lib, c, L0)
+    o = oracle_lib.Oracle(c.ref_dict(), L, c.par_list())
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    x1 = np.zeros(c.nrows)
+
+    def fn(r, group):
+        from iemic import _lib
+        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks,
+                   solver_params={"FGMRES iterations": 100, "FGMRES restarts": 20})
+        oc.setState(x)
+        info = oc.newtonStep()
+        lay = oc.layout()
+        xx = np.zeros(c.nrows)
+        _lib.check(_lib.lib().iemic_get_state(oc._h, _lib.ptr(xx)), "get_state")
+        oc.close()
+        return dict(lay=lay, info=info, x=xx)
+
+    res = _run_bands(nranks, fn)
+    for r in res:
+        jb0, jb1 = r["lay"]["jb0"], r["lay"]["jb1"]
+        rows = np.array([6 * ((k * c.m + j) * c.n + i) + q for k in range(c.l)
+                         for j in range(jb0, jb1) for i in range(c.n) for q in range(6)])
+        x1[rows] = r["x"][rows]
+        assert r["info"].solve.converged == 1
+    ov, _ = o.jacobian(x)
+    F0 = o.rhs(x)
+    lin = np.linalg.norm(F0 + o.spmv(ov, x1 - x)) / np.linalg.norm(F0)
+    assert lin <= 2e-8, lin
+
+
 def _run_bands(nranks, fn):
     """Run fn(rank, group) on nranks host threads sharing one in-process group."""
     from iemic import _lib
