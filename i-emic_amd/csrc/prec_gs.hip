@@ -1621,31 +1621,39 @@ __global__ void __launch_bounds__(256) k_mg_zline_pcr(TsLev V, int colour)
     }
 }
 
-/* coarse rhs = sum of the children's residuals b - A z; coarse iterate = 0 */
+/* coarse rhs = sum of the children's residuals b - A z; coarse iterate = 0.  Four lanes
+ * per coarse cell, one child each (the residual loads of the children run in parallel),
+ * summed by two shuffle steps ((c00 + c10) + (c01 + c11), a fixed order). */
 __global__ void k_mg_restrict(TsLev F, TsLev C, double* __restrict__ bc, double* __restrict__ zc)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t ncl = (int64_t)C.n * C.mb * C.l;
-    if (t >= ncl) return;
+    const int64_t t = g >> 2;
+    const int ch = (int)(g & 3);
+    if (t >= ncl) return;                     /* whole 4-lane groups exit together */
     const int I = (int)(t % C.n), k = (int)((t / C.n) % C.l), J = (int)(t / ((int64_t)C.n * C.l));
+    const int i = 2 * I + (ch & 1), jl = 2 * J + (ch >> 1);
     double st = 0.0, ss = 0.0;
-    for (int b = 0; b < 2; b++)
-        for (int a = 0; a < 2; a++) {
-            const int i = 2 * I + a, jl = 2 * J + b;
-            if (i >= F.n || jl >= F.mb) continue;
-            const int64_t c = mg_cell(F, i, jl, k);
-            double at, as;
-            mg_offmul(F, i, jl, k, c, at, as);
-            const double zt = F.zt[c], zs = F.zs[c];
-            at += F.diag[c] * zt + F.diag[F.cstr + c] * zs;
-            as += F.diag[2 * F.cstr + c] * zt + F.diag[3 * F.cstr + c] * zs;
-            st += F.bt[c * F.bstr] - at;
-            ss += F.bs[c * F.bstr] - as;
-        }
-    bc[t] = st;
-    bc[ncl + t] = ss;
-    zc[t] = 0.0;
-    zc[ncl + t] = 0.0;
+    if (i < F.n && jl < F.mb) {
+        const int64_t c = mg_cell(F, i, jl, k);
+        double at, as;
+        mg_offmul(F, i, jl, k, c, at, as);
+        const double zt = F.zt[c], zs = F.zs[c];
+        at += F.diag[c] * zt + F.diag[F.cstr + c] * zs;
+        as += F.diag[2 * F.cstr + c] * zt + F.diag[3 * F.cstr + c] * zs;
+        st = F.bt[c * F.bstr] - at;
+        ss = F.bs[c * F.bstr] - as;
+    }
+    st += __shfl_xor(st, 1, 64);
+    ss += __shfl_xor(ss, 1, 64);
+    st += __shfl_xor(st, 2, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    if (ch == 0) {
+        bc[t] = st;
+        bc[ncl + t] = ss;
+        zc[t] = 0.0;
+        zc[ncl + t] = 0.0;
+    }
 }
 /* fine iterate += coarse correction of its aggregate (active unknowns only) */
 __global__ void k_mg_prolong(TsLev F, TsLev C)
@@ -2138,7 +2146,7 @@ static int mg_vcycle(iemic_ctx* c, int q)
     if ((rc = mg_smooth(c, q, nu, false))) return rc;
     const TsLev F = mg_view(c, q), C = mg_view(c, q + 1);
     if ((rc = mg_halo(c, F))) return rc;
-    hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
+    hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(4 * C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
                        gs.mg_z[q + 1].p);
     if ((rc = mg_vcycle(c, q + 1))) return rc;
     hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)F.n * F.mb * F.l)), dim3(256), 0, s, F, C);
