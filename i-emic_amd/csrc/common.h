@@ -98,6 +98,11 @@ struct BlockGS {
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
     DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_dinv[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
     DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
+    /* bands: the coarsest T/S level solved globally (all bands' coarsest cells plus the
+     * cross-band couplings; band LU + inverse on the device, redundant on every rank) */
+    int mg_glob = 0, mg_gN = 0, mg_g0 = 0;
+    DevBuf<double> mg_gX, mg_gband, mg_gvec, mg_gtmp, mg_glpan;
+    DevBuf<int> mg_gpiv, mg_ginfo, mg_gcols;
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work                               */
 };
 

@@ -1982,6 +1982,180 @@ static void dense_inverse(std::vector<double>& A, int N, std::vector<double>& X)
     }
 }
 
+/* Bands: the coarsest T/S level as one global problem.  Unknown (J, i, k, var) of the
+ * stacked bands' coarsest grids (J = band row offset + local row) is 2((J nc + i) l + k)
+ * + var, a band matrix of half-width 2 l nc + 1.  Every rank writes its own rows — its
+ * band-local coarsest operator plus the couplings of its edge rows to the neighbour
+ * bands' edge aggregates, taken from the level-0 couplings across the band edge (the
+ * Galerkin sum of piecewise-constant aggregates) — the rows are summed over the ranks,
+ * and every rank factorises (k_band_lu) and inverts (k_band_inv_pan) the whole matrix. */
+static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const std::vector<double>& dg)
+{
+    BlockGS& gs = c->gs;
+    gs.mg_glob = 0;
+    static const int enabled = [] {
+        const char* e = getenv("IEMIC_TS_GLOBAL");
+        return e ? atoi(e) : 1;
+    }();
+    if (c->nranks <= 1 || !enabled || c->l > 64) return 0;
+    const int P = c->nranks, me = c->rank, l = c->l, qc = gs.mg_nlev - 1;
+    const int nc = gs.mg_n[qc], cm = gs.mg_m[qc], mb = c->jb1 - c->jb0;
+    const int64_t ncl = (int64_t)nc * cm * l;
+    int rc;
+    /* coarsest rows of every band */
+    std::vector<double> rows(P, 0.0);
+    rows[me] = cm;
+    {
+        DevBuf<double> rb;
+        if (rb.alloc(P)) return IEMIC_ENOMEM;
+        if ((rc = h2d(c, rb.p, rows.data(), sizeof(double) * P))) return rc;
+        if ((rc = allreduce_sum(c, rb.p, P))) return rc;
+        if ((rc = d2h(c, rows.data(), rb.p, sizeof(double) * P))) return rc;
+    }
+    std::vector<int> joff(P + 1, 0);
+    for (int r = 0; r < P; r++) joff[r + 1] = joff[r] + (int)rows[r];
+    const int MG = joff[P];
+    const int NG = 2 * nc * MG * l;
+    const int bl = 2 * l * nc + 1, bu = bl, W = 2 * bl + bu + 1;
+    {
+        /* LDS of the band kernels (same rules as the Schur band) */
+        const size_t lb = sizeof(double) * ((size_t)(NBP + bl) * (NBP + 1) + (size_t)NBP * (bl + bu));
+        const size_t li = sizeof(double) * (size_t)(std::max(bl + NBP + 1, bl + bu + 1) + 2 * NBP) * 16;
+        if (lb > 150 * 1024 || li > 150 * 1024 || (int64_t)NG * W > INT32_MAX) return 0;   /* stay band-local */
+    }
+    auto gidx = [&](int J, int i, int k, int var) { return 2 * ((J * nc + i) * l + k) + var; };
+    std::vector<double> H((size_t)NG * W, 0.0);
+    auto add = [&](int row, int col, double v) {
+        const int d = col - row;
+        if (d < -bl || d > bu) return false;
+        H[(size_t)row * W + (d + bl)] += v;
+        return true;
+    };
+    bool ok = true;
+    for (int64_t t = 0; t < ncl; t++) {
+        const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+        const int J = joff[me] + jl;
+        for (int R = 0; R < 2; R++) {
+            const int row = gidx(J, i, k, R);
+            ok &= add(row, gidx(J, i, k, R), dg[(3 * R) * ncl + t]);
+            ok &= add(row, gidx(J, i, k, 1 - R), dg[(1 + R) * ncl + t]);
+            for (int qq = 0; qq < 8; qq++) {
+                const double v = off[(8 * R + qq) * ncl + t];
+                if (v == 0.0) continue;
+                int ii = i, jj = jl, kk = k;
+                switch (qq < 6 ? qq : qq - 2) {
+                case 0: ii--; break;
+                case 1: ii++; break;
+                case 2: jj--; break;
+                case 3: jj++; break;
+                case 4: kk--; break;
+                default: kk++; break;
+                }
+                if (jj < 0 || jj >= cm || kk < 0 || kk >= l) continue;
+                if (ii < 0 || ii >= nc) {
+                    if (!c->cfg.periodic) continue;
+                    ii = (ii + nc) % nc;
+                }
+                ok &= add(row, gidx(joff[me] + jj, ii, kk, qq < 6 ? R : 1 - R), v);
+            }
+        }
+    }
+    /* cross-band couplings: level-0 T/S couplings of the band's first (-j) and last (+j)
+     * latitude rows, summed into the edge aggregates */
+    {
+        const int64_t slab = (int64_t)l * c->n;
+        std::vector<double> e(slab);
+        for (int side = 0; side < 2; side++) {
+            if (side == 0 && me == 0) continue;
+            if (side == 1 && me == P - 1) continue;
+            const int jl = side == 0 ? 0 : mb - 1;
+            const int Jsrc = joff[me] + (jl >> qc);
+            const int Jdst = side == 0 ? joff[me] - 1 : joff[me + 1];
+            for (int R = 0; R < 2; R++) {
+                const int q = side == 0 ? 2 : 3;
+                const double* src = gs.tsoff.p + (int64_t)(R * 8 + q) * c->next + c->own0 + (int64_t)jl * slab;
+                if ((rc = d2h(c, e.data(), src, sizeof(double) * slab))) return rc;
+                for (int k = 0; k < l; k++)
+                    for (int i = 0; i < c->n; i++) {
+                        const double v = e[(int64_t)k * c->n + i];
+                        if (v != 0.0)
+                            ok &= add(gidx(Jsrc, i >> qc, k, R), gidx(Jdst, i >> qc, k, R), v);
+                    }
+            }
+        }
+    }
+    if (!ok) return 0;                        /* outside the assumed band: stay band-local */
+    /* own rows without entries (inactive unknowns) become identity rows */
+    const int g0 = gidx(joff[me], 0, 0, 0), g1 = gidx(joff[me + 1], 0, 0, 0);
+    for (int row = g0; row < g1; row++) {
+        bool any = false;
+        for (int d = 0; d < W; d++) any |= H[(size_t)row * W + d] != 0.0;
+        if (!any) H[(size_t)row * W + bl] = 1.0;
+    }
+    const size_t npan = (size_t)(NG + NBP - 1) / NBP;
+    if (gs.mg_gband.n < (size_t)NG * W) {
+        if (gs.mg_gband.alloc((size_t)NG * W) || gs.mg_gX.alloc((size_t)NG * NG) ||
+            gs.mg_gvec.alloc(NG) || gs.mg_gtmp.alloc(NG) || gs.mg_gpiv.alloc(NG) ||
+            gs.mg_ginfo.alloc(1) || gs.mg_gcols.alloc(NG) ||
+            gs.mg_glpan.alloc(npan * (NBP + bl) * NBP))
+            return IEMIC_ENOMEM;
+        std::vector<int> cols(NG);
+        for (int q = 0; q < NG; q++) cols[q] = q;
+        if ((rc = h2d(c, gs.mg_gcols.p, cols.data(), sizeof(int) * NG))) return rc;
+    }
+    if ((rc = h2d(c, gs.mg_gband.p, H.data(), sizeof(double) * H.size()))) return rc;
+    if ((rc = allreduce_sum(c, gs.mg_gband.p, (int)((size_t)NG * W)))) return rc;
+    {
+        const size_t lb = sizeof(double) * ((size_t)(NBP + bl) * (NBP + 1) + (size_t)2 * NBP * (bl + bu));
+        const int stage_o = lb <= 150 * 1024 ? 1 : 0;
+        const size_t lbu = stage_o ? lb : lb - sizeof(double) * (size_t)NBP * (bl + bu);
+        HIP_OK(hipFuncSetAttribute((const void*)k_band_lu, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lbu));
+        hipLaunchKernelGGL(k_band_lu, dim3(1), dim3(1024), lbu, c->stream, gs.mg_gband.p, NG, bl, bu,
+                           gs.mg_gpiv.p, gs.mg_ginfo.p, gs.mg_glpan.p, stage_o);
+        int info = 0;
+        HIP_OK(hipGetLastError());
+        if ((rc = d2h(c, &info, gs.mg_ginfo.p, sizeof(int)))) return rc;
+        if (info != 0) return 0;              /* singular global coarse problem: band-local */
+        const int ring = std::max(bl + NBP + 1, bl + bu + 1);
+        const size_t li = (size_t)(ring + 2 * NBP) * 16 * sizeof(double);
+        HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_pan<16, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)li));
+        hipLaunchKernelGGL((k_band_inv_pan<16, false>), dim3((unsigned)((NG + 15) / 16)), dim3(256), li,
+                           c->stream, gs.mg_gband.p, gs.mg_glpan.p, gs.mg_gpiv.p, NG, bl, bu,
+                           gs.mg_gcols.p, NG, gs.mg_gX.p);
+        HIP_OK(hipGetLastError());
+    }
+    gs.mg_gN = NG;
+    gs.mg_g0 = g0;
+    gs.mg_glob = 1;
+    (void)ncl;
+    return 0;
+}
+
+/* local coarsest rhs (T block, S block) -> its entries of the global vector */
+__global__ void k_mg_gput(const double* __restrict__ b, int64_t ncl, int nc, int l, int g0,
+                          double* __restrict__ g)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ncl) return;
+    const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+    const int64_t q = g0 + 2 * (((int64_t)jl * nc + i) * l + k);
+    g[q] = b[t];
+    g[q + 1] = b[ncl + t];
+}
+/* own rows of the global solution (global order) -> local (T block, S block) */
+__global__ void k_mg_gget(const double* __restrict__ y, int64_t ncl, int nc, int l,
+                          double* __restrict__ z)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ncl) return;
+    const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+    const int64_t q = 2 * (((int64_t)jl * nc + i) * l + k);
+    z[t] = y[q];
+    z[ncl + t] = y[q + 1];
+}
+
 /* coarse levels, Galerkin operators and the coarsest inverse (once per Jacobian) */
 static int mg_setup(iemic_ctx* c)
 {
@@ -2067,7 +2241,8 @@ static int mg_setup(iemic_ctx* c)
         }
     }
     dense_inverse(A, N, X);
-    return h2d(c, gs.mg_cinv.p, X.data(), sizeof(double) * X.size());
+    if ((rc = h2d(c, gs.mg_cinv.p, X.data(), sizeof(double) * X.size()))) return rc;
+    return mg_global_setup(c, off, dg);
 }
 
 /* refresh the level-0 iterate's latitude halo rows (bands coupled in the T/S smoother) */
@@ -2138,6 +2313,20 @@ static int mg_vcycle(iemic_ctx* c, int q)
     int rc;
     if (q == gs.mg_nlev - 1) {
         const int N = 2 * gs.mg_n[q] * gs.mg_m[q] * c->l;
+        if (gs.mg_glob) {
+            /* global coarsest: gather the bands' right-hand sides, own rows of X b */
+            const int64_t ncl = N / 2;
+            HIP_OK(hipMemsetAsync(gs.mg_gvec.p, 0, sizeof(double) * gs.mg_gN, s));
+            hipLaunchKernelGGL(k_mg_gput, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_b[q].p, ncl,
+                               gs.mg_n[q], c->l, gs.mg_g0, gs.mg_gvec.p);
+            if ((rc = allreduce_sum(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
+            hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s,
+                               gs.mg_gX.p + (int64_t)gs.mg_g0 * gs.mg_gN, N, gs.mg_gN, gs.mg_gvec.p,
+                               gs.mg_gtmp.p);
+            hipLaunchKernelGGL(k_mg_gget, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_gtmp.p, ncl,
+                               gs.mg_n[q], c->l, gs.mg_z[q].p);
+            return 0;
+        }
         hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
                            gs.mg_b[q].p, gs.mg_z[q].p);
         return 0;
