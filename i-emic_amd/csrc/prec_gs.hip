@@ -1556,14 +1556,26 @@ __device__ __forceinline__ B2 shfl_b2(const B2& x, int src)
 {
     return {__shfl(x.a, src, P), __shfl(x.b, src, P), __shfl(x.c, src, P), __shfl(x.d, src, P)};
 }
+/* launched over the columns of one colour only: row jl holds the columns
+ * i = 2h + ((colour + jl) & 1), h < ceil(n'/2) (n' = n - 1 on an odd periodic level, whose
+ * last column has colour 2 or 3 by row parity, see mg_lcolour) */
 template <int P>
 __global__ void __launch_bounds__(256) k_mg_zline_pcr(TsLev V, int colour)
 {
-    const int t = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
-    if (t >= V.n * V.mb) return;                       /* whole column groups exit */
-    const int i = t % V.n, jl = t / V.n;
-    if (mg_lcolour(V, i, jl) != colour) return;
+    const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
+    const int per_row = colour < 2 ? (np + 1) / 2 : 1;
+    if (g >= per_row * V.mb) return;                   /* whole column groups exit */
+    const int jl = g / per_row;
+    int i;
+    if (colour < 2) {
+        i = 2 * (g % per_row) + ((colour + jl) & 1);
+        if (i >= np) return;
+    } else {
+        i = V.n - 1;
+        if ((jl & 1) != colour - 2) return;
+    }
     const int64_t cs = V.cstr;
     B2 A{1.0, 0.0, 0.0, 1.0}, Bm{0.0, 0.0, 0.0, 0.0}, Cm{0.0, 0.0, 0.0, 0.0};
     double d0 = 0.0, d1 = 0.0;
@@ -2263,7 +2275,8 @@ static int mg_smooth(iemic_ctx* c, int q, int nu, bool post)
         const TsLev V = mg_view(c, q);
         const int ncolour = (V.periodic && (V.n & 1)) ? 4 : 2;
         const int P = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : 64);
-        const unsigned gp = (unsigned)(((int64_t)V.n * V.mb * P + 255) / 256);
+        const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
+        const unsigned gp = (unsigned)(((int64_t)((np + 1) / 2) * V.mb * P + 255) / 256);
         for (int sw = 0; sw < nu; sw++)
             for (int h = 0; h < ncolour; h++) {
                 const int col = post ? ncolour - 1 - h : h;
