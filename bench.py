@@ -63,7 +63,6 @@ def parse():
                    help="defect-correction passes on the dynamics block of the block GS")
     p.add_argument("--dyn-omega", type=float, default=0.95, help="step of the correction passes")
     p.add_argument("--dyn-mr", action="store_true", help="minimal-residual step per pass")
-    p.add_argument("--schur-fp64", action="store_true", help="Schur inverse in fp64 (default fp32)")
     p.add_argument("--ts-mg", type=int, default=1,
                    help="T/S aggregation-multigrid V-cycles (0: --ts-sweeps plain sweeps)")
     p.add_argument("--mg-sweeps", type=int, default=1, help="sweeps per multigrid level")
@@ -173,7 +172,7 @@ def main():
           "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth,
           "Dyn iterations": args.dyn_iters,
-          "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr, "Schur fp32": not args.schur_fp64,
+          "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps}
     comm_id = None
     if world > 1:
@@ -257,7 +256,7 @@ def main():
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
-                   "schur": "fp64" if args.schur_fp64 else "fp32",
+                   "schur": "cyclic reduction (fp64, exact)",
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps,
                    "parallelism": f"latitude-bands x{world}" if world > 1 else "single",
                    "band_rows": [lay["jb0"], lay["jb1"]]},

@@ -52,6 +52,30 @@ template <typename T> struct DevBuf {
     ~DevBuf() { free(); }
 };
 
+/* Block cyclic reduction of the 2-D Schur complement (schur_cr.hip).  m x m blocks,
+ * column-major; level l has N[l] blocks (N[nlev] = 1). */
+struct CrGemm {                      /* C = C0 + C0b + s1 A1 B1 + s2 A2 B2                 */
+    double* C;
+    const double *C0, *C0b, *A1, *B1, *A2, *B2;
+    double s1, s2;
+};
+struct SchurCR {
+    int n = 0, m = 0, periodic = 0, nlev = 0;
+    std::vector<int> N, per, merge;  /* blocks, periodic coupling, periodic pair merged   */
+    std::vector<size_t> dlr_off;     /* level l: D, L, R blocks (3 N[l])                  */
+    std::vector<size_t> ap_off;      /* level l: XL, XR (evens), Dinv, YL, YR (odds);      */
+                                     /* level nlev: the last block's inverse              */
+    std::vector<size_t> v_off;       /* level vectors b_l, x_l (l >= 1)                   */
+    std::vector<int> g_off, g_cnt;   /* GEMM descriptor ranges: 3 per level               */
+    DevBuf<double> dlr, ap, bv, xv;
+    DevBuf<CrGemm> gd;
+    DevBuf<int> info;
+};
+int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic);
+int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij);
+int cr_check(iemic_ctx* c, SchurCR& cr);
+int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s);
+
 /* Preconditioner state (prec.hip: block Jacobi, prec_gs.hip: block Gauss-Seidel). */
 struct BlockGS {
     int ready = 0;
@@ -61,13 +85,12 @@ struct BlockGS {
     /* structure (rebuilt when the identity-row pattern changes) */
     std::vector<double> flags_h;     /* global (active column, U/V point) flags the      */
                                      /* structure was built for                         */
-    int ncol = 0, bl = 0, bu = 0;    /* active water columns, Schur band widths          */
-    int ncol_own = 0;                /* columns of this band (inverse slab width)       */
-    DevBuf<int> own_cols;            /* their Schur indices, ascending                  */
-    DevBuf<int> own_pos;             /* Schur index -> position in own_cols or -1       */
+    int ncol = 0;                    /* active water columns                            */
+    DevBuf<int> own_pos;             /* Schur index -> itself for this band's active     */
+                                     /* columns, -1 otherwise                           */
     DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8), halo-filled */
     DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
-    DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index (band order) or -1       */
+    DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index i*m+j, or -1 (no water)   */
     DevBuf<int> ij_of_col;           /* Schur index -> j*n+i                            */
     DevBuf<uint8_t> pinned;          /* Schur index pinned to 0 (null-space pins)       */
     /* numeric factors */
@@ -77,12 +100,8 @@ struct BlockGS {
     DevBuf<double> tsoff;            /* compact T/S off-diagonal couplings, 16 x ncell  */
     DevBuf<double> tsc, tic, bc;     /* the same per colour (even n), T/S rhs per colour */
     DevBuf<double> zt, zs, tcell;    /* T/S iterates, per-cell work                      */
-    DevBuf<double> band;             /* Schur band, row-wise, width 2*bl+bu+1           */
-    DevBuf<int> piv, info;
-    DevBuf<double> lpan;             /* band-LU panel multipliers                       */
-    DevBuf<double> sinv;             /* Schur inverse columns of this band, ncol x ncol_own */
-    DevBuf<float> sinvf;             /* the same in fp32, rows padded to ldf (16-B rows)  */
-    int ldf = 0, fp32 = 1;           /* fp32: the apply's GEMV reads sinvf               */
+    DevBuf<double> S9;               /* Schur rows, 9 couplings per column (i*m+j)       */
+    SchurCR cr;                      /* its cyclic-reduction factors                     */
     int dyn_iters = 1;               /* defect-correction passes on the dynamics block   */
     DevBuf<double> dres, zc;         /* dynamics defect and correction (ext rows)        */
     DevBuf<double> dq, dzero, dmr;   /* MR passes: -A_DD zc, a zero vector, dot partials  */
@@ -103,7 +122,8 @@ struct BlockGS {
     int mg_glob = 0, mg_gN = 0, mg_g0 = 0;
     DevBuf<double> mg_gX, mg_gband, mg_gvec, mg_gtmp, mg_glpan;
     DevBuf<int> mg_gpiv, mg_ginfo, mg_gcols;
-    DevBuf<double> rr, bts, colv, colv2, colv_own; /* work                               */
+    DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
+                                     /* summed into colv), solution colv2               */
 };
 
 struct Krylov {

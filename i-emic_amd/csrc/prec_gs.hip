@@ -13,15 +13,15 @@
  *   2. uv*  : D^-1 (r_uv - Guv ptil), D = per-point 2x2 U/V (Coriolis) block
  *   3. pbar : depth-integrated continuity per water column, 2-D Schur complement
  *             S = Mz2 Duv D^-1 Guv Mz1^T (9-point, corner-staggered), null space pinned
- *             (one column per checkerboard colour and basin), solved with a dense inverse
- *             built on the GPU from a band LU with partial pivoting
+ *             (one column per checkerboard colour and basin), solved exactly by block
+ *             cyclic reduction over longitudes (schur_cr.hip)
  *   4. uv   : uv* - D^-1 Guv Mz1^T pbar,  p = ptil + Mz1^T pbar
  *   5. w    : continuity rows Dw w = r_p - Duv uv, column-wise bottom-up
  *   6. ts   : A_ts ts = r_ts - B_ts,uv uv - B_ts,w w, by symmetric red-black Gauss-Seidel
  *             sweeps with 2x2 T/S cell blocks (parity of i+j+k)
  * Every step is a structured-grid kernel over cells or water columns reading the
- * stencil-ELL Jacobian in place; the only dense object is the Schur inverse
- * (ncol^2 doubles, 0.7 GB at 2 degrees).
+ * stencil-ELL Jacobian in place; the only dense objects are the m x m blocks of the
+ * Schur cyclic reduction (O(n m^2) doubles, 40 MB at 2 degrees).
  */
 #include <algorithm>
 #include <cstdlib>
@@ -154,36 +154,33 @@ __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __
     pw[cell] = w;
 }
 
-/* Schur entry S[c][c'] for c' = column (i+di, j+dj), written into the band (row-wise).
+/* Schur entry S[c][c'] for c' = column (i+di, j+dj): S9[c*9 + (dj+1)*3 + (di+1)], c = i*m + j.
  * Only the rows of this band's columns are built (the bands' rows are summed over the
  * ranks afterwards); corner U/V points one latitude row below the band are read from the
  * halo-filled per-cell arrays (known, uvinv, gslot). */
 __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __restrict__ known,
                               const double* __restrict__ uvinv, const double* __restrict__ gslot,
-                              const double* __restrict__ pw,
-                              const int* __restrict__ col_of_ij, const int* __restrict__ ij_of_col,
-                              const uint8_t* __restrict__ pinned, int ncol, int bl, int bu,
-                              Lay L, int jb1, double* __restrict__ band)
+                              const double* __restrict__ pw, const int* __restrict__ col_of_ij,
+                              const uint8_t* __restrict__ pinned, Lay L, int jb1,
+                              double* __restrict__ S9)
 {
     LAY_ALIASES;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)ncol * 9) return;
-    const int c = (int)(t / 9), o = (int)(t % 9);
+    if (t >= (int64_t)n * (jb1 - L.jb0) * 9) return;
+    const int q = (int)(t / 9), o = (int)(t % 9);
     const int di = o % 3 - 1, dj = o / 3 - 1;
-    const int ij = ij_of_col[c];
-    const int i = ij % n, j = ij / n;
-    if (j < L.jb0 || j >= jb1) return;
+    const int i = q % n, j = L.jb0 + q / n;
+    const int c = col_of_ij[j * n + i];
+    if (c < 0) return;
+    double* row = S9 + (int64_t)c * 9;
+    if (pinned[c]) {
+        if (o == 4) row[4] = 1.0;
+        return;
+    }
     int ti = i + di, tj = j + dj;
     if (!hnb(ti, tj, n, m, periodic)) return;
     const int c2 = col_of_ij[tj * n + ti];
-    if (c2 < 0 || c2 - c < -bl || c2 - c > bl + bu) return;
-    const int W = 2 * bl + bu + 1;
-    double* row = band + (int64_t)c * W;
-    if (pinned[c]) {
-        if (c2 == c) row[bl] = 1.0;
-        return;
-    }
-    if (pinned[c2]) return;
+    if (c2 < 0 || pinned[c2]) return;
     const int64_t ncell = L.nloc;
     double s = 0.0;
     for (int k = 0; k < l; k++) {
@@ -214,7 +211,7 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
         }
         s += pw[pc] * acc;
     }
-    row[c2 - c + bl] += s;
+    row[o] = s;
 }
 
 /* per owned cell: the U and V rows' couplings to the 4 P corners (slots 20..23, 42..45) */
@@ -434,90 +431,6 @@ __global__ void __launch_bounds__(1024) k_band_lu(double* __restrict__ ab, int n
  *   forward  (P, L^-1): rows k..k+bl      y is written to X
  *   backward (U^-1)   : rows i+1..i+bl+bu x overwrites y in X
  * Two barriers per elimination step; the factors are read from L2. */
-template <int NB>
-__global__ void __launch_bounds__(256) k_band_inv_blk(const double* __restrict__ ab,
-                                                      const double* __restrict__ lpan,
-                                                      const int* __restrict__ piv, int ncol,
-                                                      int bl, int bu, const int* __restrict__ cols,
-                                                      int nq, double* __restrict__ Xs)
-{
-    extern __shared__ double lds[];
-    constexpr int G = 256 / NB;              /* row groups */
-    const int W = 2 * bl + bu + 1;
-    const int col = threadIdx.x % NB, grp = threadIdx.x / NB;
-    const int q0 = blockIdx.x * NB;
-    const int q = q0 + col;
-    const bool on = q < nq;
-    const int c0 = cols[q0];
-    const int c = on ? cols[q] : -1;
-    double* red = lds;                       /* G x NB partial sums */
-    double* win = lds + G * NB;              /* ring buffer         */
-    /* ---- forward, panel by panel: ring of R1 = bl + NBP + 1 rows ---- */
-    const int R1 = bl + NBP + 1;
-    const int kst = (max(0, c0 - bl - NBP + 1) / NBP) * NBP;
-    for (int r = kst + grp; r <= min(kst + NBP - 1 + bl, ncol - 1); r += G)
-        win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
-    for (int k0 = kst; k0 < ncol; k0 += NBP) {
-        const int nbk = min(NBP, ncol - k0);
-        const int pend = min(k0 + nbk - 1 + bl, ncol - 1);
-        const int nprow = pend - k0 + 1;
-        const double* Lp = lpan + (int64_t)(k0 / NBP) * (NBP + bl) * NBP;
-        __syncthreads();
-        if (grp == 0)
-            for (int t = 0; t < nbk; t++) {
-                const int rp = piv[k0 + t] - k0;
-                if (rp != t) {
-                    double* a = win + ((k0 + t) % R1) * NB + col;
-                    double* b = win + ((k0 + rp) % R1) * NB + col;
-                    const double x = *a; *a = *b; *b = x;
-                }
-            }
-        __syncthreads();
-        for (int t = 0; t < nbk; t++) {
-            const double bk = win[((k0 + t) % R1) * NB + col];
-            if (bk != 0.0)
-                for (int r = t + 1 + grp; r < nprow; r += G)
-                    win[((k0 + r) % R1) * NB + col] -= Lp[r * NBP + t] * bk;
-            __syncthreads();
-        }
-        /* rows k0 .. k0+nbk-1 are final: y -> X; bring in the rows of the next panel */
-        for (int t = grp; t < nbk; t += G)
-            if (on) Xs[(int64_t)(k0 + t) * nq + q] = win[((k0 + t) % R1) * NB + col];
-        __syncthreads();
-        for (int r = pend + 1 + grp; r <= min(k0 + 2 * NBP - 1 + bl, ncol - 1); r += G)
-            win[(r % R1) * NB + col] = (r == c) ? 1.0 : 0.0;
-    }
-    /* rows above the first panel are zero in y */
-    if (grp == 0 && on)
-        for (int r = 0; r < kst; r++) Xs[(int64_t)r * nq + q] = 0.0;
-    /* ---- backward: ring of R2 = bl + bu + 1 rows holding x(i+1 .. i+bl+bu) ---- */
-    const int R2 = bl + bu + 1;
-    __syncthreads();
-    for (int i = ncol - 1; i >= 0; i--) {
-        const int jend = min(i + bl + bu, ncol - 1);
-        const double* ar = ab + (int64_t)i * W + (bl - i);
-        double s = 0.0;
-        for (int j = i + 1 + grp; j <= jend; j += G) s += ar[j] * win[(j % R2) * NB + col];
-        red[grp * NB + col] = s;
-        __syncthreads();
-        if (grp == 0) {
-            double t = 0.0;
-            for (int g2 = 0; g2 < G; g2++) t += red[g2 * NB + col];
-            const double y = on ? Xs[(int64_t)i * nq + q] : 0.0;
-            const double x = (y - t) / ar[i];
-            win[(i % R2) * NB + col] = x;
-            if (on) Xs[(int64_t)i * nq + q] = x;
-        }
-        __syncthreads();
-    }
-}
-
-/* Panel-blocked variant of k_band_inv_blk (same inputs, same output): per panel of NBP
- * rows the triangular part is solved by the NB lanes of wavefront 0 (one right-hand side
- * per lane, no workgroup barrier inside the panel) and the coupling to the rest of the
- * window is one parallel block update, so a panel costs ~3 barriers instead of 2 per row.
- *   forward : swaps, L11 solve (wave 0), rows below -= L21 y_panel (all threads)
- *   backward: t = U(panel, right of panel) x (all threads), U11 solve (wave 0)          */
 template <int NB, bool STAGE>
 __global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__ ab,
                                                       const double* __restrict__ lpan,
@@ -1038,84 +951,6 @@ __global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int 
     double s = (s0 + s1) + (s2 + s3);
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     if (lane == 0) y[row] = s;
-}
-
-/* b_own[q] = b[cols[q]] */
-__global__ void k_gather(const double* __restrict__ b, const int* __restrict__ cols, int nq,
-                         double* __restrict__ bo)
-{
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nq) bo[q] = b[cols[q]];
-}
-
-/* fp32 copy of the Schur inverse slab, rows padded to ld floats (16-B aligned rows) */
-__global__ void k_to_f32(const double* __restrict__ X, int nr, int nc, float* __restrict__ Y, int ld)
-{
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)nr * ld) return;
-    const int r = (int)(t / ld), c = (int)(t % ld);
-    Y[t] = c < nc ? (float)X[(int64_t)r * nc + c] : 0.0f;
-}
-
-/* 3b'. y = X b with X fp32 (row-major, ld floats per row, ld % 4 == 0), fp64 accumulation:
- * RPW rows per wavefront, 16-B loads of X, each b element loaded once per RPW rows; UNR
- * column steps unrolled so RPW * UNR loads per lane are in flight */
-template <int RPW, int UNR>
-__global__ void __launch_bounds__(256) k_gemv_f(const float* __restrict__ X, int nr, int nc, int ld,
-                                                const double* __restrict__ b, double* __restrict__ y)
-{
-    const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-    const int lane = threadIdx.x & 63;
-    if (r0 >= nr) return;
-    const int nrow = min(RPW, nr - r0);
-    const float4* xr[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; q++)
-        xr[q] = reinterpret_cast<const float4*>(X + (int64_t)(r0 + min(q, nrow - 1)) * ld);
-    double s[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; q++) s[q] = 0.0;
-    const int n4 = ld >> 2;
-    int c4 = lane;
-    for (; c4 + 64 * (UNR - 1) < n4; c4 += 64 * UNR) {
-        float4 v[UNR][RPW];
-#pragma unroll
-        for (int u = 0; u < UNR; u++)
-#pragma unroll
-            for (int q = 0; q < RPW; q++) v[u][q] = xr[q][c4 + 64 * u];
-#pragma unroll
-        for (int u = 0; u < UNR; u++) {
-            const int c = 4 * (c4 + 64 * u);
-            const double b0 = c < nc ? b[c] : 0.0, b1 = c + 1 < nc ? b[c + 1] : 0.0;
-            const double b2 = c + 2 < nc ? b[c + 2] : 0.0, b3 = c + 3 < nc ? b[c + 3] : 0.0;
-#pragma unroll
-            for (int q = 0; q < RPW; q++)
-                s[q] += (double)v[u][q].x * b0 + (double)v[u][q].y * b1 + (double)v[u][q].z * b2 +
-                        (double)v[u][q].w * b3;
-        }
-    }
-    for (; c4 < n4; c4 += 64) {
-        const int c = 4 * c4;
-        const double b0 = c < nc ? b[c] : 0.0, b1 = c + 1 < nc ? b[c + 1] : 0.0;
-        const double b2 = c + 2 < nc ? b[c + 2] : 0.0, b3 = c + 3 < nc ? b[c + 3] : 0.0;
-#pragma unroll
-        for (int q = 0; q < RPW; q++) {
-            const float4 v = xr[q][c4];
-            s[q] += (double)v.x * b0 + (double)v.y * b1 + (double)v.z * b2 + (double)v.w * b3;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; q++) {
-        double t = s[q];
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
-        if (lane == 0 && q < nrow) y[r0 + q] = t;
-    }
-}
-/* measured at 2 deg (325 MB fp32 slab): <4, 2> 1-2 % faster than <4, 1>, <2, *>, <1, 4>, <8, 1> */
-static void gemv_f(const BlockGS& gs, hipStream_t s)
-{
-    hipLaunchKernelGGL((k_gemv_f<4, 2>), dim3((unsigned)((gs.ncol + 15) / 16)), dim3(256), 0, s,
-                       gs.sinvf.p, gs.ncol, gs.ncol_own, gs.ldf, gs.colv_own.p, gs.colv2.p);
 }
 
 /* dynamics defect: d = rr - A_DD z on the active U/V/W/P rows (couplings to active
@@ -1800,22 +1635,28 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
             if (act[(size_t)j * n + i]) ord.push_back({(int64_t)ipos[i] * m + j, j * n + i});
     std::sort(ord.begin(), ord.end());
     const int ncol = (int)ord.size();
-    std::vector<int> ij_of_col(ncol);
+    /* Schur index of column (i, j): c = i*m + j (the cyclic reduction's block order); the
+     * band order above only fixes which column of a null-space set is pinned (its first),
+     * the same choice as the CPU twin */
+    const int NC = n * m;
+    std::vector<int> ij_of_col(NC);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < m; j++) ij_of_col[(size_t)i * m + j] = j * n + i;
     for (int q = 0; q < ncol; q++) {
-        ij_of_col[q] = ord[q].second;
-        colid[ord[q].second] = q;
+        const int ij = ord[q].second;
+        colid[ij] = (ij % n) * m + ij / n;
     }
     /* couplings: columns sharing an active U/V corner */
-    int bw = 0;
-    std::vector<std::vector<int>> adj(ncol);
+    std::vector<std::vector<int>> adj(NC);
     for (int q = 0; q < ncol; q++) {
-        const int i = ij_of_col[q] % n, j = ij_of_col[q] / n;
+        const int ij0 = ord[q].second;
+        const int i = ij0 % n, j = ij0 / n, cq = colid[ij0];
         for (int dj = -1; dj <= 1; dj++)
             for (int di = -1; di <= 1; di++) {
                 int ti = i + di, tj = j + dj;
                 if (!wrap(ti, tj)) continue;
                 const int q2 = colid[(size_t)tj * n + ti];
-                if (q2 < 0 || q2 == q) continue;
+                if (q2 < 0 || q2 == cq) continue;
                 bool shared = false;
                 for (int a = -1; a <= 0 && !shared; a++)
                     for (int b = -1; b <= 0 && !shared; b++) {
@@ -1826,77 +1667,60 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
                         if (!wrap(qi, qj)) continue;
                         if (uva[(size_t)qj * n + qi]) shared = true;
                     }
-                if (!shared) continue;
-                adj[q].push_back(q2);
-                bw = std::max(bw, std::abs(q2 - q));
+                if (shared) adj[cq].push_back(q2);
             }
     }
     /* null space of the B-grid pressure Schur: constant on each connected set of
      * same-colour columns linked diagonally through an active U/V corner (checkerboard
      * modes, local ones around islands and straits included) -> one pin per set */
-    std::vector<uint8_t> pin(ncol, 0);
-    std::vector<int> comp(ncol, -1);
-    for (int s = 0; s < ncol; s++) {
-        if (comp[s] >= 0) continue;
-        std::vector<int> stack{s};
-        comp[s] = s;
-        pin[s] = 1; /* band order: s is the first column of its set */
+    std::vector<uint8_t> pin(NC, 0);
+    std::vector<int> comp(NC, -1);
+    for (int q = 0; q < ncol; q++) {
+        const int s0 = colid[ord[q].second];       /* band order: first column of its set */
+        if (comp[s0] >= 0) continue;
+        std::vector<int> stack{s0};
+        comp[s0] = s0;
+        pin[s0] = 1;
         while (!stack.empty()) {
-            const int q = stack.back();
+            const int cq = stack.back();
             stack.pop_back();
-            const int qi0 = ij_of_col[q] % n, qj0 = ij_of_col[q] / n;
-            for (int q2 : adj[q]) {
-                int di = ij_of_col[q2] % n - qi0;
-                const int dj = ij_of_col[q2] / n - qj0;
+            for (int q2 : adj[cq]) {
+                int di = q2 / m - cq / m;
+                const int dj = q2 % m - cq % m;
                 if (di > 1) di -= n;
                 if (di < -1) di += n;
                 if (di == 0 || dj == 0) continue; /* other colour */
-                if (comp[q2] < 0) { comp[q2] = s; stack.push_back(q2); }
+                if (comp[q2] < 0) { comp[q2] = s0; stack.push_back(q2); }
             }
         }
     }
-    if ((int64_t)ncol * std::max<int64_t>(1, ncol / std::max(1, c->nranks)) > (int64_t)4 << 30) {
-        set_error("block GS: too many water columns for the dense Schur inverse");
-        return IEMIC_EINVAL;
-    }
-    std::vector<int> own;
+    std::vector<int> own(NC, -1);
     for (int q = 0; q < ncol; q++) {
-        const int j = ij_of_col[q] / n;
-        if (j >= c->jb0 && j < c->jb1) own.push_back(q);
+        const int ij = ord[q].second;
+        if (ij / n >= c->jb0 && ij / n < c->jb1) own[colid[ij]] = colid[ij];
     }
-    const int nq = std::max(1, (int)own.size());
-    if (own.empty()) own.push_back(0);     /* keeps the kernels' shapes valid; b_own = 0 */
     gs.ncol = ncol;
-    gs.ncol_own = (int)own.size();
-    gs.bl = gs.bu = std::max(bw, 1);
-    const int W = 2 * gs.bl + gs.bu + 1;
     int rc = 0;
     rc |= gs.col_of_ij.alloc((size_t)n * m);
-    rc |= gs.ij_of_col.alloc(ncol);
-    rc |= gs.pinned.alloc(ncol);
-    rc |= gs.band.alloc((size_t)ncol * W);
-    rc |= gs.piv.alloc(ncol);
-    rc |= gs.lpan.alloc((size_t)((ncol + NBP - 1) / NBP) * (NBP + gs.bl) * NBP);
-    rc |= gs.info.alloc(1);
-    rc |= gs.sinv.alloc((size_t)ncol * nq);
-    rc |= gs.colv.alloc(ncol);
-    rc |= gs.colv2.alloc(ncol);
-    rc |= gs.colv_own.alloc(nq);
-    rc |= gs.own_cols.alloc(nq);
-    rc |= gs.own_pos.alloc(ncol);
+    rc |= gs.ij_of_col.alloc(NC);
+    rc |= gs.pinned.alloc(NC);
+    rc |= gs.S9.alloc((size_t)9 * NC);
+    rc |= gs.colv2.alloc(NC);
+    rc |= gs.colv_own.alloc(NC);
+    rc |= gs.colv.alloc(NC);
+    rc |= gs.own_pos.alloc(NC);
     if (rc) {
         set_error("block GS: out of device memory");
         return IEMIC_ENOMEM;
     }
     if ((rc = h2d(c, gs.col_of_ij.p, colid.data(), sizeof(int) * colid.size()))) return rc;
-    if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * ncol))) return rc;
-    if ((rc = h2d(c, gs.pinned.p, pin.data(), ncol))) return rc;
-    if ((rc = h2d(c, gs.own_cols.p, own.data(), sizeof(int) * own.size()))) return rc;
-    {
-        std::vector<int> pos(ncol, -1);
-        for (size_t q = 0; q < own.size(); q++) pos[own[q]] = (int)q;
-        if ((rc = h2d(c, gs.own_pos.p, pos.data(), sizeof(int) * pos.size()))) return rc;
-    }
+    if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * NC))) return rc;
+    if ((rc = h2d(c, gs.pinned.p, pin.data(), NC))) return rc;
+    if ((rc = h2d(c, gs.own_pos.p, own.data(), sizeof(int) * NC))) return rc;
+    /* entries of inactive and foreign columns stay 0 (the rhs of the reduced solve) */
+    HIP_OK(hipMemsetAsync(gs.colv_own.p, 0, sizeof(double) * NC, c->stream));
+    HIP_OK(hipMemsetAsync(gs.colv2.p, 0, sizeof(double) * NC, c->stream));
+    if ((rc = cr_init(c, gs.cr, n, m, periodic))) return rc;
     gs.flags_h = flags;
     return 0;
 }
@@ -2438,111 +2262,16 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     if ((c->n & 1) == 0)
         hipLaunchKernelGGL(k_ts_pack, dim3(gc), dim3(256), 0, c->stream, gs.tsoff.p, gs.tsinv.p,
                            gs.tsc.p, gs.tic.p, L, next);
-    const int W = 2 * gs.bl + gs.bu + 1;
-    HIP_OK(hipMemsetAsync(gs.band.p, 0, sizeof(double) * (size_t)gs.ncol * W, c->stream));
-    const int64_t nt = (int64_t)gs.ncol * 9;
+    const int NC = c->n * c->m;
+    HIP_OK(hipMemsetAsync(gs.S9.p, 0, sizeof(double) * 9 * (size_t)NC, c->stream));
+    const int64_t nt = (int64_t)c->n * (c->jb1 - c->jb0) * 9;
     hipLaunchKernelGGL(k_schur_build, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream,
                        c->d_val.p, gs.known.p, gs.uvinv.p, gs.gslot.p, gs.pw.p, gs.col_of_ij.p,
-                       gs.ij_of_col.p, gs.pinned.p, gs.ncol, gs.bl, gs.bu, L, c->jb1, gs.band.p);
-    /* every band built the rows of its own columns: the sum is the whole Schur band */
-    if ((rc = allreduce_sum(c, gs.band.p, gs.ncol * W))) return rc;
-    {
-        size_t lb = sizeof(double) * ((size_t)(NBP + gs.bl) * (NBP + 1) + (size_t)2 * NBP * (gs.bl + gs.bu));
-        int stage_o = 1;                        /* pivot rows below the panel staged in LDS */
-        if (lb > 150 * 1024) {
-            lb -= sizeof(double) * (size_t)NBP * (gs.bl + gs.bu);
-            stage_o = 0;
-        }
-        if (lb > 150 * 1024) {
-            set_error("block GS: Schur band too wide for the LDS band LU");
-            return IEMIC_EINVAL;
-        }
-        HIP_OK(hipFuncSetAttribute((const void*)k_band_lu, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lb));
-        hipLaunchKernelGGL(k_band_lu, dim3(1), dim3(1024), lb, c->stream, gs.band.p, gs.ncol, gs.bl,
-                           gs.bu, gs.piv.p, gs.info.p, gs.lpan.p, stage_o);
-    }
-    int info = 0;
-    HIP_OK(hipGetLastError());
-    if ((rc = d2h(c, &info, gs.info.p, sizeof(int)))) return rc;
-    if (info != 0) {
-        set_error("block GS: singular Schur complement (pivot " + std::to_string(info - 1) + ")");
-        return IEMIC_EINVAL;
-    }
-    {
-        /* pick the widest RHS block whose ring buffers fit in LDS */
-        const int rows = std::max(gs.bl + NBP + 1, gs.bl + gs.bu + 1);
-        auto bytes = [&](int nb) { return (size_t)(rows + 256 / nb) * nb * sizeof(double); };
-        const size_t lmax = 150 * 1024;
-        static const int force_nb = [] {
-            const char* e = getenv("IEMIC_INV_NB");
-            return e ? atoi(e) : 0;
-        }();
-        static const bool old_inv = getenv("IEMIC_INV_OLD") != nullptr;
-        if (!old_inv) {
-            /* panel-blocked inverse: LDS = panel sums + ring of max(bl+NBP+1, bl+bu+1) rows
-             * (+ the staged panel multipliers / U rows when they fit) */
-            const int ring = std::max(gs.bl + NBP + 1, gs.bl + gs.bu + 1);
-            const size_t stg = (size_t)std::max((NBP + gs.bl) * NBP, NBP * (gs.bl + gs.bu + 1));
-            auto pbytes = [&](int nb, bool st) {
-                return ((size_t)(ring + 2 * NBP) * nb + (st ? stg : 0)) * sizeof(double);
-            };
-            int nb = 0;
-            bool st = false;
-            /* measured at 2 deg (ncol_own 9024, 1 GPU): NB 16 without staging keeps 3 blocks per
-             * CU resident and fills the chip in one round (60.7 ms set-up vs 75.2 for NB 32
-             * staged, whose 282 blocks of 126 KB LDS need two rounds) */
-            for (int cand : {16, 32})
-                for (bool sv : {false, true})
-                    if (!nb && pbytes(cand, sv) <= lmax && (force_nb == 0 || force_nb == cand)) {
-                        nb = cand;
-                        st = sv;
-                    }
-            if (!nb) {
-                set_error("block GS: Schur band too wide for the LDS inverse");
-                return IEMIC_EINVAL;
-            }
-            const unsigned nblk = (unsigned)((gs.ncol_own + nb - 1) / nb);
-            const size_t lb = pbytes(nb, st);
-            const void* fn = nb == 32 ? (st ? (const void*)k_band_inv_pan<32, true> : (const void*)k_band_inv_pan<32, false>)
-                                      : (st ? (const void*)k_band_inv_pan<16, true> : (const void*)k_band_inv_pan<16, false>);
-            HIP_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
-            if (nb == 32 && st)
-                hipLaunchKernelGGL((k_band_inv_pan<32, true>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
-                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-            else if (nb == 32)
-                hipLaunchKernelGGL((k_band_inv_pan<32, false>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
-                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-            else if (st)
-                hipLaunchKernelGGL((k_band_inv_pan<16, true>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
-                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-            else
-                hipLaunchKernelGGL((k_band_inv_pan<16, false>), dim3(nblk), dim3(256), lb, c->stream, gs.band.p,
-                                   gs.lpan.p, gs.piv.p, gs.ncol, gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-        } else
-        if (bytes(32) <= lmax && (force_nb == 0 || force_nb == 32)) {
-            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<32>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(32)));
-            hipLaunchKernelGGL(k_band_inv_blk<32>, dim3((unsigned)((gs.ncol_own + 31) / 32)),
-                               dim3(256), bytes(32), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
-                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-        } else if (bytes(16) <= lmax && (force_nb == 0 || force_nb == 16)) {
-            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<16>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(16)));
-            hipLaunchKernelGGL(k_band_inv_blk<16>, dim3((unsigned)((gs.ncol_own + 15) / 16)),
-                               dim3(256), bytes(16), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
-                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-        } else if (bytes(8) <= lmax) {
-            HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_blk<8>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes(8)));
-            hipLaunchKernelGGL(k_band_inv_blk<8>, dim3((unsigned)((gs.ncol_own + 7) / 8)),
-                               dim3(256), bytes(8), c->stream, gs.band.p, gs.lpan.p, gs.piv.p, gs.ncol,
-                               gs.bl, gs.bu, gs.own_cols.p, gs.ncol_own, gs.sinv.p);
-        } else {
-            set_error("block GS: Schur band too wide for the LDS inverse");
-            return IEMIC_EINVAL;
-        }
-    }
+                       gs.pinned.p, L, c->jb1, gs.S9.p);
+    /* every band built the rows of its own columns: the sum is the whole Schur matrix */
+    if ((rc = allreduce_sum(c, gs.S9.p, 9 * NC))) return rc;
+    if ((rc = cr_factor(c, gs.cr, gs.S9.p, gs.col_of_ij.p))) return rc;
+    if ((rc = cr_check(c, gs.cr))) return rc;
     {
         const char* e = getenv("IEMIC_TS_HALO");
         gs.ts_halo = e ? atoi(e) : 1;
@@ -2550,16 +2279,7 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.ts_mg = opt ? std::max(0, opt->ts_mg) : 0;
     gs.mg_sweeps = opt ? std::max(1, opt->mg_sweeps) : 1;
     if (gs.ts_mg > 0 && (rc = mg_setup(c))) return rc;
-    gs.fp32 = opt ? (opt->schur_fp32 != 0) : 1;
     gs.dyn_iters = opt ? std::max(1, opt->dyn_iters) : 1;
-    if (gs.fp32) {
-        gs.ldf = (gs.ncol_own + 3) & ~3;
-        const size_t nf = (size_t)gs.ncol * gs.ldf;
-        if (gs.sinvf.n < nf && gs.sinvf.alloc(nf)) return IEMIC_ENOMEM;
-        const int64_t tot = (int64_t)nf;
-        hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
-                           gs.sinv.p, gs.ncol, gs.ncol_own, gs.sinvf.p, gs.ldf);
-    }
     gs.dyn_mr = opt ? (opt->dyn_mr != 0) : 0;
     gs.dyn_omega = opt && opt->dyn_omega > 0.0 ? opt->dyn_omega : 1.0;
     if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
@@ -2607,9 +2327,7 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
         hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
                            rr, z, gs.tcell.p, L, 0);
         hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                           gs.pinned.p, gs.colv.p, L);
-        hipLaunchKernelGGL(k_gather, dim3((unsigned)((gs.ncol_own + 255) / 256)), dim3(256), 0, s,
-                           gs.colv.p, gs.own_cols.p, gs.ncol_own, gs.colv_own.p);
+                           gs.pinned.p, gs.colv_own.p, L);
     } else if (Pl == 16) {
         hipLaunchKernelGGL(k_gs_pcol_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
                            gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
@@ -2620,13 +2338,17 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
         hipLaunchKernelGGL(k_gs_pcol_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
                            gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
     }
-    /* pbar = S^-1 b: this band's columns of the inverse times its entries of b, summed */
-    if (gs.fp32)
-        gemv_f(gs, s);
-    else
-        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.ncol + 3) / 4)), dim3(256), 0, s, gs.sinv.p,
-                           gs.ncol, gs.ncol_own, gs.colv_own.p, gs.colv2.p);
-    if ((rc = allreduce_sum(c, gs.colv2.p, gs.ncol))) return rc;
+    /* pbar = S^-1 b: the bands' entries of b summed, then the cyclic-reduction solve
+     * (redundant on every rank: O(n m^2) bytes) */
+    const double* sb = gs.colv_own.p;
+    if (band) {
+        /* colv_own keeps 0 outside this band's columns; the sum goes to colv */
+        HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
+                              hipMemcpyDeviceToDevice, s));
+        if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
+        sb = gs.colv.p;
+    }
+    if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        gs.col_of_ij.p, gs.colv2.p, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */

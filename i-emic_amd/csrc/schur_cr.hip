@@ -1,0 +1,566 @@
+/*
+ * schur_cr.hip -- exact solve of the 2-D (barotropic) Schur complement of the block
+ * Gauss-Seidel preconditioner by block cyclic reduction over longitudes.
+ *
+ * The pinned Schur matrix S (prec_gs.hip, step 3; the depth-averaged pressure problem that
+ * TRIOS::BlockPreconditioner solves iteratively with AztecOO/ML, TRIOS_BlockPreconditioner.C:
+ * 1479-1611 SolveLower1 and 2113-2173 Compute) couples water column (i, j) only to
+ * (i+di, j+dj), |di|, |dj| <= 1.  Numbered c = i*m + j it is block tridiagonal in i with
+ * m x m blocks (periodic in i for a periodic grid):
+ *     L_i x_{i-1} + D_i x_i + R_i x_{i+1} = b_i .
+ * Cyclic reduction eliminates the odd blocks of every level,
+ *     D'_e = D_e - L_e D_{e-1}^-1 R_{e-1} - R_e D_{e+1}^-1 L_{e+1},
+ *     L'_e = -L_e D_{e-1}^-1 L_{e-1},  R'_e = -R_e D_{e+1}^-1 R_{e+1},
+ * halving the block count per level (ceil(log2 n) levels, a direct coupling kept where an
+ * odd count leaves two even blocks adjacent across the periodic wrap, the two couplings of
+ * a periodic pair merged), down to one m x m block.  Set-up per level: one Gauss-Jordan
+ * inverse per odd block (one workgroup each) and two batched GEMM launches; the apply is one
+ * GEMV launch per level down and one per level up.  Cost: O(n m^3) set-up flops spread over
+ * n/2 workgroups per level and O(n m^2) apply bytes -- against the O(ncol^2) dense inverse
+ * and the single-workgroup band LU it replaces.  Land columns are identity rows; pivoting
+ * happens inside the diagonal blocks only (tested against the band LU with partial
+ * pivoting of the CPU twin, oracle/prec_oracle.c).
+ *
+ * Every m x m block is stored column-major: a(r, c) at [r + c*m].
+ */
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+
+namespace iemic {
+
+namespace {
+
+constexpr int CR_MAXM = 512;
+
+/* level-0 blocks from the 9-point rows S9[c*9 + (dj+1)*3 + (di+1)], c = i*m + j; inactive
+ * columns (no water) become identity rows.  One thread per row (i, j): no write races. */
+__global__ void k_cr_expand(const double* __restrict__ S9, const int* __restrict__ col_of_ij, int n,
+                            int m, int periodic, double* __restrict__ D, double* __restrict__ Lb,
+                            double* __restrict__ Rb)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n * m) return;
+    const int i = c / m, j = c % m;
+    const size_t mm = (size_t)m * m;
+    double* Di = D + (size_t)i * mm;
+    if (col_of_ij[j * n + i] < 0) {
+        Di[j + (size_t)j * m] = 1.0;
+        return;
+    }
+    for (int o = 0; o < 9; o++) {
+        const double v = S9[(size_t)c * 9 + o];
+        if (v == 0.0) continue;
+        const int di = o % 3 - 1, dj = o / 3 - 1;
+        int ti = i + di;
+        const int tj = j + dj;
+        if (tj < 0 || tj >= m) continue;
+        if (ti < 0 || ti >= n) {
+            if (!periodic) continue;
+            ti = (ti + n) % n;
+        }
+        double* B = ti == i ? Di : (di < 0 ? Lb + (size_t)i * mm : Rb + (size_t)i * mm);
+        B[j + (size_t)tj * m] += v;
+    }
+}
+
+/* Gauss-Jordan inverse with row pivoting of src block (s0 + blockIdx.x * sstep) into dst
+ * block blockIdx.x, the matrix held in registers: 1024 threads as a 32 x 32 grid, thread
+ * (tr, tc) owns rows tr + 32 a and columns tc + 32 b (a, b < RPT; m <= 32 RPT); per
+ * elimination step the pivot column and row go through LDS.  A zero pivot sets *info. */
+template <int RPT>
+__global__ void __launch_bounds__(1024) k_cr_inv(const double* __restrict__ src, int s0, int sstep,
+                                                 double* __restrict__ dst, int m, int* __restrict__ info)
+{
+    const size_t mm = (size_t)m * m;
+    const double* A = src + (size_t)(s0 + blockIdx.x * sstep) * mm;
+    double* X = dst + (size_t)blockIdx.x * mm;
+    const int t = threadIdx.x, tr = t & 31, tc = t >> 5;
+    __shared__ double pcol[32 * RPT], prow[32 * RPT], rk[32 * RPT], rp[32 * RPT];
+    __shared__ int perm[32 * RPT];
+    __shared__ int s_p;
+    double a[RPT][RPT];
+#pragma unroll
+    for (int x = 0; x < RPT; x++)
+#pragma unroll
+        for (int y = 0; y < RPT; y++) {
+            const int i = tr + 32 * x, j = tc + 32 * y;
+            a[x][y] = (i < m && j < m) ? A[i + (size_t)j * m] : 0.0;
+        }
+    for (int k = 0; k < m; k++) {
+        const int kc = k & 31, kb = k >> 5;
+        /* pivot column k -> LDS */
+        if (tc == kc) {
+#pragma unroll
+            for (int x = 0; x < RPT; x++) {
+                double v = 0.0;
+#pragma unroll
+                for (int y = 0; y < RPT; y++) v = y == kb ? a[x][y] : v;
+                pcol[tr + 32 * x] = v;
+            }
+        }
+        __syncthreads();
+        if (t < 64) {
+            double best = -1.0;
+            int bi = k;
+            for (int i = k + t; i < m; i += 64) {
+                const double v = fabs(pcol[i]);
+                if (v > best) { best = v; bi = i; }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ob = __shfl_xor(best, off, 64);
+                const int oi = __shfl_xor(bi, off, 64);
+                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+            }
+            if (t == 0) {
+                if (!(best > 0.0)) *info = 1;
+                s_p = bi;
+                perm[k] = bi;
+            }
+        }
+        __syncthreads();
+        const int p = s_p;
+        const int pr = p & 31, pa = p >> 5, kr = k & 31, ka = k >> 5;
+        /* rows k and p -> LDS */
+        if (tr == kr || tr == pr) {
+#pragma unroll
+            for (int y = 0; y < RPT; y++) {
+                double vk = 0.0, vp = 0.0;
+#pragma unroll
+                for (int x = 0; x < RPT; x++) {
+                    vk = x == ka ? a[x][y] : vk;
+                    vp = x == pa ? a[x][y] : vp;
+                }
+                if (tr == kr) rk[tc + 32 * y] = vk;
+                if (tr == pr) rp[tc + 32 * y] = vp;
+            }
+        }
+        __syncthreads();
+        /* swap, scale the pivot row: row k = row p / a(p,k), entry (k,k) = 1 / a(p,k) */
+        const double piv = rp[k];
+        const double inv = piv != 0.0 ? 1.0 / piv : 0.0;
+        if (tr == pr && p != k) {
+#pragma unroll
+            for (int y = 0; y < RPT; y++)
+#pragma unroll
+                for (int x = 0; x < RPT; x++)
+                    if (x == pa) a[x][y] = rk[tc + 32 * y];
+        }
+        if (tr == kr) {
+#pragma unroll
+            for (int y = 0; y < RPT; y++) {
+                const int j = tc + 32 * y;
+                const double v = j == k ? inv : rp[j] * inv;
+#pragma unroll
+                for (int x = 0; x < RPT; x++)
+                    if (x == ka) a[x][y] = v;
+                prow[j] = v;
+            }
+        }
+        /* the pivot column after the swap (row p now holds the old row k) */
+        if (tc == kc) {
+#pragma unroll
+            for (int x = 0; x < RPT; x++) {
+                const int i = tr + 32 * x;
+                if (i == p && p != k) pcol[i] = rk[k];
+            }
+        }
+        __syncthreads();
+        /* eliminate column k from every other row */
+#pragma unroll
+        for (int x = 0; x < RPT; x++) {
+            const int i = tr + 32 * x;
+            if (i == k) continue;
+            const double f = pcol[i];
+#pragma unroll
+            for (int y = 0; y < RPT; y++) {
+                const int j = tc + 32 * y;
+                const double old = j == k ? 0.0 : a[x][y];
+                a[x][y] = old - f * prow[j];
+            }
+        }
+        __syncthreads();
+    }
+    /* undo the row interchanges as column interchanges, in reverse order: column j of the
+     * result is column q(j) of the eliminated matrix, q = the composed permutation */
+    __shared__ int colmap[32 * RPT];
+    if (t == 0) {
+        for (int j = 0; j < m; j++) colmap[j] = j;
+        for (int k = m - 1; k >= 0; k--) {
+            const int p = perm[k];
+            if (p != k) { const int x = colmap[k]; colmap[k] = colmap[p]; colmap[p] = x; }
+        }
+    }
+    __syncthreads();
+    /* column j of the eliminated matrix is column dest[j] of the inverse */
+    double* T = X;
+    __shared__ int dest[32 * RPT];
+    if (t < m) dest[colmap[t]] = t;
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < RPT; x++)
+#pragma unroll
+        for (int y = 0; y < RPT; y++) {
+            const int i = tr + 32 * x, j = tc + 32 * y;
+            if (i < m && j < m) T[i + (size_t)dest[j] * m] = a[x][y];
+        }
+}
+
+/* C = C0 + C0b + s1 A1 B1 + s2 A2 B2 for a batch of m x m column-major blocks: one 32x32
+ * tile of one descriptor per workgroup (blockIdx.y = descriptor) */
+__global__ void __launch_bounds__(256) k_cr_gemm(const CrGemm* __restrict__ dd, int m)
+{
+    const CrGemm d = dd[blockIdx.y];
+    const int T = (m + 31) / 32;
+    const int r0 = (blockIdx.x % T) * 32, c0 = (blockIdx.x / T) * 32;
+    const int t = threadIdx.x, tr = t & 31, tc = t >> 5;
+    __shared__ double As[32][33], Bs[32][33];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int prod = 0; prod < 2; prod++) {
+        const double* A = prod ? d.A2 : d.A1;
+        const double* B = prod ? d.B2 : d.B1;
+        if (!A) continue;
+        const double s = prod ? d.s2 : d.s1;
+        double pa[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < m; k0 += 32) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int e = t + 256 * q;
+                const int rr = e & 31, kk = e >> 5;
+                As[kk][rr] = (r0 + rr < m && k0 + kk < m) ? A[(r0 + rr) + (size_t)(k0 + kk) * m] : 0.0;
+                const int kb = e & 31, cc = e >> 5;
+                Bs[cc][kb] = (k0 + kb < m && c0 + cc < m) ? B[(k0 + kb) + (size_t)(c0 + cc) * m] : 0.0;
+            }
+            __syncthreads();
+#pragma unroll 8
+            for (int kk = 0; kk < 32; kk++) {
+                const double a = As[kk][tr];
+#pragma unroll
+                for (int q = 0; q < 4; q++) pa[q] += a * Bs[tc + 8 * q][kk];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[q] += s * pa[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int r = r0 + tr, c = c0 + tc + 8 * q;
+        if (r >= m || c >= m) continue;
+        const size_t idx = r + (size_t)c * m;
+        double v = acc[q];
+        if (d.C0) v += d.C0[idx];
+        if (d.C0b) v += d.C0b[idx];
+        d.C[idx] = v;
+    }
+}
+
+/* Rows [r0, r0 + CR_RC) of y = y0 + s0 (A0 v0 + A1 v1 + A2 v2) for m x m column-major
+ * blocks (m <= CR_RC * CR_CPT): thread = (row, column group), CR_RC rows x CR_G groups,
+ * each thread CR_CPT columns per block.  The block entries are loaded into registers BEFORE
+ * the vectors arrive in LDS (crf_load, then the caller's vector loads and barrier, then
+ * crf_finish), so both memory latencies overlap; the groups' partial sums are added in LDS
+ * in a fixed order (deterministic). */
+constexpr int CR_RC = 16, CR_G = 256 / CR_RC, CR_CPT = 12;
+struct CrFrag {
+    double a[3][CR_CPT];
+};
+__device__ __forceinline__ void crf_load(CrFrag& f, const double* __restrict__ A0, const double* __restrict__ A1,
+                                         const double* __restrict__ A2, int m, int r0)
+{
+    const int t = threadIdx.x, g = t / CR_RC, r = r0 + t % CR_RC;
+    const double* A[3] = {A0, A1, A2};
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+#pragma unroll
+        for (int u = 0; u < CR_CPT; u++) {
+            const int c = g + CR_G * u;
+            f.a[q][u] = (A[q] && r < m && c < m) ? A[q][r + (size_t)c * m] : 0.0;
+        }
+}
+__device__ __forceinline__ void crf_finish(const CrFrag& f, const double* v0, const double* v1, const double* v2,
+                                           double s0, const double* __restrict__ y0, double* __restrict__ y,
+                                           int m, int r0, double* red)
+{
+    const int t = threadIdx.x, g = t / CR_RC, r = r0 + t % CR_RC;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < CR_CPT; u++) {
+        const int c = g + CR_G * u;
+        if (c < m) {
+            a0 += f.a[0][u] * v0[c];
+            a1 += f.a[1][u] * v1[c];
+            a2 += f.a[2][u] * v2[c];
+        }
+    }
+    red[t] = (a0 + a1) + a2;
+    __syncthreads();
+    if (t < CR_RC && r < m) {
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < CR_G; q++) sum += red[q * CR_RC + t];
+        y[r] = (y0 ? y0[r] : 0.0) + s0 * sum;
+    }
+}
+
+/* level down, one row chunk of one even block per workgroup (blockIdx.x = q * nch + chunk):
+ * b'_q = b_e - XL_q b_{e-1} - XR_q b_{e+1} (odd neighbours only), e = 2q */
+__global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, double* __restrict__ bn,
+                                                const double* __restrict__ XL, const double* __restrict__ XR,
+                                                int N, int per, int m, int nch)
+{
+    __shared__ double vl[CR_MAXM], vr[CR_MAXM], red[256];
+    const int q = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, e = 2 * q;
+    const bool lex = e > 0 || per, rex = e + 1 < N || per;
+    const int lnb = e > 0 ? e - 1 : N - 1, rnb = (e + 1) % N;
+    const bool lo = lex && (lnb & 1), ro = rex && (rnb & 1);
+    const size_t mm = (size_t)m * m;
+    CrFrag f;
+    crf_load(f, lo ? XL + q * mm : nullptr, ro ? XR + q * mm : nullptr, nullptr, m, r0);
+    for (int c = threadIdx.x; c < m; c += 256) {
+        vl[c] = lo ? bl[(size_t)lnb * m + c] : 0.0;
+        vr[c] = ro ? bl[(size_t)rnb * m + c] : 0.0;
+    }
+    __syncthreads();
+    crf_finish(f, vl, vr, vl, -1.0, bl + (size_t)e * m, bn + (size_t)q * m, m, r0, red);
+}
+
+/* level up, one row chunk of one odd block per workgroup (blockIdx.x = p * nch + chunk):
+ * x_o = Dinv b_o - YL x_{o-1} - YR x_{o+1}, o = 2p + 1; the even blocks are copied from
+ * the level below (x_{o-1} by block o, the last even block of an odd count by block N-2) */
+__global__ void __launch_bounds__(256) k_cr_bwd(const double* __restrict__ bl, const double* __restrict__ xn,
+                                                double* __restrict__ xl, const double* __restrict__ Dinv,
+                                                const double* __restrict__ YL, const double* __restrict__ YR,
+                                                int N, int per, int m, int nch)
+{
+    __shared__ double vb[CR_MAXM], vl[CR_MAXM], vr[CR_MAXM], red[256];
+    const int p = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, b = 2 * p + 1;
+    const bool rex = b + 1 < N || per;
+    const int rn = (b + 1) % N;
+    const size_t mm = (size_t)m * m;
+    CrFrag f;
+    crf_load(f, Dinv + p * mm, YL + p * mm, rex ? YR + p * mm : nullptr, m, r0);
+    for (int c = threadIdx.x; c < m; c += 256) {
+        vb[c] = bl[(size_t)b * m + c];
+        vl[c] = -xn[(size_t)p * m + c];
+        vr[c] = rex ? -xn[(size_t)(rn / 2) * m + c] : 0.0;
+    }
+    if (threadIdx.x < CR_RC && r0 + threadIdx.x < m) {
+        const int r = r0 + threadIdx.x;
+        xl[(size_t)(b - 1) * m + r] = xn[(size_t)p * m + r];
+        if (b == N - 2) xl[(size_t)(N - 1) * m + r] = xn[(size_t)((N - 1) / 2) * m + r];
+    }
+    __syncthreads();
+    crf_finish(f, vb, vl, vr, 1.0, nullptr, xl + (size_t)b * m, m, r0, red);
+}
+
+/* the last level: x = Dfin b, one row chunk per workgroup */
+__global__ void __launch_bounds__(256) k_cr_final(const double* __restrict__ Dfin, const double* __restrict__ b,
+                                                  double* __restrict__ x, int m)
+{
+    __shared__ double vb[CR_MAXM], red[256];
+    CrFrag f;
+    crf_load(f, Dfin, nullptr, nullptr, m, blockIdx.x * CR_RC);
+    for (int c = threadIdx.x; c < m; c += 256) vb[c] = b[c];
+    __syncthreads();
+    crf_finish(f, vb, vb, vb, 1.0, nullptr, x, m, blockIdx.x * CR_RC, red);
+}
+
+}  // namespace
+
+/* level sizes, storage offsets and the GEMM descriptors (host, once per grid) */
+int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
+{
+    if (m > 192) {
+        set_error("Schur cyclic reduction: more than 192 latitudes");
+        return IEMIC_EINVAL;
+    }
+    cr.n = n; cr.m = m; cr.periodic = periodic;
+    cr.N.clear(); cr.per.clear(); cr.merge.clear();
+    int N = n, P = periodic;
+    while (N > 1) {
+        const int mg = (N == 2 && P) ? 1 : 0;
+        if (mg) P = 0;
+        cr.N.push_back(N); cr.per.push_back(P); cr.merge.push_back(mg);
+        N = (N + 1) / 2;
+    }
+    cr.N.push_back(1); cr.per.push_back(0); cr.merge.push_back(0);
+    cr.nlev = (int)cr.N.size() - 1;
+    const size_t mm = (size_t)m * m;
+    cr.dlr_off.assign(cr.nlev + 1, 0);
+    cr.ap_off.assign(cr.nlev + 1, 0);
+    cr.v_off.assign(cr.nlev + 1, 0);
+    size_t nd = 0, na = 0, nv = 0;
+    for (int l = 0; l <= cr.nlev; l++) {
+        cr.dlr_off[l] = nd;
+        nd += 3 * (size_t)cr.N[l] * mm;
+        cr.ap_off[l] = na;
+        na += l < cr.nlev ? (size_t)(2 * ((cr.N[l] + 1) / 2) + 3 * (cr.N[l] / 2)) * mm : mm;
+        cr.v_off[l] = nv;
+        if (l > 0) nv += (size_t)cr.N[l] * m;
+    }
+    int rc = 0;
+    rc |= cr.dlr.alloc(nd);
+    rc |= cr.ap.alloc(na);
+    rc |= cr.bv.alloc(std::max<size_t>(nv, 1));
+    rc |= cr.xv.alloc(std::max<size_t>(nv, 1));
+    rc |= cr.info.alloc(1);
+    if (rc) {
+        set_error("Schur cyclic reduction: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    /* descriptors: per level the periodic-pair merge (g0), X/Y products (g1), next level (g2) */
+    std::vector<CrGemm> g;
+    cr.g_off.assign(3 * cr.nlev, 0);
+    cr.g_cnt.assign(3 * cr.nlev, 0);
+    auto blk = [&](int l, int which, int b) { return cr.dlr.p + cr.dlr_off[l] + ((size_t)which * cr.N[l] + b) * mm; };
+    for (int l = 0; l < cr.nlev; l++) {
+        const int Nl = cr.N[l], per = cr.per[l], ne = (Nl + 1) / 2, no = Nl / 2;
+        double* ap = cr.ap.p + cr.ap_off[l];
+        auto XL = [&](int q) { return ap + (size_t)q * mm; };
+        auto XR = [&](int q) { return ap + (size_t)(ne + q) * mm; };
+        auto DI = [&](int p) { return ap + (size_t)(2 * ne + p) * mm; };
+        auto YL = [&](int p) { return ap + (size_t)(2 * ne + no + p) * mm; };
+        auto YR = [&](int p) { return ap + (size_t)(2 * ne + 2 * no + p) * mm; };
+        const auto D = [&](int b) { return blk(l, 0, b); };
+        const auto Lb = [&](int b) { return blk(l, 1, b); };
+        const auto Rb = [&](int b) { return blk(l, 2, b); };
+        cr.g_off[3 * l] = (int)g.size();
+        if (cr.merge[l]) {
+            g.push_back({Rb(0), Lb(0), Rb(0), nullptr, nullptr, nullptr, nullptr, 0.0, 0.0});
+            g.push_back({Lb(1), Lb(1), Rb(1), nullptr, nullptr, nullptr, nullptr, 0.0, 0.0});
+        }
+        cr.g_cnt[3 * l] = (int)g.size() - cr.g_off[3 * l];
+        cr.g_off[3 * l + 1] = (int)g.size();
+        for (int q = 0; q < ne; q++) {
+            const int e = 2 * q;
+            const bool lex = e > 0 || per, rex = e + 1 < Nl || per;
+            const int lnb = e > 0 ? e - 1 : Nl - 1, rnb = (e + 1) % Nl;
+            if (lex && (lnb & 1)) g.push_back({XL(q), nullptr, nullptr, Lb(e), DI(lnb / 2), nullptr, nullptr, 1.0, 0.0});
+            if (rex && (rnb & 1)) g.push_back({XR(q), nullptr, nullptr, Rb(e), DI(rnb / 2), nullptr, nullptr, 1.0, 0.0});
+        }
+        for (int p = 0; p < no; p++) {
+            g.push_back({YL(p), nullptr, nullptr, DI(p), Lb(2 * p + 1), nullptr, nullptr, 1.0, 0.0});
+            g.push_back({YR(p), nullptr, nullptr, DI(p), Rb(2 * p + 1), nullptr, nullptr, 1.0, 0.0});
+        }
+        cr.g_cnt[3 * l + 1] = (int)g.size() - cr.g_off[3 * l + 1];
+        cr.g_off[3 * l + 2] = (int)g.size();
+        for (int q = 0; q < ne; q++) {
+            const int e = 2 * q;
+            const bool lex = e > 0 || per, rex = e + 1 < Nl || per;
+            const int lnb = e > 0 ? e - 1 : Nl - 1, rnb = (e + 1) % Nl;
+            const bool lo = lex && (lnb & 1), ro = rex && (rnb & 1);
+            CrGemm dg{blk(l + 1, 0, q), D(e), nullptr, nullptr, nullptr, nullptr, nullptr, -1.0, -1.0};
+            if (lo) { dg.A1 = XL(q); dg.B1 = Rb(lnb); }
+            if (ro) { dg.A2 = XR(q); dg.B2 = Lb(rnb); }
+            if (!dg.A1 && dg.A2) { dg.A1 = dg.A2; dg.B1 = dg.B2; dg.A2 = dg.B2 = nullptr; }
+            g.push_back(dg);
+            if (lo) g.push_back({blk(l + 1, 1, q), nullptr, nullptr, XL(q), Lb(lnb), nullptr, nullptr, -1.0, 0.0});
+            else g.push_back({blk(l + 1, 1, q), lex ? Lb(e) : nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.0, 0.0});
+            if (ro) g.push_back({blk(l + 1, 2, q), nullptr, nullptr, XR(q), Rb(rnb), nullptr, nullptr, -1.0, 0.0});
+            else g.push_back({blk(l + 1, 2, q), rex ? Rb(e) : nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.0, 0.0});
+        }
+        cr.g_cnt[3 * l + 2] = (int)g.size() - cr.g_off[3 * l + 2];
+    }
+    if (cr.gd.alloc(std::max<size_t>(g.size(), 1))) {
+        set_error("Schur cyclic reduction: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    if (!g.empty() && (rc = h2d(c, cr.gd.p, g.data(), sizeof(CrGemm) * g.size()))) return rc;
+    return 0;
+}
+
+static int cr_inverse(hipStream_t s, int m, int count, const double* src, int s0, int sstep, double* dst,
+                      int* info)
+{
+    if (count <= 0) return 0;
+    const int rpt = (m + 31) / 32;
+#define CR_INV(R) hipLaunchKernelGGL(k_cr_inv<R>, dim3(count), dim3(1024), 0, s, src, s0, sstep, dst, m, info)
+    switch (rpt) {
+    case 1: CR_INV(1); break;
+    case 2: CR_INV(2); break;
+    case 3: CR_INV(3); break;
+    case 4: CR_INV(4); break;
+    case 5: CR_INV(5); break;
+    case 6: CR_INV(6); break;
+    default:
+        set_error("Schur cyclic reduction: more than 192 latitudes");
+        return IEMIC_EINVAL;
+    }
+#undef CR_INV
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+/* set-up from the 9-point rows (stream-ordered, no host synchronisation) */
+int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
+{
+    hipStream_t s = c->stream;
+    int rc;
+    const int m = cr.m;
+    const size_t mm = (size_t)m * m;
+    const int T = (m + 31) / 32;
+    HIP_OK(hipMemsetAsync(cr.info.p, 0, sizeof(int), s));
+    HIP_OK(hipMemsetAsync(cr.dlr.p, 0, sizeof(double) * 3 * (size_t)cr.n * mm, s));
+    const int nm = cr.n * m;
+    hipLaunchKernelGGL(k_cr_expand, dim3((nm + 255) / 256), dim3(256), 0, s, S9, col_of_ij, cr.n, m,
+                       cr.periodic, cr.dlr.p, cr.dlr.p + (size_t)cr.n * mm, cr.dlr.p + 2 * (size_t)cr.n * mm);
+    for (int l = 0; l < cr.nlev; l++) {
+        const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
+        if (cr.g_cnt[3 * l])
+            hipLaunchKernelGGL(k_cr_gemm, dim3(T * T, cr.g_cnt[3 * l]), dim3(256), 0, s, cr.gd.p + cr.g_off[3 * l], m);
+        if ((rc = cr_inverse(s, m, no, cr.dlr.p + cr.dlr_off[l], 1, 2, cr.ap.p + cr.ap_off[l] + (size_t)2 * ne * mm,
+                             cr.info.p)))
+            return rc;
+        hipLaunchKernelGGL(k_cr_gemm, dim3(T * T, cr.g_cnt[3 * l + 1]), dim3(256), 0, s,
+                           cr.gd.p + cr.g_off[3 * l + 1], m);
+        hipLaunchKernelGGL(k_cr_gemm, dim3(T * T, cr.g_cnt[3 * l + 2]), dim3(256), 0, s,
+                           cr.gd.p + cr.g_off[3 * l + 2], m);
+    }
+    if ((rc = cr_inverse(s, m, 1, cr.dlr.p + cr.dlr_off[cr.nlev], 0, 1, cr.ap.p + cr.ap_off[cr.nlev], cr.info.p)))
+        return rc;
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int cr_check(iemic_ctx* c, SchurCR& cr)
+{
+    int info = 0, rc;
+    if ((rc = d2h(c, &info, cr.info.p, sizeof(int)))) return rc;
+    if (info) {
+        set_error("block GS: singular block in the Schur cyclic reduction");
+        return IEMIC_EINVAL;
+    }
+    return 0;
+}
+
+/* x = S^-1 b (b, x: n*m, c = i*m + j) */
+int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)
+{
+    (void)c;
+    const int m = cr.m;
+    const size_t mm = (size_t)m * m;
+    const int nch = (m + CR_RC - 1) / CR_RC;
+    auto bvec = [&](int l) { return l == 0 ? b : cr.bv.p + cr.v_off[l]; };
+    auto xvec = [&](int l) { return l == 0 ? x : cr.xv.p + cr.v_off[l]; };
+    for (int l = 0; l < cr.nlev; l++) {
+        const int Nl = cr.N[l], ne = (Nl + 1) / 2;
+        const double* ap = cr.ap.p + cr.ap_off[l];
+        hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch), dim3(256), 0, s, bvec(l), cr.bv.p + cr.v_off[l + 1], ap,
+                           ap + (size_t)ne * mm, Nl, cr.per[l], m, nch);
+    }
+    hipLaunchKernelGGL(k_cr_final, dim3(nch), dim3(256), 0, s, (const double*)(cr.ap.p + cr.ap_off[cr.nlev]),
+                       bvec(cr.nlev), xvec(cr.nlev), m);
+    for (int l = cr.nlev - 1; l >= 0; l--) {
+        const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
+        const double* ap = cr.ap.p + cr.ap_off[l];
+        hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch), dim3(256), 0, s, bvec(l), (const double*)xvec(l + 1), xvec(l),
+                           ap + (size_t)2 * ne * mm, ap + (size_t)(2 * ne + no) * mm,
+                           ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace iemic

@@ -55,7 +55,7 @@ class Ocean:
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
-              "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "Schur fp32": True, "TS multigrid cycles": 1,
+              "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
               "Multigrid sweeps": 1}
         if solver_params:
             sp.update(solver_params)
@@ -148,7 +148,7 @@ class Ocean:
         return _lib.Krylov(float(sp["FGMRES tolerance"]), int(sp["FGMRES iterations"]),
                            int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
                            int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0,
-                           int(sp["Dyn iterations"]), int(bool(sp["Schur fp32"])),
+                           int(sp["Dyn iterations"]), 0,
                            int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]),
                            float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])))
 

@@ -73,8 +73,8 @@ typedef struct {
     int orth;                    /* 0: DCGS2 (default), 1: DGKS (Belos' default)     */
     int dyn_iters;               /* block GS: defect-correction passes on the U/V/W/P */
                                  /* block (<= 1: one pass, the plain block GS)        */
-    int schur_fp32;              /* block GS: Schur inverse stored in fp32 (GEMV bytes */
-                                 /* halved; accumulation in fp64)                     */
+    int reserved0;               /* unused (was the fp32 Schur inverse; the Schur     */
+                                 /* solve is now an exact fp64 cyclic reduction)      */
     int ts_mg;                   /* block GS: T/S solve by this many aggregation-      */
                                  /* multigrid V-cycles (0: ts_sweeps plain sweeps)    */
     int mg_sweeps;               /* symmetric red-black sweeps before/after the coarse */

@@ -393,6 +393,7 @@ def _load_gs():
         lib.orc_gs_apply.argtypes = [C.c_void_p, PD, PD]
         lib.orc_gs_ncol.argtypes = [C.c_void_p]
         lib.orc_gs_band.argtypes = [C.c_void_p]
+        lib.orc_gs_schur.argtypes = [C.c_void_p, PD, PI, C.POINTER(C.c_uint8)]
         lib.orc_fgmres_gs.argtypes = [C.c_int, P64, PI, PD, C.c_void_p, PD, PD, C.c_double,
                                       C.c_int, C.c_int, PD, PD]
         lib._gs_ready = True
@@ -417,6 +418,22 @@ class BlockGS:
             raise RuntimeError("BlockGS: singular Schur complement")
         self.ncol = lib.orc_gs_ncol(self.h)
         self.band = lib.orc_gs_band(self.h)
+
+    def schur(self):
+        """the pinned 2-D Schur matrix (scipy CSR over the water columns in band order),
+        the (j*n+i) position and the pin flag of every column"""
+        import scipy.sparse as sp
+        ncol, bl = self.ncol, self.band
+        W = 3 * bl + 1
+        band = np.zeros(ncol * W)
+        ij = np.zeros(ncol, dtype=np.int32)
+        pin = np.zeros(ncol, dtype=np.uint8)
+        self.lib.orc_gs_schur(self.h, _p(band, C.c_double), _p(ij, C.c_int),
+                              _p(pin, C.c_uint8))
+        band = band.reshape(ncol, W)
+        r, d = np.nonzero(band)
+        S = sp.csr_matrix((band[r, d], (r, r + d - bl)), shape=(ncol, ncol))
+        return S, ij, pin.astype(bool)
 
     def __del__(self):
         try:

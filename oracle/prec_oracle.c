@@ -31,6 +31,7 @@ typedef struct {
     int* ij_of_col;
     uint8_t* pinned;
     double* band;    /* row-wise LU factors, width 2bl+bu+1 */
+    double* band0;   /* the Schur band before the LU (exported for studies/tests) */
     int* piv;
     double *uvinv, *tsinv, *pw, *rr, *bts, *colv;
 } gs_t;
@@ -82,7 +83,7 @@ void orc_gs_destroy(void* h)
     if (!g) return;
     free(g->known); free(g->colid); free(g->ij_of_col); free(g->pinned); free(g->band);
     free(g->piv); free(g->uvinv); free(g->tsinv); free(g->pw); free(g->rr); free(g->bts);
-    free(g->colv);
+    free(g->colv); free(g->band0);
     free(g);
 }
 
@@ -255,6 +256,8 @@ void* orc_gs_create(int n, int m, int l, int periodic, const int64_t* rowptr, co
                 row[q2 - q + bl] += s;
             }
     }
+    g->band0 = (double*)malloc(sizeof(double) * (size_t)(ncol ? ncol : 1) * W);
+    memcpy(g->band0, g->band, sizeof(double) * (size_t)(ncol ? ncol : 1) * W);
     /* band LU, partial pivoting (same scheme as k_band_lu) */
     g->piv = (int*)malloc(sizeof(int) * (ncol ? ncol : 1));
     double* ab = g->band;
@@ -486,3 +489,14 @@ void orc_gs_apply(void* h, const double* r, double* z)
 
 int orc_gs_ncol(void* h) { return ((gs_t*)h)->ncol; }
 int orc_gs_band(void* h) { return ((gs_t*)h)->bl; }
+
+/* the pinned Schur matrix before factorisation: band rows (width 2bl+bu+1, offset bl),
+ * the (j*n+i) position and pin flag of every column */
+void orc_gs_schur(void* h, double* band, int* ij_of_col, uint8_t* pinned)
+{
+    gs_t* g = (gs_t*)h;
+    const size_t W = (size_t)(2 * g->bl + g->bu + 1);
+    memcpy(band, g->band0, sizeof(double) * (size_t)g->ncol * W);
+    memcpy(ij_of_col, g->ij_of_col, sizeof(int) * (size_t)g->ncol);
+    memcpy(pinned, g->pinned, (size_t)g->ncol);
+}
