@@ -52,8 +52,15 @@ def parse():
     p.add_argument("--mixing", type=int, default=1,
                    help="THCM 'Mixing' (vmix): 1 as in run/ocean/global/ocean_params.xml")
     p.add_argument("--prec", type=int, default=2, help="0 none, 1 block Jacobi, 2 block GS")
+    p.add_argument("--state", default="branch", choices=["branch", "synthetic"],
+                   help="branch: the near-solution state bench_data/<config>_cf05.npz (the config "
+                        "continued from rest to Combined Forcing 0.5, scripts/branch_state.py); "
+                        "synthetic: the splitmix64 state of SURVEY.md §8d")
     p.add_argument("--amp-ts", type=float, default=1e-3,
                    help="T/S amplitude of the synthetic state (DESIGN.md: benchmark state)")
+    p.add_argument("--newton-seq", type=int, default=3,
+                   help="untimed Newton iterations from the benchmark state, reported as the "
+                        "residual sequence")
     p.add_argument("--tol", type=float, default=1e-8)
     p.add_argument("--krylov", type=int, default=100)
     p.add_argument("--restarts", type=int, default=20)
@@ -183,7 +190,22 @@ def main():
         comm_id = bytes(idt.cpu().numpy().tobytes())
     oc = Ocean(cfg, device=local, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
-    x0h = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
+    fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
+    state = args.state if (args.state == "synthetic" or os.path.exists(fix)) else "synthetic"
+    if state == "branch":
+        with np.load(fix, allow_pickle=False) as d:
+            x0h = d["x"].astype(np.float64)
+        if args.mixing != 1:
+            raise SystemExit("the branch state was continued with Mixing = 1")
+        data = ("near-solution state: global2 continued on the GPU from rest to Combined Forcing "
+                "0.5 with the reference's run/ocean continuation settings (scripts/branch_state.py; "
+                "bench_data/global2_cf05.npz, fp32-rounded); one Newton step at Combined Forcing 0.5 "
+                "from it. SURVEY §8d's synthetic U(+-0.1) T/S state is not a Newton iterate "
+                "(the step from it diverges; --state synthetic)")
+    else:
+        x0h = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
+        data = (f"synthetic (splitmix64 seed 20261015 state, u,v,w,p ~ U(+-1e-3), T,S ~ "
+                f"U(+-{args.amp_ts:g}); Combined Forcing 0.5)")
     x0 = torch.from_numpy(x0h).to(dev)
     L_ = _lib.lib()
     torch.cuda.synchronize()
@@ -242,6 +264,15 @@ def main():
         if pm.get("config") == args.config:
             traffic = pm.get("hbm_bytes_per_launch")
 
+    # the Newton residual sequence from the benchmark state (untimed)
+    seq = []
+    if args.newton_seq > 0:
+        _lib.check(L_.iemic_set_state_dev(oc._h, x0.data_ptr()), "set_state_dev")
+        for _ in range(args.newton_seq):
+            inf = oc.newtonStep(allow_unconverged=True)
+            seq.append({"norm_f0": inf.norm_f0, "norm_f1": inf.norm_f1, "fgmres_iters": inf.solve.iters,
+                        "converged": inf.solve.converged})
+
     last = infos[-1]
     s = last.solve
     out = {
@@ -249,8 +280,7 @@ def main():
         "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": False, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-        "data": (f"synthetic (splitmix64 seed 20261015 state, u,v,w,p ~ U(+-1e-3), T,S ~ "
-                 f"U(+-{args.amp_ts:g}); Combined Forcing 0.5)"),
+        "data": data,
         "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing={args.mixing}, one Newton "
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
@@ -266,7 +296,7 @@ def main():
                    "t_jac_ms": last.t_jac_ms, "t_prec_ms": last.t_prec_ms,
                    "t_solve_ms": last.t_solve_ms, "t_solve_prec_ms": s.t_prec_ms,
                    "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms,
-                   "dgks_reorth": s.reorth},
+                   "dgks_reorth": s.reorth, "sequence": seq},
         "spmv_gbps": round(achieved, 1),
         "roofline": {"kernel": "k_spmv (per GPU, rank 0; in-solve launches)", "bound": "hbm",
                      "achieved": round(achieved, 1),

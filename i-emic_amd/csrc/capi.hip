@@ -541,7 +541,9 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     c->jac_valid = 1;
     inf.t_total_ms = ms(T0);
     if (info) *info = inf;
-    return 0;
+    /* Newton.H applies the update whatever the solver reported; the caller learns that the
+     * solve missed its tolerance from a distinct status */
+    return inf.solve.converged ? 0 : IEMIC_ENOCONV;
 }
 
 /* mean duration of the SpMV kernel alone (no halo exchange), HIP events on its stream */

@@ -418,8 +418,11 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
     }
 }
 
-/* DCGS2 update pass, one read of Q:  q_j = (u - Q a) * inv_beta,  w -= Q c + gamma * u
- * (coef = [a (nvec) | c (nvec)]); u is overwritten by q_j. */
+/* DCGS2 update pass, one read of Q:  q_j = (u - Q a) * inv_beta,
+ * w = (w - Q c - gamma * u) * inv_beta  (coef = [a (nvec) | c (nvec)]); u is overwritten by
+ * q_j.  Scaling the next candidate w by the same 1/beta (lagged normalisation) keeps every
+ * candidate at the scale of a normalised Arnoldi vector, so its norm never compounds the
+ * earlier subdiagonals (no overflow / false breakdown over long cycles). */
 __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ V, int64_t ldv,
                                                      int nvec, const double* __restrict__ coef,
                                                      double inv_beta, double gamma,
@@ -447,7 +450,7 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
         }
         const double ue = u[e];
         u[e] = (ue - su) * inv_beta;
-        w[e] = w[e] - sw - gamma * ue;
+        w[e] = (w[e] - sw - gamma * ue) * inv_beta;
     }
 }
 
@@ -653,6 +656,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     double* r = c->kr.r.p;
     const unsigned G = grid_for(NL);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
+    std::vector<double> zs(m + 1, 1.0);   /* DCGS2: scale of the stored z_j (1 for DGKS) */
     if (2 * m + 3 > RED_ROWS) {
         set_error("fgmres: Krylov dimension too large");
         return IEMIC_EINVAL;
@@ -761,6 +765,9 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
              * the Hessenberg column j-1 is final (and the residual known) at iteration j. */
             std::vector<double> htent(m + 1), col(m + 1), coef(2 * (size_t)m + 2);
             int ncolf = 0;                 /* finalised columns */
+            /* z_jj = M u_jj with u_jj of norm bt_jj: the Hessenberg column of z_jj / bt_jj is
+             * the one assembled below, so the solution update divides y_jj by bt_jj */
+            std::fill(zs.begin(), zs.end(), 1.0);
             for (int jj = 0; jj <= m; jj++) {
                 double* u = V + (int64_t)jj * NE;
                 double* wv = jj < m ? V + (int64_t)(jj + 1) * NE : nullptr;
@@ -843,9 +850,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 for (int i = 0; i < nv; i++) {
                     coef[i] = hr[2 * i];
                     coef[nv + i] = hr[2 * i + 1] - hr[2 * i] * gamma;
-                    htent[i] = hr[2 * i + 1];
+                    htent[i] = hr[2 * i + 1] / bt;
                 }
-                htent[nv] = hjj;
+                htent[nv] = hjj / bt;
+                zs[jj] = bt;
                 if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
                 hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V + o, NE, nv,
                                    c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u + o, wv + o, NL);
@@ -860,6 +868,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             y[i] = t / H[(size_t)i * m + i];
         }
         if (k > 0) {
+            for (int i = 0; i < k; i++) y[i] /= zs[i];
             if ((rc = upload_coeffs(c, y.data(), k))) return rc;
             hipLaunchKernelGGL(k_mupdate_add, dim3(G), dim3(256), 0, c->stream, Z + o, NE, k,
                                c->d_hbuf.p + RED_ROWS, x + o, NL);

@@ -14,6 +14,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libiemic_amd.so")
 
 IEMIC_ENODEV = -19
+IEMIC_ENOCONV = 1           # iemic_newton_step: applied, but the solve missed its tolerance
 
 
 class Grid(C.Structure):

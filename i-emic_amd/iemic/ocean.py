@@ -184,11 +184,20 @@ class Ocean:
         pass
 
     # ---- fused device-resident Newton step -------------------------------------------
-    def newtonStep(self) -> _lib.NewtonInfo:
-        """F, J, preconditioner, J dx = -F, x += dx, F (transient/Newton.H:92-99)."""
+    def newtonStep(self, allow_unconverged: bool = False) -> _lib.NewtonInfo:
+        """F, J, preconditioner, J dx = -F, x += dx, F (transient/Newton.H:92-99).  The
+        update is applied either way (as Newton.H does); a solve that missed its tolerance
+        raises IemicError unless allow_unconverged."""
         k = self._krylov()
         info = _lib.NewtonInfo()
-        check(lib().iemic_newton_step(self._h, C.byref(k), C.byref(info)), "iemic_newton_step")
+        rc = lib().iemic_newton_step(self._h, C.byref(k), C.byref(info))
+        if rc == _lib.IEMIC_ENOCONV and allow_unconverged:
+            rc = 0
+        if rc == _lib.IEMIC_ENOCONV:
+            raise _lib.IemicError(
+                f"iemic_newton_step: FGMRES did not converge ({info.solve.iters} steps, "
+                f"relative residual {info.solve.explicit_rel_res:.3e})")
+        check(rc, "iemic_newton_step")
         return info
 
     # ---- inspection -----------------------------------------------------------------

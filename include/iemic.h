@@ -40,6 +40,8 @@ extern "C" {
 #define IEMIC_EDEVICE (-5)
 #define IEMIC_ESTATE  (-71)
 #define IEMIC_ERANGE  (-34)   /* non-finite value in the operator / preconditioner output */
+#define IEMIC_ENOCONV (1)     /* warning: the step was applied but its linear solve did not
+                                 reach the tolerance (iemic_newton_step)                   */
 
 typedef struct iemic_ctx iemic_ctx;
 

@@ -1,6 +1,6 @@
 """FGMRES steps of the bench's Newton step when the grid is split into N latitude bands
 (in-process group on one GPU): the block-GS couples the bands block-Jacobi style, so the
-step count is what the multi-GPU bench pays per band.  usage: python tools/band_iters.py"""
+step count is what the multi-GPU bench pays per band.  usage: python scripts/band_iters.py"""
 import os
 import sys
 import threading

@@ -8,10 +8,10 @@ export TMPDIR=/tmp
 CFG=${CFG:-global2}
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 60 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/calib_$ctr -o run \
-      -- ./tools/_build/pmc_calib > gpurun_out/pmc/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; exit 1; }
+      -- ./scripts/_build/pmc_calib > gpurun_out/pmc/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/spmv_$ctr -o run \
-      -- python3 -u tools/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_$ctr.log 2>&1 || { echo "spmv $ctr failed"; exit 1; }
+      -- python3 -u scripts/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_$ctr.log 2>&1 || { echo "spmv $ctr failed"; exit 1; }
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/spmv_trace -o run \
-    -- python3 -u tools/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_trace.log 2>&1 || { echo "trace failed"; exit 1; }
+    -- python3 -u scripts/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "pmc ok"

@@ -4,6 +4,6 @@ set -o pipefail
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
 for v in 1 2 6; do
-  IEMIC_SPMV=$v timeout -k 10 120 python3 -u tools/spmv_probe.py global2 20 > gpurun_out/ab/spmv_$v.log 2>&1 || { echo "variant $v failed"; exit 1; }
+  IEMIC_SPMV=$v timeout -k 10 120 python3 -u scripts/spmv_probe.py global2 20 > gpurun_out/ab/spmv_$v.log 2>&1 || { echo "variant $v failed"; exit 1; }
   echo "variant $v: $(tail -1 gpurun_out/ab/spmv_$v.log)"
 done

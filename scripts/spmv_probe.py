@@ -1,9 +1,9 @@
 """SpMV probe for the PMC passes: builds the 2-degree Jacobian on the GPU and launches
 k_spmv `reps` times, each after an Infinity Cache flush (the in-solve, cold-cache
 condition), timed with HIP events on the library stream.  Run under rocprofv3 --pmc
-(tools/gpu_pmc.sh); tools/pmc_report.py turns the counters into bytes per launch.
+(scripts/gpu_pmc.sh); tools/pmc_report.py turns the counters into bytes per launch.
 
-usage: python tools/spmv_probe.py [config] [reps]
+usage: python scripts/spmv_probe.py [config] [reps]
 """
 import json
 import os

@@ -210,6 +210,31 @@ def test_fgmres_solve(oracle_lib, Ocean, name, prec):
     assert abs(oc.last_solve.explicit_rel_res - res) <= 1e-9
 
 
+@pytest.mark.parametrize("orth", ["DCGS2", "DGKS"])
+@pytest.mark.parametrize("name,prec", [("natl8", 0), ("natl8", 1), ("global4", 0), ("global4", 1)])
+def test_fgmres_long_cycle(oracle_lib, Ocean, name, prec, orth):
+    """One 500-step cycle with a weak (prec 1, block Jacobi) or no preconditioner: the
+    Krylov candidates stay normalised (DCGS2's lagged normalisation), so a long cycle ends
+    without a spurious non-finite error or false breakdown, the residual decreases and the
+    reported explicit residual is the true one of the oracle's J."""
+    c, oc, o, L = make(Ocean, oracle_lib, name,
+                       solver_params={"Preconditioner": prec, "FGMRES iterations": 500,
+                                      "FGMRES restarts": 0, "FGMRES tolerance": 1e-8,
+                                      "Orthogonalization": orth})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    ov, _ = o.jacobian(x)
+    b = o.spmv(ov, cf.synthetic_vector(c, seed=5))
+    sol = oc.solve(b)
+    res = np.linalg.norm(b - o.spmv(ov, sol)) / np.linalg.norm(b)
+    s_ = oc.last_solve
+    assert np.all(np.isfinite(sol))
+    assert res <= 1.0 + 1e-12          # minimal residual over the cycle: never above ||b||
+    assert s_.converged == 1 or s_.iters == 500
+    assert abs(s_.explicit_rel_res - res) <= 1e-8 + 1e-6 * res
+
+
 def test_fgmres_nonfinite_is_an_error(oracle_lib, Ocean):
     """A NaN reaching the Krylov basis raises instead of passing for a breakdown (res = 0)."""
     from iemic._lib import IemicError

@@ -2,7 +2,7 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE under-counts wide streaming
 reads (MI355X_MICROARCH.md, HBM section), so the counts are converted with factors
-measured in the same call on streams of a known byte count (tools/pmc_calib.hip: 8-B and
+measured in the same call on streams of a known byte count (scripts/pmc_calib.hip: 8-B and
 16-B lanes, 1 GiB, beyond the Infinity Cache).  The SpMV reads its values with 8-B lanes,
 so the 8-B read factor applies to its FETCH_SIZE.
 
