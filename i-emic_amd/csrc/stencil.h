@@ -19,6 +19,7 @@
 #define IEMIC_STENCIL_H
 
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #define HD __host__ __device__ __forceinline__
@@ -857,6 +858,120 @@ HD void boundaries_row(const Geo& g, const CellCtx& c, double* A, bool& frc_zero
  *   mix(T)   = (Ftimp(k) - Ftimp(k-1)) / (dz dfzT(k))
  * and its Jacobian by forward differences (eps 1e-8) w.r.t. the T/S unknowns of the
  * column neighbours k-1, k, k+1 (the only nonzero entries of the 27-point FD pattern). */
+/* tanh exactly as the host C library computes it (glibc 2.35, sysdeps/ieee754/dbl-64
+ * s_tanh.c / s_expm1.c, the fdlibm algorithms with glibc's split polynomial in expm1), so
+ * the device mixing matches the reference's Fortran bit for bit: its forward-difference
+ * Jacobian (mix_imp.f:729-815, eps = 1e-8) would amplify a last-bit difference of tanh by
+ * 1/eps.  Checked bitwise against the host libm over 1.3e7 arguments in [2^-60, 2^7]
+ * (tests/test_mixing.py).  Needs -ffp-contract=off like the rest of this header. */
+HD int64_t f64_bits(double x)
+{
+    int64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+HD double f64_from(int64_t u)
+{
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
+}
+HD int32_t f64_hi(double x) { return (int32_t)(f64_bits(x) >> 32); }
+HD double f64_sethi(double x, int32_t h)
+{
+    return f64_from((int64_t)(((uint64_t)(uint32_t)h << 32) | ((uint64_t)f64_bits(x) & 0xffffffffull)));
+}
+HD double libm_expm1(double x)
+{
+    const double one = 1.0, huge = 1.0e+300, tiny = 1.0e-300, o_threshold = 7.09782712893383973096e+02,
+                 ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00, Q1 = -3.33333333333331316428e-02,
+                 Q2 = 1.58730158725481460165e-03, Q3 = -7.93650757867487942473e-05,
+                 Q4 = 4.00821782732936239552e-06, Q5 = -2.01099218183624371326e-07;
+    double y, hi, lo, c = 0.0, t, e;
+    int k;
+    uint32_t hx = (uint32_t)f64_hi(x);
+    const uint32_t xsb = hx & 0x80000000u;
+    hx &= 0x7fffffffu;
+    if (hx >= 0x4043687Au) {                      /* |x| >= 56 ln2 */
+        if (hx >= 0x40862E42u) {                  /* |x| >= 709.78 */
+            if (hx >= 0x7ff00000u) {
+                if (((hx & 0xfffffu) | (uint32_t)f64_bits(x)) != 0) return x + x;
+                return xsb == 0 ? x : -1.0;
+            }
+            if (x > o_threshold) return huge * huge;
+        }
+        if (xsb != 0 && x + tiny < 0.0) return tiny - one;
+    }
+    if (hx > 0x3fd62e42u) {                       /* |x| > 0.5 ln2: reduce */
+        if (hx < 0x3FF0A2B2u) {
+            if (xsb == 0) { hi = x - ln2_hi; lo = ln2_lo; k = 1; }
+            else { hi = x + ln2_hi; lo = -ln2_lo; k = -1; }
+        } else {
+            k = (int)(invln2 * x + ((xsb == 0) ? 0.5 : -0.5));
+            t = k;
+            hi = x - t * ln2_hi;
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+        c = (hi - x) - lo;
+    } else if (hx < 0x3c900000u) {                /* |x| < 2^-54 */
+        t = huge + x;
+        return x - (t - (huge + x));
+    } else
+        k = 0;
+    const double hfx = 0.5 * x, hxs = x * hfx;
+    const double R1 = one + hxs * Q1, h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3, h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    t = 3.0 - r1 * hfx;
+    e = hxs * ((r1 - t) / (6.0 - x * t));
+    if (k == 0) return x - (x * e - hxs);
+    e = (x * (e - c) - c);
+    e -= hxs;
+    if (k == -1) return 0.5 * (x - e) - 0.5;
+    if (k == 1) {
+        if (x < -0.25) return -2.0 * (e - (x + 0.5));
+        return one + 2.0 * (x - e);
+    }
+    if (k <= -2 || k > 56) {
+        y = one - (e - x);
+        y = f64_sethi(y, f64_hi(y) + (k << 20));
+        return y - one;
+    }
+    if (k < 20) {
+        t = f64_sethi(one, 0x3ff00000 - (0x200000 >> k));
+        y = t - (e - x);
+        y = f64_sethi(y, f64_hi(y) + (k << 20));
+    } else {
+        t = f64_sethi(one, (0x3ff - k) << 20);
+        y = x - (e + t);
+        y += one;
+        y = f64_sethi(y, f64_hi(y) + (k << 20));
+    }
+    return y;
+}
+HD double libm_tanh(double x)
+{
+    const double one = 1.0, two = 2.0, tiny = 1.0e-300;
+    double t, z;
+    const int32_t jx = f64_hi(x), ix = jx & 0x7fffffff;
+    if (ix >= 0x7ff00000) return jx >= 0 ? one / x + one : one / x - one;
+    if (ix < 0x40360000) {                        /* |x| < 22 */
+        if (ix < 0x3c800000) return x * (one + x); /* |x| < 2^-55 */
+        if (ix >= 0x3ff00000) {
+            t = libm_expm1(two * fabs(x));
+            z = one - two / (t + two);
+        } else {
+            t = libm_expm1(-two * fabs(x));
+            z = -t / (t + two);
+        }
+    } else
+        z = one - tiny;
+    return jx >= 0 ? z : -z;
+}
+
 HD double mix_isoc(const Geo& g, int i, int j, int k)
 {
     const int lm = LM(g, i, j, k);
@@ -877,7 +992,7 @@ HD void mix_face(const Geo& g, int i, int j, int k, double t0, double t1, double
     /* tprstb(-drhodzt, SPL1) (mix_imp.f:836-856) */
     const double fac = g.alphaT * sp1;
     const double xx = -(-drdz) * fac;
-    const double th = tanh(xx * xx * xx);
+    const double th = libm_tanh(xx * xx * xx);
     const double tpr = th > 0.0 ? th : 0.0;
     ft = -tpr * kvc * dtdz;
     fs = -tpr * kvc * dsdz;

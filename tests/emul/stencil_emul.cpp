@@ -46,6 +46,12 @@ static void rhs_rows(const Geo& g, const double* x, const double* frc, int64_t n
 
 extern "C" {
 
+/* the device mixing's tanh (stencil.h), for the bitwise check against the host libm */
+void emul_tanh(const double* x, double* y, long n)
+{
+    for (long q = 0; q < n; q++) y[q] = iemic::libm_tanh(x[q]);
+}
+
 void* emul_create_band(const iemic_grid* grid, const int* landm, int jb0, int jb1)
 {
     Emul* e = new Emul();

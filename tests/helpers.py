@@ -63,6 +63,11 @@ def mask_fix(orc, cfg, L, max_fix: int = 5):
     return L
 
 
+def emul_lib():
+    """the CPU emulation library of the device assembly (tests/emul)"""
+    return C.CDLL(EMUL_LIB)
+
+
 class Emul:
     """ctypes wrapper of tests/emul/stencil_emul.cpp (one latitude band, default: all)."""
 
