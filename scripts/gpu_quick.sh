@@ -3,7 +3,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${K:-block_gs}" \
+# heartbeat: long single steps (1-degree tests, benches) still write under gpurun_out
+( while sleep 45; do date +%T >> gpurun_out/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 ${QT:-300} python -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread -k "${K:-block_gs}" \
     > gpurun_out/pytest_quick.log 2>&1 && echo "quick ok" || { echo "quick FAILED"; exit 1; }
 if [ -n "$FULL" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \

@@ -28,7 +28,7 @@ def Ocean():
 
 def make(Ocean, orc, name, mixing=0, **kw):
     c = cf.preset(name, mixing=mixing)
-    L0 = golden_landm(name) if name != "global2" else cf.init_landmask(c, cf.landmask(c))
+    L0 = golden_landm(name) if name not in ("global2", "global1") else cf.init_landmask(c, cf.landmask(c))
     oc = Ocean(c, landm=L0, **kw)
     L = mask_fix(orc, c, L0)
     o = orc.Oracle(c.ref_dict(), L, c.par_list())
@@ -61,6 +61,34 @@ def test_jacobian_rhs_bitexact(oracle_lib, Ocean, name, kind):
         assert abs(F[ri] - oF[ri]) <= 1e-13 * max(1.0, abs(oF[ri]))
         F[ri] = oF[ri]
     np.testing.assert_array_equal(bits(F), bits(oF))
+
+
+@pytest.mark.timeout(600)
+def test_global1_full_size(oracle_lib, Ocean):
+    """SURVEY config C5, the 1-degree grid (384x152x32, Mixing = 1): 11,206,656 rows and
+    192,314,880 maximal-graph entries.  J and F bit-exact against the oracle, and one
+    Newton step whose FGMRES solve reaches 1e-8 on the oracle's own J."""
+    c, oc, o, L = make(Ocean, oracle_lib, "global1", mixing=1,
+                       solver_params={"FGMRES tolerance": 1e-8, "FGMRES iterations": 100,
+                                      "FGMRES restarts": 30})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    _, col, val = oc.exportCSR()
+    ov, _ = o.jacobian(x)
+    assert len(val) == 192_314_880
+    np.testing.assert_array_equal(col, o.col)
+    del col
+    np.testing.assert_array_equal(bits(val), bits(ov))
+    del val
+    F0 = o.rhs(x)
+    np.testing.assert_array_equal(bits(oc.computeRHS()), bits(F0))
+    info = oc.newtonStep()
+    assert info.solve.converged == 1 and info.solve.explicit_rel_res <= 1e-8
+    lin = np.linalg.norm(F0 + o.spmv(ov, oc.getState() - x)) / np.linalg.norm(F0)
+    assert lin <= 1e-8, lin
+    print(f"global1 Newton step: {info.solve.iters} FGMRES steps, |F0| {info.norm_f0:.4e} "
+          f"|F1| {info.norm_f1:.4e}, {info.t_total_ms:.0f} ms")
 
 
 @pytest.mark.parametrize("name", NAMES)
