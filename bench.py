@@ -78,86 +78,47 @@ def parse():
     p.add_argument("--cold-reps", type=int, default=0,
                    help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-iters", type=int, default=48)
     return p.parse_args()
 
 
-def cpu_baseline(cfg, L, x, gpu_iters: int, krylov_dim: int, prec: int, ts_sweeps: int):
-    """The oracle port timed on the host cores over a bounded sample of the same step:
-    full F and J assembly of the 2-degree problem, the preconditioner set-up, and two
-    FGMRES runs of K1 and K2 iterations (K2 = --cpu-iters) with the same preconditioner,
-    from which the cost of iteration j (a + b*j: CGS2 grows with j) is fitted and summed
-    over the GPU's iteration count."""
-    import ctypes as C
-
+def cpu_baseline(cfg, L, x, args):
+    """The oracle port timed on the host cores for one full Newton step of the same
+    workload with the same algorithm: F and J assembly, the block Gauss-Seidel set-up (4
+    damped defect-correction passes on the dynamics block, one T/S aggregation-multigrid
+    V-cycle with z-line smoothing: oracle/prec_oracle.c, the GPU apply's CPU twin; Schur by
+    band LU), FGMRES(krylov) with restarts to the same tolerance (CGS2), x += dx, new F."""
     from oracle import oracle as orc
-    lib = orc._load_krylov()
-    PD, P64, PI = C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int)
-    lib.orc_bj_compute.argtypes = [C.c_int, P64, PI, PD, PD]
-    lib.orc_fgmres_bj.argtypes = [C.c_int, P64, PI, PD, PD, PD, PD, C.c_double, C.c_int, C.c_int,
-                                  PD, PD]
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
+    T0 = time.perf_counter()
+    t = time.perf_counter()
+    F = o.rhs(x)
+    t_rhs = time.perf_counter() - t
     t = time.perf_counter()
     val, _ = o.jacobian(x)
     t_jac = time.perf_counter() - t
     t = time.perf_counter()
-    F = o.rhs(x)
-    t_rhs = time.perf_counter() - t
-    ncell = cfg.ncell
-    b = np.ascontiguousarray(-F)
-    t = time.perf_counter()
-    if prec == 2:
-        P = orc.BlockGS(o, val, ts_sweeps)
-        pname = f"block Gauss-Seidel ({ts_sweeps} T/S sweeps, band-LU Schur)"
-    else:
-        dinv = np.zeros(ncell * 36)
-        lib.orc_bj_compute(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
-                           val.ctypes.data_as(PD), dinv.ctypes.data_as(PD))
-        pname = "block Jacobi"
+    P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
+                    ts_mg=args.ts_mg)
     t_prec = time.perf_counter() - t
-
-    def run(k):
-        t0 = time.perf_counter()
-        if prec == 2:
-            P.fgmres(b, tol=1e-300, m=k, maxit=k)
-        else:
-            xs = np.zeros(cfg.nrows)
-            rel = C.c_double()
-            lib.orc_fgmres_bj(ncell, o.rowptr.ctypes.data_as(P64), o.col.ctypes.data_as(PI),
-                              val.ctypes.data_as(PD), dinv.ctypes.data_as(PD),
-                              b.ctypes.data_as(PD), xs.ctypes.data_as(PD), 1e-300, k, k,
-                              C.byref(rel), None)
-        return time.perf_counter() - t0
-
-    k2 = max(4, args_cpu_iters)
-    k1 = max(2, k2 // 3)
-    run(2)  # warm-up: first-touch of the basis arrays
-    t1, t2 = run(k1), run(k2)
-    # t(K) = a*(K+2) + b*K(K-1)/2   (K iterations + initial and final residual SpMVs)
-    A = np.array([[k1 + 2, k1 * (k1 - 1) / 2], [k2 + 2, k2 * (k2 - 1) / 2]])
-    a, bq = np.linalg.solve(A, np.array([t1, t2]))
-    a, bq = max(a, 0.0), max(bq, 0.0)
-    est = sum(a + bq * (it % max(1, krylov_dim)) for it in range(gpu_iters)) + 2 * a
-    total = t_jac + 2 * t_rhs + t_prec + est
+    t = time.perf_counter()
+    dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=args.tol, m=args.krylov,
+                               maxit=args.krylov * (args.restarts + 1))
+    t_solve = time.perf_counter() - t
+    F1 = o.rhs(x + dx)
+    total = time.perf_counter() - T0
     return {
         "value": round(total * 1e3, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
-        "sample": (f"oracle C port (OpenMP {cores} threads), same state: F and J assembly timed "
-                   f"in full ({t_jac*1e3:.0f} + {t_rhs*1e3:.0f} ms), {pname} set-up "
-                   f"{t_prec*1e3:.0f} ms, CPU FGMRES timed for {k1} and {k2} iterations "
-                   f"({t1:.2f} s, {t2:.2f} s) and extrapolated to the GPU's {gpu_iters} "
-                   f"iterations (iteration j costs a+b*j, a={a*1e3:.1f} ms, b={bq*1e3:.3f} ms)"),
-        "norm_f0": float(np.linalg.norm(F)),
+        "sample": (f"timed, one full Newton step on the oracle C port (OpenMP {cores} threads), same "
+                   f"state and algorithm: F {t_rhs*1e3:.0f} ms, J {t_jac*1e3:.0f} ms, block GS set-up "
+                   f"{t_prec*1e3:.0f} ms (dyn x{args.dyn_iters}, T/S multigrid x{args.ts_mg}), FGMRES"
+                   f"({args.krylov}) {its} iterations to {rel:.1e} in {t_solve:.1f} s"),
+        "iters": its, "norm_f0": float(np.linalg.norm(F)), "norm_f1": float(np.linalg.norm(F1)),
     }
 
 
-args_cpu_iters = 24
-
-
 def main():
-    global args_cpu_iters
     args = parse()
-    args_cpu_iters = args.cpu_iters
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -308,8 +269,9 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(cfg, L, x0h, s.iters, args.krylov, args.prec, args.ts_sweeps)
+        cb = cpu_baseline(cfg, L, x0h, args)
         out["newton"]["norm_f0_rel_diff_vs_oracle"] = abs(last.norm_f0 - cb.pop("norm_f0")) / last.norm_f0
+        out["newton"]["norm_f1_cpu"] = cb.pop("norm_f1")
         out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)

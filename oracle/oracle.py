@@ -394,6 +394,7 @@ def _load_gs():
         lib.orc_gs_ncol.argtypes = [C.c_void_p]
         lib.orc_gs_band.argtypes = [C.c_void_p]
         lib.orc_gs_schur.argtypes = [C.c_void_p, PD, PI, C.POINTER(C.c_uint8)]
+        lib.orc_gs_config.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int]
         lib.orc_fgmres_gs.argtypes = [C.c_int, P64, PI, PD, C.c_void_p, PD, PD, C.c_double,
                                       C.c_int, C.c_int, PD, PD]
         lib._gs_ready = True
@@ -403,7 +404,11 @@ def _load_gs():
 class BlockGS:
     """CPU block Gauss-Seidel preconditioner on the oracle's CSR Jacobian."""
 
-    def __init__(self, o: "Oracle", val, ts_sweeps: int = 3):
+    def __init__(self, o: "Oracle", val, ts_sweeps: int = 3, dyn_iters: int = 1,
+                 dyn_omega: float = 1.0, ts_mg: int = 0):
+        """ts_sweeps plain T/S sweeps, or (ts_mg > 0) the GPU's default variant: dyn_iters
+        defect-correction passes of step dyn_omega on the dynamics block and ts_mg
+        aggregation-multigrid V-cycles with z-line smoothing on the T/S block."""
         lib = _load_gs()
         self.lib = lib
         d = o.d
@@ -416,6 +421,8 @@ class BlockGS:
                                    _p(self.intc, C.c_double), ts_sweeps)
         if not self.h:
             raise RuntimeError("BlockGS: singular Schur complement")
+        if lib.orc_gs_config(self.h, dyn_iters, dyn_omega, ts_mg) != 0:
+            raise RuntimeError("BlockGS: the T/S multigrid needs a coarse level")
         self.ncol = lib.orc_gs_ncol(self.h)
         self.band = lib.orc_gs_band(self.h)
 

@@ -34,6 +34,12 @@ typedef struct {
     double* band0;   /* the Schur band before the LU (exported for studies/tests) */
     int* piv;
     double *uvinv, *tsinv, *pw, *rr, *bts, *colv;
+    /* variant of prec_gs.hip's defaults: defect-correction passes on the dynamics block,
+     * T/S by aggregation-multigrid V-cycles (orc_gs_config) */
+    int dyn_iters, ts_mg;
+    double dyn_omega;
+    double *dres, *zc;
+    void* mg;
 } gs_t;
 
 static double A(const gs_t* g, int64_t row, int64_t c)
@@ -77,13 +83,16 @@ static int cmp64(const void* a, const void* b)
     return x < y ? -1 : x > y;
 }
 
+static void mg_free(void* p);
+
 void orc_gs_destroy(void* h)
 {
     gs_t* g = (gs_t*)h;
     if (!g) return;
     free(g->known); free(g->colid); free(g->ij_of_col); free(g->pinned); free(g->band);
     free(g->piv); free(g->uvinv); free(g->tsinv); free(g->pw); free(g->rr); free(g->bts);
-    free(g->colv); free(g->band0);
+    free(g->colv); free(g->band0); free(g->dres); free(g->zc);
+    mg_free(g->mg);
     free(g);
 }
 
@@ -286,6 +295,8 @@ void* orc_gs_create(int n, int m, int l, int periodic, const int64_t* rowptr, co
         }
     }
     g->rr = (double*)calloc(N, sizeof(double));
+    g->dyn_iters = 1;
+    g->dyn_omega = 1.0;
     g->bts = (double*)calloc(N, sizeof(double));
     g->colv = (double*)calloc(ncol ? ncol : 1, sizeof(double));
     return g;
@@ -331,23 +342,15 @@ static void guv(const gs_t* g, int i, int j, int k, const double* z, const doubl
         }
 }
 
-void orc_gs_apply(void* h, const double* r, double* z)
+/* dynamics block (steps 1-5): z at the active U/V/W/P rows from the right-hand side rr
+ * (active rows; identity rows of z untouched) */
+static void dyn_solve(gs_t* g, const double* rr, double* z)
 {
-    gs_t* g = (gs_t*)h;
     const int n = g->n, m = g->m, l = g->l;
-    const int64_t N = g->N, nc = g->ncell;
+    const int64_t nc = g->ncell;
     const uint8_t* kn = g->known;
-    memset(z, 0, sizeof(double) * N);
-    /* known rows and rr */
-    for (int64_t row = 0; row < N; row++) {
-        if (kn[row]) { z[row] = r[row]; g->rr[row] = 0.0; continue; }
-        double acc = r[row];
-        for (int64_t p = g->rowptr[row]; p < g->rowptr[row + 1]; p++)
-            if (kn[g->col[p]]) acc -= g->val[p] * r[g->col[p]];
-        g->rr[row] = acc;
-    }
-    double* rr = g->rr;
     /* 1. ptil */
+#pragma omp parallel for schedule(static)
     for (int q = 0; q < g->ncol; q++) {
         int i = g->ij_of_col[q] % n, j = g->ij_of_col[q] / n;
         double pabove = 0.0;
@@ -365,6 +368,7 @@ void orc_gs_apply(void* h, const double* r, double* z)
         }
     }
     /* 2. uv* */
+#pragma omp parallel for schedule(static)
     for (int64_t c = 0; c < nc; c++) {
         int ua = !kn[NUN * c + UU], va = !kn[NUN * c + VV];
         if (!ua && !va) continue;
@@ -377,6 +381,7 @@ void orc_gs_apply(void* h, const double* r, double* z)
         if (va) z[NUN * c + VV] = D[2] * ru + D[3] * rv;
     }
     /* 3. Schur rhs and band solve */
+#pragma omp parallel for schedule(static)
     for (int q = 0; q < g->ncol; q++) {
         int i = g->ij_of_col[q] % n, j = g->ij_of_col[q] / n;
         double s = 0.0;
@@ -405,6 +410,7 @@ void orc_gs_apply(void* h, const double* r, double* z)
         }
     }
     /* 4. uv correction */
+#pragma omp parallel for schedule(static)
     for (int64_t c = 0; c < nc; c++) {
         int ua = !kn[NUN * c + UU], va = !kn[NUN * c + VV];
         if (!ua && !va) continue;
@@ -418,6 +424,7 @@ void orc_gs_apply(void* h, const double* r, double* z)
         if (va) z[NUN * c + VV] -= D[2] * gu + D[3] * gv;
     }
     /* 4b/5. p and w */
+#pragma omp parallel for schedule(static)
     for (int q = 0; q < g->ncol; q++) {
         int i = g->ij_of_col[q] % n, j = g->ij_of_col[q] / n;
         double wbelow = 0.0;
@@ -437,7 +444,435 @@ void orc_gs_apply(void* h, const double* r, double* z)
             wbelow = wa ? w : 0.0;
         }
     }
+}
+
+/* the dynamics rows of rr - A z (z: identity rows = r, T/S = 0), 0 elsewhere */
+static void dyn_defect(gs_t* g, const double* z, double* d)
+{
+    const int64_t N = g->N;
+#pragma omp parallel for schedule(static)
+    for (int64_t row = 0; row < N; row++) {
+        const int var = (int)(row % NUN);
+        if (var > PP || g->known[row]) { d[row] = 0.0; continue; }
+        double acc = g->rr[row];
+        for (int64_t p = g->rowptr[row]; p < g->rowptr[row + 1]; p++) {
+            const int cl = g->col[p], cv = cl % NUN;
+            if (cv > PP || g->known[cl]) continue;
+            acc -= g->val[p] * z[cl];
+        }
+        d[row] = acc;
+    }
+}
+
+
+
+/* ---- T/S aggregation multigrid (prec_gs.hip's mg_setup / mg_vcycle restated on the
+ * CPU, one band): levels of n x m x l cells merging 2x2 horizontal neighbours over the
+ * full depth, Galerkin coarse operators with piecewise-constant transfers, z-line
+ * (block-tridiagonal along k) relaxation by horizontal colour, forward before and
+ * backward after the coarse correction, a dense inverse on the coarsest level (<= 128
+ * cells).  Cell index on every level: (j*l + k)*n + i. ------------------------------- */
+enum { MG_MAXL = 12 };
+typedef struct {
+    int nlev, l, periodic;
+    int n[MG_MAXL], m[MG_MAXL];
+    double *off[MG_MAXL], *diag[MG_MAXL], *dinv[MG_MAXL], *b[MG_MAXL], *z[MG_MAXL];
+    double* cinv;
+} mg_t;
+
+static void mg_free(void* p)
+{
+    mg_t* M = (mg_t*)p;
+    if (!M) return;
+    for (int q = 0; q < M->nlev; q++) {
+        free(M->off[q]); free(M->diag[q]); free(M->dinv[q]); free(M->b[q]); free(M->z[q]);
+    }
+    free(M->cinv);
+    free(M);
+}
+
+static int64_t mg_ncl(const mg_t* M, int q) { return (int64_t)M->n[q] * M->m[q] * M->l; }
+
+/* neighbour q (-i,+i,-j,+j,-k,+k) of (i,j,k) on level lv; 0 outside */
+static int mg_nb(const mg_t* M, int lv, int q, int* i, int* j, int* k)
+{
+    switch (q) {
+    case 0: (*i)--; break;
+    case 1: (*i)++; break;
+    case 2: (*j)--; break;
+    case 3: (*j)++; break;
+    case 4: (*k)--; break;
+    default: (*k)++; break;
+    }
+    if (*j < 0 || *j >= M->m[lv] || *k < 0 || *k >= M->l) return 0;
+    if (*i < 0 || *i >= M->n[lv]) {
+        if (!M->periodic) return 0;
+        *i = (*i + M->n[lv]) % M->n[lv];
+    }
+    return 1;
+}
+
+/* Gauss-Jordan inverse with partial pivoting; rows without coupling become identity rows */
+static void dense_inverse(double* A, int N, double* X)
+{
+    memset(X, 0, sizeof(double) * (size_t)N * N);
+    for (int i = 0; i < N; i++) {
+        X[(size_t)i * N + i] = 1.0;
+        int any = 0;
+        for (int j = 0; j < N; j++) any |= A[(size_t)i * N + j] != 0.0;
+        if (!any) A[(size_t)i * N + i] = 1.0;
+    }
+    for (int k = 0; k < N; k++) {
+        int p = k;
+        for (int i = k + 1; i < N; i++)
+            if (fabs(A[(size_t)i * N + k]) > fabs(A[(size_t)p * N + k])) p = i;
+        if (p != k)
+            for (int j = 0; j < N; j++) {
+                double t = A[(size_t)p * N + j]; A[(size_t)p * N + j] = A[(size_t)k * N + j]; A[(size_t)k * N + j] = t;
+                t = X[(size_t)p * N + j]; X[(size_t)p * N + j] = X[(size_t)k * N + j]; X[(size_t)k * N + j] = t;
+            }
+        const double d = A[(size_t)k * N + k];
+        const double qd = d != 0.0 ? 1.0 / d : 0.0;
+        for (int j = 0; j < N; j++) { A[(size_t)k * N + j] *= qd; X[(size_t)k * N + j] *= qd; }
+        for (int i = 0; i < N; i++) {
+            if (i == k) continue;
+            const double f = A[(size_t)i * N + k];
+            if (f == 0.0) continue;
+            for (int j = 0; j < N; j++) {
+                A[(size_t)i * N + j] -= f * A[(size_t)k * N + j];
+                X[(size_t)i * N + j] -= f * X[(size_t)k * N + j];
+            }
+        }
+    }
+}
+
+static void* mg_build(gs_t* g)
+{
+    const int n = g->n, m = g->m, l = g->l;
+    mg_t* M = (mg_t*)calloc(1, sizeof(mg_t));
+    M->l = l;
+    M->periodic = g->periodic;
+    int nn = n, mm = m, q = 0;
+    M->n[0] = n; M->m[0] = m;
+    while (q + 1 < MG_MAXL && (q == 0 || (int64_t)nn * mm * l > 128) && (nn > 1 || mm > 1)) {
+        nn = (nn + 1) / 2; mm = (mm + 1) / 2; q++;
+        M->n[q] = nn; M->m[q] = mm;
+    }
+    if (q == 0) { free(M); return NULL; }
+    M->nlev = q + 1;
+    for (int lv = 0; lv < M->nlev; lv++) {
+        const int64_t ncl = mg_ncl(M, lv);
+        M->off[lv] = (double*)calloc(16 * ncl, sizeof(double));
+        M->diag[lv] = (double*)calloc(4 * ncl, sizeof(double));
+        M->dinv[lv] = (double*)calloc(4 * ncl, sizeof(double));
+        M->b[lv] = (double*)calloc(2 * ncl, sizeof(double));
+        M->z[lv] = (double*)calloc(2 * ncl, sizeof(double));
+    }
+    /* level 0: the T/S block of the Jacobian (k_ts_compact / k_cell_factors) */
+    const uint8_t* kn = g->known;
+    const int64_t nc0 = mg_ncl(M, 0);
+    static const int dd[8][4] = {{-1, 0, 0, 0}, {1, 0, 0, 0}, {0, -1, 0, 0}, {0, 1, 0, 0},
+                                 {0, 0, -1, 0}, {0, 0, 1, 0}, {0, 0, -1, 1}, {0, 0, 1, 1}};
+    for (int j = 0; j < m; j++)
+        for (int k = 0; k < l; k++)
+            for (int i = 0; i < n; i++) {
+                const int64_t c = ((int64_t)j * l + k) * n + i, rc = cel(g, i, j, k);
+                for (int R = 0; R < 2; R++) {
+                    const int var = TT + R, oth = SS - R;
+                    const int64_t row = NUN * rc + var;
+                    const int act = !kn[row] && row != g->rowintcon;
+                    for (int qq = 0; qq < 8; qq++) {
+                        double v = 0.0;
+                        if (act) {
+                            int ii = i + dd[qq][0], jj = j + dd[qq][1];
+                            const int kk = k + dd[qq][2];
+                            if (kk >= 0 && kk < l && wrap(g, &ii, &jj)) {
+                                const int64_t cl = NUN * cel(g, ii, jj, kk) + (dd[qq][3] ? oth : var);
+                                if (!kn[cl]) v = A(g, row, cl);
+                            }
+                        }
+                        M->off[0][(int64_t)(R * 8 + qq) * nc0 + c] = v;
+                    }
+                }
+                const int64_t u = NUN * rc;
+                const int ta = !kn[u + TT], sa = !kn[u + SS];
+                double sd = A(g, u + SS, u + SS), st = A(g, u + SS, u + TT);
+                if (u + SS == g->rowintcon) { sd = g->int_sign * g->intc[u + SS]; st = 0.0; }
+                M->diag[0][c] = ta ? A(g, u + TT, u + TT) : 0.0;
+                M->diag[0][nc0 + c] = ta && sa ? A(g, u + TT, u + SS) : 0.0;
+                M->diag[0][2 * nc0 + c] = ta && sa ? st : 0.0;
+                M->diag[0][3 * nc0 + c] = sa ? sd : 0.0;
+                for (int e = 0; e < 4; e++) M->dinv[0][e * nc0 + c] = g->tsinv[4 * rc + e];
+            }
+    /* Galerkin coarse levels (k_mg_galerkin) */
+    for (int lv = 1; lv < M->nlev; lv++) {
+        const int Fn = M->n[lv - 1], Fm = M->m[lv - 1];
+        const int64_t fcl = mg_ncl(M, lv - 1), ccl = mg_ncl(M, lv);
+        for (int64_t t = 0; t < ccl; t++) {
+            const int I = (int)(t % M->n[lv]), k = (int)((t / M->n[lv]) % l), J = (int)(t / ((int64_t)M->n[lv] * l));
+            double o[16] = {0}, d[4] = {0};
+            for (int bb = 0; bb < 2; bb++)
+                for (int a = 0; a < 2; a++) {
+                    const int i = 2 * I + a, j = 2 * J + bb;
+                    if (i >= Fn || j >= Fm) continue;
+                    const int64_t c = ((int64_t)j * l + k) * Fn + i;
+                    for (int e = 0; e < 4; e++) d[e] += M->diag[lv - 1][e * fcl + c];
+                    for (int R = 0; R < 2; R++)
+                        for (int qq = 0; qq < 8; qq++) {
+                            const double v = M->off[lv - 1][(int64_t)(8 * R + qq) * fcl + c];
+                            if (v == 0.0) continue;
+                            int ii = i, jj = j, kk = k;
+                            if (!mg_nb(M, lv - 1, qq < 6 ? qq : qq - 2, &ii, &jj, &kk)) continue;
+                            if (qq < 6 && (ii >> 1) == I && (jj >> 1) == J && kk == k) d[3 * R] += v;
+                            else o[8 * R + qq] += v;
+                        }
+                }
+            const int at = d[0] != 0.0, as = d[3] != 0.0;
+            if (!at) { d[1] = d[2] = 0.0; for (int qq = 0; qq < 8; qq++) o[qq] = 0.0; }
+            if (!as) { d[1] = d[2] = 0.0; for (int qq = 8; qq < 16; qq++) o[qq] = 0.0; }
+            for (int e = 0; e < 16; e++) M->off[lv][e * ccl + t] = o[e];
+            for (int e = 0; e < 4; e++) M->diag[lv][e * ccl + t] = d[e];
+            double inv[4];
+            inv2(d[0], d[1], d[2], d[3], at, as, inv);
+            for (int e = 0; e < 4; e++) M->dinv[lv][e * ccl + t] = inv[e];
+        }
+    }
+    /* coarsest: dense operator and its inverse */
+    const int qc = M->nlev - 1;
+    const int64_t ncl = mg_ncl(M, qc);
+    const int N = (int)(2 * ncl);
+    double* Ad = (double*)calloc((size_t)N * N, sizeof(double));
+    M->cinv = (double*)calloc((size_t)N * N, sizeof(double));
+    for (int64_t t = 0; t < ncl; t++) {
+        const int i = (int)(t % M->n[qc]), k = (int)((t / M->n[qc]) % l), jl = (int)(t / ((int64_t)M->n[qc] * l));
+        for (int R = 0; R < 2; R++) {
+            const int64_t row = R * ncl + t;
+            Ad[row * N + R * ncl + t] += M->diag[qc][(3 * R) * ncl + t];
+            Ad[row * N + (1 - R) * ncl + t] += M->diag[qc][(1 + R) * ncl + t];
+            for (int qq = 0; qq < 8; qq++) {
+                const double v = M->off[qc][(8 * R + qq) * ncl + t];
+                if (v == 0.0) continue;
+                int ii = i, jj = jl, kk = k;
+                if (!mg_nb(M, qc, qq < 6 ? qq : qq - 2, &ii, &jj, &kk)) continue;
+                const int64_t nb = ((int64_t)jj * l + kk) * M->n[qc] + ii;
+                Ad[row * N + (qq < 6 ? R : 1 - R) * ncl + nb] += v;
+            }
+        }
+    }
+    dense_inverse(Ad, N, M->cinv);
+    free(Ad);
+    return M;
+}
+
+/* off-diagonal part of (T, S) rows at cell c of level lv applied to the iterate */
+static void mg_offmul(const mg_t* M, int lv, int i, int j, int k, int64_t c, double* at, double* as)
+{
+    const int64_t ncl = mg_ncl(M, lv);
+    const double *off = M->off[lv], *zt = M->z[lv], *zs = M->z[lv] + ncl;
+    *at = *as = 0.0;
+    for (int q = 0; q < 6; q++) {
+        int ii = i, jj = j, kk = k;
+        if (!mg_nb(M, lv, q, &ii, &jj, &kk)) continue;
+        const int64_t nc = ((int64_t)jj * M->l + kk) * M->n[lv] + ii;
+        *at += off[q * ncl + c] * zt[nc];
+        *as += off[(8 + q) * ncl + c] * zs[nc];
+        if (q == 4) { *at += off[6 * ncl + c] * zs[nc]; *as += off[14 * ncl + c] * zt[nc]; }
+        else if (q == 5) { *at += off[7 * ncl + c] * zs[nc]; *as += off[15 * ncl + c] * zt[nc]; }
+    }
+}
+
+/* z-line relaxation of the columns of one horizontal colour (block Thomas along k) */
+static void mg_zline(mg_t* M, int lv, int colour)
+{
+    const int n = M->n[lv], mb = M->m[lv], l = M->l;
+    const int64_t ncl = mg_ncl(M, lv);
+    const double *off = M->off[lv], *dg = M->diag[lv], *bt = M->b[lv], *bs = M->b[lv] + ncl;
+    double *zt = M->z[lv], *zs = M->z[lv] + ncl;
+    const int odd = M->periodic && (n & 1);
+#pragma omp parallel for schedule(static)
+    for (int col = 0; col < n * mb; col++) {
+        const int i = col % n, j = col / n;
+        const int cc = (odd && i == n - 1) ? 2 + (j & 1) : ((i + j) & 1);
+        if (cc != colour) continue;
+        double Cp[64][4], dp[64][2];
+        for (int k = 0; k < l; k++) {
+            const int64_t c = ((int64_t)j * l + k) * n + i;
+            double rt = bt[c], rs = bs[c];
+            for (int q = 0; q < 4; q++) {
+                int ii = i, jj = j, kk = k;
+                if (!mg_nb(M, lv, q, &ii, &jj, &kk)) continue;
+                const int64_t nc = ((int64_t)jj * l + kk) * n + ii;
+                rt -= off[q * ncl + c] * zt[nc];
+                rs -= off[(8 + q) * ncl + c] * zs[nc];
+            }
+            double Am[4] = {dg[c], dg[ncl + c], dg[2 * ncl + c], dg[3 * ncl + c]};
+            double Bm[4] = {off[4 * ncl + c], off[6 * ncl + c], off[14 * ncl + c], off[12 * ncl + c]};
+            double Cm[4] = {off[5 * ncl + c], off[7 * ncl + c], off[15 * ncl + c], off[13 * ncl + c]};
+            const int at = dg[c] != 0.0, as = dg[3 * ncl + c] != 0.0;
+            if (!at) { Am[0] = 1.0; Am[1] = Am[2] = 0.0; Bm[0] = Bm[1] = 0.0; Cm[0] = Cm[1] = 0.0; rt = 0.0; }
+            if (!as) { Am[3] = 1.0; Am[1] = Am[2] = 0.0; Bm[2] = Bm[3] = 0.0; Cm[2] = Cm[3] = 0.0; rs = 0.0; }
+            if (k > 0) {       /* Am -= Bm Cp[k-1], r -= Bm dp[k-1] */
+                const double* P = Cp[k - 1];
+                const double a0 = Am[0] - (Bm[0] * P[0] + Bm[1] * P[2]), a1 = Am[1] - (Bm[0] * P[1] + Bm[1] * P[3]);
+                const double a2 = Am[2] - (Bm[2] * P[0] + Bm[3] * P[2]), a3 = Am[3] - (Bm[2] * P[1] + Bm[3] * P[3]);
+                Am[0] = a0; Am[1] = a1; Am[2] = a2; Am[3] = a3;
+                rt -= Bm[0] * dp[k - 1][0] + Bm[1] * dp[k - 1][1];
+                rs -= Bm[2] * dp[k - 1][0] + Bm[3] * dp[k - 1][1];
+            }
+            const double det = Am[0] * Am[3] - Am[1] * Am[2];
+            const double qd = det != 0.0 ? 1.0 / det : 0.0;
+            const double I0 = Am[3] * qd, I1 = -Am[1] * qd, I2 = -Am[2] * qd, I3 = Am[0] * qd;
+            Cp[k][0] = I0 * Cm[0] + I1 * Cm[2]; Cp[k][1] = I0 * Cm[1] + I1 * Cm[3];
+            Cp[k][2] = I2 * Cm[0] + I3 * Cm[2]; Cp[k][3] = I2 * Cm[1] + I3 * Cm[3];
+            dp[k][0] = I0 * rt + I1 * rs;
+            dp[k][1] = I2 * rt + I3 * rs;
+        }
+        double x0 = 0.0, x1 = 0.0;
+        for (int k = l - 1; k >= 0; k--) {
+            const int64_t c = ((int64_t)j * l + k) * n + i;
+            const double y0 = dp[k][0] - (Cp[k][0] * x0 + Cp[k][1] * x1);
+            const double y1 = dp[k][1] - (Cp[k][2] * x0 + Cp[k][3] * x1);
+            x0 = y0; x1 = y1;
+            zt[c] = x0; zs[c] = x1;
+        }
+    }
+}
+
+static void mg_smooth(mg_t* M, int lv, int post)
+{
+    const int ncol = (M->periodic && (M->n[lv] & 1)) ? 4 : 2;
+    for (int h = 0; h < ncol; h++) mg_zline(M, lv, post ? ncol - 1 - h : h);
+}
+
+static void mg_vcycle(gs_t* g, void* mgp, int q)
+{
+    (void)g;
+    mg_t* M = (mg_t*)mgp;
+    if (q == M->nlev - 1) {
+        const int64_t ncl = mg_ncl(M, q);
+        const int N = (int)(2 * ncl);
+#pragma omp parallel for schedule(static)
+        for (int r = 0; r < N; r++) {
+            double acc = 0.0;
+            for (int c = 0; c < N; c++) acc += M->cinv[(size_t)r * N + c] * M->b[q][c];
+            M->z[q][r] = acc;
+        }
+        return;
+    }
+    mg_smooth(M, q, 0);
+    /* restriction: coarse rhs = sum of the children's residuals, coarse iterate 0 */
+    const int Fn = M->n[q], Fm = M->m[q], l = M->l;
+    const int64_t fcl = mg_ncl(M, q), ccl = mg_ncl(M, q + 1);
+    const double* dg = M->diag[q];
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < ccl; t++) {
+        const int I = (int)(t % M->n[q + 1]), k = (int)((t / M->n[q + 1]) % l), J = (int)(t / ((int64_t)M->n[q + 1] * l));
+        double rs4[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        for (int ch = 0; ch < 4; ch++) {
+            const int i = 2 * I + (ch & 1), j = 2 * J + (ch >> 1);
+            if (i >= Fn || j >= Fm) continue;
+            const int64_t c = ((int64_t)j * l + k) * Fn + i;
+            double at, as;
+            mg_offmul(M, q, i, j, k, c, &at, &as);
+            const double zt = M->z[q][c], zs = M->z[q][fcl + c];
+            at += dg[c] * zt + dg[fcl + c] * zs;
+            as += dg[2 * fcl + c] * zt + dg[3 * fcl + c] * zs;
+            rs4[ch][0] = M->b[q][c] - at;
+            rs4[ch][1] = M->b[q][fcl + c] - as;
+        }
+        M->b[q + 1][t] = (rs4[0][0] + rs4[1][0]) + (rs4[2][0] + rs4[3][0]);
+        M->b[q + 1][ccl + t] = (rs4[0][1] + rs4[1][1]) + (rs4[2][1] + rs4[3][1]);
+        M->z[q + 1][t] = M->z[q + 1][ccl + t] = 0.0;
+    }
+    mg_vcycle(g, mgp, q + 1);
+    /* prolongation: fine iterate += its aggregate's correction (active unknowns) */
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < fcl; t++) {
+        const int i = (int)(t % Fn), k = (int)((t / Fn) % l), j = (int)(t / ((int64_t)Fn * l));
+        const int64_t p = ((int64_t)(j >> 1) * l + k) * M->n[q + 1] + (i >> 1);
+        if (dg[t] != 0.0) M->z[q][t] += M->z[q + 1][p];
+        if (dg[3 * fcl + t] != 0.0) M->z[q][fcl + t] += M->z[q + 1][ccl + p];
+    }
+    mg_smooth(M, q, 1);
+}
+
+/* level-0 right-hand side from bts, iterate 0 */
+static void mg_begin(gs_t* g, void* mgp, double* z)
+{
+    (void)z;
+    mg_t* M = (mg_t*)mgp;
+    const int n = g->n, m = g->m, l = g->l;
+    const int64_t nc0 = mg_ncl(M, 0);
+    for (int j = 0; j < m; j++)
+        for (int k = 0; k < l; k++)
+            for (int i = 0; i < n; i++) {
+                const int64_t c = ((int64_t)j * l + k) * n + i, rc = cel(g, i, j, k);
+                M->b[0][c] = g->known[NUN * rc + TT] ? 0.0 : g->bts[NUN * rc + TT];
+                M->b[0][nc0 + c] = g->known[NUN * rc + SS] ? 0.0 : g->bts[NUN * rc + SS];
+                M->z[0][c] = M->z[0][nc0 + c] = 0.0;
+            }
+}
+static void mg_end(gs_t* g, void* mgp, double* z)
+{
+    mg_t* M = (mg_t*)mgp;
+    const int n = g->n, m = g->m, l = g->l;
+    const int64_t nc0 = mg_ncl(M, 0);
+    for (int j = 0; j < m; j++)
+        for (int k = 0; k < l; k++)
+            for (int i = 0; i < n; i++) {
+                const int64_t c = ((int64_t)j * l + k) * n + i, rc = cel(g, i, j, k);
+                if (!g->known[NUN * rc + TT]) z[NUN * rc + TT] = M->z[0][c];
+                if (!g->known[NUN * rc + SS]) z[NUN * rc + SS] = M->z[0][nc0 + c];
+            }
+}
+
+/* variant: dyn_iters defect-correction passes with step omega, ts_mg V-cycles (0: the
+ * ts_sweeps plain sweeps); returns 0, or -1 if the T/S multigrid has no coarse level */
+int orc_gs_config(void* h, int dyn_iters, double omega, int ts_mg)
+{
+    gs_t* g = (gs_t*)h;
+    g->dyn_iters = dyn_iters > 1 ? dyn_iters : 1;
+    g->dyn_omega = omega > 0.0 ? omega : 1.0;
+    if (g->dyn_iters > 1 && !g->dres) {
+        g->dres = (double*)calloc(g->N, sizeof(double));
+        g->zc = (double*)calloc(g->N, sizeof(double));
+    }
+    g->ts_mg = ts_mg > 0 ? ts_mg : 0;
+    if (g->ts_mg > 0 && !g->mg) {
+        g->mg = mg_build(g);
+        if (!g->mg) { g->ts_mg = 0; return -1; }
+    }
+    return 0;
+}
+
+void orc_gs_apply(void* h, const double* r, double* z)
+{
+    gs_t* g = (gs_t*)h;
+    const int n = g->n, m = g->m;
+    const int64_t N = g->N, nc = g->ncell;
+    const uint8_t* kn = g->known;
+    memset(z, 0, sizeof(double) * N);
+    /* known rows and rr */
+#pragma omp parallel for schedule(static)
+    for (int64_t row = 0; row < N; row++) {
+        if (kn[row]) { z[row] = r[row]; g->rr[row] = 0.0; continue; }
+        double acc = r[row];
+        for (int64_t p = g->rowptr[row]; p < g->rowptr[row + 1]; p++)
+            if (kn[g->col[p]]) acc -= g->val[p] * r[g->col[p]];
+        g->rr[row] = acc;
+    }
+    double* rr = g->rr;
+    dyn_solve(g, rr, z);
+    /* defect correction: z_D += omega M_D^-1 (rr - A z)_D */
+    for (int it = 1; it < g->dyn_iters; it++) {
+        dyn_defect(g, z, g->dres);
+        memset(g->zc, 0, sizeof(double) * N);
+        dyn_solve(g, g->dres, g->zc);
+        for (int64_t row = 0; row < N; row++)
+            if (row % NUN <= PP && !kn[row]) z[row] += g->dyn_omega * g->zc[row];
+    }
     /* 6. T/S */
+#pragma omp parallel for schedule(static)
     for (int64_t row = 0; row < N; row++) {
         int var = (int)(row % NUN);
         if (var < TT || kn[row]) continue;
@@ -449,6 +884,12 @@ void orc_gs_apply(void* h, const double* r, double* z)
         }
         g->bts[row] = acc;
         z[row] = 0.0;
+    }
+    if (g->ts_mg > 0 && g->mg) {
+        mg_begin(g, g->mg, z);
+        for (int cyc = 0; cyc < g->ts_mg; cyc++) mg_vcycle(g, g->mg, 0);
+        mg_end(g, g->mg, z);
+        return;
     }
     /* colours: parity of i+j+k; odd periodic n: column n-1 gets colours 2/3 */
     const int four = g->periodic && (n & 1);

@@ -140,6 +140,26 @@ def test_block_gs_apply_matches_cpu(oracle_lib, Ocean, name):
     assert np.max(np.abs(z - zc)) <= 1e-8 * np.max(np.abs(zc))
 
 
+@pytest.mark.parametrize("name", ["natl8", "gateway16", "global4", "global2"])
+def test_block_gs_default_apply_matches_cpu(oracle_lib, Ocean, name):
+    """The default block GS (4 damped defect-correction passes on the dynamics block, one
+    T/S aggregation-multigrid V-cycle with z-line smoothing, Mixing = 1) == its CPU twin
+    (prec_oracle.c: band-LU Schur, block-Thomas z-lines)."""
+    c, oc, o, L = make(Ocean, oracle_lib, name, mixing=1, solver_params={"Preconditioner": 2})
+    sp = oc.solver_params
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    oc.buildPreconditioner(force=True)
+    ov, _ = o.jacobian(x)
+    P = oracle_lib.BlockGS(o, ov, 3, dyn_iters=sp["Dyn iterations"], dyn_omega=sp["Dyn damping"],
+                           ts_mg=sp["TS multigrid cycles"])
+    r = cf.synthetic_vector(c, seed=3)
+    z, zc = oc.applyPrecon(r), P.apply(r)
+    assert np.all(np.isfinite(z))
+    assert np.max(np.abs(z - zc)) <= 1e-8 * np.max(np.abs(zc))
+
+
 @pytest.mark.parametrize("mixing", [0, 1])
 def test_block_gs_apply_global2(oracle_lib, Ocean, mixing):
     """The same at the bench size (2 degrees, 192x76x16, 8,996 water columns: 192 blocks of
