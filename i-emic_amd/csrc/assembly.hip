@@ -116,9 +116,9 @@ __global__ void k_sum_partials(const double* __restrict__ part, int nb, double* 
 }
 /* F[rowintcon] = intSign*(coeff . x - intCorrection)  (THCM.C:1005-1018) */
 __global__ void k_intcond_set(const double* __restrict__ dotv, double* __restrict__ F, int64_t row,
-                              int sign)
+                              int sign, double corr)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) F[row] = sign * (*dotv - 0.0);
+    if (threadIdx.x == 0 && blockIdx.x == 0) F[row] = sign * (*dotv - corr);
 }
 
 __global__ void k_qint(Geo g, const double* __restrict__ ftab, double* __restrict__ qcor,
@@ -141,6 +141,34 @@ __global__ void k_forcing(Geo g, const double* __restrict__ ftab, const double* 
     for (int v = 0; v < NUN; v++) frc[NUN * cell + v] = f[v];
 }
 
+/* block partials of sum T^2 and sum S^2 over the owned cells (fixed order) */
+__global__ void __launch_bounds__(256) k_ts_sq_partial(const double* __restrict__ x, int64_t own0,
+                                                       int64_t nloc, double* __restrict__ part)
+{
+    __shared__ double sm[2][256];
+    double st = 0.0, ss = 0.0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nloc;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const double t = x[NUN * (own0 + q) + TT], sv = x[NUN * (own0 + q) + SS];
+        st += t * t;
+        ss += sv * sv;
+    }
+    sm[0][threadIdx.x] = st;
+    sm[1][threadIdx.x] = ss;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            sm[0][threadIdx.x] += sm[0][threadIdx.x + w];
+            sm[1][threadIdx.x] += sm[1][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = sm[0][0];
+        part[gridDim.x + blockIdx.x] = sm[1][0];
+    }
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* vmix_control (mix_imp.f:131-166) for Mixing = 2: the Ocean layer calls fixMixing(0)
  * before every evaluation (Ocean.C:1271/1292), so whether T and S mix (L2 norm of the
@@ -151,20 +179,18 @@ static int mix_control(iemic_ctx* c, const double* x_dev)
     host::Setup& su = c->su;
     if (su.cfg.vmix == 0) return 0;
     if (su.cfg.vmix == 2) {   /* Ocean.C:1271/1292: fixMixing(0) before every evaluation */
-        std::vector<double> h((size_t)c->nerows);
-        int rc = d2h(c, h.data(), x_dev, sizeof(double) * h.size());
+        /* squared field norms on the device (block partials + fixed-order sums), summed
+         * over the bands; only the two totals come to the host */
+        const int nb = 256;
+        double* part = c->d_red.p;
+        hipLaunchKernelGGL(k_ts_sq_partial, dim3(nb), dim3(256), 0, c->stream, x_dev, (int64_t)c->own0,
+                           (int64_t)c->nloc, part);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, c->stream, part, nb, part + 2 * nb);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, c->stream, part + nb, nb, part + 2 * nb + 1);
+        int rc = allreduce_sum(c, part + 2 * nb, 2);
         if (rc) return rc;
         double sq[2] = {0.0, 0.0};
-        for (int64_t lc = 0; lc < c->nloc; lc++) {
-            const double t = h[NUN * (c->own0 + lc) + TT], sv = h[NUN * (c->own0 + lc) + SS];
-            sq[0] += t * t;
-            sq[1] += sv * sv;
-        }
-        if (c->nranks > 1) {
-            if ((rc = h2d(c, c->d_red.p, sq, sizeof(sq)))) return rc;
-            if ((rc = allreduce_sum(c, c->d_red.p, 2))) return rc;
-            if ((rc = d2h(c, sq, c->d_red.p, sizeof(sq)))) return rc;
-        }
+        if ((rc = d2h(c, sq, part + 2 * nb, sizeof(sq)))) return rc;
         su.vmix_t = std::sqrt(sq[0]) > 1.0e-12;
         su.vmix_s = std::sqrt(sq[1]) > 1.0e-12;
         /* vmix_control partitions only when T mixes (mix_imp.f:158): salinity-only mixing
@@ -219,10 +245,27 @@ int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev)
         if (rc) return rc;
         if (c->rowintcon >= 0)
             hipLaunchKernelGGL(k_intcond_set, dim3(1), dim3(64), 0, c->stream, c->d_red.p + nb, F_dev,
-                               (int64_t)c->rowintcon, c->cfg.int_sign);
+                               (int64_t)c->rowintcon, c->cfg.int_sign, c->int_correction);
     }
     HIP_OK(hipGetLastError());
     return 0;
+}
+
+/* THCM::setIntCondCorrection (THCM.C:2020-2038): intCorrection = coeff . x (SRES = 0) */
+int intcond_correction(iemic_ctx* c, const double* x_dev)
+{
+    if (c->su.rowintcon_ref < 0) {
+        c->int_correction = 0.0;
+        return 0;
+    }
+    const int nb = 256;
+    const int64_t o = NUN * c->own0;
+    hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(256), 0, c->stream, c->d_intc.p + o, x_dev + o, c->nlrows,
+                       c->d_red.p);
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, c->stream, c->d_red.p, nb, c->d_red.p + nb);
+    int rc = allreduce_sum(c, c->d_red.p + nb, 1);
+    if (rc) return rc;
+    return d2h(c, &c->int_correction, c->d_red.p + nb, sizeof(double));
 }
 
 int compute_forcing(iemic_ctx* c)

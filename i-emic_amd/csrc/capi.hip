@@ -371,6 +371,24 @@ extern "C" int iemic_set_state(iemic_ctx* c, const double* x)
     c->jac_valid = 0;
     return 0;
 }
+extern "C" int iemic_set_intcond_correction(iemic_ctx* c, const double* x)
+{
+    CTX_CHECK(c);
+    const double* xd = c->d_x.p;
+    if (x) {
+        int rc = put_ref(c, x, c->d_tmp1.p);
+        if (rc) return rc;
+        xd = c->d_tmp1.p;
+    }
+    return intcond_correction(c, xd);
+}
+extern "C" int iemic_get_intcond_correction(iemic_ctx* c, double* corr)
+{
+    CTX_CHECK(c);
+    if (!corr) return IEMIC_EINVAL;
+    *corr = c->int_correction;
+    return 0;
+}
 extern "C" int iemic_set_state_dev(iemic_ctx* c, const double* x_dev)
 {
     CTX_CHECK(c);

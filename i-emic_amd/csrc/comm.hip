@@ -12,7 +12,9 @@
 
 #include <condition_variable>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -41,6 +43,8 @@ struct LocalGroup {
     std::vector<std::vector<double>> slot;
     std::vector<double*> vec;
     std::vector<iemic_ctx*> ctxs;
+    /* point-to-point mailbox: (src, dst, k) -> the k-th message src sent to dst in a batch */
+    std::map<std::tuple<int, int, int>, std::vector<double>> box;
     explicit LocalGroup(int p) : P(p), slot(p), vec(p, nullptr), ctxs(p, nullptr) {}
     void barrier()
     {
@@ -69,31 +73,6 @@ static int local_allreduce(iemic_ctx* c, double* dev, int count)
         for (int q = 0; q < count; q++) sum[q] += g->slot[r][q];
     g->barrier();
     return h2d(c, dev, sum.data(), sizeof(double) * count);
-}
-
-static int local_halo(iemic_ctx* c, double* v, int width, int rows_j)
-{
-    LocalGroup* g = (LocalGroup*)c->group;
-    const int64_t slab = (int64_t)width * c->l * c->n, cnt = slab * rows_j;
-    const int64_t own_first = (int64_t)width * c->own0, own_end = own_first + (int64_t)width * c->nloc;
-    HIP_OK(hipStreamSynchronize(c->stream));
-    g->vec[c->rank] = v;
-    g->barrier();
-    /* neighbours' ext vectors have the same halo depth; their owned rows start at HALO */
-    if (c->rank > 0) {
-        /* lower halo <- last rows of rank-1's band; rank-1 owns the band below: its owned end */
-        iemic_ctx* nb = g->ctxs[c->rank - 1];
-        const double* src = g->vec[c->rank - 1] + (int64_t)width * (nb->own0 + nb->nloc) - cnt;
-        HIP_OK(hipMemcpyAsync(v + own_first - cnt, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
-    }
-    if (c->rank < g->P - 1) {
-        iemic_ctx* nb = g->ctxs[c->rank + 1];
-        const double* src = g->vec[c->rank + 1] + (int64_t)width * nb->own0;
-        HIP_OK(hipMemcpyAsync(v + own_end, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
-    }
-    HIP_OK(hipStreamSynchronize(c->stream));
-    g->barrier();
-    return 0;
 }
 
 void* local_group_new(int nranks) { return nranks > 0 ? new LocalGroup(nranks) : nullptr; }
@@ -139,53 +118,117 @@ int allreduce_sum(iemic_ctx* c, double* dev, int count)
     return 0;
 }
 
-/* exchange rows_j (<= HALO) latitude rows of a per-cell array (width doubles per ext
- * cell) with the neighbouring bands */
-int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
+/* One batch of point-to-point messages.  The halo exchanges build their batch once
+ * (halo_ops) and hand it to the transport: RCCL (one ncclGroupStart/End, messages to the
+ * same peer matched in order, as NCCL requires) or, for in-process band groups, the host
+ * mailbox below, which pairs the k-th send of rank a to b with the k-th receive of b from
+ * a -- the same pairing rule, so the batches the tests run are the ones RCCL runs. */
+struct P2P {
+    bool send;
+    double* buf;
+    int64_t cnt;
+    int peer;
+};
+
+/* rows_j (<= HALO) latitude rows of a per-cell array (width doubles per ext cell) to and
+ * from the neighbouring bands */
+static void halo_ops(const iemic_ctx* c, double* v, int width, int rows_j, std::vector<P2P>& ops)
 {
-    if (c->nranks <= 1) return 0;
-    if (c->group) return local_halo(c, v, width, rows_j);
     const int64_t slab = (int64_t)width * c->l * c->n;        /* doubles per latitude row */
     const int64_t cnt = slab * rows_j;
     const int64_t own_first = (int64_t)width * c->own0;        /* first owned cell         */
     const int64_t own_end = own_first + (int64_t)width * c->nloc; /* one past the last     */
-    ncclComm_t comm = (ncclComm_t)c->comm;
-    NCCL_OK(ncclGroupStart());
     if (c->rank > 0) {
-        NCCL_OK(ncclSend(v + own_first, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
-        NCCL_OK(ncclRecv(v + own_first - cnt, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
+        ops.push_back({true, v + own_first, cnt, c->rank - 1});
+        ops.push_back({false, v + own_first - cnt, cnt, c->rank - 1});
     }
     if (c->rank < c->nranks - 1) {
-        NCCL_OK(ncclSend(v + own_end - cnt, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
-        NCCL_OK(ncclRecv(v + own_end, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
+        ops.push_back({true, v + own_end - cnt, cnt, c->rank + 1});
+        ops.push_back({false, v + own_end, cnt, c->rank + 1});
     }
-    NCCL_OK(ncclGroupEnd());
+}
+
+static int run_local(iemic_ctx* c, const std::vector<P2P>& ops)
+{
+    LocalGroup* g = (LocalGroup*)c->group;
+    std::map<int, int> ksend, krecv;
+    for (const P2P& op : ops) {
+        if (!op.send) continue;
+        std::vector<double> h((size_t)op.cnt);
+        int rc = d2h(c, h.data(), op.buf, sizeof(double) * h.size());
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->box[std::make_tuple(c->rank, op.peer, ksend[op.peer]++)] = std::move(h);
+    }
+    g->barrier();
+    for (const P2P& op : ops) {
+        if (op.send) continue;
+        std::vector<double> h;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            auto it = g->box.find(std::make_tuple(op.peer, c->rank, krecv[op.peer]++));
+            if (it == g->box.end() || (int64_t)it->second.size() != op.cnt) {
+                set_error("band group: unmatched receive");
+                return IEMIC_EINVAL;
+            }
+            h = std::move(it->second);
+            g->box.erase(it);
+        }
+        int rc = h2d(c, op.buf, h.data(), sizeof(double) * h.size());
+        if (rc) return rc;
+    }
+    g->barrier();
     return 0;
+}
+
+static int run_ops(iemic_ctx* c, const std::vector<P2P>& ops)
+{
+    if (c->group) return run_local(c, ops);
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    ncclResult_t first = ncclSuccess;
+    std::string what;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+        return IEMIC_EDEVICE;
+    }
+    for (const P2P& op : ops) {
+        r = op.send ? ncclSend(op.buf, (size_t)op.cnt, ncclDouble, op.peer, comm, c->stream)
+                    : ncclRecv(op.buf, (size_t)op.cnt, ncclDouble, op.peer, comm, c->stream);
+        if (r != ncclSuccess && first == ncclSuccess) {
+            first = r;
+            what = op.send ? "ncclSend" : "ncclRecv";
+        }
+    }
+    /* the group is always closed, also after a failed enqueue, so the communicator stays
+     * usable for the peers' matching calls and later collectives */
+    r = ncclGroupEnd();
+    if (first == ncclSuccess && r != ncclSuccess) {
+        first = r;
+        what = "ncclGroupEnd";
+    }
+    if (first != ncclSuccess) {
+        set_error(what + ": " + ncclGetErrorString(first));
+        return IEMIC_EDEVICE;
+    }
+    return 0;
+}
+
+int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
+{
+    if (c->nranks <= 1) return 0;
+    std::vector<P2P> ops;
+    halo_ops(c, v, width, rows_j, ops);
+    return run_ops(c, ops);
 }
 
 int halo_exchange_pair(iemic_ctx* c, double* a, double* b)
 {
     if (c->nranks <= 1) return 0;
-    if (c->group) {
-        int rc = local_halo(c, a, 1, 1);
-        return rc ? rc : local_halo(c, b, 1, 1);
-    }
-    const int64_t cnt = (int64_t)c->l * c->n;                   /* one latitude row */
-    const int64_t own_first = c->own0, own_end = own_first + c->nloc;
-    ncclComm_t comm = (ncclComm_t)c->comm;
-    NCCL_OK(ncclGroupStart());
-    for (double* v : {a, b}) {
-        if (c->rank > 0) {
-            NCCL_OK(ncclSend(v + own_first, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
-            NCCL_OK(ncclRecv(v + own_first - cnt, (size_t)cnt, ncclDouble, c->rank - 1, comm, c->stream));
-        }
-        if (c->rank < c->nranks - 1) {
-            NCCL_OK(ncclSend(v + own_end - cnt, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
-            NCCL_OK(ncclRecv(v + own_end, (size_t)cnt, ncclDouble, c->rank + 1, comm, c->stream));
-        }
-    }
-    NCCL_OK(ncclGroupEnd());
-    return 0;
+    std::vector<P2P> ops;
+    halo_ops(c, a, 1, 1, ops);
+    halo_ops(c, b, 1, 1, ops);
+    return run_ops(c, ops);
 }
 
 /* state-vector halo (NUN doubles per cell) */

@@ -151,6 +151,7 @@ struct iemic_ctx {
     int64_t next = 0, nerows = 0;    /* cells / rows of an ext vector (band + 2 HALO)     */
     int64_t own0 = 0;                /* ext cell of the first owned cell                  */
     int64_t rowintcon = -1;          /* ext row of the integral condition if owned        */
+    double int_correction = 0.0;     /* THCM::intCorrection_ (setIntCondCorrection)      */
     void* comm = nullptr;            /* ncclComm_t when nranks > 1                        */
     void* group = nullptr;           /* in-process band group (test facility), else null  */
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
@@ -219,6 +220,7 @@ void comm_destroy(iemic_ctx* c);
 int assemble_jacobian(iemic_ctx* c, const double* x_dev);
 int assemble_rhs(iemic_ctx* c, const double* x_dev, double* F_dev);
 int compute_forcing(iemic_ctx* c);
+int intcond_correction(iemic_ctx* c, const double* x_dev);
 /* krylov.hip */
 /* y = J x on the owned rows; x (ext layout) gets its halo rows exchanged first */
 int spmv(iemic_ctx* c, double* x, double* y, hipStream_t s);

@@ -1149,7 +1149,12 @@ HD void diagB_cell(const Geo& g, int i, int j, int k, double* b)
  * ftab = [wfun(yv) (m+2) | temfun(y) (m+2) | salfun(y) (m+2) | spert (n*m)]          */
 HD void forcing_qint(const Geo& g, const double* ftab, double* qcor, int need_t, int need_s)
 {
-    /* qint (forcing.F90:536-548 -> THCM.C:2704-2737): sequential, reference order */
+    /* qint (forcing.F90:536-548 -> THCM.C:2704-2737): sequential, reference order; the
+     * corrections are used only with TRES = 0 or SRES = 0 (zero otherwise) */
+    if (!need_t && !need_s) {
+        qcor[0] = qcor[1] = qcor[2] = qcor[3] = 0.0;
+        return;
+    }
     const int n = g.n, m = g.m, l = g.l;
     const double* temf = ftab + (m + 2);
     const double* salf = ftab + 2 * (m + 2);

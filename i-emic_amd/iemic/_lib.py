@@ -128,7 +128,8 @@ def lib():
 EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",
-            "iemic_set_par", "iemic_get_par", "iemic_nrows", "iemic_graph_nnz",
+            "iemic_set_par", "iemic_get_par", "iemic_set_intcond_correction",
+            "iemic_get_intcond_correction", "iemic_nrows", "iemic_graph_nnz",
             "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",

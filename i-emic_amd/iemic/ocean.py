@@ -104,6 +104,19 @@ class Ocean:
         check(lib().iemic_get_par(self._h, idx, C.byref(v)), "iemic_get_par")
         return v.value
 
+    def setIntCondCorrection(self, x: Optional[np.ndarray] = None) -> float:
+        """THCM::setIntCondCorrection (THCM.C:2020-2038): the integral-condition entry of F
+        becomes intSign (coeff . x - coeff . x0) with x0 = x (default: the current state),
+        as Ocean does for a loaded SRES = 0 state (Ocean.C:144-148).  Returns it."""
+        xp = None
+        if x is not None:
+            x = np.ascontiguousarray(x, dtype=np.float64)
+            xp = ptr(x)
+        check(lib().iemic_set_intcond_correction(self._h, xp), "iemic_set_intcond_correction")
+        v = C.c_double()
+        check(lib().iemic_get_intcond_correction(self._h, C.byref(v)), "iemic_get_intcond_correction")
+        return v.value
+
     # ---- state --------------------------------------------------------------------
     def setState(self, x: np.ndarray) -> None:
         x = np.ascontiguousarray(x, dtype=np.float64)

@@ -129,6 +129,12 @@ const char* iemic_last_error(void);
 
 /* ---- parameters (setparcs_/getparcs_, usrc.F90:163-198; index 1..30 = par2int) --- */
 int  iemic_set_par(iemic_ctx* ctx, int idx, double value);
+/* THCM::setIntCondCorrection (THCM.C:2020-2038, called by Ocean at Ocean.C:144-148 for a
+ * loaded SRES = 0 state): intCorrection = intcond coefficients . x, subtracted from the
+ * integral-condition entry of F from then on.  x: global state in reference order, or NULL
+ * for the current state.  No-op (correction 0) when SRES != 0. */
+int  iemic_set_intcond_correction(iemic_ctx* ctx, const double* x);
+int  iemic_get_intcond_correction(iemic_ctx* ctx, double* corr);
 int  iemic_get_par(iemic_ctx* ctx, int idx, double* value);
 
 /* ---- geometry queries ------------------------------------------------------------ */

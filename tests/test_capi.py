@@ -73,9 +73,15 @@ def test_no_gpu_fails_loudly(built):
         Ocean(c)
 
 
-def test_mixing_not_silently_ignored(built):
+@pytest.mark.gpu
+def test_unrestated_mixing_rejected(built):
+    """Mixing parameters outside the restated vmix_fun subset (here MIXP != 0: neutral
+    physics) are refused loudly, not silently ignored."""
     if built.iemic_device_count() <= 0:
         pytest.skip("needs a device to reach the configuration check")
     from iemic.ocean import Ocean
-    with pytest.raises(_lib.IemicError, match="Mixing"):
-        Ocean(cf.preset("test6x6x4", mixing=1))
+    c = cf.preset("test6x6x4", mixing=1)
+    oc = Ocean(c)
+    oc.setPar("MIXP", 1.0)
+    with pytest.raises(_lib.IemicError, match="neutral physics"):
+        oc.computeRHS()

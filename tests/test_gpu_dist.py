@@ -208,16 +208,30 @@ def _rccl_worker(rank, nranks, port, q):
         from iemic.ocean import Ocean
         ids = [Ocean.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, 0)
-        c = cf.preset("natl8", mixing=0)
-        Ocean(c, landm=golden_landm("natl8"), rank=rank, nranks=nranks, comm_id=ids[0]).close()
-        q.put((rank, "ok"))
+        c = cf.preset("gateway16", mixing=0)
+        L0 = golden_landm("gateway16")
+        oc = Ocean(c, landm=L0, device=rank, rank=rank, nranks=nranks, comm_id=ids[0],
+                   solver_params={"FGMRES tolerance": 1e-10})
+        L = oc.landmask().reshape(c.l + 2, c.m + 2, c.n + 2)
+        x = cf.synthetic_state(c, L, amp_ts=1e-3)
+        v = cf.synthetic_vector(c, seed=5)
+        oc.setState(x)
+        oc.computeJacobian()
+        y = oc.applyMatrix(v)
+        sol = oc.solve(y)
+        lay = oc.layout()
+        q.put((rank, {"jb": (lay["jb0"], lay["jb1"]), "y": y, "sol": sol, "x": x, "v": v,
+                      "converged": oc.last_solve.converged}))
+        oc.close()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_rccl_ranks():
+def test_rccl_ranks(oracle_lib):
+    """Two ranks, one GPU each, over RCCL: J (through J v), the halo exchanges and the
+    Krylov all-reduces of a solve; the gathered owned rows match the oracle."""
     import torch
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
@@ -229,4 +243,22 @@ def test_rccl_ranks():
     out = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(60)
-    assert all(v == "ok" for v in out.values()), out
+    assert all(isinstance(v, dict) for v in out.values()), out
+    c = cf.preset("gateway16", mixing=0)
+    L = mask_fix(oracle_lib, c, golden_landm("gateway16"))
+    o = oracle_lib.Oracle(c.ref_dict(), L, c.par_list())
+    x, v = out[0]["x"], out[0]["v"]
+    ov, _ = o.jacobian(x)
+    yref = o.spmv(ov, v)
+    y = np.zeros(c.nrows)
+    xs = np.zeros(c.nrows)
+    for r in out.values():
+        jb0, jb1 = r["jb"]
+        rows = np.array([6 * ((k * c.m + j) * c.n + i) + qv for k in range(c.l)
+                         for j in range(jb0, jb1) for i in range(c.n) for qv in range(6)])
+        y[rows] = r["y"][rows]
+        xs[rows] = r["sol"][rows]
+        assert r["converged"] == 1
+    assert np.max(np.abs(y - yref)) <= 1e-13 * np.abs(ov).max() * np.abs(v).max()
+    lin = np.linalg.norm(yref - o.spmv(ov, xs)) / np.linalg.norm(yref)
+    assert lin <= 1e-8, lin

@@ -319,3 +319,25 @@ def test_newton_step(oracle_lib, Ocean, name, prec):
     lin = np.linalg.norm(F0 + o.spmv(ov, x1 - x)) / np.linalg.norm(F0)
     assert info.solve.converged == 1
     assert lin <= 1e-8
+
+
+def test_intcond_correction(oracle_lib, Ocean):
+    """THCM::setIntCondCorrection on an SRES = 0 grid: the integral-condition entry of F
+    becomes intSign (coeff . x - coeff . x0); every other entry is unchanged."""
+    c, oc, o, L = make(Ocean, oracle_lib, "natl8")
+    ric = oc.rowintcon
+    assert ric >= 0
+    x0 = cf.synthetic_state(c, L, amp_ts=1e-3)
+    corr = oc.setIntCondCorrection(x0)
+    coeff = o.intcond_coeff()
+    assert abs(corr - coeff @ x0) <= 1e-13 * np.abs(coeff) @ np.abs(x0)
+    x = cf.synthetic_state(c, L, seed=99, amp_ts=1e-3)
+    oc.setState(x)
+    F = oc.computeRHS()
+    oF = o.rhs(x)
+    keep = np.ones(c.nrows, bool)
+    keep[ric] = False
+    np.testing.assert_array_equal(F[keep], oF[keep])
+    sign = o.d["int_sign"]
+    assert abs(F[ric] - (oF[ric] - sign * corr)) <= 1e-12 * max(1.0, abs(oF[ric]))
+    assert abs(oc.setIntCondCorrection() - coeff @ x) <= 1e-12 * np.abs(coeff) @ np.abs(x)
