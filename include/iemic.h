@@ -54,7 +54,7 @@ typedef struct {
     int tres, sres;              /* "Restoring Temperature/Salinity Profile"         */
     int forcing_type;            /* "Forcing Type"                                   */
     int ih;                      /* "Inhomogeneous Mixing"                           */
-    int vmix;                    /* "Mixing" (only 0 implemented: SURVEY §8f row 1)  */
+    int vmix;                    /* "Mixing" (vmix_GLB): 0, 1 or 2, default vmix_par   */
     int coriolis_on;             /* "Coriolis Force"                                 */
     double alpha_t, alpha_s;     /* "Linear EOS: alpha T/S"                          */
     int int_sign;                /* "Salinity Integral Sign"                         */
