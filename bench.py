@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--restarts", type=int, default=20)
     p.add_argument("--ts-sweeps", type=int, default=12)
     p.add_argument("--orth", default="DCGS2", choices=["DCGS2", "DGKS"])
+    p.add_argument("--solver", default="FGMRES", choices=["FGMRES", "IDR"],
+                   help="Krylov method (IDR: IDRSolver.H's IDR(s), --idr-s)")
+    p.add_argument("--idr-s", type=int, default=4)
     p.add_argument("--dyn-iters", type=int, default=4,
                    help="defect-correction passes on the dynamics block of the block GS")
     p.add_argument("--dyn-omega", type=float, default=0.95, help="step of the correction passes")
@@ -141,7 +144,8 @@ def main():
           "TS sweeps": args.ts_sweeps, "Orthogonalization": args.orth,
           "Dyn iterations": args.dyn_iters,
           "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
-          "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps}
+          "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps,
+          "Solver": args.solver, "IDR s": args.idr_s}
     comm_id = None
     if world > 1:
         idt = torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -246,6 +250,7 @@ def main():
                                f"step (F, J, prec, FGMRES tol {args.tol:g}, update, F)",
                    "rows": cfg.nrows, "nnz": nnz, "prec": args.prec,
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
+                   "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
                    "schur": "cyclic reduction (fp64, exact)",
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps,

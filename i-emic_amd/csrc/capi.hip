@@ -485,7 +485,7 @@ extern "C" int iemic_solve_dev(iemic_ctx* c, const double* b, double* x, const i
 {
     CTX_CHECK(c);
     if (!opt) return IEMIC_EINVAL;
-    return fgmres(c, b, x, opt, info);
+    return krylov_solve(c, b, x, opt, info);
 }
 
 extern "C" int iemic_solve(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
@@ -497,7 +497,7 @@ extern "C" int iemic_solve(iemic_ctx* c, const double* b, double* x, const iemic
     if (db.alloc(c->nerows) || dx.alloc(c->nerows)) return IEMIC_ENOMEM;
     int rc = put_ref(c, b, db.p);
     if (rc) return rc;
-    if ((rc = fgmres(c, db.p, dx.p, opt, info))) return rc;
+    if ((rc = krylov_solve(c, db.p, dx.p, opt, info))) return rc;
     return get_ref(c, dx.p, x);
 }
 
@@ -546,7 +546,7 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     inf.t_prec_ms = ms(t);
     hipLaunchKernelGGL(k_neg, dim3(G), dim3(256), 0, c->stream, c->d_F.p + o, c->d_tmp1.p + o, NL);
     t = clk::now();
-    if ((rc = fgmres(c, c->d_tmp1.p, c->d_tmp2.p, opt, &inf.solve))) return rc;
+    if ((rc = krylov_solve(c, c->d_tmp1.p, c->d_tmp2.p, opt, &inf.solve))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     inf.t_solve_ms = ms(t);
     hipLaunchKernelGGL(k_newton_update, dim3(G), dim3(256), 0, c->stream, c->d_x.p + o, c->d_tmp2.p + o, NL);

@@ -226,6 +226,10 @@ int intcond_correction(iemic_ctx* c, const double* x_dev);
 int spmv(iemic_ctx* c, double* x, double* y, hipStream_t s);
 int spmv_kernel(iemic_ctx* c, const double* x, double* y);
 double dot(iemic_ctx* c, const double* a, const double* b, int64_t n);
+int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info);
+/* opt->method: 0 FGMRES, 1 IDR(s) */
+int krylov_solve(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
+                 iemic_solve_info* info);
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
            iemic_solve_info* info);
 /* prec.hip */

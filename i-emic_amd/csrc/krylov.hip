@@ -905,3 +905,268 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
 }
 
 }  // namespace iemic
+
+/* ---- IDR(s) (src/idrsolver/IDRSolver.H:109-340, van Gijzen & Sonneveld) -------------- */
+namespace iemic {
+
+/* y = a y + sum_i c_i X_i (i < nv <= 16), coefficients by value */
+struct LinComb {
+    int nv;
+    double a;
+    double c[16];
+    const double* X[16];
+};
+__global__ void __launch_bounds__(256) k_lincomb(LinComb L, double* __restrict__ y, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = L.a == 0.0 ? 0.0 : L.a * y[q];
+        for (int i = 0; i < L.nv; i++) acc += L.c[i] * L.X[i][q];
+        y[q] = acc;
+    }
+}
+
+/* the IDR shadow space P: s vectors uniform in [-1, 1] from splitmix64 over the global
+ * row index (identical for every band split), orthonormalised (IDRSolver::createP) */
+__global__ void k_idr_random(double* __restrict__ P, int64_t ldp, int s, int64_t NL, int64_t row0,
+                             int n, int m, int l, int jb0)
+{
+    const int64_t lr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lr >= NL) return;
+    /* owned row -> global reference row 6((k m + j) n + i) + v */
+    const int64_t lc = lr / NUN;
+    const int v = (int)(lr % NUN);
+    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    const uint64_t g = (uint64_t)(NUN * (((int64_t)k * m + j) * n + i) + v);
+    for (int q = 0; q < s; q++) {
+        uint64_t z = 0x9E3779B97F4A7C15ull * (g * 16 + (uint64_t)q + 1) + 20261015ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        P[(int64_t)q * ldp + row0 + lr] = 2.0 * ((double)(z >> 11) * (1.0 / 9007199254740992.0)) - 1.0;
+    }
+}
+
+static void lincomb(iemic_ctx* c, double a, double* y, std::initializer_list<std::pair<double, const double*>> terms,
+                    int64_t o, int64_t NL)
+{
+    LinComb L{};
+    L.a = a;
+    for (auto& t : terms) {
+        if (L.nv == 16) break;
+        L.c[L.nv] = t.first;
+        L.X[L.nv] = t.second + o;
+        L.nv++;
+    }
+    hipLaunchKernelGGL(k_lincomb, dim3(grid_for(NL)), dim3(256), 0, c->stream, L, y + o, NL);
+}
+static void lincomb_v(iemic_ctx* c, double a, double* y, const std::vector<double>& cs,
+                      const std::vector<const double*>& xs, int64_t o, int64_t NL)
+{
+    LinComb L{};
+    L.a = a;
+    for (size_t q = 0; q < cs.size() && q < 16; q++) {
+        L.c[L.nv] = cs[q];
+        L.X[L.nv] = xs[q] + o;
+        L.nv++;
+    }
+    hipLaunchKernelGGL(k_lincomb, dim3(grid_for(NL)), dim3(256), 0, c->stream, L, y + o, NL);
+}
+
+int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
+{
+    const int s = std::max(1, std::min(opt->idr_s > 0 ? opt->idr_s : 4, 8));
+    const double angle = opt->idr_angle > 0.0 ? opt->idr_angle : 0.7;
+    const double mp = 1e-13;
+    const int maxit = std::max(1, opt->krylov_dim * (opt->max_restarts + 1));
+    const int64_t NE = c->nerows, o = NUN * c->own0, NL = c->nlrows;
+    /* vectors: P (s) | U (s) | G (s) | t | r | v  in the Krylov basis storage */
+    int rc = ensure_krylov(c, 3 * s + 3);
+    if (rc) return rc;
+    iemic_solve_info inf{};
+    auto T0 = std::chrono::steady_clock::now();
+    double* base = c->kr.V.p;
+    double* P = base;
+    double* U = base + (int64_t)s * NE;
+    double* G = base + (int64_t)2 * s * NE;
+    double* t = base + (int64_t)3 * s * NE;
+    double* r = t + NE;                          /* t, r adjacent: one multi-dot for omega */
+    double* v = r + NE;
+    auto Ui = [&](int i) { return U + (int64_t)i * NE; };
+    auto Gi = [&](int i) { return G + (int64_t)i * NE; };
+    auto Pi = [&](int i) { return P + (int64_t)i * NE; };
+    const unsigned GR = grid_for(NL);
+    /* shadow space (createP: random, orthonormalised in order) */
+    hipLaunchKernelGGL(k_idr_random, dim3((unsigned)((NL + 255) / 256)), dim3(256), 0, c->stream, P, NE, s, NL,
+                       o, c->n, c->m, c->l, c->jb0);
+    for (int j = 0; j < s; j++) {
+        std::vector<double> al(j + 1);
+        if (j > 0 && (rc = mdot_host(c, P + o, NE, j, Pi(j) + o, al.data()))) return rc;
+        std::vector<double> cs;
+        std::vector<const double*> xs;
+        for (int k = 0; k < j; k++) { cs.push_back(-al[k]); xs.push_back(Pi(k)); }
+        if (j > 0) lincomb_v(c, 1.0, Pi(j), cs, xs, o, NL);
+        const double nn = sqrt0(dot(c, Pi(j), Pi(j), 0));
+        if (!(nn > 0.0)) return nonfinite();
+        hipLaunchKernelGGL(k_scale_copy, dim3(GR), dim3(256), 0, c->stream, Pi(j) + o, 1.0 / nn, Pi(j) + o, NL);
+    }
+    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
+    HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
+    const double normb = sqrt0(dot(c, b, b, 0));
+    if (!std::isfinite(normb)) return nonfinite();
+    if (!(normb > 0.0)) {
+        inf.converged = 1;
+        if (info) *info = inf;
+        return 0;
+    }
+    const double tolb = opt->tol * normb;
+    double normr = normb;
+    std::vector<double> f(s, 0.0), gamma(s, 0.0), d(s + 2, 0.0);
+    std::vector<std::vector<double>> M(s, std::vector<double>(s, 0.0));
+    double om = 1.0;
+    int jj = 0, iter = 0;
+    bool trueres = false;
+    hipEvent_t e0, e1, e2;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventCreate(&e2));
+    struct Ev { hipEvent_t a, b, c2; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c2); } } evg{e0, e1, e2};
+    auto prec = [&](const double* in, double* out) -> int {
+        HIP_OK(hipEventRecord(e0, c->stream));
+        int r2 = 0;
+        if (opt->prec > 0) r2 = prec_apply(c, in, out);
+        else HIP_OK(hipMemcpyAsync(out, in, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
+        HIP_OK(hipEventRecord(e1, c->stream));
+        return r2;
+    };
+    auto matvec = [&](double* in, double* out) -> int {
+        int r2 = spmv(c, in, out, c->stream);
+        HIP_OK(hipEventRecord(e2, c->stream));
+        HIP_OK(hipEventSynchronize(e2));
+        float a1 = 0.f, a2 = 0.f;
+        (void)hipEventElapsedTime(&a1, e0, e1);
+        (void)hipEventElapsedTime(&a2, e1, e2);
+        inf.t_prec_ms += a1;
+        inf.t_spmv_ms += a2;
+        inf.n_spmv++;
+        return r2;
+    };
+    while (normr > tolb && iter < maxit) {
+        if ((rc = mdot_host(c, P + o, NE, s, r + o, f.data()))) return rc;      /* f = P' r */
+        for (int k = 0; k < s; k++) {
+            if (jj > 0) {
+                /* gamma from the lower-triangular M(k:s, k:s); v = r - G(:, k:s) gamma */
+                std::vector<double> cs;
+                std::vector<const double*> xs;
+                for (int i = k; i < s; i++) {
+                    double gi = f[i];
+                    for (int j = k; j < i; j++) gi -= M[i][j] * gamma[j];
+                    gamma[i] = gi / M[i][i];
+                    cs.push_back(-gamma[i]);
+                    xs.push_back(Gi(i));
+                }
+                HIP_OK(hipMemcpyAsync(v, r, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
+                lincomb_v(c, 1.0, v, cs, xs, o, NL);
+                if ((rc = prec(v, t))) return rc;
+                /* U(:,k) = om t + U(:, k:s) gamma */
+                cs.clear();
+                xs.clear();
+                cs.push_back(om);
+                xs.push_back(t);
+                for (int i = k; i < s; i++) { cs.push_back(gamma[i]); xs.push_back(Ui(i)); }
+                lincomb_v(c, 0.0, Ui(k), cs, xs, o, NL);
+            } else {
+                if ((rc = prec(r, Ui(k)))) return rc;                           /* initial space */
+            }
+            if ((rc = matvec(Ui(k), Gi(k)))) return rc;                          /* G(:,k) = A U(:,k) */
+            /* bi-orthogonalise against P(:, 0:k) (the modified Gram-Schmidt of the reference
+             * restated as one multi-dot + forward substitution) and the new column of M */
+            if ((rc = mdot_host(c, P + o, NE, s, Gi(k) + o, d.data()))) return rc;
+            std::vector<double> al(k, 0.0);
+            for (int i = 0; i < k; i++) {
+                double a = d[i];
+                for (int j = 0; j < i; j++) a -= al[j] * M[i][j];
+                al[i] = a / M[i][i];
+            }
+            for (int i = k; i < s; i++) {
+                double mik = d[i];
+                for (int j = 0; j < k; j++) mik -= al[j] * M[i][j];
+                M[i][k] = mik;
+            }
+            if (k > 0) {
+                std::vector<double> cs;
+                std::vector<const double*> xg, xu;
+                for (int i = 0; i < k; i++) { cs.push_back(-al[i]); xg.push_back(Gi(i)); xu.push_back(Ui(i)); }
+                lincomb_v(c, 1.0, Gi(k), cs, xg, o, NL);
+                lincomb_v(c, 1.0, Ui(k), cs, xu, o, NL);
+            }
+            if (!std::isfinite(M[k][k])) return nonfinite();
+            if (M[k][k] == 0.0) {
+                set_error("IDR(s): breakdown (M[k][k] == 0)");
+                return IEMIC_ERANGE;
+            }
+            const double beta = f[k] / M[k][k];
+            lincomb(c, 1.0, r, {{-beta, Gi(k)}}, o, NL);                         /* r -= beta G */
+            lincomb(c, 1.0, x, {{beta, Ui(k)}}, o, NL);                          /* x += beta U */
+            normr = sqrt0(dot(c, r, r, 0));
+            if (!std::isfinite(normr)) return nonfinite();
+            if (opt->idr_replace && normr > tolb / mp) trueres = true;
+            for (int i = k + 1; i < s; i++) f[i] -= beta * M[i][k];
+            iter++;
+            if (normr < tolb || iter >= maxit) break;
+        }
+        if (normr < tolb || iter >= maxit) break;
+        jj++;
+        /* first residual of G_{j+1}: v = M^-1 r, t = A v, omega, r -= om t, x += om v */
+        if ((rc = prec(r, v))) return rc;
+        if ((rc = matvec(v, t))) return rc;
+        double tt_tr[2];
+        if ((rc = mdot_host(c, t + o, NE, 2, t + o, tt_tr))) return rc;       /* t.t, r.t */
+        const double nt = sqrt0(tt_tr[0]), ts = tt_tr[1];
+        if (!(nt > 0.0) || !std::isfinite(ts)) return nonfinite();
+        const double rho = std::fabs(ts / (nt * normr));
+        om = ts / (nt * nt);
+        if (rho < angle) om = om * angle / rho;                                 /* calc_omega */
+        lincomb(c, 1.0, r, {{-om, t}}, o, NL);
+        lincomb(c, 1.0, x, {{om, v}}, o, NL);
+        normr = sqrt0(dot(c, r, r, 0));
+        if (!std::isfinite(normr)) return nonfinite();
+        if (opt->idr_replace && normr > tolb / mp) trueres = true;
+        if (trueres && normr < normb) {
+            /* residual replacement: r = b - A x */
+            if ((rc = spmv(c, x, r, c->stream))) return rc;
+            hipLaunchKernelGGL(k_axpby, dim3(GR), dim3(256), 0, c->stream, 1.0, b + o, -1.0, r + o, r + o, NL);
+            normr = sqrt0(dot(c, r, r, 0));
+            trueres = false;
+            inf.reorth++;
+        }
+        iter++;
+    }
+    /* explicit residual */
+    if ((rc = spmv(c, x, t, c->stream))) return rc;
+    hipLaunchKernelGGL(k_axpby, dim3(GR), dim3(256), 0, c->stream, 1.0, b + o, -1.0, t + o, t + o, NL);
+    const double e2v = dot(c, t, t, 0);
+    inf.iters = iter;
+    inf.implicit_rel_res = normr / normb;
+    inf.explicit_rel_res = sqrt0(e2v) / normb;
+    inf.converged = normr <= tolb && inf.explicit_rel_res <= 2.0 * opt->tol;
+    inf.t_total_ms = ms_since(T0);
+    inf.t_orth_ms = std::max(0.0, inf.t_total_ms - inf.t_prec_ms - inf.t_spmv_ms);
+    HIP_OK(hipGetLastError());
+    if (info) *info = inf;
+    return 0;
+}
+
+}  // namespace iemic
+
+namespace iemic {
+int krylov_solve(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
+{
+    if (opt->method == 1) return idrs(c, b, x, opt, info);
+    if (opt->method != 0) {
+        set_error("krylov: unknown method");
+        return IEMIC_EINVAL;
+    }
+    return fgmres(c, b, x, opt, info);
+}
+}  // namespace iemic

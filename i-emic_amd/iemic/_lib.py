@@ -38,8 +38,9 @@ class Dist(C.Structure):
 class Krylov(C.Structure):
     _fields_ = [("tol", C.c_double), ("krylov_dim", C.c_int), ("max_restarts", C.c_int),
                 ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int),
-                ("dyn_iters", C.c_int), ("reserved0", C.c_int), ("ts_mg", C.c_int),
-                ("mg_sweeps", C.c_int), ("dyn_omega", C.c_double), ("dyn_mr", C.c_int)]
+                ("dyn_iters", C.c_int), ("method", C.c_int), ("ts_mg", C.c_int),
+                ("mg_sweeps", C.c_int), ("dyn_omega", C.c_double), ("dyn_mr", C.c_int),
+                ("idr_s", C.c_int), ("idr_angle", C.c_double), ("idr_replace", C.c_int)]
 
 
 class SolveInfo(C.Structure):

@@ -56,6 +56,7 @@ class Ocean:
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
               "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
+              "Solver": "FGMRES", "IDR s": 4, "IDR angle": 0.7, "IDR replace residuals": False,
               "Multigrid sweeps": 1}
         if solver_params:
             sp.update(solver_params)
@@ -161,9 +162,11 @@ class Ocean:
         return _lib.Krylov(float(sp["FGMRES tolerance"]), int(sp["FGMRES iterations"]),
                            int(sp["FGMRES restarts"]), int(sp["Preconditioner"]),
                            int(sp["TS sweeps"]), 1 if sp["Orthogonalization"] == "DGKS" else 0,
-                           int(sp["Dyn iterations"]), 0,
+                           int(sp["Dyn iterations"]), 1 if str(sp["Solver"]).upper() == "IDR" else 0,
                            int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]),
-                           float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])))
+                           float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])),
+                           int(sp["IDR s"]), float(sp["IDR angle"]),
+                           int(bool(sp["IDR replace residuals"])))
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""

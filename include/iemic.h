@@ -75,8 +75,8 @@ typedef struct {
     int orth;                    /* 0: DCGS2 (default), 1: DGKS (Belos' default)     */
     int dyn_iters;               /* block GS: defect-correction passes on the U/V/W/P */
                                  /* block (<= 1: one pass, the plain block GS)        */
-    int reserved0;               /* unused (was the fp32 Schur inverse; the Schur     */
-                                 /* solve is now an exact fp64 cyclic reduction)      */
+    int method;                  /* 0: FGMRES (Belos, Ocean.C:961-1137), 1: IDR(s)    */
+                                 /* (IDRSolver.H:109-340, right preconditioned)       */
     int ts_mg;                   /* block GS: T/S solve by this many aggregation-      */
                                  /* multigrid V-cycles (0: ts_sweeps plain sweeps)    */
     int mg_sweeps;               /* symmetric red-black sweeps before/after the coarse */
@@ -84,6 +84,9 @@ typedef struct {
     double dyn_omega;            /* block GS: step of the defect-correction passes    */
                                  /* (z_D += omega M_D^-1 d; 0 means 1)                */
     int dyn_mr;                  /* 1: minimal-residual step per pass instead         */
+    int idr_s;                   /* "IDR s" (default 4)                               */
+    double idr_angle;            /* "IDR angle" (omega safeguard, default 0.7)         */
+    int idr_replace;             /* "IDR replace residuals" (default 0)               */
 } iemic_krylov;
 
 typedef struct {

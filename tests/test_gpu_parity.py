@@ -341,3 +341,37 @@ def test_intcond_correction(oracle_lib, Ocean):
     sign = o.d["int_sign"]
     assert abs(F[ric] - (oF[ric] - sign * corr)) <= 1e-12 * max(1.0, abs(oF[ric]))
     assert abs(oc.setIntCondCorrection() - coeff @ x) <= 1e-12 * np.abs(coeff) @ np.abs(x)
+
+
+@pytest.mark.parametrize("name,s", [("natl8", 4), ("gateway16", 4), ("global4", 4), ("global4", 8)])
+def test_idr_solve(oracle_lib, Ocean, name, s):
+    """IDR(s) (IDRSolver.H:109-340) with the block-GS preconditioner: the solution meets the
+    tolerance on the oracle's J, and the reported explicit residual is the true one."""
+    c, oc, o, L = make(Ocean, oracle_lib, name,
+                       solver_params={"Solver": "IDR", "IDR s": s, "FGMRES tolerance": 1e-8,
+                                      "FGMRES iterations": 1000, "FGMRES restarts": 0})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    ov, _ = o.jacobian(x)
+    b = o.spmv(ov, cf.synthetic_vector(c, seed=5))
+    sol = oc.solve(b)
+    res = np.linalg.norm(b - o.spmv(ov, sol)) / np.linalg.norm(b)
+    assert oc.last_solve.converged == 1, (oc.last_solve.iters, res)
+    assert res <= 2e-8
+    assert abs(oc.last_solve.explicit_rel_res - res) <= 1e-9
+
+
+def test_idr_newton_step_global2(oracle_lib, Ocean):
+    """The bench's Newton step (2 degrees, Mixing = 1) with IDR(4) instead of FGMRES."""
+    c, oc, o, L = make(Ocean, oracle_lib, "global2", mixing=1,
+                       solver_params={"Solver": "IDR", "IDR s": 4, "FGMRES tolerance": 1e-8,
+                                      "FGMRES iterations": 2000, "FGMRES restarts": 0})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    info = oc.newtonStep()
+    F0 = o.rhs(x)
+    ov, _ = o.jacobian(x)
+    lin = np.linalg.norm(F0 + o.spmv(ov, oc.getState() - x)) / np.linalg.norm(F0)
+    assert info.solve.converged == 1 and lin <= 2e-8, (info.solve.iters, lin)
+    print(f"IDR(4) global2 Newton step: {info.solve.iters} iterations, {info.t_total_ms:.0f} ms")
