@@ -194,6 +194,105 @@ __global__ void __launch_bounds__(384) k_spmv6(int n, int m, int l, int periodic
     y[NUN * ((int64_t)HALO * l * n + lc) + R] = acc;
 }
 
+
+/* ---- k_spmv7: LDS-staged x, slot-balanced waves ----------------------------------------
+ * One workgroup (4 waves) per tile of up to 64 cells along i of one (j, k) grid row.  The
+ * x values of the tile's neighbourhood -- the six (dj, dk) grid rows the slot table reaches
+ * ((0,0), (+-1,0), (0,+-1), (+1,-1)), cells i0-1 .. i0+64, all six unknowns -- are copied
+ * into LDS with contiguous loads, so the 104 gathers per cell become LDS reads.  The 104
+ * slots are split into four runs of 26 (one per wave: U+V, V+W, W+P+T, T+S) instead of one
+ * wave per equation (24/22/7/11/20/20), so the waves of a tile finish together; their row
+ * partials meet in LDS and the 384 results of the tile are stored contiguously. */
+constexpr int SP7_T = 64;
+__host__ __device__ constexpr int sp7_row(int s)
+{
+    return s < 24 ? 0 : s < 46 ? 1 : s < 53 ? 2 : s < 64 ? 3 : s < 84 ? 4 : 5;
+}
+__host__ __device__ constexpr int sp7_combo(int dj, int dk)
+{
+    return dk == 0 ? (dj + 1) : (dk == -1 ? (dj == 0 ? 3 : 5) : 4);  /* (-1,0)0 (0,0)1 (1,0)2 (0,-1)3 (0,1)4 (1,-1)5 */
+}
+template <int S0, int S1>
+__device__ __forceinline__ void sp7_load(const double* __restrict__ val, int64_t nloc, int64_t lc, bool act,
+                                         double* v)
+{
+#pragma unroll
+    for (int s = S0; s < S1; s++) v[s - S0] = act ? val[(int64_t)s * nloc + lc] : 0.0;
+}
+template <int S0, int S1>
+__device__ __forceinline__ void sp7_compute(const double* v, const double* xs, int c, double* acc)
+{
+#pragma unroll
+    for (int s = S0; s < S1; s++) {
+        const Slot sl = SLOTS[s];
+        const int q = sp7_combo(sl.dj, sl.dk);
+        acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
+    }
+}
+__global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic, int jb0,
+                                               const double* __restrict__ val,
+                                               const double* __restrict__ x,
+                                               double* __restrict__ y, int nloc, int ntile, int tpr)
+{
+    __shared__ double xs[6 * (SP7_T + 2) * NUN];
+    __shared__ double red[4][3][SP7_T];
+    const int per = (ntile + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= ntile) return;
+    const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
+    const int k = row % l, jl = row / l, j = jb0 + jl;
+    const int nc = min(SP7_T, n - i0);
+    const int lc0 = row * n + i0;
+    const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    /* stage x: 6 grid rows x (nc + 2) cells x 6 unknowns, contiguous runs */
+    {
+        const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
+        const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
+        const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
+        const int il = i0 > 0 ? i0 - 1 : (periodic ? n - 1 : 0);
+        const int ir = i0 + nc < n ? i0 + nc : (periodic ? 0 : n - 1);
+        const int per_row = (nc + 2) * NUN;
+        for (int e = t; e < 6 * per_row; e += 256) {
+            const int q = e / per_row, w = e - q * per_row;
+            const int p = w / NUN, var = w - p * NUN;
+            const int i = p == 0 ? il : (p == nc + 1 ? ir : i0 + p - 1);
+            const int64_t cell = ((int64_t)(rj[q] - jb0 + HALO) * l + rk[q]) * n + i;
+            xs[(q * (SP7_T + 2) + p) * NUN + var] = x[NUN * cell + var];
+        }
+    }
+    const bool act = c < nc;
+    const int64_t lc = lc0 + c;
+    double acc[3] = {0.0, 0.0, 0.0};
+    double v[26];
+    /* the coefficient loads are issued before the barrier, overlapping the x staging */
+    if (g == 0) sp7_load<0, 26>(val, nloc, lc, act, v);
+    else if (g == 1) sp7_load<26, 52>(val, nloc, lc, act, v);
+    else if (g == 2) sp7_load<52, 78>(val, nloc, lc, act, v);
+    else sp7_load<78, 104>(val, nloc, lc, act, v);
+    __syncthreads();
+    if (g == 0) sp7_compute<0, 26>(v, xs, c, acc);
+    else if (g == 1) sp7_compute<26, 52>(v, xs, c, acc);
+    else if (g == 2) sp7_compute<52, 78>(v, xs, c, acc);
+    else sp7_compute<78, 104>(v, xs, c, acc);
+#pragma unroll
+    for (int q = 0; q < 3; q++) red[g][q][c] = acc[q];
+    __syncthreads();
+    /* rows of the groups: g0 {U,V} g1 {V,W} g2 {W,P,T} g3 {T,S}; first row of group g */
+    for (int o = t; o < nc * NUN; o += 256) {
+        const int cc = o / NUN, R = o - cc * NUN;
+        double v;
+        switch (R) {
+        case 0: v = red[0][0][cc]; break;
+        case 1: v = red[0][1][cc] + red[1][0][cc]; break;
+        case 2: v = red[1][1][cc] + red[2][0][cc]; break;
+        case 3: v = red[2][1][cc]; break;
+        case 4: v = red[2][2][cc] + red[3][0][cc]; break;
+        default: v = red[3][1][cc]; break;
+        }
+        y[NUN * ((int64_t)HALO * l * n + lc0) + o] = v;
+    }
+}
+
 /* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
@@ -499,9 +598,15 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
     hipStream_t s = c->stream;
     static const int variant = [] {
         const char* e = getenv("IEMIC_SPMV");
-        return e ? atoi(e) : 6;
+        return e ? atoi(e) : 7;
     }();
-    if (variant == 6) {
+    if (variant == 7 && c->nloc < INT32_MAX) {
+        const int tpr = (c->n + SP7_T - 1) / SP7_T;
+        const int ntile = (int)(c->nloc / c->n) * tpr;
+        const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
+        hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
+                           c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
+    } else if (variant == 6 || variant == 7) {
         const int nblk = (int)((c->nloc + 63) / 64);
         const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
         hipLaunchKernelGGL(k_spmv6, dim3(grid), dim3(384), 0, s, c->n, c->m, c->l, c->cfg.periodic,
