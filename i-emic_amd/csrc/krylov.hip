@@ -293,6 +293,72 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
     }
 }
 
+
+/* the dynamics defect (see k_spmv_dyn below) with k_spmv7's LDS staging: the U/V/W/P rows
+ * only (slots 0..63), four 16-slot waves (U | U+V | V+W | W+P) */
+__global__ void __launch_bounds__(256) k_spmv7_dyn(int n, int m, int l, int periodic, int jb0,
+                                                   const double* __restrict__ val,
+                                                   const double* __restrict__ z,
+                                                   const double* __restrict__ r,
+                                                   const uint8_t* __restrict__ known,
+                                                   double* __restrict__ d, int nloc, int ntile, int tpr)
+{
+    __shared__ double xs[6 * (SP7_T + 2) * NUN];
+    __shared__ double red[4][2][SP7_T];
+    const int per = (ntile + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= ntile) return;
+    const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
+    const int k = row % l, jl = row / l, j = jb0 + jl;
+    const int nc = min(SP7_T, n - i0);
+    const int lc0 = row * n + i0;
+    const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    {
+        const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
+        const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
+        const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
+        const int il = i0 > 0 ? i0 - 1 : (periodic ? n - 1 : 0);
+        const int ir = i0 + nc < n ? i0 + nc : (periodic ? 0 : n - 1);
+        const int per_row = (nc + 2) * NUN;
+        for (int e = t; e < 6 * per_row; e += 256) {
+            const int q = e / per_row, w = e - q * per_row;
+            const int p = w / NUN, var = w - p * NUN;
+            const int i = p == 0 ? il : (p == nc + 1 ? ir : i0 + p - 1);
+            const int64_t cell = ((int64_t)(rj[q] - jb0 + HALO) * l + rk[q]) * n + i;
+            xs[(q * (SP7_T + 2) + p) * NUN + var] = z[NUN * cell + var];
+        }
+    }
+    const bool act = c < nc;
+    const int64_t lc = lc0 + c;
+    double acc[3] = {0.0, 0.0, 0.0};
+    double v[16];
+    if (g == 0) sp7_load<0, 16>(val, nloc, lc, act, v);
+    else if (g == 1) sp7_load<16, 32>(val, nloc, lc, act, v);
+    else if (g == 2) sp7_load<32, 48>(val, nloc, lc, act, v);
+    else sp7_load<48, 64>(val, nloc, lc, act, v);
+    __syncthreads();
+    if (g == 0) sp7_compute<0, 16>(v, xs, c, acc);
+    else if (g == 1) sp7_compute<16, 32>(v, xs, c, acc);
+    else if (g == 2) sp7_compute<32, 48>(v, xs, c, acc);
+    else sp7_compute<48, 64>(v, xs, c, acc);
+    red[g][0][c] = acc[0];
+    red[g][1][c] = acc[1];
+    __syncthreads();
+    /* g0 {U} g1 {U,V} g2 {V,W} g3 {W,P} */
+    for (int o = t; o < nc * 4; o += 256) {
+        const int cc = o >> 2, R = o & 3;
+        double a;
+        switch (R) {
+        case 0: a = red[0][0][cc] + red[1][0][cc]; break;
+        case 1: a = red[1][1][cc] + red[2][0][cc]; break;
+        case 2: a = red[2][1][cc] + red[3][0][cc]; break;
+        default: a = red[3][1][cc]; break;
+        }
+        const int64_t rw = NUN * ((int64_t)HALO * l * n + lc0 + cc) + R;
+        d[rw] = known[rw] ? 0.0 : r[rw] - a;
+    }
+}
+
 /* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
@@ -338,6 +404,18 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int perio
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d)
 {
+    static const int variant = [] {
+        const char* e = getenv("IEMIC_SPMV_DYN");
+        return e ? atoi(e) : 6;      /* measured in-solve: 29.6 us (6) vs 35.5 us (7) at 2 degrees */
+    }();
+    if (variant == 7 && c->nloc < INT32_MAX) {
+        const int tpr = (c->n + SP7_T - 1) / SP7_T;
+        const int ntile = (int)(c->nloc / c->n) * tpr;
+        const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
+        hipLaunchKernelGGL(k_spmv7_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l, c->cfg.periodic,
+                           c->jb0, c->d_val.p, z, r, known, d, (int)c->nloc, ntile, tpr);
+        return 0;
+    }
     const int nblk = (int)((c->nloc + 63) / 64);
     const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
     hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,

@@ -367,6 +367,146 @@ __global__ void __launch_bounds__(256) k_cr_final(const double* __restrict__ Dfi
     crf_finish(f, vb, vb, vb, 1.0, nullptr, x, m, blockIdx.x * CR_RC, red);
 }
 
+
+/* The deepest levels (few blocks) in one workgroup of 1024 threads: the level-down steps,
+ * the last block's solve and the level-up steps run back to back with workgroup barriers
+ * instead of one launch each (7 launches -> 1 at 2 degrees).  Each step is a set of
+ * block GEMVs spread over (output block, row, column group); partial sums meet in LDS. */
+constexpr int CR_DEEP_MAX = 8;
+struct CrDeep {
+    int nd, m;                        /* deep levels l0 .. l0+nd-1, then the last block */
+    int N[CR_DEEP_MAX], per[CR_DEEP_MAX];
+    const double* ap[CR_DEEP_MAX];    /* apply matrices of the level                   */
+    const double* b[CR_DEEP_MAX + 1]; /* level vectors b_l (b[nd] = last level)         */
+    double* x[CR_DEEP_MAX + 1];       /* level solutions x_l                            */
+    const double* Dfin;
+};
+/* y_o = y0_o + s (A_o0 v_o0 + A_o1 v_o1 + A_o2 v_o2), o < nout (<= 8), m x m column-major */
+struct DeepMV {
+    int nout;
+    const double* A[8][3];
+    const double* v[8][3];
+    const double* y0[8];
+    double* y[8];
+    double s;
+};
+__device__ void deep_mv(const DeepMV& D, int m, double* red)
+{
+    const int t = threadIdx.x;
+    const int R = D.nout * m;
+    const int G = R >= 1024 ? 1 : 1024 / R;
+    for (int r0 = 0; r0 < R; r0 += 1024 / G) {
+        const int rr = r0 + t % (1024 / G), g = t / (1024 / G);
+        double acc = 0.0;
+        if (g < G && rr < R) {
+            const int o = rr / m, r = rr - o * m;
+            /* four independent column steps per matrix in flight (latency, not bytes) */
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+            for (int q = 0; q < 3; q++) {
+                const double* A = D.A[o][q];
+                if (!A) continue;
+                const double* v = D.v[o][q];
+                int c = g;
+                for (; c + 3 * G < m; c += 4 * G) {
+                    a0 += A[r + (size_t)c * m] * v[c];
+                    a1 += A[r + (size_t)(c + G) * m] * v[c + G];
+                    a2 += A[r + (size_t)(c + 2 * G) * m] * v[c + 2 * G];
+                    a3 += A[r + (size_t)(c + 3 * G) * m] * v[c + 3 * G];
+                }
+                for (; c < m; c += G) a0 += A[r + (size_t)c * m] * v[c];
+            }
+            acc = (a0 + a1) + (a2 + a3);
+        }
+        red[t] = acc;
+        __syncthreads();
+        const int nr = 1024 / G;
+        if (t < nr && r0 + t < R) {
+            double sum = 0.0;
+            for (int q = 0; q < G; q++) sum += red[q * nr + t];
+            const int o = (r0 + t) / m, r = (r0 + t) - o * m;
+            D.y[o][r] = (D.y0[o] ? D.y0[o][r] : 0.0) + D.s * sum;
+        }
+        __syncthreads();
+    }
+}
+__global__ void __launch_bounds__(1024) k_cr_deep(CrDeep P)
+{
+    __shared__ double red[1024];
+    __shared__ DeepMV D;                                 /* filled by thread 0 per step */
+    const int m = P.m;
+    const size_t mm = (size_t)m * m;
+    const int t = threadIdx.x;
+    for (int d = 0; d < P.nd; d++) {                     /* level down */
+        const int N = P.N[d], per = P.per[d], ne = (N + 1) / 2;
+        if (t == 0) {
+            D.nout = ne;
+            D.s = -1.0;
+            for (int q = 0; q < ne; q++) {
+                const int e = 2 * q;
+                const bool lex = e > 0 || per, rex = e + 1 < N || per;
+                const int lnb = e > 0 ? e - 1 : N - 1, rnb = (e + 1) % N;
+                D.A[q][0] = (lex && (lnb & 1)) ? P.ap[d] + q * mm : nullptr;
+                D.v[q][0] = P.b[d] + (size_t)lnb * m;
+                D.A[q][1] = (rex && (rnb & 1)) ? P.ap[d] + (ne + q) * mm : nullptr;
+                D.v[q][1] = P.b[d] + (size_t)rnb * m;
+                D.A[q][2] = nullptr;
+                D.v[q][2] = nullptr;
+                D.y0[q] = P.b[d] + (size_t)e * m;
+                D.y[q] = const_cast<double*>(P.b[d + 1]) + (size_t)q * m;
+            }
+        }
+        __syncthreads();
+        deep_mv(D, m, red);
+    }
+    if (t == 0) {
+        D.nout = 1;
+        D.s = 1.0;
+        D.A[0][0] = P.Dfin;
+        D.v[0][0] = P.b[P.nd];
+        D.A[0][1] = D.A[0][2] = nullptr;
+        D.y0[0] = nullptr;
+        D.y[0] = P.x[P.nd];
+    }
+    __syncthreads();
+    deep_mv(D, m, red);
+    for (int d = P.nd - 1; d >= 0; d--) {                /* level up */
+        const int N = P.N[d], per = P.per[d], ne = (N + 1) / 2, no = N / 2;
+        for (int e = t; e < ne * m; e += 1024) {
+            const int q = e / m, r = e - q * m;
+            P.x[d][(size_t)(2 * q) * m + r] = P.x[d + 1][(size_t)q * m + r];
+        }
+        const double* ap = P.ap[d];
+        /* x_o = Dinv b_o, then x_o -= YL x_{o-1} + YR x_{o+1} */
+        for (int pass = 0; pass < 2; pass++) {
+            if (t == 0) {
+                D.nout = no;
+                D.s = pass == 0 ? 1.0 : -1.0;
+                for (int p = 0; p < no; p++) {
+                    const int b = 2 * p + 1;
+                    const bool rex = b + 1 < N || per;
+                    const int rn = (b + 1) % N;
+                    D.y[p] = P.x[d] + (size_t)b * m;
+                    if (pass == 0) {
+                        D.A[p][0] = ap + (2 * ne + p) * mm;
+                        D.v[p][0] = P.b[d] + (size_t)b * m;
+                        D.A[p][1] = D.A[p][2] = nullptr;
+                        D.y0[p] = nullptr;
+                    } else {
+                        D.A[p][0] = nullptr;
+                        D.A[p][1] = ap + (2 * ne + no + p) * mm;
+                        D.v[p][1] = P.x[d + 1] + (size_t)p * m;
+                        D.A[p][2] = rex ? ap + (2 * ne + 2 * no + p) * mm : nullptr;
+                        D.v[p][2] = P.x[d + 1] + (size_t)(rn / 2) * m;
+                        D.y0[p] = P.x[d] + (size_t)b * m;
+                    }
+                }
+            }
+            __syncthreads();
+            deep_mv(D, m, red);
+        }
+    }
+}
+
 }  // namespace
 
 /* level sizes, storage offsets and the GEMM descriptors (host, once per grid) */
@@ -544,6 +684,46 @@ int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStr
     const int nch = (m + CR_RC - 1) / CR_RC;
     auto bvec = [&](int l) { return l == 0 ? b : cr.bv.p + cr.v_off[l]; };
     auto xvec = [&](int l) { return l == 0 ? x : cr.xv.p + cr.v_off[l]; };
+    /* optionally (IEMIC_CR_DEEP=N) the levels of at most N blocks go to the one-workgroup
+     * kernel; off by default: measured at 2 degrees it takes 65 us against 33 us for the 7
+     * launches it replaces (one CU's dependent load chain is longer than 6 launch gaps) */
+    static const int deep_n = [] {
+        const char* e = getenv("IEMIC_CR_DEEP");
+        return e ? atoi(e) : 0;
+    }();
+    int l0 = cr.nlev;
+    while (l0 > 0 && cr.N[l0 - 1] <= deep_n && cr.nlev - (l0 - 1) <= CR_DEEP_MAX && 8 * m >= 0) l0--;
+    if (l0 < cr.nlev) {
+        for (int l = 0; l < l0; l++) {
+            const int Nl = cr.N[l], ne = (Nl + 1) / 2;
+            const double* ap = cr.ap.p + cr.ap_off[l];
+            hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch), dim3(256), 0, s, bvec(l), cr.bv.p + cr.v_off[l + 1], ap,
+                               ap + (size_t)ne * mm, Nl, cr.per[l], m, nch);
+        }
+        CrDeep P{};
+        P.nd = cr.nlev - l0;
+        P.m = m;
+        for (int d = 0; d < P.nd; d++) {
+            P.N[d] = cr.N[l0 + d];
+            P.per[d] = cr.per[l0 + d];
+            P.ap[d] = cr.ap.p + cr.ap_off[l0 + d];
+        }
+        for (int d = 0; d <= P.nd; d++) {
+            P.b[d] = bvec(l0 + d);
+            P.x[d] = xvec(l0 + d);
+        }
+        P.Dfin = cr.ap.p + cr.ap_off[cr.nlev];
+        hipLaunchKernelGGL(k_cr_deep, dim3(1), dim3(1024), 0, s, P);
+        for (int l = l0 - 1; l >= 0; l--) {
+            const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
+            const double* ap = cr.ap.p + cr.ap_off[l];
+            hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch), dim3(256), 0, s, bvec(l), (const double*)xvec(l + 1), xvec(l),
+                               ap + (size_t)2 * ne * mm, ap + (size_t)(2 * ne + no) * mm,
+                               ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch);
+        }
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     for (int l = 0; l < cr.nlev; l++) {
         const int Nl = cr.N[l], ne = (Nl + 1) / 2;
         const double* ap = cr.ap.p + cr.ap_off[l];

@@ -117,6 +117,14 @@ def lib():
         "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
         "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
         "iemic_time_spmv_cold": (C.c_int, [vp, C.c_int, vp, C.c_int64, PD]),
+        "iemic_set_intcond_correction": (C.c_int, [vp, PD]),
+        "iemic_get_intcond_correction": (C.c_int, [vp, PD]),
+        "iemic_ilu_create": (C.c_int, [P(vp), C.c_int, C.c_int, C.c_int64, P64, PI, PD, C.c_int]),
+        "iemic_ilu_compute": (C.c_int, [vp]),
+        "iemic_ilu_apply": (C.c_int, [vp, PD, PD]),
+        "iemic_ilu_apply_dev": (C.c_int, [vp, vp, vp]),
+        "iemic_ilu_stats": (C.c_int, [vp, PI, PI, PI]),
+        "iemic_ilu_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -135,7 +143,9 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
-            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold")
+            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold",
+            "iemic_ilu_create", "iemic_ilu_compute", "iemic_ilu_apply", "iemic_ilu_apply_dev",
+            "iemic_ilu_stats", "iemic_ilu_destroy")
 
 
 class IemicError(RuntimeError):

@@ -196,6 +196,22 @@ int iemic_time_spmv(iemic_ctx* ctx, int nrep, double* ms_per_launch);
 int iemic_time_spmv_cold(iemic_ctx* ctx, int nrep, void* flush_dev, int64_t flush_bytes,
                          double* ms_per_launch);
 
+/* ---- block ILU(0) factor handles: the MRILU seam (Ifpack_MRILU.cpp:22-39,
+ * mrilucpp.F90:120-553), re-designed: a rank-local 0-based CSR (int64 row pointers) is
+ * copied to the device as bs x bs blocks (bs = 6: the THCM cell block) and factorised by
+ * block ILU(0) with level scheduling.  create ~ mrilucpp_create(id, n, nnz, beg, jco, co),
+ * compute ~ mrilucpp_compute (once per handle: the matrix is consumed), apply ~
+ * mrilucpp_apply(id, n, rhs, sol) (rhs, sol distinct), destroy ~ mrilucpp_destroy. */
+typedef struct iemic_ilu iemic_ilu;
+int  iemic_ilu_create(iemic_ilu** h, int device, int n, int64_t nnz, const int64_t* rowptr,
+                      const int* col, const double* val, int blocksize);
+int  iemic_ilu_compute(iemic_ilu* h);
+int  iemic_ilu_apply(iemic_ilu* h, const double* rhs, double* sol);          /* host vectors   */
+int  iemic_ilu_apply_dev(iemic_ilu* h, const double* rhs, double* sol);      /* device vectors */
+/* levels of the two triangular solves and the pivot columns completed by a unit pivot */
+int  iemic_ilu_stats(const iemic_ilu* h, int* lower_levels, int* upper_levels, int* perturbed);
+void iemic_ilu_destroy(iemic_ilu* h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -466,3 +466,43 @@ class BlockGS:
                                     _p(x, C.c_double), tol, m, maxit, C.byref(rel),
                                     _p(hist, C.c_double))
         return x, it, rel.value, hist[:it]
+
+
+# ------------------------------------------------------------------------------------
+# block ILU(0) (ilu_oracle.c) -- CPU twin of ilu.hip (the MRILU seam)
+
+class BlockILU:
+    """CPU block ILU(0) of a 0-based CSR matrix (int64 row pointers), block size bs."""
+
+    def __init__(self, rowptr, col, val, bs: int = 6):
+        lib = _load_krylov()
+        if not hasattr(lib, "_ilu_ready"):
+            lib.orc_ilu_create.restype = C.c_void_p
+            lib.orc_ilu_create.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_double), C.c_int]
+            lib.orc_ilu_apply.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+            lib.orc_ilu_destroy.argtypes = [C.c_void_p]
+            lib.orc_ilu_perturbed.argtypes = [C.c_void_p]
+            lib._ilu_ready = True
+        self.lib = lib
+        self.rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        self.col = np.ascontiguousarray(col, dtype=np.int32)
+        self.val = np.ascontiguousarray(val, dtype=np.float64)
+        self.n = len(self.rowptr) - 1
+        self.h = lib.orc_ilu_create(self.n, _p(self.rowptr, C.c_int64), _p(self.col, C.c_int),
+                                    _p(self.val, C.c_double), bs)
+        if not self.h:
+            raise RuntimeError("BlockILU: bad block size")
+        self.perturbed = lib.orc_ilu_perturbed(self.h)
+
+    def apply(self, r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros_like(r)
+        self.lib.orc_ilu_apply(self.h, _p(r, C.c_double), _p(z, C.c_double))
+        return z
+
+    def __del__(self):
+        try:
+            self.lib.orc_ilu_destroy(self.h)
+        except Exception:
+            pass
