@@ -118,6 +118,68 @@ class Ocean:
         check(lib().iemic_get_intcond_correction(self._h, C.byref(v)), "iemic_get_intcond_correction")
         return v.value
 
+    # ---- state files (Model::saveStateToFile / loadStateFromFile, Model.H:149-330) -----
+    def saveStateToFile(self, filename: str) -> None:
+        """HDF5 file in the reference's layout (EpetraExt::HDF5 conventions): State
+        (an Epetra_MultiVector: Values, GlobalLength, NumVectors, __type__), Parameters (one
+        scalar per continuation parameter, THCM::int2par names), Grid (n, m, l, nun, aux,
+        bounds in radians, hdim, the uniform horizontal coordinates) and Ocean's MaskGlobal
+        (Ocean.C:1904-2113).  Written by iemic.h5 (no libhdf5 in this build)."""
+        import math
+        from . import h5
+        c = self.cfg
+        x = self.getState()
+        pars = {}
+        for name in PAR_INDEX:
+            pars[name] = np.array(self.getPar(name), dtype=np.float64)
+        xmin, xmax = math.radians(c.xmin), math.radians(c.xmax)
+        ymin, ymax = math.radians(c.ymin), math.radians(c.ymax)
+        dx, dy = (xmax - xmin) / c.n, (ymax - ymin) / c.m
+        L = self.landmask().astype(np.int32)
+        tree = {
+            "State": {"Values": x.reshape(1, -1), "GlobalLength": np.array(len(x), dtype=np.int32),
+                      "NumVectors": np.array(1, dtype=np.int32),
+                      "__type__": np.array([b"Epetra_MultiVector"], dtype="S19")},
+            "Parameters": pars,
+            "Grid": {"n": np.array(c.n, dtype=np.int32), "m": np.array(c.m, dtype=np.int32),
+                     "l": np.array(c.l, dtype=np.int32), "nun": np.array(6, dtype=np.int32),
+                     "aux": np.array(0, dtype=np.int32), "xmin": np.array(xmin), "xmax": np.array(xmax),
+                     "ymin": np.array(ymin), "ymax": np.array(ymax), "hdim": np.array(float(c.hdim)),
+                     "x": xmin + dx * (np.arange(c.n) + 0.5), "y": ymin + dy * (np.arange(c.m) + 0.5),
+                     "xu": xmin + dx * np.arange(1, c.n + 1), "yv": ymin + dy * np.arange(1, c.m + 1)},
+            "MaskGlobal": {"Global": L, "GlobalSize": np.array(L.size, dtype=np.int32),
+                           "Label": np.array([b"current"], dtype="S8")},
+        }
+        h5.write(filename, tree)
+
+    def loadStateFromFile(self, filename: str) -> int:
+        """Model::loadStateFromFile: the state (global length must match), every parameter
+        the file holds under a THCM name (unknown names are skipped, as the reference's
+        try/catch does; the older label FPER is read as Flux Perturbation), and for an
+        SRES = 0 grid the integral-condition correction of the loaded state (Ocean.C:144-148).
+        Returns 1 (state untouched) if the file does not exist, 0 otherwise."""
+        import os
+        from . import h5
+        if not os.path.exists(filename):
+            return 1
+        t = h5.read(filename)
+        if "/State/Values" not in t:
+            raise IemicError(f"The group <State> is not contained in hdf5 {filename}")
+        x = np.asarray(t["/State/Values"][0], dtype=np.float64).reshape(-1)
+        if x.size != self.N:
+            raise IemicError(f"{filename}: state of length {x.size}, this model has {self.N}")
+        self.setState(x)
+        alias = {"FPER": "Flux Perturbation"}
+        for path, (v, _) in t.items():
+            if not path.startswith("/Parameters/"):
+                continue
+            name = alias.get(path.split("/", 2)[2], path.split("/", 2)[2])
+            if name in PAR_INDEX:
+                self.setPar(name, float(np.asarray(v).reshape(-1)[0]))
+        if self.rowintcon >= 0:
+            self.setIntCondCorrection()
+        return 0
+
     # ---- state --------------------------------------------------------------------
     def setState(self, x: np.ndarray) -> None:
         x = np.ascontiguousarray(x, dtype=np.float64)
