@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PMC_TAG = "r01"         # profiles/<tag>_spmv_pmc.json: PMC HBM bytes per k_spmv launch
+PMC_TAG = "r02"         # profiles/<tag>_spmv_pmc.json: PMC HBM bytes per k_spmv launch
 
 
 def spmv_bytes(nnz: int, n: int) -> int:

@@ -15,3 +15,9 @@ done
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/spmv_trace -o run \
     -- python3 -u scripts/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "pmc ok"
+# in-solve counters of every kernel of one benchmark Newton step (warm caches, as timed)
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/bench_$ctr -o run \
+      -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 > gpurun_out/pmc/bench_$ctr.log 2>&1 || { echo "bench $ctr failed"; exit 1; }
+done
+echo "bench pmc ok"

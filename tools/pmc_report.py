@@ -60,7 +60,7 @@ def main():
                 if "k_spmv" in row["Name"]:
                     trace = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"])}
     print(json.dumps({
-        "config": cfgname, "kernel": "k_spmv", "condition": "Infinity Cache flushed before each launch",
+        "config": cfgname, "kernel": ", ".join(sorted({k.split("(")[0] for k in sf if "k_spmv" in k})), "condition": "Infinity Cache flushed before each launch",
         "launches": nf, "fetch_kib": fs, "write_kib": ws,
         "calibration": {"read8_factor": round(f8, 4), "read16_factor": round(f16, 4),
                         "write8_factor": round(fw, 4), "bytes": CALIB_BYTES},
