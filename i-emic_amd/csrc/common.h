@@ -67,7 +67,10 @@ struct SchurCR {
                                      /* level nlev: the last block's inverse              */
     std::vector<size_t> v_off;       /* level vectors b_l, x_l (l >= 1)                   */
     std::vector<int> g_off, g_cnt;   /* GEMM descriptor ranges: 3 per level               */
+    int lt = 0, tM = 0;              /* dense tail: levels >= lt as one explicit inverse  */
+    std::vector<size_t> tb_off;      /* tail set-up: batched level vectors, tM columns    */
     DevBuf<double> dlr, ap, bv, xv;
+    DevBuf<double> tinv, tb, tx;     /* tail inverse (row-major tM x tM), set-up batches  */
     DevBuf<CrGemm> gd;
     DevBuf<int> info;
 };

@@ -15,7 +15,10 @@
  * odd count leaves two even blocks adjacent across the periodic wrap, the two couplings of
  * a periodic pair merged), down to one m x m block.  Set-up per level: one Gauss-Jordan
  * inverse per odd block (one workgroup each) and two batched GEMM launches; the apply is one
- * GEMV launch per level down and one per level up.  Cost: O(n m^3) set-up flops spread over
+ * GEMV launch per level down and one per level up.  The deepest levels (the first level of
+ * at most 1024 unknowns and below) form a dense tail: its explicit inverse is built at set-up
+ * by running those levels on the identity, and the apply replaces their 2 (nlev - lt) + 1
+ * launches with one GEMV (9 -> 1 at 2 degrees).  Cost: O(n m^3) set-up flops spread over
  * n/2 workgroups per level and O(n m^2) apply bytes -- against the O(ncol^2) dense inverse
  * and the single-workgroup band LU it replaces.  Land columns are identity rows; pivoting
  * happens inside the diagonal blocks only (tested against the band LU with partial
@@ -308,9 +311,11 @@ __device__ __forceinline__ void crf_finish(const CrFrag& f, const double* v0, co
  * b'_q = b_e - XL_q b_{e-1} - XR_q b_{e+1} (odd neighbours only), e = 2q */
 __global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, double* __restrict__ bn,
                                                 const double* __restrict__ XL, const double* __restrict__ XR,
-                                                int N, int per, int m, int nch)
+                                                int N, int per, int m, int nch, int64_t sl, int64_t sn)
 {
     __shared__ double vl[CR_MAXM], vr[CR_MAXM], red[256];
+    bl += blockIdx.y * sl;                               /* batched right-hand sides (set-up) */
+    bn += blockIdx.y * sn;
     const int q = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, e = 2 * q;
     const bool lex = e > 0 || per, rex = e + 1 < N || per;
     const int lnb = e > 0 ? e - 1 : N - 1, rnb = (e + 1) % N;
@@ -332,9 +337,12 @@ __global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, d
 __global__ void __launch_bounds__(256) k_cr_bwd(const double* __restrict__ bl, const double* __restrict__ xn,
                                                 double* __restrict__ xl, const double* __restrict__ Dinv,
                                                 const double* __restrict__ YL, const double* __restrict__ YR,
-                                                int N, int per, int m, int nch)
+                                                int N, int per, int m, int nch, int64_t sl, int64_t sn)
 {
     __shared__ double vb[CR_MAXM], vl[CR_MAXM], vr[CR_MAXM], red[256];
+    bl += blockIdx.y * sl;
+    xl += blockIdx.y * sl;
+    xn += blockIdx.y * sn;
     const int p = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, b = 2 * p + 1;
     const bool rex = b + 1 < N || per;
     const int rn = (b + 1) % N;
@@ -360,6 +368,8 @@ __global__ void __launch_bounds__(256) k_cr_final(const double* __restrict__ Dfi
                                                   double* __restrict__ x, int m)
 {
     __shared__ double vb[CR_MAXM], red[256];
+    b += (size_t)blockIdx.y * m;
+    x += (size_t)blockIdx.y * m;
     CrFrag f;
     crf_load(f, Dfin, nullptr, nullptr, m, blockIdx.x * CR_RC);
     for (int c = threadIdx.x; c < m; c += 256) vb[c] = b[c];
@@ -368,146 +378,72 @@ __global__ void __launch_bounds__(256) k_cr_final(const double* __restrict__ Dfi
 }
 
 
-/* The deepest levels (few blocks) in one workgroup of 1024 threads: the level-down steps,
- * the last block's solve and the level-up steps run back to back with workgroup barriers
- * instead of one launch each (7 launches -> 1 at 2 degrees).  Each step is a set of
- * block GEMVs spread over (output block, row, column group); partial sums meet in LDS. */
-constexpr int CR_DEEP_MAX = 8;
-struct CrDeep {
-    int nd, m;                        /* deep levels l0 .. l0+nd-1, then the last block */
-    int N[CR_DEEP_MAX], per[CR_DEEP_MAX];
-    const double* ap[CR_DEEP_MAX];    /* apply matrices of the level                   */
-    const double* b[CR_DEEP_MAX + 1]; /* level vectors b_l (b[nd] = last level)         */
-    double* x[CR_DEEP_MAX + 1];       /* level solutions x_l                            */
-    const double* Dfin;
-};
-/* y_o = y0_o + s (A_o0 v_o0 + A_o1 v_o1 + A_o2 v_o2), o < nout (<= 8), m x m column-major */
-struct DeepMV {
-    int nout;
-    const double* A[8][3];
-    const double* v[8][3];
-    const double* y0[8];
-    double* y[8];
-    double s;
-};
-__device__ void deep_mv(const DeepMV& D, int m, double* red)
+/* dense tail, set-up: the identity as tM right-hand sides of the tail's first level */
+__global__ void k_cr_eye(double* __restrict__ B, int M)
 {
-    const int t = threadIdx.x;
-    const int R = D.nout * m;
-    const int G = R >= 1024 ? 1 : 1024 / R;
-    for (int r0 = 0; r0 < R; r0 += 1024 / G) {
-        const int rr = r0 + t % (1024 / G), g = t / (1024 / G);
-        double acc = 0.0;
-        if (g < G && rr < R) {
-            const int o = rr / m, r = rr - o * m;
-            /* four independent column steps per matrix in flight (latency, not bytes) */
-            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-            for (int q = 0; q < 3; q++) {
-                const double* A = D.A[o][q];
-                if (!A) continue;
-                const double* v = D.v[o][q];
-                int c = g;
-                for (; c + 3 * G < m; c += 4 * G) {
-                    a0 += A[r + (size_t)c * m] * v[c];
-                    a1 += A[r + (size_t)(c + G) * m] * v[c + G];
-                    a2 += A[r + (size_t)(c + 2 * G) * m] * v[c + 2 * G];
-                    a3 += A[r + (size_t)(c + 3 * G) * m] * v[c + 3 * G];
-                }
-                for (; c < m; c += G) a0 += A[r + (size_t)c * m] * v[c];
-            }
-            acc = (a0 + a1) + (a2 + a3);
-        }
-        red[t] = acc;
-        __syncthreads();
-        const int nr = 1024 / G;
-        if (t < nr && r0 + t < R) {
-            double sum = 0.0;
-            for (int q = 0; q < G; q++) sum += red[q * nr + t];
-            const int o = (r0 + t) / m, r = (r0 + t) - o * m;
-            D.y[o][r] = (D.y0[o] ? D.y0[o][r] : 0.0) + D.s * sum;
-        }
-        __syncthreads();
-    }
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < (int64_t)M * M) B[e] = (e / M == e % M) ? 1.0 : 0.0;
 }
-__global__ void __launch_bounds__(1024) k_cr_deep(CrDeep P)
+
+/* T = X^T for the M x M column-major X (32 x 32 tiles through LDS) */
+__global__ void k_cr_transpose(const double* __restrict__ X, double* __restrict__ T, int M)
 {
-    __shared__ double red[1024];
-    __shared__ DeepMV D;                                 /* filled by thread 0 per step */
-    const int m = P.m;
-    const size_t mm = (size_t)m * m;
-    const int t = threadIdx.x;
-    for (int d = 0; d < P.nd; d++) {                     /* level down */
-        const int N = P.N[d], per = P.per[d], ne = (N + 1) / 2;
-        if (t == 0) {
-            D.nout = ne;
-            D.s = -1.0;
-            for (int q = 0; q < ne; q++) {
-                const int e = 2 * q;
-                const bool lex = e > 0 || per, rex = e + 1 < N || per;
-                const int lnb = e > 0 ? e - 1 : N - 1, rnb = (e + 1) % N;
-                D.A[q][0] = (lex && (lnb & 1)) ? P.ap[d] + q * mm : nullptr;
-                D.v[q][0] = P.b[d] + (size_t)lnb * m;
-                D.A[q][1] = (rex && (rnb & 1)) ? P.ap[d] + (ne + q) * mm : nullptr;
-                D.v[q][1] = P.b[d] + (size_t)rnb * m;
-                D.A[q][2] = nullptr;
-                D.v[q][2] = nullptr;
-                D.y0[q] = P.b[d] + (size_t)e * m;
-                D.y[q] = const_cast<double*>(P.b[d + 1]) + (size_t)q * m;
-            }
-        }
-        __syncthreads();
-        deep_mv(D, m, red);
-    }
-    if (t == 0) {
-        D.nout = 1;
-        D.s = 1.0;
-        D.A[0][0] = P.Dfin;
-        D.v[0][0] = P.b[P.nd];
-        D.A[0][1] = D.A[0][2] = nullptr;
-        D.y0[0] = nullptr;
-        D.y[0] = P.x[P.nd];
-    }
+    __shared__ double t[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int y = ty; y < 32; y += 8)
+        if (r0 + tx < M && c0 + y < M) t[y][tx] = X[(r0 + tx) + (size_t)(c0 + y) * M];
     __syncthreads();
-    deep_mv(D, m, red);
-    for (int d = P.nd - 1; d >= 0; d--) {                /* level up */
-        const int N = P.N[d], per = P.per[d], ne = (N + 1) / 2, no = N / 2;
-        for (int e = t; e < ne * m; e += 1024) {
-            const int q = e / m, r = e - q * m;
-            P.x[d][(size_t)(2 * q) * m + r] = P.x[d + 1][(size_t)q * m + r];
-        }
-        const double* ap = P.ap[d];
-        /* x_o = Dinv b_o, then x_o -= YL x_{o-1} + YR x_{o+1} */
-        for (int pass = 0; pass < 2; pass++) {
-            if (t == 0) {
-                D.nout = no;
-                D.s = pass == 0 ? 1.0 : -1.0;
-                for (int p = 0; p < no; p++) {
-                    const int b = 2 * p + 1;
-                    const bool rex = b + 1 < N || per;
-                    const int rn = (b + 1) % N;
-                    D.y[p] = P.x[d] + (size_t)b * m;
-                    if (pass == 0) {
-                        D.A[p][0] = ap + (2 * ne + p) * mm;
-                        D.v[p][0] = P.b[d] + (size_t)b * m;
-                        D.A[p][1] = D.A[p][2] = nullptr;
-                        D.y0[p] = nullptr;
-                    } else {
-                        D.A[p][0] = nullptr;
-                        D.A[p][1] = ap + (2 * ne + no + p) * mm;
-                        D.v[p][1] = P.x[d + 1] + (size_t)p * m;
-                        D.A[p][2] = rex ? ap + (2 * ne + 2 * no + p) * mm : nullptr;
-                        D.v[p][2] = P.x[d + 1] + (size_t)(rn / 2) * m;
-                        D.y0[p] = P.x[d] + (size_t)b * m;
-                    }
-                }
-            }
-            __syncthreads();
-            deep_mv(D, m, red);
-        }
+    for (int y = ty; y < 32; y += 8)
+        if (c0 + tx < M && r0 + y < M) T[(r0 + y) * (size_t)M + c0 + tx] = t[tx][y];
+}
+
+/* dense tail, apply: x = Tinv b (row-major, M <= CR_TAIL_MAX), one wave per row, b staged
+ * in LDS, four independent accumulators per lane, a fixed shuffle tree (deterministic) */
+constexpr int CR_TAIL_MAX = 2048;
+__global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv, const double* __restrict__ b,
+                                                 double* __restrict__ x, int M)
+{
+    __shared__ double vb[CR_TAIL_MAX];
+    for (int c = threadIdx.x; c < M; c += 256) vb[c] = b[c];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= M) return;
+    const double* A = Tinv + (size_t)r * M;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int c = lane;
+    for (; c + 192 < M; c += 256) {
+        a0 += A[c] * vb[c];
+        a1 += A[c + 64] * vb[c + 64];
+        a2 += A[c + 128] * vb[c + 128];
+        a3 += A[c + 192] * vb[c + 192];
     }
+    for (; c < M; c += 64) a0 += A[c] * vb[c];
+    double v = (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) x[r] = v;
 }
 
 }  // namespace
+
+/* one level down / up for nrhs right-hand sides (level vectors N[l] m apart) */
+static void cr_down(const SchurCR& cr, int l, const double* bl, double* bn, int nrhs, hipStream_t s)
+{
+    const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC, Nl = cr.N[l], ne = (Nl + 1) / 2;
+    const size_t mm = (size_t)m * m;
+    const double* ap = cr.ap.p + cr.ap_off[l];
+    hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch, nrhs), dim3(256), 0, s, bl, bn, ap, ap + (size_t)ne * mm, Nl,
+                       cr.per[l], m, nch, (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m);
+}
+static void cr_up(const SchurCR& cr, int l, const double* bl, const double* xn, double* xl, int nrhs, hipStream_t s)
+{
+    const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC, Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
+    const size_t mm = (size_t)m * m;
+    const double* ap = cr.ap.p + cr.ap_off[l];
+    hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch, nrhs), dim3(256), 0, s, bl, xn, xl, ap + (size_t)2 * ne * mm,
+                       ap + (size_t)(2 * ne + no) * mm, ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch,
+                       (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m);
+}
 
 /* level sizes, storage offsets and the GEMM descriptors (host, once per grid) */
 int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
@@ -608,6 +544,33 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
         return IEMIC_ENOMEM;
     }
     if (!g.empty() && (rc = h2d(c, cr.gd.p, g.data(), sizeof(CrGemm) * g.size()))) return rc;
+    /* dense tail: the first level of at most IEMIC_CR_TAIL (default 1024) unknowns and its
+     * descendants become one explicit inverse (built at set-up by solving the tail for the
+     * identity), so the apply spends one GEMV launch instead of 2 (nlev - lt) + 1 */
+    static const int tail_max = [] {
+        const char* e = getenv("IEMIC_CR_TAIL");
+        return std::min(e ? atoi(e) : 1024, CR_TAIL_MAX);
+    }();
+    cr.lt = cr.nlev;
+    cr.tM = 0;
+    for (int l = 0; l < cr.nlev; l++)
+        if (cr.N[l] > 1 && (int64_t)cr.N[l] * m <= tail_max) {
+            cr.lt = l;
+            cr.tM = cr.N[l] * m;
+            break;
+        }
+    if (cr.tM) {
+        cr.tb_off.assign(cr.nlev - cr.lt + 1, 0);
+        size_t nt = 0;
+        for (int l = cr.lt; l <= cr.nlev; l++) {
+            cr.tb_off[l - cr.lt] = nt;
+            nt += (size_t)cr.N[l] * m * cr.tM;
+        }
+        if (cr.tinv.alloc((size_t)cr.tM * cr.tM) || cr.tb.alloc(nt) || cr.tx.alloc(nt)) {
+            set_error("Schur cyclic reduction: out of device memory");
+            return IEMIC_ENOMEM;
+        }
+    }
     return 0;
 }
 
@@ -660,6 +623,18 @@ int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
     }
     if ((rc = cr_inverse(s, m, 1, cr.dlr.p + cr.dlr_off[cr.nlev], 0, 1, cr.ap.p + cr.ap_off[cr.nlev], cr.info.p)))
         return rc;
+    if (cr.tM) {                           /* the tail's inverse, column r = tail solve of e_r */
+        const int M = cr.tM;
+        auto tb = [&](int l) { return cr.tb.p + cr.tb_off[l - cr.lt]; };
+        auto tx = [&](int l) { return cr.tx.p + cr.tb_off[l - cr.lt]; };
+        hipLaunchKernelGGL(k_cr_eye, dim3((unsigned)(((int64_t)M * M + 255) / 256)), dim3(256), 0, s, tb(cr.lt), M);
+        for (int l = cr.lt; l < cr.nlev; l++) cr_down(cr, l, tb(l), tb(l + 1), M, s);
+        hipLaunchKernelGGL(k_cr_final, dim3((m + CR_RC - 1) / CR_RC, M), dim3(256), 0, s,
+                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), (const double*)tb(cr.nlev), tx(cr.nlev), m);
+        for (int l = cr.nlev - 1; l >= cr.lt; l--) cr_up(cr, l, tb(l), tx(l + 1), tx(l), M, s);
+        hipLaunchKernelGGL(k_cr_transpose, dim3((M + 31) / 32, (M + 31) / 32), dim3(256), 0, s,
+                           (const double*)tx(cr.lt), cr.tinv.p, M);
+    }
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -675,70 +650,22 @@ int cr_check(iemic_ctx* c, SchurCR& cr)
     return 0;
 }
 
-/* x = S^-1 b (b, x: n*m, c = i*m + j) */
+/* x = S^-1 b (b, x: n*m, c = i*m + j): the levels above the tail one launch each way, the
+ * tail (levels >= lt, tM = N[lt] m unknowns) one dense GEMV */
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)
 {
     (void)c;
-    const int m = cr.m;
-    const size_t mm = (size_t)m * m;
-    const int nch = (m + CR_RC - 1) / CR_RC;
     auto bvec = [&](int l) { return l == 0 ? b : cr.bv.p + cr.v_off[l]; };
     auto xvec = [&](int l) { return l == 0 ? x : cr.xv.p + cr.v_off[l]; };
-    /* optionally (IEMIC_CR_DEEP=N) the levels of at most N blocks go to the one-workgroup
-     * kernel; off by default: measured at 2 degrees it takes 65 us against 33 us for the 7
-     * launches it replaces (one CU's dependent load chain is longer than 6 launch gaps) */
-    static const int deep_n = [] {
-        const char* e = getenv("IEMIC_CR_DEEP");
-        return e ? atoi(e) : 0;
-    }();
-    int l0 = cr.nlev;
-    while (l0 > 0 && cr.N[l0 - 1] <= deep_n && cr.nlev - (l0 - 1) <= CR_DEEP_MAX && 8 * m >= 0) l0--;
-    if (l0 < cr.nlev) {
-        for (int l = 0; l < l0; l++) {
-            const int Nl = cr.N[l], ne = (Nl + 1) / 2;
-            const double* ap = cr.ap.p + cr.ap_off[l];
-            hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch), dim3(256), 0, s, bvec(l), cr.bv.p + cr.v_off[l + 1], ap,
-                               ap + (size_t)ne * mm, Nl, cr.per[l], m, nch);
-        }
-        CrDeep P{};
-        P.nd = cr.nlev - l0;
-        P.m = m;
-        for (int d = 0; d < P.nd; d++) {
-            P.N[d] = cr.N[l0 + d];
-            P.per[d] = cr.per[l0 + d];
-            P.ap[d] = cr.ap.p + cr.ap_off[l0 + d];
-        }
-        for (int d = 0; d <= P.nd; d++) {
-            P.b[d] = bvec(l0 + d);
-            P.x[d] = xvec(l0 + d);
-        }
-        P.Dfin = cr.ap.p + cr.ap_off[cr.nlev];
-        hipLaunchKernelGGL(k_cr_deep, dim3(1), dim3(1024), 0, s, P);
-        for (int l = l0 - 1; l >= 0; l--) {
-            const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
-            const double* ap = cr.ap.p + cr.ap_off[l];
-            hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch), dim3(256), 0, s, bvec(l), (const double*)xvec(l + 1), xvec(l),
-                               ap + (size_t)2 * ne * mm, ap + (size_t)(2 * ne + no) * mm,
-                               ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch);
-        }
-        HIP_OK(hipGetLastError());
-        return 0;
-    }
-    for (int l = 0; l < cr.nlev; l++) {
-        const int Nl = cr.N[l], ne = (Nl + 1) / 2;
-        const double* ap = cr.ap.p + cr.ap_off[l];
-        hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch), dim3(256), 0, s, bvec(l), cr.bv.p + cr.v_off[l + 1], ap,
-                           ap + (size_t)ne * mm, Nl, cr.per[l], m, nch);
-    }
-    hipLaunchKernelGGL(k_cr_final, dim3(nch), dim3(256), 0, s, (const double*)(cr.ap.p + cr.ap_off[cr.nlev]),
-                       bvec(cr.nlev), xvec(cr.nlev), m);
-    for (int l = cr.nlev - 1; l >= 0; l--) {
-        const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
-        const double* ap = cr.ap.p + cr.ap_off[l];
-        hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch), dim3(256), 0, s, bvec(l), (const double*)xvec(l + 1), xvec(l),
-                           ap + (size_t)2 * ne * mm, ap + (size_t)(2 * ne + no) * mm,
-                           ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch);
-    }
+    const int le = cr.tM ? cr.lt : cr.nlev;
+    for (int l = 0; l < le; l++) cr_down(cr, l, bvec(l), cr.bv.p + cr.v_off[l + 1], 1, s);
+    if (cr.tM)
+        hipLaunchKernelGGL(k_cr_tail, dim3((cr.tM + 3) / 4), dim3(256), 0, s, (const double*)cr.tinv.p, bvec(le),
+                           xvec(le), cr.tM);
+    else
+        hipLaunchKernelGGL(k_cr_final, dim3((cr.m + CR_RC - 1) / CR_RC), dim3(256), 0, s,
+                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), bvec(le), xvec(le), cr.m);
+    for (int l = le - 1; l >= 0; l--) cr_up(cr, l, bvec(l), xvec(l + 1), xvec(l), 1, s);
     HIP_OK(hipGetLastError());
     return 0;
 }
