@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--ts-mg", type=int, default=1,
                    help="T/S aggregation-multigrid V-cycles (0: --ts-sweeps plain sweeps)")
     p.add_argument("--mg-sweeps", type=int, default=1, help="sweeps per multigrid level")
+    p.add_argument("--ts-at", type=int, default=0,
+                   help="form the T/S right-hand side after this many dynamics passes (0: the last); "
+                        "earlier lets the T/S multigrid run on a second stream beside the rest")
     p.add_argument("--spmv-reps", type=int, default=0,
                    help="extra back-to-back (hot Infinity Cache) SpMV launches, reported apart")
     p.add_argument("--cold-reps", type=int, default=0,
@@ -102,7 +105,7 @@ def cpu_baseline(cfg, L, x, args):
     t_jac = time.perf_counter() - t
     t = time.perf_counter()
     P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
-                    ts_mg=args.ts_mg)
+                    ts_mg=args.ts_mg, ts_at=args.ts_at)
     t_prec = time.perf_counter() - t
     t = time.perf_counter()
     dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=args.tol, m=args.krylov,
@@ -145,7 +148,7 @@ def main():
           "Dyn iterations": args.dyn_iters,
           "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps,
-          "Solver": args.solver, "IDR s": args.idr_s}
+          "Solver": args.solver, "IDR s": args.idr_s, "TS after dyn pass": args.ts_at}
     comm_id = None
     if world > 1:
         idt = torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -253,7 +256,7 @@ def main():
                    "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
                    "schur": "cyclic reduction (fp64, exact)",
-                   "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps,
+                   "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
                    "parallelism": f"latitude-bands x{world}" if world > 1 else "single",
                    "band_rows": [lay["jb0"], lay["jb1"]]},
         "newton": {"iters": s.iters, "converged": s.converged,

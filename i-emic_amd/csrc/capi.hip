@@ -41,8 +41,14 @@ iemic_ctx::~iemic_ctx()
     if (stream) (void)hipStreamSynchronize(stream);
     if (h_red) (void)hipHostFree(h_red);
     h_red = nullptr;
+    if (side) (void)hipStreamSynchronize(side);
+    if (gs.mg_exec) (void)hipGraphExecDestroy(gs.mg_exec);
+    gs.mg_exec = nullptr;
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
-    stream = nullptr;
+    stream = side = nullptr;
     /* device buffers are members: released after this body, with the stream drained */
 }
 
@@ -179,7 +185,10 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     iemic_ctx* c = new iemic_ctx();
     c->cfg = *grid;
     c->device = std::min(std::max(grid->device, 0), ndev - 1);
-    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         set_error("iemic_create: cannot initialise the HIP device");
         delete c;
         return IEMIC_EDEVICE;
@@ -584,6 +593,33 @@ extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     *ms_per_launch = ms / nrep;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+extern "C" int iemic_time_prec(iemic_ctx* c, int nrep, double* ms_per_apply, double* host_ms_per_apply)
+{
+    CTX_CHECK(c);
+    if (!c->gs.ready || nrep < 1 || !ms_per_apply || !host_ms_per_apply) return IEMIC_ESTATE;
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, c->stream));
+    int rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);   /* warm */
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_OK(hipEventRecord(e0, c->stream));
+    for (int r = 0; r < nrep && !rc; r++) rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);
+    HIP_OK(hipEventRecord(e1, c->stream));
+    const double host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    HIP_OK(hipEventSynchronize(e1));
+    if (rc) return rc;
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    *ms_per_apply = ms / nrep;
+    *host_ms_per_apply = host / nrep;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return 0;

@@ -110,6 +110,8 @@ struct BlockGS {
     DevBuf<double> dq, dzero, dmr;   /* MR passes: -A_DD zc, a zero vector, dot partials  */
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
+    int ts_at = 0;                   /* T/S rhs after this many passes (0: after all)     */
+    hipGraphExec_t mg_exec = nullptr; /* the ts_mg V-cycles captured once (fixed buffers)  */
     /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local):
      * level 0 is the fine T/S block (tsoff/tsdiag/tsinv, ext cells); coarse level q has
      * mg_n[q] x mg_m[q] x l cells with 16 couplings, 2x2 block and inverse, rhs, iterate */
@@ -145,6 +147,8 @@ struct iemic_ctx {
     iemic_grid cfg;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;      /* second stream: block GS T/S solve (one rank)      */
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n = 0, m = 0, l = 0;
     int64_t ncell = 0, nrows = 0;    /* global cells / rows                               */
     /* latitude-band decomposition (stencil.h ext layout): owned band [jb0, jb1) */

@@ -2282,6 +2282,40 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.dyn_iters = opt ? std::max(1, opt->dyn_iters) : 1;
     gs.dyn_mr = opt ? (opt->dyn_mr != 0) : 0;
     gs.dyn_omega = opt && opt->dyn_omega > 0.0 ? opt->dyn_omega : 1.0;
+    gs.ts_at = opt ? std::max(0, opt->ts_at) : 0;
+    /* one rank, early T/S right-hand side: the ts_mg V-cycles (fixed buffers and arguments)
+     * captured once as a graph, so the fork costs the host one launch instead of ~40 while
+     * the main stream waits for its next passes (IEMIC_GRAPH=0: plain launches).  Measured
+     * at 2 degrees (scripts/prec_probe.py): the side-stream V-cycle contends with the passes
+     * for HBM (apply 849 -> 739 us with ts_at = 2, not the 560 us of a full overlap) and
+     * FGMRES needs 240 instead of 208 iterations, so the default stays ts_at = 0. */
+    static const int use_graph = [] {
+        const char* e = getenv("IEMIC_GRAPH");
+        return e ? atoi(e) : 1;
+    }();
+    if (gs.mg_exec) {
+        HIP_OK(hipGraphExecDestroy(gs.mg_exec));
+        gs.mg_exec = nullptr;
+    }
+    if (use_graph && gs.ts_mg > 0 && gs.mg_nlev >= 2 && c->nranks == 1 && c->side && !gs.dyn_mr &&
+        gs.ts_at >= 1 && gs.ts_at < gs.dyn_iters) {
+        HIP_OK(hipStreamSynchronize(c->stream));
+        hipStream_t s0 = c->stream;
+        c->stream = c->side;
+        hipGraph_t g = nullptr;
+        HIP_OK(hipStreamBeginCapture(c->side, hipStreamCaptureModeThreadLocal));
+        for (int cyc = 0; cyc < gs.ts_mg && !rc; cyc++) rc = mg_vcycle(c, 0);
+        const hipError_t ec = hipStreamEndCapture(c->side, &g);
+        c->stream = s0;
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        HIP_OK(ec);
+        const hipError_t ei = hipGraphInstantiate(&gs.mg_exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_OK(ei);
+    }
     if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
         if (gs.dres.alloc(NE) || gs.zc.alloc(NE) || gs.dq.alloc(NE) || gs.dzero.alloc(NE) ||
             gs.dmr.alloc(2 * MR_NB + 2))
@@ -2382,12 +2416,55 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
     int rc = 0;
+    /* the T/S right-hand side rr_TS - A_TS,D z_D is formed after ts_at dynamics passes (the
+     * CPU twin: orc_gs_apply); before the last pass, the T/S multigrid depends on nothing
+     * the remaining passes write and runs beside them on the side stream (one rank) */
+    const int ts_at = (!gs.dyn_mr && gs.ts_at >= 1 && gs.ts_at < gs.dyn_iters) ? gs.ts_at : gs.dyn_iters;
+    const bool early = ts_at < gs.dyn_iters;
+    const bool par = early && !band && gs.ts_mg > 0 && c->side;
+    auto mg_cycles = [&]() -> int {
+        if (gs.mg_exec) {
+            HIP_OK(hipGraphLaunch(gs.mg_exec, c->stream));
+            return 0;
+        }
+        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
+            if ((rc = mg_vcycle(c, 0))) return rc;
+        return 0;
+    };
+    auto ts_rhs = [&]() -> int {
+        if (band && (early || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
+        if ((n & 1) == 0) {
+            hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                               gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
+        } else {
+            hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                               gs.bts.p, L);
+            if (gs.ts_mg > 0) {
+                HIP_OK(hipMemsetAsync(gs.zt.p, 0, sizeof(double) * c->next, s));
+                HIP_OK(hipMemsetAsync(gs.zs.p, 0, sizeof(double) * c->next, s));
+            }
+        }
+        if (par) {
+            /* fork: the side stream runs the V-cycles on (bts, zt, zs, mg_*), which the
+             * remaining dynamics passes neither read nor write (one graph launch, so the
+             * host's work for it never holds up the main stream) */
+            HIP_OK(hipEventRecord(c->ev_fork, s));
+            HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+            c->stream = c->side;
+            rc = mg_cycles();
+            c->stream = s;
+            if (rc) return rc;
+            HIP_OK(hipEventRecord(c->ev_join, c->side));
+        }
+        return 0;
+    };
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
     if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;
+    if (early && ts_at == 1 && (rc = ts_rhs())) return rc;
     /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
      * minimal-residual w (dyn_mr) or the fixed w = dyn_omega */
     if (gs.dyn_mr && gs.dyn_iters > 1) {
@@ -2411,21 +2488,15 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
         if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
         if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
         hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zc.p, z, L, gs.dyn_omega);
+        if (early && it + 1 == ts_at && (rc = ts_rhs())) return rc;
     }
-    if (band && gs.dyn_iters > 1 && (rc = halo_exchange(c, z, 1))) return rc;
+    if (!early && (rc = ts_rhs())) return rc;
     if (gs.ts_mg > 0) {
         /* T/S by aggregation-multigrid V-cycles on (zt, zs) with rhs bts */
-        if ((n & 1) == 0) {
-            hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                               gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
-        } else {
-            hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                               gs.bts.p, L);
-            HIP_OK(hipMemsetAsync(gs.zt.p, 0, sizeof(double) * c->next, s));
-            HIP_OK(hipMemsetAsync(gs.zs.p, 0, sizeof(double) * c->next, s));
-        }
-        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
-            if ((rc = mg_vcycle(c, 0))) return rc;
+        if (par)
+            HIP_OK(hipStreamWaitEvent(s, c->ev_join, 0));   /* join */
+        else if ((rc = mg_cycles()))
+            return rc;
         hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
         HIP_OK(hipGetLastError());
         return 0;
@@ -2434,8 +2505,6 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     if ((n & 1) == 0) {
         /* colour-compacted symmetric red-black sweeps */
         const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
-        hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                           gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
         const int seq[4] = {0, 1, 1, 0};
         for (int sw = 0; sw < nsw; sw++)
             for (int h = 0; h < 4; h++)
@@ -2443,8 +2512,6 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
                                    gs.zt.p, gs.zs.p, L, seq[h]);
         hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
     } else {
-        hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                           gs.bts.p, L);
         /* symmetric sweeps: colours forward then backward */
         const bool four = c->cfg.periodic && (n & 1);
         const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};

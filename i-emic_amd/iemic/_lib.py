@@ -40,7 +40,8 @@ class Krylov(C.Structure):
                 ("prec", C.c_int), ("ts_sweeps", C.c_int), ("orth", C.c_int),
                 ("dyn_iters", C.c_int), ("method", C.c_int), ("ts_mg", C.c_int),
                 ("mg_sweeps", C.c_int), ("dyn_omega", C.c_double), ("dyn_mr", C.c_int),
-                ("idr_s", C.c_int), ("idr_angle", C.c_double), ("idr_replace", C.c_int)]
+                ("idr_s", C.c_int), ("idr_angle", C.c_double), ("idr_replace", C.c_int),
+                ("ts_at", C.c_int)]
 
 
 class SolveInfo(C.Structure):
@@ -116,6 +117,7 @@ def lib():
         "iemic_solve_dev": (C.c_int, [vp, vp, vp, P(Krylov), P(SolveInfo)]),
         "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
         "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
+        "iemic_time_prec": (C.c_int, [vp, C.c_int, PD, PD]),
         "iemic_time_spmv_cold": (C.c_int, [vp, C.c_int, vp, C.c_int64, PD]),
         "iemic_set_intcond_correction": (C.c_int, [vp, PD]),
         "iemic_get_intcond_correction": (C.c_int, [vp, PD]),
@@ -143,7 +145,7 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
-            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold",
+            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold", "iemic_time_prec",
             "iemic_ilu_create", "iemic_ilu_compute", "iemic_ilu_apply", "iemic_ilu_apply_dev",
             "iemic_ilu_stats", "iemic_ilu_destroy")
 

@@ -57,7 +57,7 @@ class Ocean:
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
               "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
               "Solver": "FGMRES", "IDR s": 4, "IDR angle": 0.7, "IDR replace residuals": False,
-              "Multigrid sweeps": 1}
+              "Multigrid sweeps": 1, "TS after dyn pass": 0}
         if solver_params:
             sp.update(solver_params)
         self.solver_params = sp
@@ -228,7 +228,7 @@ class Ocean:
                            int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]),
                            float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])),
                            int(sp["IDR s"]), float(sp["IDR angle"]),
-                           int(bool(sp["IDR replace residuals"])))
+                           int(bool(sp["IDR replace residuals"])), int(sp["TS after dyn pass"]))
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""
@@ -302,6 +302,13 @@ class Ocean:
         ms = C.c_double()
         check(lib().iemic_time_spmv(self._h, int(nrep), C.byref(ms)), "iemic_time_spmv")
         return ms.value
+
+    def time_prec(self, nrep: int = 20):
+        """(GPU ms, host enqueue ms) per preconditioner apply, nrep applies back to back."""
+        ms, hms = C.c_double(), C.c_double()
+        self.buildPreconditioner()
+        check(lib().iemic_time_prec(self._h, int(nrep), C.byref(ms), C.byref(hms)), "iemic_time_prec")
+        return ms.value, hms.value
 
     def time_spmv_cold(self, flush_ptr: int, flush_bytes: int, nrep: int = 10) -> float:
         """Mean SpMV kernel ms with the Infinity Cache flushed (device memset of a caller

@@ -87,6 +87,10 @@ typedef struct {
     int idr_s;                   /* "IDR s" (default 4)                               */
     double idr_angle;            /* "IDR angle" (omega safeguard, default 0.7)         */
     int idr_replace;             /* "IDR replace residuals" (default 0)               */
+    int ts_at;                   /* block GS: form the T/S right-hand side after this  */
+                                 /* many dynamics passes (0: after the last); earlier, */
+                                 /* the T/S multigrid runs on a second stream beside   */
+                                 /* the remaining passes (one rank)                    */
 } iemic_krylov;
 
 typedef struct {
@@ -191,6 +195,10 @@ int iemic_newton_step(iemic_ctx* ctx, const iemic_krylov* opt, iemic_newton_info
 /* ---- profiling helpers (bench): time n launches of the SpMV kernel with HIP events
  * on the stream it runs on; returns mean kernel milliseconds. */
 int iemic_time_spmv(iemic_ctx* ctx, int nrep, double* ms_per_launch);
+/* measurement helper (no reference counterpart): nrep back-to-back preconditioner applies
+ * (iemic_prec_compute first) on the device, GPU ms per apply (events) and host ms per apply
+ * spent enqueueing */
+int iemic_time_prec(iemic_ctx* ctx, int nrep, double* ms_per_apply, double* host_ms_per_apply);
 /* Same, with the Infinity Cache flushed before every launch (a streaming read of
  * flush_bytes of flush_dev on the library stream, outside the timed span): the cold rate. */
 int iemic_time_spmv_cold(iemic_ctx* ctx, int nrep, void* flush_dev, int64_t flush_bytes,

@@ -37,6 +37,7 @@ typedef struct {
     /* variant of prec_gs.hip's defaults: defect-correction passes on the dynamics block,
      * T/S by aggregation-multigrid V-cycles (orc_gs_config) */
     int dyn_iters, ts_mg;
+    int ts_at;                       /* T/S right-hand side after this many dynamics passes */
     double dyn_omega;
     double *dres, *zc;
     void* mg;
@@ -845,6 +846,33 @@ int orc_gs_config(void* h, int dyn_iters, double omega, int ts_mg)
     return 0;
 }
 
+/* 6. T/S right-hand side bts = rr_TS - A_TS,D z_D (z's T/S entries stay 0 until the T/S
+ * solve) */
+static void ts_rhs(gs_t* g, double* z)
+{
+    const int64_t N = g->N;
+    const uint8_t* kn = g->known;
+#pragma omp parallel for schedule(static)
+    for (int64_t row = 0; row < N; row++) {
+        int var = (int)(row % NUN);
+        if (var < TT || kn[row]) continue;
+        double acc = g->rr[row];
+        for (int64_t p = g->rowptr[row]; p < g->rowptr[row + 1]; p++) {
+            int cv = g->col[p] % NUN;
+            if (cv == TT || cv == SS || kn[g->col[p]]) continue;
+            acc -= g->val[p] * z[g->col[p]];
+        }
+        g->bts[row] = acc;
+        z[row] = 0.0;
+    }
+}
+
+/* the T/S right-hand side after ts_at dynamics passes (0: after the last one) */
+void orc_gs_ts_at(void* h, int ts_at)
+{
+    ((gs_t*)h)->ts_at = ts_at;
+}
+
 void orc_gs_apply(void* h, const double* r, double* z)
 {
     gs_t* g = (gs_t*)h;
@@ -863,27 +891,17 @@ void orc_gs_apply(void* h, const double* r, double* z)
     }
     double* rr = g->rr;
     dyn_solve(g, rr, z);
-    /* defect correction: z_D += omega M_D^-1 (rr - A z)_D */
+    /* defect correction: z_D += omega M_D^-1 (rr - A z)_D; the T/S right-hand side
+     * rr_TS - A_TS,D z_D is formed after ts_at passes (default: all of them) */
+    const int ts_at = (g->ts_at >= 1 && g->ts_at < g->dyn_iters) ? g->ts_at : g->dyn_iters;
+    if (ts_at == 1) ts_rhs(g, z);
     for (int it = 1; it < g->dyn_iters; it++) {
         dyn_defect(g, z, g->dres);
         memset(g->zc, 0, sizeof(double) * N);
         dyn_solve(g, g->dres, g->zc);
         for (int64_t row = 0; row < N; row++)
             if (row % NUN <= PP && !kn[row]) z[row] += g->dyn_omega * g->zc[row];
-    }
-    /* 6. T/S */
-#pragma omp parallel for schedule(static)
-    for (int64_t row = 0; row < N; row++) {
-        int var = (int)(row % NUN);
-        if (var < TT || kn[row]) continue;
-        double acc = rr[row];
-        for (int64_t p = g->rowptr[row]; p < g->rowptr[row + 1]; p++) {
-            int cv = g->col[p] % NUN;
-            if (cv == TT || cv == SS || kn[g->col[p]]) continue;
-            acc -= g->val[p] * z[g->col[p]];
-        }
-        g->bts[row] = acc;
-        z[row] = 0.0;
+        if (it + 1 == ts_at) ts_rhs(g, z);
     }
     if (g->ts_mg > 0 && g->mg) {
         mg_begin(g, g->mg, z);

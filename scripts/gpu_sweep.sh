@@ -1,6 +1,6 @@
 #!/bin/bash
 # Preconditioner-parameter sweep of the Newton-step bench (one GPU call): each line of
-# $SWEEP is a set of bench.py flags; results go to gpurun_out/sweep/<n>.json.
+# $SWEEP (or the file $SWEEP_FILE) is a set of bench.py flags; results go to gpurun_out/sweep/<n>.json.
 set -o pipefail
 mkdir -p gpurun_out/sweep
 export TMPDIR=/tmp
@@ -11,5 +11,5 @@ while IFS= read -r flags; do
   echo "$flags" > gpurun_out/sweep/$n.flags
   timeout -k 10 120 python -u bench.py --steps 1 --warmup 1 --no-cpu --newton-seq 0 $flags \
       > gpurun_out/sweep/$n.json 2> gpurun_out/sweep/$n.err || { echo "sweep $n failed: $flags"; exit 1; }
-done <<< "$SWEEP"
+done <<< "${SWEEP:-$(cat ${SWEEP_FILE:-/dev/null})}"
 echo "sweep ok ($n runs)"
