@@ -1187,6 +1187,69 @@ __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __rest
     for (int e = 0; e < 4; e++) tic[(int64_t)(c * 4 + e) * half + q] = tsinv[4 * cell + e];
 }
 
+/* T/S right-hand side bts = rr_TS - A_TS,D z_D into the colour layout and bts; zt = zs = 0.
+ * One wave per (64 cells, T or S row): the row's 10 dynamics slots unrolled at compile
+ * time, neighbour indices clamped as in the SpMV (the ELL holds zeros outside the domain),
+ * identity-row columns (their couplings are in rr already) skipped by the slot bitmask
+ * kmask instead of a byte gather per slot.  Dealt to the XCDs in contiguous runs. */
+template <int R>
+__device__ __forceinline__ double bts_row(const double* __restrict__ val, const double* __restrict__ z,
+                                          int64_t lc, int64_t nloc, const int* rb, const int* ii,
+                                          uint64_t kbits, double acc)
+{
+    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const Slot sl = SLOTS[B + s];
+        if (sl.var == TT || sl.var == SS) continue;
+        if ((kbits >> (B + s - 64)) & 1) continue;
+        const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
+        acc -= val[(int64_t)(B + s) * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+    }
+    return acc;
+}
+__global__ void __launch_bounds__(128) k_gs_bts2(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                                                 const uint64_t* __restrict__ kmask,
+                                                 const double* __restrict__ rr, const double* __restrict__ z,
+                                                 double* __restrict__ bc, double* __restrict__ zt,
+                                                 double* __restrict__ zs, Lay L, double* __restrict__ bts,
+                                                 int nblk)
+{
+    LAY_ALIASES;
+    const int per = (nblk + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= nblk) return;
+    const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
+    if (lc >= L.nloc) return;
+    const int R = TT + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int i, j, k;
+    lc_ijk(L, lc, i, j, k);
+    const int64_t cell = L.own0 + lc;
+    int ii[3] = {i - 1, i, i + 1};
+    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
+    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
+    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
+    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
+    int rb[9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - L.jb0 + HALO) * l + kk[a]) * n;
+    const int64_t row = NUN * cell + R;
+    double acc = 0.0;
+    if (!known[row]) {
+        const uint64_t kb = kmask[2 * cell + 1];
+        acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, rb, ii, kb, rr[row])
+                      : bts_row<SS>(val, z, lc, L.nloc, rb, ii, kb, rr[row]);
+    }
+    const int64_t half = L.nloc / 2;
+    const int c = (i + j + k) & 1;
+    bc[(int64_t)(c * 2 + (R - TT)) * half + (lc >> 1)] = acc;
+    bts[row] = acc;
+    if (R == TT) zt[cell] = 0.0;
+    else zs[cell] = 0.0;
+}
+
 /* T/S right-hand side into the colour layout; zt = zs = 0 */
 __global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ rr, const double* __restrict__ z,
@@ -2434,8 +2497,9 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     auto ts_rhs = [&]() -> int {
         if (band && (early || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
         if ((n & 1) == 0) {
-            hipLaunchKernelGGL(k_gs_bts_c, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                               gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p);
+            const int nblk = (int)((c->nloc + 63) / 64);
+            hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, c->d_val.p,
+                               gs.known.p, gs.kmask.p, gs.rr.p, z, gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p, nblk);
         } else {
             hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
                                gs.bts.p, L);
