@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) k_spmv2(int n, int m, int l, int periodic
  * adjacent cells of one slot), the per-lane work is one row (7-24 slots), and the grid
  * has 6x more wavefronts than a thread-per-cell launch, enough to keep HBM busy at the
  * 2-degree size (233k cells per GPU).  Blocks are dealt to the XCDs in contiguous runs. */
-template <int R>
+template <int R, bool NT = false>
 __device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, const double* __restrict__ x,
                                              int64_t lc, int64_t nloc, const int* rb, const int* ii)
 {
@@ -155,7 +155,8 @@ __device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, con
     for (int s = 0; s < NS; s++) {
         const Slot sl = SLOTS[B + s];
         const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
-        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * (int64_t)cidx + sl.var];
+        const double* vp = val + (int64_t)(B + s) * nloc + lc;
+        acc += (NT ? __builtin_nontemporal_load(vp) : *vp) * x[NUN * (int64_t)cidx + sl.var];
     }
     return acc;
 }
@@ -212,12 +213,14 @@ __host__ __device__ constexpr int sp7_combo(int dj, int dk)
 {
     return dk == 0 ? (dj + 1) : (dk == -1 ? (dj == 0 ? 3 : 5) : 4);  /* (-1,0)0 (0,0)1 (1,0)2 (0,-1)3 (0,1)4 (1,-1)5 */
 }
-template <int S0, int S1>
+template <int S0, int S1, bool NT = false>
 __device__ __forceinline__ void sp7_load(const double* __restrict__ val, int64_t nloc, int64_t lc, bool act,
                                          double* v)
 {
 #pragma unroll
-    for (int s = S0; s < S1; s++) v[s - S0] = act ? val[(int64_t)s * nloc + lc] : 0.0;
+    for (int s = S0; s < S1; s++)
+        v[s - S0] = !act ? 0.0 : NT ? __builtin_nontemporal_load(val + (int64_t)s * nloc + lc)
+                                    : val[(int64_t)s * nloc + lc];
 }
 template <int S0, int S1>
 __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, int c, double* acc)
@@ -229,6 +232,7 @@ __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, i
         acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
     }
 }
+template <bool NT>
 __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic, int jb0,
                                                const double* __restrict__ val,
                                                const double* __restrict__ x,
@@ -265,10 +269,10 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
     double acc[3] = {0.0, 0.0, 0.0};
     double v[26];
     /* the coefficient loads are issued before the barrier, overlapping the x staging */
-    if (g == 0) sp7_load<0, 26>(val, nloc, lc, act, v);
-    else if (g == 1) sp7_load<26, 52>(val, nloc, lc, act, v);
-    else if (g == 2) sp7_load<52, 78>(val, nloc, lc, act, v);
-    else sp7_load<78, 104>(val, nloc, lc, act, v);
+    if (g == 0) sp7_load<0, 26, NT>(val, nloc, lc, act, v);
+    else if (g == 1) sp7_load<26, 52, NT>(val, nloc, lc, act, v);
+    else if (g == 2) sp7_load<52, 78, NT>(val, nloc, lc, act, v);
+    else sp7_load<78, 104, NT>(val, nloc, lc, act, v);
     __syncthreads();
     if (g == 0) sp7_compute<0, 26>(v, xs, c, acc);
     else if (g == 1) sp7_compute<26, 52>(v, xs, c, acc);
@@ -363,6 +367,7 @@ __global__ void __launch_bounds__(256) k_spmv7_dyn(int n, int m, int l, int peri
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
  * full rows of the SpMV are used: one wavefront per (64 cells, dynamics equation). */
+template <bool NT>
 __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int periodic, int jb0,
                                                   const double* __restrict__ val,
                                                   const double* __restrict__ z,
@@ -394,10 +399,10 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int perio
     }
     double acc;
     switch (R) {
-    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, rb, ii); break;
-    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, rb, ii); break;
-    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, rb, ii); break;
-    default: acc = row_dot_rb<PP>(val, z, lc, nloc, rb, ii); break;
+    case UU: acc = row_dot_rb<UU, NT>(val, z, lc, nloc, rb, ii); break;
+    case VV: acc = row_dot_rb<VV, NT>(val, z, lc, nloc, rb, ii); break;
+    case WW: acc = row_dot_rb<WW, NT>(val, z, lc, nloc, rb, ii); break;
+    default: acc = row_dot_rb<PP, NT>(val, z, lc, nloc, rb, ii); break;
     }
     d[row] = r[row] - acc;
 }
@@ -418,8 +423,12 @@ int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_
     }
     const int nblk = (int)((c->nloc + 63) / 64);
     const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
-                       c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
+    if (variant == 8)          /* 8: the coefficient stream read non-temporally */
+        hipLaunchKernelGGL(k_spmv_dyn<true>, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
+                           c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
+    else
+        hipLaunchKernelGGL(k_spmv_dyn<false>, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
+                           c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
     return 0;
 }
 
@@ -676,14 +685,19 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
     hipStream_t s = c->stream;
     static const int variant = [] {
         const char* e = getenv("IEMIC_SPMV");
-        return e ? atoi(e) : 7;
+        return e ? atoi(e) : 8;       /* 8: in-solve 43.4 us vs 45.9 us (7) at 2 degrees */
     }();
-    if (variant == 7 && c->nloc < INT32_MAX) {
+    if ((variant == 7 || variant == 8) && c->nloc < INT32_MAX) {
+        /* 8: the coefficient stream read non-temporally */
         const int tpr = (c->n + SP7_T - 1) / SP7_T;
         const int ntile = (int)(c->nloc / c->n) * tpr;
         const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-        hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
-                           c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
+        if (variant == 8)
+            hipLaunchKernelGGL(k_spmv7<true>, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
+                               c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
+        else
+            hipLaunchKernelGGL(k_spmv7<false>, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
+                               c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
     } else if (variant == 6 || variant == 7) {
         const int nblk = (int)((c->nloc + 63) / 64);
         const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
