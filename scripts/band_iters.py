@@ -1,6 +1,7 @@
 """FGMRES steps of the bench's Newton step when the grid is split into N latitude bands
-(in-process group on one GPU): the block-GS couples the bands block-Jacobi style, so the
-step count is what the multi-GPU bench pays per band.  usage: python scripts/band_iters.py"""
+(in-process group on one GPU) at the bench's branch state (STATE=synthetic: the synthetic
+state): the step count is what the multi-GPU bench pays per band.
+usage: python scripts/band_iters.py ['{"solver param": value}'] [1,2,4,8]"""
 import os
 import sys
 import threading
@@ -47,7 +48,12 @@ def main():
     ns = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4, 8]
     c = cf.preset("global2", mixing=1)
     L0 = cf.init_landmask(c, cf.landmask(c))
-    x = cf.synthetic_state(c, L0, amp_ts=1e-3)
+    fix = os.path.join(ROOT, "bench_data", "global2_cf05.npz")
+    if os.path.exists(fix) and os.environ.get("STATE", "branch") == "branch":
+        with np.load(fix, allow_pickle=False) as d:
+            x = d["x"].astype(np.float64)
+    else:
+        x = cf.synthetic_state(c, L0, amp_ts=1e-3)
     for n in ns:
         print(n, run(n, c, L0, x), flush=True)
 
