@@ -34,7 +34,7 @@ extern "C" int iemic_device_count(void)
     return n;
 }
 
-Geo iemic_ctx::geo() const { return su.geo(d_landm.p, d_tab.p); }
+Geo iemic_ctx::geo() const { return su.geo(d_landm.p, d_tab.p, d_atm.p); }
 
 iemic_ctx::~iemic_ctx()
 {
@@ -222,6 +222,7 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     rc |= c->d_frc.alloc(NE);
     rc |= c->d_qcor.alloc(8);
     rc |= c->d_intc.alloc(NE);
+    rc |= c->d_atm.alloc((size_t)3 * n * m);
     rc |= c->d_x.alloc(NE);
     rc |= c->d_F.alloc(NE);
     rc |= c->d_B.alloc(NE);
@@ -237,7 +238,7 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
         delete c;
         return IEMIC_ENOMEM;
     }
-    for (DevBuf<double>* b : {&c->d_x, &c->d_F, &c->d_B, &c->d_frc, &c->d_tmp1, &c->d_tmp2})
+    for (DevBuf<double>* b : {&c->d_x, &c->d_F, &c->d_B, &c->d_frc, &c->d_tmp1, &c->d_tmp2, &c->d_atm})
         (void)hipMemsetAsync(b->p, 0, sizeof(double) * b->n, c->stream);
     if (c->d_tab.alloc(c->su.tab.size()) ||
         h2d(c, c->d_tab.p, c->su.tab.data(), sizeof(double) * c->su.tab.size()) != 0) {
@@ -320,6 +321,53 @@ __global__ void k_ref_to_ext(const double* __restrict__ ref, double* __restrict_
     for (int v = 0; v < NUN; v++) ext[e + v] = ref[r + v];
 }
 }  // namespace iemic
+
+/* Ocean::synchronize(atmos) (Ocean.C:1443-1472): THCM::setAtmosphereT/Q/A/P (inserted
+ * into tatm/qatm/albe/patm, inserts.F90:12-100) and set_atmos_parameters (usrc.F90:237-293:
+ * CommPars -> qdim, eta, dqso, eo0, albe0, albed, nus, lvsc; then forcing and lin).  The
+ * fields are n*m surface vectors, (j, i) with i fastest; p (patm) only enters with
+ * "Coupled Salinity" = 1, which is not supported. */
+extern "C" int iemic_set_atmosphere(iemic_ctx* c, const double* t, const double* q, const double* a,
+                                    const double* p, const double* commpars)
+{
+    CTX_CHECK(c);
+    (void)p;
+    if (!c->cfg.coupled_t) {
+        set_error("iemic_set_atmosphere: the context was not created with coupled_t = 1");
+        return IEMIC_EINVAL;
+    }
+    if (!t || !q || !a || !commpars) return IEMIC_EINVAL;
+    const size_t nm = (size_t)c->n * c->m;
+    int rc = h2d(c, c->d_atm.p, t, sizeof(double) * nm);
+    if (!rc) rc = h2d(c, c->d_atm.p + nm, q, sizeof(double) * nm);
+    if (!rc) rc = h2d(c, c->d_atm.p + 2 * nm, a, sizeof(double) * nm);
+    if (rc) return rc;
+    c->su.set_atmos(commpars);
+    c->jac_valid = 0;
+    return compute_forcing(c);
+}
+
+/* getdeps (usrc.F90:201-219): Ooa, Os, nus, eta, lvsc, qdim, pQSnd */
+extern "C" int iemic_get_deps(iemic_ctx* c, double* out7)
+{
+    if (!c || !out7) return IEMIC_EINVAL;
+    const host::Setup& su = c->su;
+    const double v[7] = {su.Ooa, su.Os, su.nus, su.eta_a, su.lvsc, su.qdim_a,
+                         su.par[P_COMB] * su.par[P_SALT] * su.qsnd};
+    for (int i = 0; i < 7; i++) out7[i] = v[i];
+    return 0;
+}
+
+/* THCM::getSunO (THCM.C:1517-1527, m_probe get_suno): suno(j) on the n*m surface */
+extern "C" int iemic_get_suno(iemic_ctx* c, double* out_nm)
+{
+    if (!c || !out_nm) return IEMIC_EINVAL;
+    const host::Setup& su = c->su;
+    const double* suno = su.tab.data() + 9 * (su.m + 2) + 2 * (su.l + 2);
+    for (int j = 0; j < su.m; j++)
+        for (int i = 0; i < su.n; i++) out_nm[(size_t)j * su.n + i] = suno[j + 1];
+    return 0;
+}
 
 extern "C" int iemic_set_par(iemic_ctx* c, int idx, double value)
 {

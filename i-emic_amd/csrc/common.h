@@ -170,6 +170,7 @@ struct iemic_ctx {
     iemic::DevBuf<double> d_frc;     /* Frc (forcing.F90), before boundaries zeroing     */
     iemic::DevBuf<double> d_qcor;    /* qint corrections                                 */
     iemic::DevBuf<double> d_intc;    /* intcond coefficients (THCM.C:2549)               */
+    iemic::DevBuf<double> d_atm;     /* coupled: tatm | qatm | albe (n*m each, surface)  */
     /* state and operator */
     iemic::DevBuf<double> d_x, d_F, d_B, d_val; /* d_val: NSLOT x ncell                    */
     iemic::DevBuf<double> d_tmp1, d_tmp2, d_red;

@@ -31,6 +31,9 @@ constexpr double omegadim = 7.292e-05, r0dim = 6.37e+06, udim = 0.1e+00, gdim = 
 constexpr double rhodim = 1.024e+03, deltas = 1.0, s0 = 35.0, cp0 = 4.2e+03;
 constexpr double ah = 2.5e+05, av = 1.0e-03, kappah = 1.0e+03, kappav = 1.0e-04;
 constexpr double zmin = -1.0, zmax = 0.0;
+/* m_atm constants (atm.F90:5-19) */
+constexpr double rhoa_atm = 1.25, ch_atm = 0.94 * 1.3e-03, cpa_atm = 1000., uw_atm = 8.5;
+constexpr double sun0_atm = 1360., c0_atm = 0.43, lv_atm = 2.5e+06;
 
 inline double fz(double z, double qz)
 {
@@ -79,6 +82,25 @@ struct Setup {
     std::vector<double> tab;         /* Geo table block (see geo())            */
     double par[31] = {0};
     double qtnd = 0, qsnd = 0;
+    /* coupled atmosphere (m_atm): Ooa, Os from atmos_coef (usrc.F90:1183-1223); the
+     * CommPars-derived values from set_atmos_parameters (usrc.F90:237-293), zero before */
+    double Ooa = 0, Os = 0, lvsc = 0, eta_a = 0, qdim_a = 0, dqso = 0, eo0 = 0, albe0 = 0,
+           albed = 0, nus = 0;
+    /* set_atmos_parameters: pars = AtmosLocal::CommPars (tdim, qdim, nuq, eta, dqso, dqsi,
+     * dqdt, Eo0, Ei0, Cs, t0o, t0i, a0, da, tauf, tauc, comb, albf) */
+    void set_atmos(const double* pars)
+    {
+        qdim_a = pars[1];
+        eta_a = pars[3];
+        dqso = pars[4];
+        eo0 = pars[7];
+        albe0 = pars[12];
+        albed = pars[13];
+        nus = par[P_COMB] * par[P_SALT] * eta_a * qdim_a * qsnd;
+        lvsc = par[P_COMB] * par[P_TEMP] * rhodim * lv_atm * qtnd;
+    }
+    /* lin's latent-heat coefficient dedt = lvsc eta qdim (deltat/qdim) dqso (usrc.F90:726) */
+    double dedt() const { return lvsc * eta_a * qdim_a * (1.0 / qdim_a) * dqso; }
     int rowintcon_ref = -1;          /* reference (global) row of the integral condition */
     int64_t rowintcon = -1;          /* its ext row when this band owns it, else -1       */
     int jb0 = 0, jb1 = 0;            /* owned latitude band [jb0, jb1)                    */
@@ -168,7 +190,7 @@ struct Setup {
         }
         dfzW[0] = dfdz(zmin, cfg.qz);
         const int ih = cfg.ih;
-        tab.assign((size_t)9 * M2 + 2 * (l + 2), 0.0);
+        tab.assign((size_t)10 * M2 + 2 * (l + 2), 0.0);
         for (int j = 0; j <= m + 1; j++) {
             tab[j] = std::cos(y[j]);
             tab[4 * M2 + j] = amh(y[j], ih);
@@ -189,6 +211,15 @@ struct Setup {
         double dzne = dz * dfzT[l];
         qtnd = r0dim / (udim * cp0 * rhodim * cfg.hdim * dzne);
         qsnd = s0 * r0dim / (deltas * udim * cfg.hdim * dzne);
+        /* atmos_coef (usrc.F90:1183-1223) with the m_atm constants (atm.F90:5-19) */
+        const double muoa = rhoa_atm * ch_atm * cpa_atm * uw_atm;
+        Os = sun0_atm * c0_atm / 4 * qtnd;
+        Ooa = muoa * qtnd;
+        double* suno = tab.data() + 9 * M2 + 2 * (l + 2);
+        for (int j = 1; j <= m; j++) {
+            const double sy = std::sin(y[j]);
+            suno[j] = Os * (1 - .482 * (3 * (sy * sy) - 1.) / 2.);
+        }
     }
 
     void stpnt()
@@ -355,7 +386,7 @@ struct Setup {
     }
 
     /* Geo over externally owned copies of landm / tab */
-    Geo geo(const int* landm_p, const double* tab_p) const
+    Geo geo(const int* landm_p, const double* tab_p, const double* atm_p = nullptr) const
     {
         Geo g{};
         g.n = n; g.m = m; g.l = l;
@@ -381,6 +412,17 @@ struct Setup {
         g.vmix_s = cfg.vmix != 0 && vmix_s;
         g.rho_mixing = cfg.rho_mixing;
         g.alphaT = cfg.alpha_t;
+        g.coupled_t = cfg.coupled_t;
+        g.Ooa = Ooa;
+        g.dedt = qdim_a != 0.0 ? dedt() : 0.0;
+        g.lvsc = lvsc;
+        g.eta_a = eta_a;
+        g.qdim_a = qdim_a;
+        g.eo0 = eo0;
+        g.albe0 = albe0;
+        g.albed = albed;
+        g.suno = tab_p + 9 * M2 + 2 * (l + 2);
+        g.atm = atm_p;
         return g;
     }
 };

@@ -134,6 +134,13 @@ struct Geo {
      * vmix_init/vmix_control), "Rho mixing", alphaT of the taper */
     int vmix_t, vmix_s, rho_mixing;
     double alphaT;
+    /* coupled atmosphere ("Coupled Temperature" = 1; usrc.F90:726-736, forcing.F90:75-95,
+     * m_atm after atmos_coef 1183-1223 and set_atmos_parameters 237-293).  No sea ice:
+     * the mask msi is zero, so its terms vanish */
+    int coupled_t;
+    double Ooa, dedt, lvsc, eta_a, qdim_a, eo0, albe0, albed;
+    const double* suno;             /* suno(j), j = 0..m+1 (atmos_coef)                 */
+    const double* atm;              /* tatm | qatm | albe, each (j-1)*n + (i-1), n*m    */
 };
 
 HD int LM(const Geo& g, int i, int j, int k)
@@ -430,6 +437,11 @@ template <int R> HD double lin_val(const Geo& g, const CellCtx& c, int pos, int 
         if (col == VV) return at_vyc(g, c, pos);
         if (col == WW) return at_wzc(g, c, pos);
     } else if (R == TT) {
+        /* coupled: + Ooa tc (sensible heat) + dedt sc (latent heat); the sea-ice terms
+         * (mc = 0) add zeros (usrc.F90:728-739) */
+        if (col == TT && g.coupled_t)
+            return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
+                   g.Ooa * at_tc(g, c, pos) + g.dedt * at_tc(g, c, pos);
         if (col == TT)
             return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
                    g.tres * bi * at_tc(g, c, pos);
@@ -1193,7 +1205,18 @@ HD void forcing_cell(const Geo& g, const double* ftab, const double* qcor, int i
             f[VV] = sigma * 0.0;
         }
         const double etabi = par[P_COMB] * par[P_TEMP] * ((double)(1 - TRES) + TRES * par[P_BIOT]);
-        f[TT] = etabi * (temf[j] - qcor[0]);
+        if (g.coupled_t) {
+            /* QToa = QSW - QSH - QLH from the atmosphere fields (forcing.F90:75-94); the
+             * sea-ice mix msi (QTos - QToa) is zero */
+            const int64_t q = (int64_t)(j - 1) * n + (i - 1);
+            const int64_t nm = (int64_t)n * m;
+            const double tatm = g.atm[q], qatm = g.atm[nm + q], albe = g.atm[2 * nm + q];
+            const double QToa = par[P_COMB] * par[P_SUNP] * g.suno[j] * (1 - g.albe0 - g.albed * albe) +
+                                g.Ooa * tatm + g.lvsc * g.eta_a * g.qdim_a * qatm - g.lvsc * g.eo0;
+            f[TT] = QToa * (double)(1 - LM(g, i, j, l));
+        } else {
+            f[TT] = etabi * (temf[j] - qcor[0]);
+        }
         const double gamma = par[P_COMB] * par[P_SALT] * ((double)(1 - SRES) + SRES * par[P_BIOT]);
         const double emip = salf[j] * (1 - LM(g, i, j, l));
         f[SS] = gamma * (1 - par[P_HMTP]) * (emip - qcor[1]) +

@@ -63,6 +63,8 @@ typedef struct {
     int max_mask_fixes;          /* Ocean "Max mask fixes" (default 5)               */
     int device;                  /* HIP device ordinal                               */
     int rho_mixing;              /* "Rho mixing" (vmix_fun: mix T and S as density)  */
+    int coupled_t;               /* "Coupled Temperature" (THCM.C:232): surface heat    */
+                                 /* flux from an atmosphere (iemic_set_atmosphere)      */
 } iemic_grid;
 
 /* Krylov settings (Ocean.C:961-1020, getDefaultInitParameters 2232-2237). */
@@ -143,6 +145,20 @@ int  iemic_set_par(iemic_ctx* ctx, int idx, double value);
 int  iemic_set_intcond_correction(iemic_ctx* ctx, const double* x);
 int  iemic_get_intcond_correction(iemic_ctx* ctx, double* corr);
 int  iemic_get_par(iemic_ctx* ctx, int idx, double* value);
+
+/* ---- coupled atmosphere (grid.coupled_t = 1) ---------- */
+/* Ocean::synchronize(atmos), Ocean.C:1443-1472: atmosphere T, q, albedo and dimensional
+ * P on the n*m surface ((j, i), i fastest) and the 18 AtmosLocal::CommPars
+ * (AtmosLocal.H:40-60) -> THCM::setAtmosphereT/Q/A/P + set_atmos_parameters_
+ * (usrc.F90:237-293).  Refreshes the forcing; the next iemic_jacobian uses the new
+ * latent-heat coefficient. */
+int  iemic_set_atmosphere(iemic_ctx* ctx, const double* t, const double* q, const double* a,
+                          const double* p, const double* commpars);
+/* getdeps_ (usrc.F90:201-219, called by AtmosLocal::setup and Ocean::getBlock):
+ * out7 = Ooa, Os, nus, eta, lvsc, qdim, pQSnd */
+int  iemic_get_deps(iemic_ctx* ctx, double* out7);
+/* THCM::getSunO (THCM.C:1517-1527): suno(j) broadcast on the n*m surface */
+int  iemic_get_suno(iemic_ctx* ctx, double* out_nm);
 
 /* ---- geometry queries ------------------------------------------------------------ */
 int     iemic_nrows(const iemic_ctx* ctx);

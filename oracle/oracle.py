@@ -201,6 +201,14 @@ assert rc == 0, rc
 lib.thcmref_set_par.argtypes = [C.c_int, C.c_double]
 for idx, v in d["pars"]:
     lib.thcmref_set_par(int(idx), float(v))
+if "atm_t" in d.files:
+    atm = [np.ascontiguousarray(d["atm_" + k], dtype=np.float64) for k in "tqap"]
+    apars = np.ascontiguousarray(d["atm_pars"], dtype=np.float64)
+    lib.thcmref_set_atmos.argtypes = [C.c_void_p] * 5
+    lib.thcmref_set_atmos(*[a.ctypes.data for a in atm], apars.ctypes.data)
+deps = np.zeros(7)
+lib.thcmref_getdeps.argtypes = [C.c_void_p]
+lib.thcmref_getdeps(deps.ctypes.data)
 nrows = C.c_int(); cap = C.c_int()
 lib.thcmref_sizes(C.byref(nrows), C.byref(cap))
 N = nrows.value
@@ -220,6 +228,7 @@ lib.thcmref_get_par.restype = C.c_double
 lib.thcmref_get_par.argtypes = [C.c_int]
 for p in range(1, 31):
     out["par"][p] = lib.thcmref_get_par(p)
+out["deps"] = deps
 for s in range(int(d["nstates"])):
     x = np.ascontiguousarray(d["x%d" % s])
     beg = np.zeros(N + 1, dtype=np.int32); jco = np.zeros(cap.value, dtype=np.int32)
@@ -238,7 +247,7 @@ def reference_available() -> bool:
 
 
 def run_reference(cfgdict: dict, landm, pars, states, use_landm: bool = True,
-                  timeout: float = 600.0) -> dict:
+                  timeout: float = 600.0, atmos: dict | None = None) -> dict:
     """Run the reference THCM Fortran (init, setparcs, matrix, rhs) in a fresh process.
 
     Returns dict with per-state Fortran CSR (beg/jco/co, 1-based), coB, rhs B, the local
@@ -262,6 +271,12 @@ def run_reference(cfgdict: dict, landm, pars, states, use_landm: bool = True,
                     nstates=np.array(len(states)))
         for s, x in enumerate(states):
             arrs["x%d" % s] = np.ascontiguousarray(x, dtype=np.float64)
+        if atmos is not None:
+            # coupled ocean (coupled_T = 1): atmosphere fields t, q, a, p (n*m each) and the
+            # 18 AtmosLocal::CommPars, inserted through Ocean::synchronize's Fortran calls
+            for k in "tqap":
+                arrs["atm_" + k] = np.ascontiguousarray(atmos[k], dtype=np.float64)
+            arrs["atm_pars"] = np.ascontiguousarray(atmos["pars"], dtype=np.float64)
         np.savez(inp, **arrs)
         script = os.path.join(td, "run.py")
         with open(script, "w") as f:

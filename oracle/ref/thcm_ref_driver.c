@@ -158,8 +158,9 @@ static void do_init(void* p)
     double* tatm = (double*)calloc(nm, sizeof(double));
     double* emip = (double*)calloc(nm, sizeof(double));
     double* spert = (double*)calloc(nm, sizeof(double));
-    /* iza==2, ite==1, its==1 (idealized) give zero fields (global.F90:432-563) */
-    if (iza != 2 || ite != 1 || its != 1 || cT != 0 || cS != 0) {
+    /* iza==2, ite==1, its==1 (idealized) give zero fields (global.F90:432-563); so does
+     * coupled_T = 1 (get_temforcing puts tatm = 0, global.F90:472-510) */
+    if (iza != 2 || ite != 1 || its != 1 || cT < 0 || cT > 1 || cS != 0) {
         fprintf(stderr, "thcm_ref: only idealized ocean-only forcing is supported\n");
         a->rc = -1;
         return;
@@ -259,4 +260,44 @@ int thcmref_intcond(double* val, int* ind)
     struct int_args a = {ind, val, &len};
     run_big_stack(do_intcond, &a);
     return len;
+}
+
+/* ---- coupled atmosphere (Ocean::synchronize(atmos), Ocean.C:1443-1472) ------------
+ * THCM::setAtmosphereT/Q/A/P -> m_inserts insert_atmosphere_{t,q,a,p} (inserts.F90:12-100),
+ * then set_atmos_parameters (usrc.F90:237-293: qdim, nuq, eta, dqso, eo0, albe0, albed,
+ * nus, lvsc; calls forcing and lin).  pars = AtmosLocal::CommPars (18 doubles, in order). */
+extern void _QMm_insertsPinsert_atmosphere_t(double*);
+extern void _QMm_insertsPinsert_atmosphere_q(double*);
+extern void _QMm_insertsPinsert_atmosphere_a(double*);
+extern void _QMm_insertsPinsert_atmosphere_p(double*);
+extern void set_atmos_parameters_(double*);
+extern void getdeps_(double*, double*, double*, double*, double*, double*, double*);
+
+struct atm_args { double *t, *q, *a, *p, *pars; };
+static void do_set_atmos(void* p)
+{
+    struct atm_args* a = (struct atm_args*)p;
+    _QMm_insertsPinsert_atmosphere_t(a->t);
+    _QMm_insertsPinsert_atmosphere_q(a->q);
+    _QMm_insertsPinsert_atmosphere_a(a->a);
+    _QMm_insertsPinsert_atmosphere_p(a->p);
+    set_atmos_parameters_(a->pars);
+}
+void thcmref_set_atmos(double* t, double* q, double* a, double* p, double* pars)
+{
+    struct atm_args x = {t, q, a, p, pars};
+    run_big_stack(do_set_atmos, &x);
+}
+
+struct deps_args { double* out; };
+static void do_getdeps(void* p)
+{
+    double* o = ((struct deps_args*)p)->out;
+    getdeps_(o, o + 1, o + 2, o + 3, o + 4, o + 5, o + 6);
+}
+/* getdeps (usrc.F90:201-219): Ooa, Os, nus, eta, lvsc, qdim, pQSnd */
+void thcmref_getdeps(double* out7)
+{
+    struct deps_args x = {out7};
+    run_big_stack(do_getdeps, &x);
 }

@@ -17,6 +17,8 @@ using namespace iemic;
 struct Emul {
     host::Setup su;
     std::vector<double> frc, qcor, val;
+    std::vector<double> atm;      /* coupled: tatm | qatm | albe (n*m each) */
+    const double* atm_p() const { return atm.empty() ? nullptr : atm.data(); }
 };
 
 template <int R>
@@ -57,7 +59,27 @@ void* emul_create_band(const iemic_grid* grid, const int* landm, int jb0, int jb
     Emul* e = new Emul();
     e->su.init(*grid, landm, jb0, jb1);
     e->su.vmix_init();
+    e->atm.assign((size_t)3 * e->su.n * e->su.m, 0.0);
     return e;
+}
+/* iemic_set_atmosphere (capi.hip) on the CPU */
+void emul_set_atmosphere(void* h, const double* t, const double* q, const double* a, const double* pars)
+{
+    Emul* e = (Emul*)h;
+    const size_t nm = (size_t)e->su.n * e->su.m;
+    for (size_t r = 0; r < nm; r++) {
+        e->atm[r] = t[r];
+        e->atm[nm + r] = q[r];
+        e->atm[2 * nm + r] = a[r];
+    }
+    e->su.set_atmos(pars);
+}
+void emul_get_deps(void* h, double* out7)
+{
+    const host::Setup& su = ((Emul*)h)->su;
+    const double v[7] = {su.Ooa, su.Os, su.nus, su.eta_a, su.lvsc, su.qdim_a,
+                         su.par[P_COMB] * su.par[P_SALT] * su.qsnd};
+    for (int i = 0; i < 7; i++) out7[i] = v[i];
 }
 void* emul_create(const iemic_grid* grid, const int* landm) { return emul_create_band(grid, landm, 0, -1); }
 void emul_destroy(void* h) { delete (Emul*)h; }
@@ -69,7 +91,7 @@ int64_t emul_ext_rows(void* h) { return NUN * ((Emul*)h)->su.next; }
 static void forcing(Emul* e)
 {
     const host::Setup& su = e->su;
-    Geo g = su.geo(su.landm.data(), su.tab.data());
+    Geo g = su.geo(su.landm.data(), su.tab.data(), e->atm_p());
     std::vector<double> ft = su.forcing_tables();
     e->qcor.assign(8, 0.0);
     forcing_qint(g, ft.data(), e->qcor.data(), su.cfg.tres == 0, su.cfg.sres == 0);
@@ -104,7 +126,7 @@ void emul_jacobian_ext(void* h, const double* x, double* B)
     Emul* e = (Emul*)h;
     mix_control(e, x);
     const host::Setup& su = e->su;
-    Geo g = su.geo(su.landm.data(), su.tab.data());
+    Geo g = su.geo(su.landm.data(), su.tab.data(), e->atm_p());
     const int64_t nloc = su.nloc;
     e->val.assign((size_t)NSLOT * nloc, 0.0);
     double* val = e->val.data();
@@ -132,7 +154,7 @@ void emul_rhs_ext(void* h, const double* x, double* F, double* intcond_partial)
     mix_control(e, x);
     forcing(e);
     const host::Setup& su = e->su;
-    Geo g = su.geo(su.landm.data(), su.tab.data());
+    Geo g = su.geo(su.landm.data(), su.tab.data(), e->atm_p());
     const int64_t nloc = su.nloc;
     rhs_rows<UU>(g, x, e->frc.data(), nloc, F);
     rhs_rows<VV>(g, x, e->frc.data(), nloc, F);

@@ -147,3 +147,18 @@ class Emul:
     def rhs(self, x):
         Fe, _ = self.rhs_ext(self.to_ext(x))
         return self.to_ref(Fe)
+
+
+def emul_set_atmosphere(e: "Emul", t, q, a, pars) -> None:
+    """iemic_set_atmosphere on the CPU emulation of the device assembly."""
+    lib = e.lib
+    lib.emul_set_atmosphere.argtypes = [C.c_void_p] + [P(C.c_double)] * 4
+    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (t, q, a, pars)]
+    lib.emul_set_atmosphere(e.h, *[_lib.ptr(v) for v in arrs])
+
+
+def emul_get_deps(e: "Emul") -> np.ndarray:
+    out = np.zeros(7)
+    e.lib.emul_get_deps.argtypes = [C.c_void_p, P(C.c_double)]
+    e.lib.emul_get_deps(e.h, _lib.ptr(out))
+    return out

