@@ -52,6 +52,14 @@ class SolveInfo(C.Structure):
                 ("n_spmv", C.c_int)]
 
 
+class AtmosParams(C.Structure):
+    """iemic_atmos_params (include/iemic.h; AtmosLocal::setParameters names in order)."""
+    NAMES = ["rhoa", "rhoo", "hdima", "hdimq", "cpa", "D0", "kappa", "arad", "brad", "sun0", "c0",
+             "ce", "ch", "uw", "t0a", "t0o", "t0i", "tdim", "q0", "qdim", "lv", "udim", "r0dim",
+             "a0", "da", "tauf_days", "tauc_days", "Tm", "Tr", "Pa", "epm", "epr", "epa"]
+    _fields_ = [(k, C.c_double) for k in NAMES] + [("par", C.c_double * 7)]
+
+
 class NewtonInfo(C.Structure):
     _fields_ = [("norm_f0", C.c_double), ("norm_f1", C.c_double), ("solve", SolveInfo),
                 ("t_jac_ms", C.c_double), ("t_rhs_ms", C.c_double), ("t_prec_ms", C.c_double),
@@ -127,6 +135,32 @@ def lib():
         "iemic_ilu_apply_dev": (C.c_int, [vp, vp, vp]),
         "iemic_ilu_stats": (C.c_int, [vp, PI, PI, PI]),
         "iemic_ilu_destroy": (None, [vp]),
+        "iemic_set_atmosphere": (C.c_int, [vp, PD, PD, PD, PD, PD]),
+        "iemic_get_deps": (C.c_int, [vp, PD]),
+        "iemic_get_suno": (C.c_int, [vp, PD]),
+        "iemic_atmos_default_params": (C.c_int, [P(AtmosParams)]),
+        "iemic_atmos_create": (C.c_int, [P(vp), vp, P(AtmosParams)]),
+        "iemic_atmos_destroy": (None, [vp]),
+        "iemic_atmos_dim": (C.c_int, [vp]),
+        "iemic_atmos_set_par": (C.c_int, [vp, C.c_int, C.c_double]),
+        "iemic_atmos_set_state": (C.c_int, [vp, PD]),
+        "iemic_atmos_get_state": (C.c_int, [vp, PD]),
+        "iemic_atmos_set_sst": (C.c_int, [vp, PD]),
+        "iemic_atmos_rhs": (C.c_int, [vp, PD]),
+        "iemic_atmos_jacobian": (C.c_int, [vp]),
+        "iemic_atmos_spmv": (C.c_int, [vp, PD, PD]),
+        "iemic_atmos_prec_apply": (C.c_int, [vp, PD, PD]),
+        "iemic_atmos_export_ell": (C.c_int, [vp, PD, PI]),
+        "iemic_atmos_integral_coeff": (C.c_int, [vp, PD, PD, PI, PI]),
+        "iemic_atmos_commpars": (C.c_int, [vp, PD]),
+        "iemic_atmos_pdist": (C.c_int, [vp, PD]),
+        "iemic_coupled_create": (C.c_int, [P(vp), vp, vp]),
+        "iemic_coupled_destroy": (None, [vp]),
+        "iemic_coupled_synchronize": (C.c_int, [vp]),
+        "iemic_coupled_rhs": (C.c_int, [vp, PD, PD]),
+        "iemic_coupled_jacobian": (C.c_int, [vp]),
+        "iemic_coupled_spmv": (C.c_int, [vp, PD, PD]),
+        "iemic_coupled_solve": (C.c_int, [vp, PD, PD, P(Krylov), P(SolveInfo)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -147,7 +181,16 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
             "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold", "iemic_time_prec",
             "iemic_ilu_create", "iemic_ilu_compute", "iemic_ilu_apply", "iemic_ilu_apply_dev",
-            "iemic_ilu_stats", "iemic_ilu_destroy")
+            "iemic_ilu_stats", "iemic_ilu_destroy",
+            "iemic_set_atmosphere", "iemic_get_deps", "iemic_get_suno",
+            "iemic_atmos_default_params", "iemic_atmos_create", "iemic_atmos_destroy",
+            "iemic_atmos_dim", "iemic_atmos_set_par", "iemic_atmos_set_state",
+            "iemic_atmos_get_state", "iemic_atmos_set_sst", "iemic_atmos_rhs",
+            "iemic_atmos_jacobian", "iemic_atmos_spmv", "iemic_atmos_prec_apply",
+            "iemic_atmos_export_ell", "iemic_atmos_integral_coeff", "iemic_atmos_commpars",
+            "iemic_atmos_pdist", "iemic_coupled_create", "iemic_coupled_destroy",
+            "iemic_coupled_synchronize", "iemic_coupled_rhs", "iemic_coupled_jacobian",
+            "iemic_coupled_spmv", "iemic_coupled_solve")
 
 
 class IemicError(RuntimeError):

@@ -1,0 +1,221 @@
+"""Atmosphere and CoupledModel host interfaces over the device library.
+
+Mirrors the reference's Model surface for the coupled configuration (BASELINE config C4):
+
+* ``Atmosphere`` -- src/atmosphere/Atmosphere.H: ``computeRHS``, ``computeJacobian``,
+  ``applyMatrix``, ``applyPrecon``, ``setPar`` (AtmosLocal allParameters_,
+  AtmosLocal.C:154-170), ``getState/setState``, ``setOceanTemperature``, ``getCommPars``.
+* ``CoupledModel`` -- src/coupledmodel/CoupledModel.H: ``synchronize``, ``computeRHS``,
+  ``computeJacobian``, ``applyMatrix``, ``solve`` (FGMRES + forward block Gauss-Seidel,
+  "Preconditioning" = 'F'), ``setPar`` on every model.
+
+Everything computes on the GPU through the C ABI (include/iemic.h); errors raise
+``IemicError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .ocean import Ocean
+
+__all__ = ["Atmosphere", "CoupledModel", "ATMOS_PARAMS"]
+
+# XML parameter names (AtmosLocal::setParameters, AtmosLocal.C:109-151) -> struct fields
+ATMOS_PARAMS = {
+    "atmospheric density": "rhoa", "oceanic density": "rhoo",
+    "atmospheric scale height": "hdima", "humidity scale height": "hdimq",
+    "heat capacity": "cpa", "temperature eddy diffusivity": "D0",
+    "humidity eddy diffusivity": "kappa", "radiative flux param A": "arad",
+    "radiative flux param B": "brad", "solar constant": "sun0",
+    "atmospheric absorption coefficient": "c0", "Dalton number": "ce",
+    "exchange coefficient ch": "ch", "mean atmospheric surface wind speed": "uw",
+    "background temperature atmosphere": "t0a", "background temperature ocean": "t0o",
+    "background temperature seaice": "t0i", "temperature scale": "tdim",
+    "atmos reference humidity": "q0", "atmos humidity scale": "qdim",
+    "latent heat of vaporization": "lv", "horizontal velocity of the ocean": "udim",
+    "radius of the earth": "r0dim", "reference albedo": "a0", "albedo excursion": "da",
+    "restoring timescale tauf (in days)": "tauf_days",
+    "restoring timescale tauc (in days)": "tauc_days",
+    "melt temperature threshold (deg C)": "Tm",
+    "rain/snow temperature threshold (deg C)": "Tr",
+    "accumulation precipitation threshold (m/y)": "Pa",
+    "melt threshold width (deg C)": "epm", "rain/snow threshold width (deg C)": "epr",
+    "accumulation threshold width (m/y)": "epa",
+}
+# continuation parameters (AtmosLocal allParameters_)
+ATMOS_PARS = ["Combined Forcing", "Solar Forcing", "Longwave Forcing", "Humidity Forcing",
+              "Latent Heat Forcing", "Albedo Forcing", "T Eddy Diffusivity"]
+
+
+class Atmosphere:
+    """The atmosphere model on the ocean's grid and GPU (Atmosphere.C:13-165)."""
+
+    def __init__(self, ocean: Ocean, params: Optional[dict] = None):
+        p = _lib.AtmosParams()
+        check(lib().iemic_atmos_default_params(C.byref(p)), "iemic_atmos_default_params")
+        params = dict(params or {})
+        ch_given = "exchange coefficient ch" in params
+        for k, v in params.items():
+            if k in ATMOS_PARAMS:
+                setattr(p, ATMOS_PARAMS[k], float(v))
+            elif k in ATMOS_PARS:
+                p.par[ATMOS_PARS.index(k)] = float(v)
+            else:
+                raise KeyError(f"unknown atmosphere parameter {k!r}")
+        if not ch_given:
+            p.ch = 0.94 * p.ce          # AtmosLocal.C:122 default follows the Dalton number
+        h = C.c_void_p()
+        check(lib().iemic_atmos_create(C.byref(h), ocean._h, C.byref(p)), "iemic_atmos_create")
+        self._h = h
+        self.ocean = ocean
+        self.dim = lib().iemic_atmos_dim(h)
+        self.n, self.m = ocean.cfg.n, ocean.cfg.m
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().iemic_atmos_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def setPar(self, name, value: float) -> None:
+        idx = ATMOS_PARS.index(name) if isinstance(name, str) else int(name)
+        check(lib().iemic_atmos_set_par(self._h, idx, float(value)), "iemic_atmos_set_par")
+
+    def setState(self, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        assert x.size == self.dim
+        check(lib().iemic_atmos_set_state(self._h, ptr(x)), "iemic_atmos_set_state")
+
+    def getState(self) -> np.ndarray:
+        x = np.zeros(self.dim)
+        check(lib().iemic_atmos_get_state(self._h, ptr(x)), "iemic_atmos_get_state")
+        return x
+
+    def setOceanTemperature(self, sst: np.ndarray) -> None:
+        sst = np.ascontiguousarray(sst, dtype=np.float64)
+        check(lib().iemic_atmos_set_sst(self._h, ptr(sst)), "iemic_atmos_set_sst")
+
+    def computeRHS(self) -> np.ndarray:
+        F = np.zeros(self.dim)
+        check(lib().iemic_atmos_rhs(self._h, ptr(F)), "iemic_atmos_rhs")
+        return F
+
+    def computeJacobian(self) -> None:
+        check(lib().iemic_atmos_jacobian(self._h), "iemic_atmos_jacobian")
+
+    def applyMatrix(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(self.dim)
+        check(lib().iemic_atmos_spmv(self._h, ptr(x), ptr(y)), "iemic_atmos_spmv")
+        return y
+
+    def applyPrecon(self, r: np.ndarray) -> np.ndarray:
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros(self.dim)
+        check(lib().iemic_atmos_prec_apply(self._h, ptr(r), ptr(z)), "iemic_atmos_prec_apply")
+        return z
+
+    def getCommPars(self) -> np.ndarray:
+        out = np.zeros(18)
+        check(lib().iemic_atmos_commpars(self._h, ptr(out)), "iemic_atmos_commpars")
+        return out
+
+    def getPdist(self) -> np.ndarray:
+        out = np.zeros(self.n * self.m)
+        check(lib().iemic_atmos_pdist(self._h, ptr(out)), "iemic_atmos_pdist")
+        return out
+
+    def jacobian_ell(self):
+        """(values, columns) of the local rows, (dim-1) x 7; columns -1 unused."""
+        val = np.zeros((self.dim - 1) * 7)
+        col = np.zeros((self.dim - 1) * 7, dtype=np.int32)
+        check(lib().iemic_atmos_export_ell(self._h, ptr(val), ptr(col, C.c_int)),
+              "iemic_atmos_export_ell")
+        return val.reshape(-1, 7), col.reshape(-1, 7)
+
+    def integral_coeff(self):
+        pint = np.zeros(self.n * self.m)
+        area = C.c_double()
+        ri, rp = C.c_int(), C.c_int()
+        check(lib().iemic_atmos_integral_coeff(self._h, ptr(pint), C.byref(area), C.byref(ri),
+                                               C.byref(rp)), "iemic_atmos_integral_coeff")
+        return pint, area.value, ri.value, rp.value
+
+
+class CoupledModel:
+    """CoupledModel (CoupledModel.C:58-162) over one Ocean and one Atmosphere, solving
+    scheme 'C' (fully coupled) with preconditioning 'F' (forward block Gauss-Seidel)."""
+
+    def __init__(self, ocean: Ocean, atmos: Atmosphere, solver_params: Optional[dict] = None):
+        h = C.c_void_p()
+        check(lib().iemic_coupled_create(C.byref(h), ocean._h, atmos._h), "iemic_coupled_create")
+        self._h = h
+        self.ocean, self.atmos = ocean, atmos
+        self.N = ocean.N + atmos.dim
+        sp = {"FGMRES iterations": 200, "FGMRES tolerance": 1e-8, "FGMRES restarts": 4}
+        if solver_params:
+            sp.update(solver_params)
+        self.solver_params = sp
+        self.last_solve = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().iemic_coupled_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def setPar(self, name: str, value: float) -> None:
+        """CoupledModel::setPar: every model that knows the parameter takes it."""
+        from .config import PAR_INDEX
+        if name in PAR_INDEX:
+            self.ocean.setPar(name, value)
+        if name in ATMOS_PARS:
+            self.atmos.setPar(name, value)
+
+    def synchronize(self) -> None:
+        check(lib().iemic_coupled_synchronize(self._h), "iemic_coupled_synchronize")
+
+    def computeRHS(self) -> np.ndarray:
+        Fo = np.zeros(self.ocean.N)
+        Fa = np.zeros(self.atmos.dim)
+        check(lib().iemic_coupled_rhs(self._h, ptr(Fo), ptr(Fa)), "iemic_coupled_rhs")
+        return np.concatenate([Fo, Fa])
+
+    def computeJacobian(self) -> None:
+        check(lib().iemic_coupled_jacobian(self._h), "iemic_coupled_jacobian")
+
+    def applyMatrix(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(self.N)
+        check(lib().iemic_coupled_spmv(self._h, ptr(x), ptr(y)), "iemic_coupled_spmv")
+        return y
+
+    def solve(self, b: np.ndarray) -> np.ndarray:
+        sp = self.solver_params
+        opt = self.ocean._krylov()          # the ocean's block preconditioner settings
+        opt.tol = float(sp["FGMRES tolerance"])
+        opt.krylov_dim = int(sp["FGMRES iterations"])
+        opt.max_restarts = int(sp["FGMRES restarts"])
+        opt.prec = int(sp.get("Preconditioner", opt.prec))
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.zeros(self.N)
+        info = _lib.SolveInfo()
+        check(lib().iemic_coupled_solve(self._h, ptr(b), ptr(x), C.byref(opt), C.byref(info)),
+              "iemic_coupled_solve")
+        self.last_solve = info
+        return x

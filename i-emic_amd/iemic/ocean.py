@@ -105,6 +105,24 @@ class Ocean:
         check(lib().iemic_get_par(self._h, idx, C.byref(v)), "iemic_get_par")
         return v.value
 
+    # ---- coupled atmosphere (Ocean::synchronize(atmos), Ocean.C:1443-1472) -------------
+    def setAtmosphere(self, t, q, a, p, commpars) -> None:
+        """THCM::setAtmosphereT/Q/A/P + set_atmos_parameters (n*m surface fields, the 18
+        AtmosLocal::CommPars); the context must be created with coupled_t = 1."""
+        arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (t, q, a, p, commpars)]
+        check(lib().iemic_set_atmosphere(self._h, *[ptr(v) for v in arrs]), "iemic_set_atmosphere")
+
+    def getDeps(self) -> np.ndarray:
+        """getdeps (usrc.F90:201-219): Ooa, Os, nus, eta, lvsc, qdim, pQSnd."""
+        out = np.zeros(7)
+        check(lib().iemic_get_deps(self._h, ptr(out)), "iemic_get_deps")
+        return out
+
+    def getSunO(self) -> np.ndarray:
+        out = np.zeros(self.cfg.n * self.cfg.m)
+        check(lib().iemic_get_suno(self._h, ptr(out)), "iemic_get_suno")
+        return out
+
     def setIntCondCorrection(self, x: Optional[np.ndarray] = None) -> float:
         """THCM::setIntCondCorrection (THCM.C:2020-2038): the integral-condition entry of F
         becomes intSign (coeff . x - coeff . x0) with x0 = x (default: the current state),

@@ -160,6 +160,51 @@ int  iemic_get_deps(iemic_ctx* ctx, double* out7);
 /* THCM::getSunO (THCM.C:1517-1527): suno(j) broadcast on the n*m surface */
 int  iemic_get_suno(iemic_ctx* ctx, double* out_nm);
 
+/* ---- atmosphere (src/atmosphere: AtmosLocal.C, Atmosphere.C; one process, aux = 1) ---- */
+typedef struct iemic_atmos iemic_atmos;
+/* AtmosLocal::setParameters (AtmosLocal.C:106-171): the XML names in order */
+typedef struct {
+    double rhoa, rhoo, hdima, hdimq, cpa, D0, kappa, arad, brad, sun0, c0, ce, ch, uw;
+    double t0a, t0o, t0i, tdim, q0, qdim, lv, udim, r0dim, a0, da;
+    double tauf_days, tauc_days, Tm, Tr, Pa, epm, epr, epa;
+    double par[7];   /* Combined, Solar, Longwave, Humidity, Latent Heat, Albedo Forcing,
+                        T Eddy Diffusivity (AtmosLocal allParameters_, 154-170) */
+} iemic_atmos_params;
+int  iemic_atmos_default_params(iemic_atmos_params* p);
+/* the atmosphere on the ocean context's grid, device and stream; its surface mask is the
+ * ocean's top layer (AtmosLocal::setSurfaceMask 1722-1756), Ooa/Os from getdeps.  The
+ * ocean context must have coupled_t = 1 and one rank. */
+int  iemic_atmos_create(iemic_atmos** a, iemic_ctx* ocean, const iemic_atmos_params* p);
+void iemic_atmos_destroy(iemic_atmos* a);
+int  iemic_atmos_dim(const iemic_atmos* a);                    /* 3 n m + 1               */
+int  iemic_atmos_set_par(iemic_atmos* a, int idx, double v);   /* AtmosLocal::setPar      */
+int  iemic_atmos_set_state(iemic_atmos* a, const double* x);
+int  iemic_atmos_get_state(iemic_atmos* a, double* x);
+int  iemic_atmos_set_sst(iemic_atmos* a, const double* sst);   /* setOceanTemperature     */
+int  iemic_atmos_rhs(iemic_atmos* a, double* F);               /* Atmosphere::computeRHS  */
+int  iemic_atmos_jacobian(iemic_atmos* a);                     /* ::computeJacobian       */
+int  iemic_atmos_spmv(iemic_atmos* a, const double* x, double* y);   /* ::applyMatrix     */
+int  iemic_atmos_prec_apply(iemic_atmos* a, const double* r, double* z); /* ::applyPrecon */
+int  iemic_atmos_export_ell(iemic_atmos* a, double* val, int* col);  /* (dim-1) x 7      */
+int  iemic_atmos_integral_coeff(iemic_atmos* a, double* pint, double* total_area, int* rowint,
+                                int* rowP);
+int  iemic_atmos_commpars(iemic_atmos* a, double* out18);      /* getCommPars             */
+int  iemic_atmos_pdist(iemic_atmos* a, double* out_nm);        /* getPdist                */
+
+/* ---- coupled ocean + atmosphere (src/coupledmodel/CoupledModel.C) -------------------- */
+typedef struct iemic_coupled iemic_coupled;
+int  iemic_coupled_create(iemic_coupled** cm, iemic_ctx* ocean, iemic_atmos* atmos);
+void iemic_coupled_destroy(iemic_coupled* cm);
+int  iemic_coupled_synchronize(iemic_coupled* cm);             /* synchronize 218-233      */
+int  iemic_coupled_rhs(iemic_coupled* cm, double* F_ocean, double* F_atmos); /* 260-271    */
+int  iemic_coupled_jacobian(iemic_coupled* cm);                /* computeJacobian 236-257  */
+/* applyMatrix (436-470): x, y = [ocean (reference order) | atmosphere] */
+int  iemic_coupled_spmv(iemic_coupled* cm, const double* x, double* y);
+/* FGMRESSolve (366-432) with the forward block Gauss-Seidel preconditioner 'F'
+ * (applyPrecon 544-585) */
+int  iemic_coupled_solve(iemic_coupled* cm, const double* b, double* x, const iemic_krylov* opt,
+                         iemic_solve_info* info);
+
 /* ---- geometry queries ------------------------------------------------------------ */
 int     iemic_nrows(const iemic_ctx* ctx);
 int64_t iemic_graph_nnz(const iemic_ctx* ctx);       /* Epetra maximal-graph nnz       */

@@ -60,6 +60,11 @@ COUPLED_RUN_PARAMS = {
 }
 
 
+def _sq(v):
+    """pow(v, 2) of the reference C++: GCC and clang emit v*v for it"""
+    return v * v
+
+
 def _get(p, k, d):
     return float(p.get(k, d))
 
@@ -130,7 +135,7 @@ class AtmosParams:
         self.Tr = self.Tr - self.t0o
         self.Tm = self.Tm - self.t0o
         self.dqso = 5e-4   # AtmosLocal.C:233 ("hack")
-        self.dqsi = (c1 * c2 * c3) / math.pow(self.t0i + c3, 2)
+        self.dqsi = (c1 * c2 * c3) / ((self.t0i + c3) * (self.t0i + c3))
         self.dqsi *= math.exp((c2 * self.t0i) / (self.t0i + c3))
         self.lvscale = self.rhoo * self.lv / self.muoa
         self.Ooa, self.Os = Ooa, Os
@@ -171,11 +176,11 @@ class AtmosOracle:
         self.yv = [ymin + j * dy for j in range(m + 1)]
         self.datc = [0.9 + 1.5 * math.exp(-12 * y * y / PI) for y in self.yc]
         self.datv = [0.9 + 1.5 * math.exp(-12 * y * y / PI) for y in self.yv]
-        self.suna = [P.As * (1 - .482 * (3 * math.pow(math.sin(y), 2) - 1.) / 2.) for y in self.yc]
-        self.suno = [P.Os * (1 - .482 * (3 * math.pow(math.sin(y), 2) - 1.) / 2.) for y in self.yc]
+        self.suna = [P.As * (1 - .482 * (3 * _sq(math.sin(y)) - 1.) / 2.) for y in self.yc]
+        self.suno = [P.Os * (1 - .482 * (3 * _sq(math.sin(y)) - 1.) / 2.) for y in self.yc]
         # per-latitude stencil weights (discretize, AtmosLocal.C:1162-1232), index j = 1..m
-        self.cosdx2i = [0.0] + [1.0 / math.pow(math.cos(self.yc[j]) * dx, 2) for j in range(1, m + 1)]
-        dy2i = 1.0 / math.pow(dy, 2)
+        self.cosdx2i = [0.0] + [1.0 / _sq(math.cos(self.yc[j]) * dx) for j in range(1, m + 1)]
+        dy2i = 1.0 / _sq(dy)
         cy = [0.0] + [math.cos(self.yc[j]) for j in range(1, m + 1)]
         self.t4 = [0.0] + [dy2i * self.datv[j - 1] * math.cos(self.yv[j - 1]) / cy[j] for j in range(1, m + 1)]
         self.t6 = [0.0] + [dy2i * self.datv[j] * math.cos(self.yv[j]) / cy[j] for j in range(1, m + 1)]
@@ -186,16 +191,22 @@ class AtmosOracle:
         self.pint = np.where(self.surf == 0, area[:, None], 0.0).reshape(-1)   # (j, i)
         self.intc = np.zeros(self.dim)
         self.intc[NUN * np.arange(n * m) + QQ] = self.pint
-        self.total_area = float(np.sum(np.abs(self.pint)))
+        total = 0.0
+        for v in self.pint:          # sequential sums (the device's order)
+            total += abs(float(v))
+        self.total_area = total
         # Pdist (fillPdist 495-516, corrected by Atmosphere::setPdist 1234-1265)
         pd = np.zeros(n * m)
         for j in range(1, m + 1):
             y = self.yc[j]
-            v = 2 * math.exp(-math.pow(6 * y, 2)) + math.pow(math.sin(2.0 * y), 2)
+            v = 2 * math.exp(-_sq(6 * y)) + _sq(math.sin(2.0 * y))
             for i in range(n):
                 if self.surf[j - 1, i] == 0:
                     pd[(j - 1) * n + i] = v
-        corr = 1 - float(np.dot(self.pint, pd)) / self.total_area
+        ipd = 0.0
+        for a_, b_ in zip(self.pint, pd):
+            ipd += float(a_) * float(b_)
+        corr = 1 - ipd / self.total_area
         ones = (np.abs(self.pint) > 1e-7).astype(np.float64)
         self.pdist = corr * ones + pd
         self.msi = np.zeros(n * m)

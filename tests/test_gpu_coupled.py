@@ -1,0 +1,173 @@
+"""GPU: the coupled ocean + atmosphere model (BASELINE config C4)
+through the C ABI.
+
+* Ocean in coupled mode: Jacobian and residual bitwise against the reference Fortran
+  (coupled_natl8 full arrays; coupled4 residual by SHA-256, Jacobian equal to the CPU
+  emulation that is pinned to the Fortran on coupled_natl8).
+* Atmosphere (AtmosLocal / Atmosphere): residual and Jacobian against the restatement
+  oracle/atmos_oracle.py (local rows bitwise; the two dense integral rows are reductions,
+  rtol 1e-13).
+* CoupledModel::applyMatrix against the block matrix assembled from the device ocean CSR
+  (bit-exact, above) and the oracle's atmosphere and coupling blocks: rtol 1e-12 of |A||x|.
+* CoupledModel FGMRES with the forward block Gauss-Seidel preconditioner to 1e-8,
+  explicit residual checked with that assembled matrix.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from helpers import Emul, emul_set_atmosphere, golden
+from iemic import config as cf
+from oracle import atmos_oracle as ao
+from test_coupled import atm_args, coupled_manifest, landm_of
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.int64)
+
+
+def setup(name):
+    from iemic.ocean import Ocean
+    c = cf.preset(name)
+    g = golden(name)
+    L = landm_of(name)
+    oc = Ocean(c, landm=L, analyze_jacobian=False)
+    t, q, a, pars = atm_args(g)
+    oc.setAtmosphere(t, q, a, np.zeros_like(t), pars)
+    return c, g, L, oc
+
+
+def atmos_oracle(c, g, L):
+    surf = (L[c.l, 1:c.m + 1, 1:c.n + 1] != 0).astype(int)
+    at = ao.AtmosOracle(c.n, c.m, c.xmin, c.xmax, c.ymin, c.ymax, c.periodic, surf,
+                        Ooa=g["deps"][0], Os=g["deps"][1],
+                        params={**ao.COUPLED_RUN_PARAMS,
+                                "Combined Forcing": c.start_params["Combined Forcing"]})
+    at.suno_ocean = np.array(at.suno[1:])
+    return at
+
+
+@pytest.mark.parametrize("kind", ["zero", "synthetic"])
+def test_gpu_coupled_ocean_natl8_bitexact(oracle_lib, kind):
+    c, g, L, oc = setup("coupled_natl8")
+    np.testing.assert_array_equal(bits(oc.getDeps()), bits(g["deps"]))
+    x = g[f"{kind}_x"]
+    oc.setState(x)
+    oc.computeJacobian()
+    rowptr, col, val = oc.exportCSR()
+    ref = oracle_lib.fortran_to_graph(rowptr, col, g[f"{kind}_beg"], g[f"{kind}_jco"],
+                                      g[f"{kind}_co"], -1)
+    np.testing.assert_array_equal(val, ref)
+    F = oc.computeRHS().copy()
+    np.testing.assert_array_equal(bits(F), bits(-g[f"{kind}_B"]))
+
+
+def test_gpu_coupled4_ocean_bitexact(emul):
+    """the C4 ocean (96x38x12, Mixing 1, coupled T): F == Fortran (SHA-256), J == the CPU
+    emulation of the same code (pinned to the Fortran on coupled_natl8)."""
+    name = "coupled4"
+    c, g, L, oc = setup(name)
+    man = coupled_manifest()[name]
+    np.testing.assert_array_equal(bits(oc.getDeps()), bits(g["deps"]))
+    x = cf.synthetic_state(c, cf.landmask(c))
+    oc.setState(x)
+    oc.computeJacobian()
+    _, col, val = oc.exportCSR()
+    F = oc.computeRHS().copy()
+    assert hashlib.sha256((-F).tobytes()).hexdigest() == man["states"]["synthetic"]["B_sha"]
+    e = Emul(c, L)
+    emul_set_atmosphere(e, *atm_args(g))
+    _, ecol, evals, _ = e.jacobian_csr(x)
+    np.testing.assert_array_equal(col, ecol)
+    np.testing.assert_array_equal(val, evals)
+
+
+@pytest.fixture(scope="module")
+def coupled4():
+    from iemic.coupled import Atmosphere, CoupledModel
+    name = "coupled4"
+    c, g, L, oc = setup(name)
+    atm = Atmosphere(oc, {**ao.COUPLED_RUN_PARAMS,
+                          "Combined Forcing": c.start_params["Combined Forcing"]})
+    cm = CoupledModel(oc, atm, {"FGMRES iterations": 150, "FGMRES restarts": 6})
+    return c, g, L, oc, atm, cm
+
+
+def test_gpu_atmosphere_matches_oracle(coupled4):
+    c, g, L, oc, atm, cm = coupled4
+    at = atmos_oracle(c, g, L)
+    np.testing.assert_array_equal(bits(atm.getCommPars()), bits(g["atm_pars"]))
+    np.testing.assert_array_equal(bits(atm.getPdist()), bits(at.pdist))
+    pint, area, ri, rp = atm.integral_coeff()
+    np.testing.assert_array_equal(bits(pint), bits(at.pint))
+    assert area == at.total_area and ri == at.rowint and rp == at.rowP
+    xa = g["xa"]
+    rng = np.random.default_rng(5)
+    sst = 0.3 * rng.standard_normal(c.n * c.m)
+    atm.setState(xa)
+    atm.setOceanTemperature(sst)
+    F = atm.computeRHS()
+    oF = at.rhs(xa, sst)
+    for r in (ri, rp):
+        assert abs(F[r] - oF[r]) <= 1e-13 * max(1.0, abs(oF[r]))
+    keep = np.ones(at.dim, bool)
+    keep[[ri, rp]] = False
+    np.testing.assert_array_equal(bits(F[keep]), bits(oF[keep]))
+    atm.computeJacobian()
+    val, col = atm.jacobian_ell()
+    rows = np.repeat(np.arange(at.dim - 1), 7)
+    m = col.reshape(-1) >= 0
+    J = sp.csr_matrix((val.reshape(-1)[m], (rows[m], col.reshape(-1)[m])), shape=(at.dim, at.dim))
+    oJ = at.jacobian(xa).tolil()
+    oJ[ri, :] = 0
+    oJ[rp, :] = 0
+    D = (J - oJ.tocsr()).tocoo()
+    assert np.all(D.data == 0.0), np.abs(D.data).max()
+
+
+def assembled(cm, c, g, L, oc):
+    """[J_o C_oa; C_ao J_a] from the device ocean CSR and the oracle's blocks."""
+    at = atmos_oracle(c, g, L)
+    oc.computeJacobian()
+    rowptr, col, val = oc.exportCSR()
+    Jo = sp.csr_matrix((val, col, rowptr), shape=(c.nrows, c.nrows))
+    xa = cm.atmos.getState()
+    Ja = at.jacobian(xa)
+    Cao = at.block_from_ocean(c.l)
+    Coa = at.block_to_ocean(c.l, at.surf, oc.getDeps(), oc.getPar("Combined Forcing"),
+                            oc.getPar("Solar Forcing"))
+    return sp.bmat([[Jo, Coa], [Cao, Ja]]).tocsr()
+
+
+def test_gpu_coupled_spmv(coupled4):
+    c, g, L, oc, atm, cm = coupled4
+    x = cf.synthetic_state(c, cf.landmask(c))
+    oc.setState(x)
+    atm.setState(g["xa"])
+    cm.computeJacobian()
+    A = assembled(cm, c, g, L, oc)
+    rng = np.random.default_rng(11)
+    v = rng.standard_normal(cm.N)
+    y = cm.applyMatrix(v)
+    ref = A @ v
+    scale = abs(A) @ np.abs(v)
+    assert np.max(np.abs(y - ref) / np.maximum(scale, 1e-300)) <= 1e-12
+
+
+def test_gpu_coupled_fgmres(coupled4):
+    c, g, L, oc, atm, cm = coupled4
+    x = cf.synthetic_state(c, cf.landmask(c), amp_ts=1e-3)
+    oc.setState(x)
+    atm.setState(g["xa"])
+    cm.computeJacobian()
+    F = cm.computeRHS()
+    dx = cm.solve(-F)
+    info = cm.last_solve
+    print("coupled FGMRES iterations", info.iters, "explicit", info.explicit_rel_res)
+    A = assembled(cm, c, g, L, oc)
+    r = np.linalg.norm(A @ dx + F) / np.linalg.norm(F)
+    assert info.converged and r <= 1e-7, (info.iters, r)
