@@ -63,7 +63,7 @@ struct iemic_atmos {
     DevBuf<int> d_surf, d_col;
     /* preconditioner: 9-point T and q operators, their cyclic reductions, work vectors */
     DevBuf<double> d_s9t, d_s9q, d_bt, d_bq, d_zt, d_zq;
-    DevBuf<double> d_w, d_pred;          /* S_q^-1 (q-P column), P Schur partials + scalar   */
+    DevBuf<double> d_w, d_g, d_pred;          /* S_q^-1 (q-P column), P Schur partials + scalar   */
     DevBuf<int> d_colij;
     SchurCR crT, crQ;
     int jac_valid = 0, prec_valid = 0;
@@ -368,21 +368,27 @@ __global__ void k_atm_s9(AtmGeo G, const double* __restrict__ val, double* __res
     }
 }
 
-/* The [q; P] block is solved exactly through the scalar Schur complement of P:
- *   S_q q + c P = b_q,  rr . q - P = b_P   (c = the q rows' P column -nuq Pdist,
- *   rr = the precipitation row -(1/A) intc; Atmosphere.C:1039-1067)
- *   w = S_q^-1 c (set-up), s = -1 - rr . w;  y = S_q^-1 b_q, P = (b_P - rr . y) / s,
- *   q = y - w P.  Then A from its row (A_A z_A = r_A - A_P P), T from S_T with the A and
- *   P columns moved to the right-hand side.  The q-integral row is an identity row of S_q. */
+/* The [q; P] block is solved exactly.  Its two global rows -- the q integral condition
+ * (row k: intc . q = b_k) and the precipitation row (rr . q - P = b_P, rr = -(1/A) intc;
+ * Atmosphere.C:1039-1067) -- are bordered onto S~, the q stencil operator with row k
+ * replaced by the identity (without the integral row the [q; P] system is singular:
+ * q = -Pdist t, P = t).  With d = intc - e_k, mu = d . q:
+ *   S~ q = b - c P - e_k mu  ->  q = y - w P - g mu,  y = S~^-1 b, w = S~^-1 c, g = S~^-1 e_k
+ *   [d.w   d.g + 1] [P ]   [d.y       ]
+ *   [rr.w + 1  rr.g] [mu] = [rr.y - b_P]
+ * (c: the q rows' P column -nuq Pdist).  w, g and the 2x2 inverse at set-up; per apply one
+ * cyclic-reduction solve for y and one reduction.  Then A from its row (A_A z_A = r_A -
+ * A_P P) and T from S_T with the A and P columns moved to the right-hand side. */
 __global__ void k_atm_qcol(AtmGeo G, const double* __restrict__ val, const double* __restrict__ r,
-                           double* __restrict__ cq, double* __restrict__ bq)
+                           double* __restrict__ cq, double* __restrict__ gk, double* __restrict__ bq)
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= G.n * G.m) return;
     const int sc = (c % G.n) * G.m + c / G.n;
     const bool ri = ANUN * c + AQ == G.rowint;
     if (cq) cq[sc] = ri ? 0.0 : val[(size_t)(ANUN * c + AQ) * ASL + 3];
-    if (bq) bq[sc] = ri ? 0.0 : r[ANUN * c + AQ];
+    if (gk) gk[sc] = ri ? 1.0 : 0.0;
+    if (bq) bq[sc] = r[ANUN * c + AQ];
 }
 /* partials of sum_cells pint(cell) v(sc(cell)) */
 __global__ void __launch_bounds__(256) k_atm_pdot_sc(AtmGeo G, const double* __restrict__ pint,
@@ -400,25 +406,36 @@ __global__ void __launch_bounds__(256) k_atm_pdot_sc(AtmGeo G, const double* __r
     }
     if (threadIdx.x == 0) part[blockIdx.x] = sm[0];
 }
-/* s = -1 - rr . w  with rr = -(1/A) pint */
-__global__ void k_atm_pschur(AtmPar P, double* __restrict__ pred)
+HD int atm_sk(const AtmGeo& G) { const int ck = (G.rowint - AQ) / ANUN; return (ck % G.n) * G.m + ck / G.n; }
+/* pred[0..AR): I.w partials, [AR..2AR): I.g partials -> pred[2AR..2AR+4) = 2x2 inverse */
+__global__ void k_atm_pschur(AtmPar P, AtmGeo G, const double* __restrict__ w, const double* __restrict__ g,
+                             double* __restrict__ pred)
 {
     if (threadIdx.x || blockIdx.x) return;
-    double a = 0.0;
-    for (int q = 0; q < AR_BLOCKS; q++) a += pred[q];
-    pred[AR_BLOCKS] = -1.0 - (-1.0 / P.total_area) * a;
+    double Iw = 0.0, Ig = 0.0;
+    for (int q = 0; q < AR_BLOCKS; q++) Iw += pred[q];
+    for (int q = 0; q < AR_BLOCKS; q++) Ig += pred[AR_BLOCKS + q];
+    const int sk = atm_sk(G);
+    const double rA = -1.0 / P.total_area;
+    const double a11 = Iw - w[sk], a12 = (Ig - g[sk]) + 1.0;
+    const double a21 = rA * Iw + 1.0, a22 = rA * Ig;
+    const double det = a11 * a22 - a12 * a21;
+    double* M = pred + 2 * AR_BLOCKS;
+    M[0] = a22 / det; M[1] = -a12 / det; M[2] = -a21 / det; M[3] = a11 / det;
 }
 __global__ void k_atm_prec_a(AtmPar P, AtmGeo G, const double* __restrict__ val, const double* __restrict__ r,
-                             const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ pred,
-                             double* __restrict__ z, double* __restrict__ bt)
+                             const double* __restrict__ w, const double* __restrict__ g, const double* __restrict__ y,
+                             const double* __restrict__ pred, double* __restrict__ z, double* __restrict__ bt)
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= G.n * G.m) return;
     const int sc = (c % G.n) * G.m + c / G.n;
-    double a = 0.0;
-    for (int q = 0; q < AR_BLOCKS; q++) a += pred[AR_BLOCKS + 1 + q];
-    const double zP = (r[G.rowP] - (-1.0 / P.total_area) * a) / pred[AR_BLOCKS];
-    z[ANUN * c + AQ] = y[sc] - w[sc] * zP;
+    double Iy = 0.0;
+    for (int q = 0; q < AR_BLOCKS; q++) Iy += pred[2 * AR_BLOCKS + 4 + q];
+    const double* M = pred + 2 * AR_BLOCKS;
+    const double f1 = Iy - y[atm_sk(G)], f2 = (-1.0 / P.total_area) * Iy - r[G.rowP];
+    const double zP = M[0] * f1 + M[1] * f2, mu = M[2] * f1 + M[3] * f2;
+    z[ANUN * c + AQ] = y[sc] - w[sc] * zP - g[sc] * mu;
     const double* va = val + (size_t)(ANUN * c + AA) * ASL;
     const double zA = (r[ANUN * c + AA] - va[2] * zP) / va[1];
     z[ANUN * c + AA] = zA;
@@ -755,7 +772,8 @@ extern "C" int iemic_atmos_create(iemic_atmos** out, iemic_ctx* oc, const iemic_
     rc |= a->d_zq.alloc((size_t)n * m);
     rc |= a->d_colij.alloc((size_t)n * m);
     rc |= a->d_w.alloc((size_t)n * m);
-    rc |= a->d_pred.alloc((size_t)2 * AR_BLOCKS + 2);
+    rc |= a->d_g.alloc((size_t)n * m);
+    rc |= a->d_pred.alloc((size_t)3 * AR_BLOCKS + 8);
     if (rc) {
         delete a;
         set_error("iemic_atmos_create: out of device memory");
@@ -880,14 +898,18 @@ int atm_prec_compute(iemic_atmos* a)
     if (!rc) rc = cr_check(a->oc, a->crT);
     if (!rc) rc = cr_check(a->oc, a->crQ);
     if (rc) return rc;
-    /* P Schur complement: w = S_q^-1 c, s = -1 - rr . w */
+    /* the bordered [q; P] block: w = S~^-1 c, g = S~^-1 e_k and the 2x2 inverse */
     const AtmGeo G = atm_geo(a);
     hipLaunchKernelGGL(k_atm_qcol, dim3((nm + 255) / 256), dim3(256), 0, s, G, (const double*)a->d_val.p,
-                       (const double*)nullptr, a->d_bq.p, (double*)nullptr);
+                       (const double*)nullptr, a->d_bq.p, a->d_bt.p, (double*)nullptr);
     if ((rc = cr_solve(a->oc, a->crQ, a->d_bq.p, a->d_w.p, s))) return rc;
+    if ((rc = cr_solve(a->oc, a->crQ, a->d_bt.p, a->d_g.p, s))) return rc;
     hipLaunchKernelGGL(k_atm_pdot_sc, dim3(AR_BLOCKS), dim3(256), 0, s, G, (const double*)a->d_pint.p,
                        (const double*)a->d_w.p, a->d_pred.p);
-    hipLaunchKernelGGL(k_atm_pschur, dim3(1), dim3(64), 0, s, a->P, a->d_pred.p);
+    hipLaunchKernelGGL(k_atm_pdot_sc, dim3(AR_BLOCKS), dim3(256), 0, s, G, (const double*)a->d_pint.p,
+                       (const double*)a->d_g.p, a->d_pred.p + AR_BLOCKS);
+    hipLaunchKernelGGL(k_atm_pschur, dim3(1), dim3(64), 0, s, a->P, G, (const double*)a->d_w.p,
+                       (const double*)a->d_g.p, a->d_pred.p);
     HIP_OK(hipGetLastError());
     a->prec_valid = 1;
     return 0;
@@ -899,13 +921,14 @@ int atm_prec_apply(iemic_atmos* a, const double* r, double* z)
     const AtmGeo G = atm_geo(a);
     const unsigned gb = (nm + 255) / 256;
     hipLaunchKernelGGL(k_atm_qcol, dim3(gb), dim3(256), 0, s, G, (const double*)a->d_val.p, r, (double*)nullptr,
-                       a->d_bq.p);
+                       (double*)nullptr, a->d_bq.p);
     int rc = cr_solve(a->oc, a->crQ, a->d_bq.p, a->d_zq.p, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_atm_pdot_sc, dim3(AR_BLOCKS), dim3(256), 0, s, G, (const double*)a->d_pint.p,
-                       (const double*)a->d_zq.p, a->d_pred.p + AR_BLOCKS + 1);
+                       (const double*)a->d_zq.p, a->d_pred.p + 2 * AR_BLOCKS + 4);
     hipLaunchKernelGGL(k_atm_prec_a, dim3(gb), dim3(256), 0, s, a->P, G, (const double*)a->d_val.p, r,
-                       (const double*)a->d_w.p, (const double*)a->d_zq.p, (const double*)a->d_pred.p, z, a->d_bt.p);
+                       (const double*)a->d_w.p, (const double*)a->d_g.p, (const double*)a->d_zq.p,
+                       (const double*)a->d_pred.p, z, a->d_bt.p);
     if ((rc = cr_solve(a->oc, a->crT, a->d_bt.p, a->d_zt.p, s))) return rc;
     hipLaunchKernelGGL(k_atm_prec_b, dim3(gb), dim3(256), 0, s, G, (const double*)a->d_zt.p,
                        (const double*)a->d_zq.p, z);
