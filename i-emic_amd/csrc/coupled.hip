@@ -583,6 +583,34 @@ __global__ void k_cupdate(const double* __restrict__ X, int64_t ld, int nv, cons
         y[q] = s;
     }
 }
+/* y = a y + sum_i c_i X_i (i < nv <= 16) */
+struct LinC {
+    int nv;
+    double a;
+    double c[16];
+    const double* X[16];
+};
+__global__ void __launch_bounds__(256) k_clincomb(LinC L, double* __restrict__ y, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = L.a == 0.0 ? 0.0 : L.a * y[q];
+        for (int i = 0; i < L.nv; i++) acc += L.c[i] * L.X[i][q];
+        y[q] = acc;
+    }
+}
+/* IDR shadow space: uniform in [-1, 1] from splitmix64 over the packed row index */
+__global__ void k_cidr_random(double* __restrict__ P, int64_t ld, int s, int64_t N)
+{
+    const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q0 >= N) return;
+    for (int q = 0; q < s; q++) {
+        uint64_t z = 0x9E3779B97F4A7C15ull * ((uint64_t)q0 * 16 + (uint64_t)q + 1) + 20261017ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        P[(int64_t)q * ld + q0] = 2.0 * ((double)(z >> 11) * (1.0 / 9007199254740992.0)) - 1.0;
+    }
+}
 __global__ void k_axpby_c(double a, const double* __restrict__ x, double b, const double* __restrict__ y,
                           double* __restrict__ out, int64_t N)
 {
@@ -1244,6 +1272,167 @@ double cdot_host(iemic_coupled* cm, const double* V, int64_t ld, int nv, const d
 }
 }  // namespace
 
+namespace {
+void clin(iemic_coupled* cm, double a, double* y, const std::vector<double>& cs, const std::vector<const double*>& xs)
+{
+    LinC L{};
+    L.a = a;
+    for (size_t q = 0; q < cs.size() && q < 16; q++) {
+        L.c[L.nv] = cs[q];
+        L.X[L.nv] = xs[q];
+        L.nv++;
+    }
+    hipLaunchKernelGGL(k_clincomb, dim3(blocks_for(cm->NC)), dim3(256), 0, cm->oc->stream, L, y, cm->NC);
+}
+
+/* IDR(s) on the packed coupled vector (IDRSolver.H:109-340: the same restatement as the
+ * ocean's krylov.hip idrs -- bi-orthogonalisation against the shadow space P, omega with
+ * the angle safeguard, optional residual replacement), right preconditioned by the block
+ * Gauss-Seidel preconditioner.  b, x: device packed vectors; x starts at 0. */
+int coupled_idrs(iemic_coupled* cm, const double* b, double* x, const iemic_krylov* opt, double normb,
+                 iemic_solve_info& inf)
+{
+    hipStream_t st = cm->oc->stream;
+    const int s = std::max(1, std::min(opt->idr_s > 0 ? opt->idr_s : 4, 8));
+    const double angle = opt->idr_angle > 0.0 ? opt->idr_angle : 0.7;
+    const double mp = 1e-13;
+    const int maxit = std::max(1, opt->krylov_dim * (opt->max_restarts + 1));
+    const int64_t NC = cm->NC;
+    const int need = 3 * s + 3;
+    if (cm->mk < need) {
+        if (cm->V.alloc((size_t)(need + 1) * NC) || cm->Z.alloc((size_t)need * NC)) {
+            set_error("coupled IDR(s): out of device memory");
+            return IEMIC_ENOMEM;
+        }
+        cm->mk = need;
+    }
+    double* P = cm->V.p;
+    double* U = P + (int64_t)s * NC;
+    double* G = U + (int64_t)s * NC;
+    double* t = G + (int64_t)s * NC;
+    double* r = t + NC;
+    double* v = r + NC;
+    auto Ui = [&](int i) { return U + (int64_t)i * NC; };
+    auto Gi = [&](int i) { return G + (int64_t)i * NC; };
+    auto Pi = [&](int i) { return P + (int64_t)i * NC; };
+    std::vector<double> tmp(s + 2);
+    int rc = 0;
+    hipLaunchKernelGGL(k_cidr_random, dim3((unsigned)((NC + 255) / 256)), dim3(256), 0, st, P, NC, s, NC);
+    for (int j = 0; j < s; j++) {
+        if (j > 0) {
+            cdot_host(cm, P, NC, j, Pi(j), tmp.data());
+            std::vector<double> cs;
+            std::vector<const double*> xs;
+            for (int k = 0; k < j; k++) { cs.push_back(-tmp[k]); xs.push_back(Pi(k)); }
+            clin(cm, 1.0, Pi(j), cs, xs);
+        }
+        const double nn = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, Pi(j), tmp.data())));
+        hipLaunchKernelGGL(k_cscale, dim3(blocks_for(NC)), dim3(256), 0, st, 1.0 / nn, (const double*)Pi(j), Pi(j), NC);
+    }
+    HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NC, hipMemcpyDeviceToDevice, st));
+    const double tolb = opt->tol * normb;
+    double normr = normb;
+    std::vector<double> f(s + 1, 0.0), gamma(s, 0.0), d(s + 2, 0.0);
+    std::vector<std::vector<double>> M(s, std::vector<double>(s, 0.0));
+    double om = 1.0;
+    int jj = 0, iter = 0;
+    bool trueres = false;
+    auto prec = [&](const double* in, double* out) { return cpl_prec(cm, in, out, opt->prec > 0); };
+    while (normr > tolb && iter < maxit) {
+        cdot_host(cm, P, NC, s, r, f.data());                         /* f = P' r */
+        for (int k = 0; k < s; k++) {
+            if (jj > 0) {
+                std::vector<double> cs;
+                std::vector<const double*> xs;
+                for (int i = k; i < s; i++) {
+                    double gi = f[i];
+                    for (int j = k; j < i; j++) gi -= M[i][j] * gamma[j];
+                    gamma[i] = gi / M[i][i];
+                    cs.push_back(-gamma[i]);
+                    xs.push_back(Gi(i));
+                }
+                HIP_OK(hipMemcpyAsync(v, r, sizeof(double) * NC, hipMemcpyDeviceToDevice, st));
+                clin(cm, 1.0, v, cs, xs);
+                if ((rc = prec(v, t))) return rc;
+                cs.assign(1, om);
+                xs.assign(1, t);
+                for (int i = k; i < s; i++) { cs.push_back(gamma[i]); xs.push_back(Ui(i)); }
+                clin(cm, 0.0, Ui(k), cs, xs);
+            } else {
+                if ((rc = prec(r, Ui(k)))) return rc;
+            }
+            if ((rc = cpl_apply(cm, Ui(k), Gi(k)))) return rc;
+            cdot_host(cm, P, NC, s, Gi(k), d.data());
+            std::vector<double> al(k, 0.0);
+            for (int i = 0; i < k; i++) {
+                double a = d[i];
+                for (int j = 0; j < i; j++) a -= al[j] * M[i][j];
+                al[i] = a / M[i][i];
+            }
+            for (int i = k; i < s; i++) {
+                double mik = d[i];
+                for (int j = 0; j < k; j++) mik -= al[j] * M[i][j];
+                M[i][k] = mik;
+            }
+            if (k > 0) {
+                std::vector<double> cs;
+                std::vector<const double*> xg, xu;
+                for (int i = 0; i < k; i++) { cs.push_back(-al[i]); xg.push_back(Gi(i)); xu.push_back(Ui(i)); }
+                clin(cm, 1.0, Gi(k), cs, xg);
+                clin(cm, 1.0, Ui(k), cs, xu);
+            }
+            if (!std::isfinite(M[k][k]) || M[k][k] == 0.0) {
+                set_error("coupled IDR(s): breakdown");
+                return IEMIC_ERANGE;
+            }
+            const double beta = f[k] / M[k][k];
+            clin(cm, 1.0, r, {-beta}, {Gi(k)});
+            clin(cm, 1.0, x, {beta}, {Ui(k)});
+            normr = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, r, tmp.data())));
+            if (!std::isfinite(normr)) {
+                set_error("coupled IDR(s): non-finite residual");
+                return IEMIC_ERANGE;
+            }
+            if (opt->idr_replace && normr > tolb / mp) trueres = true;
+            for (int i = k + 1; i < s; i++) f[i] -= beta * M[i][k];
+            iter++;
+            if (normr < tolb || iter >= maxit) break;
+        }
+        if (normr < tolb || iter >= maxit) break;
+        jj++;
+        if ((rc = prec(r, v))) return rc;
+        if ((rc = cpl_apply(cm, v, t))) return rc;
+        double tt_tr[2];
+        cdot_host(cm, r, NC, 1, t, tmp.data());                      /* r.t, t.t */
+        tt_tr[0] = tmp[1];
+        tt_tr[1] = tmp[0];
+        const double nt = std::sqrt(std::max(0.0, tt_tr[0])), ts = tt_tr[1];
+        if (!(nt > 0.0) || !std::isfinite(ts)) {
+            set_error("coupled IDR(s): breakdown in omega");
+            return IEMIC_ERANGE;
+        }
+        const double rho = std::fabs(ts / (nt * normr));
+        om = ts / (nt * nt);
+        if (rho < angle) om = om * angle / rho;
+        clin(cm, 1.0, r, {-om}, {t});
+        clin(cm, 1.0, x, {om}, {v});
+        normr = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, r, tmp.data())));
+        if (opt->idr_replace && normr > tolb / mp) trueres = true;
+        if (trueres && normr < normb) {
+            if ((rc = cpl_apply(cm, x, r))) return rc;
+            hipLaunchKernelGGL(k_axpby_c, dim3(blocks_for(NC)), dim3(256), 0, st, 1.0, b, -1.0, (const double*)r, r, NC);
+            normr = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, r, tmp.data())));
+            trueres = false;
+            inf.reorth++;
+        }
+        iter++;
+    }
+    inf.iters = iter;
+    inf.implicit_rel_res = normr / normb;
+    return 0;
+}
+}  // namespace
+
 /* CoupledModel::solve -> FGMRESSolve (353-432): right-preconditioned FGMRES(m) with
  * restarts on the packed coupled vector, classical Gram-Schmidt with one
  * re-orthogonalisation pass, x0 = 0, explicit residual at the end.  b, x: host vectors
@@ -1303,9 +1492,17 @@ extern "C" int iemic_coupled_solve(iemic_coupled* cm, const double* b_host, doub
         std::fill(x_host, x_host + oc->nrows + NA, 0.0);
         return 0;
     }
-    HIP_OK(hipMemcpyAsync(r, db.p, sizeof(double) * NC, hipMemcpyDeviceToDevice, s));
     double beta = bnorm, res = 1.0;
     int it = 0;
+    if (opt->method == 1) {
+        if ((rc = coupled_idrs(cm, db.p, dxv.p, opt, bnorm, inf))) return rc;
+        it = inf.iters;
+        res = inf.implicit_rel_res;
+        if ((rc = cpl_apply(cm, dxv.p, w))) return rc;
+        hipLaunchKernelGGL(k_axpby_c, dim3(G), dim3(256), 0, s, 1.0, (const double*)db.p, -1.0, (const double*)w, r, NC);
+        beta = std::sqrt(std::max(cdot_host(cm, nullptr, 0, 0, r, tmp.data()), 0.0));
+    } else {
+    HIP_OK(hipMemcpyAsync(r, db.p, sizeof(double) * NC, hipMemcpyDeviceToDevice, s));
     for (int cycle = 0; cycle <= opt->max_restarts; cycle++) {
         hipLaunchKernelGGL(k_cscale, dim3(G), dim3(256), 0, s, 1.0 / beta, (const double*)r, V, NC);
         std::fill(g.begin(), g.end(), 0.0);
@@ -1374,6 +1571,7 @@ extern "C" int iemic_coupled_solve(iemic_coupled* cm, const double* b_host, doub
         hipLaunchKernelGGL(k_axpby_c, dim3(G), dim3(256), 0, s, 1.0, (const double*)db.p, -1.0, (const double*)w, r, NC);
         beta = std::sqrt(std::max(cdot_host(cm, nullptr, 0, 0, r, tmp.data()), 0.0));
         if (res <= opt->tol || cycle == opt->max_restarts) break;
+    }
     }
     inf.iters = it;
     inf.implicit_rel_res = res;

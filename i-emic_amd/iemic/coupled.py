@@ -205,6 +205,22 @@ class CoupledModel:
         check(lib().iemic_coupled_spmv(self._h, ptr(x), ptr(y)), "iemic_coupled_spmv")
         return y
 
+    def newtonStep(self) -> dict:
+        """One Newton iteration of the coupled model as the reference's Newton /
+        Continuation drives it (src/newton/Newton.H:76-123): F(x), J(x), solve J dx = -F,
+        x += dx, F(x + dx).  Returns the residual norms and the solve record."""
+        F0 = self.computeRHS()
+        self.computeJacobian()
+        dx = self.solve(-F0)
+        xo = self.ocean.getState() + dx[:self.ocean.N]
+        xa = self.atmos.getState() + dx[self.ocean.N:]
+        self.ocean.setState(xo)
+        self.atmos.setState(xa)
+        F1 = self.computeRHS()
+        return dict(norm_f0=float(np.linalg.norm(F0)), norm_f1=float(np.linalg.norm(F1)),
+                    iters=int(self.last_solve.iters), converged=bool(self.last_solve.converged),
+                    explicit_rel_res=float(self.last_solve.explicit_rel_res))
+
     def solve(self, b: np.ndarray) -> np.ndarray:
         sp = self.solver_params
         opt = self.ocean._krylov()          # the ocean's block preconditioner settings
@@ -212,6 +228,12 @@ class CoupledModel:
         opt.krylov_dim = int(sp["FGMRES iterations"])
         opt.max_restarts = int(sp["FGMRES restarts"])
         opt.prec = int(sp.get("Preconditioner", opt.prec))
+        # "Solver": FGMRES (CoupledModel::FGMRESSolve) or IDR (config C4: IDR(4),
+        # IDRSolver.H:109-340)
+        opt.method = 1 if str(sp.get("Solver", "FGMRES")).upper() == "IDR" else 0
+        opt.idr_s = int(sp.get("IDR s", 4))
+        opt.idr_angle = float(sp.get("IDR angle", 0.7))
+        opt.idr_replace = int(bool(sp.get("IDR replace residuals", False)))
         b = np.ascontiguousarray(b, dtype=np.float64)
         x = np.zeros(self.N)
         info = _lib.SolveInfo()

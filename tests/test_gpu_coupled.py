@@ -171,3 +171,36 @@ def test_gpu_coupled_fgmres(coupled4):
     A = assembled(cm, c, g, L, oc)
     r = np.linalg.norm(A @ dx + F) / np.linalg.norm(F)
     assert info.converged and r <= 1e-7, (info.iters, r)
+
+
+def test_gpu_coupled_idr4(coupled4):
+    """config C4's IDR(4) solver path (IDRSolver.H:109-340) on the coupled system."""
+    c, g, L, oc, atm, cm = coupled4
+    x = cf.synthetic_state(c, cf.landmask(c), amp_ts=1e-3)
+    oc.setState(x)
+    atm.setState(g["xa"])
+    cm.computeJacobian()
+    F = cm.computeRHS()
+    old = dict(cm.solver_params)
+    cm.solver_params.update({"Solver": "IDR", "IDR s": 4, "FGMRES iterations": 400,
+                             "FGMRES restarts": 0})
+    try:
+        dx = cm.solve(-F)
+    finally:
+        cm.solver_params = old
+    info = cm.last_solve
+    print("coupled IDR(4) iterations", info.iters, "explicit", info.explicit_rel_res)
+    A = assembled(cm, c, g, L, oc)
+    r = np.linalg.norm(A @ dx + F) / np.linalg.norm(F)
+    assert info.converged and r <= 1e-7, (info.iters, r)
+
+
+def test_gpu_coupled_newton_step(coupled4):
+    """A Newton step of the coupled model reduces ||F|| (Newton.H:76-123)."""
+    c, g, L, oc, atm, cm = coupled4
+    x = cf.synthetic_state(c, cf.landmask(c), amp_ts=1e-3)
+    oc.setState(x)
+    atm.setState(g["xa"])
+    rec = cm.newtonStep()
+    print("coupled Newton step", rec)
+    assert rec["converged"] and rec["norm_f1"] < rec["norm_f0"]
