@@ -123,8 +123,61 @@ def cpu_baseline(cfg, L, x, args):
     }
 
 
+def bench_coupled(args):
+    """Config C4: the coupled ocean + atmosphere model at 4 degrees (run/coupled: ocean
+    96x38x12 with Coupled Temperature = 1, Mixing 1; the atmosphere on the same grid),
+    one Newton step of CoupledModel (F, J, the block Gauss-Seidel preconditioner set-up,
+    FGMRES or IDR(s) to tol, update, F).  One GPU (the coupled grid is small)."""
+    import torch
+    from iemic import config as cf
+    from iemic.coupled import RUN_COUPLED_ATMOS, Atmosphere, CoupledModel
+    from iemic.ocean import Ocean
+    cfg = cf.preset("coupled4")
+    oc = Ocean(cfg, solver_params={"Dyn iterations": args.dyn_iters})
+    atm = Atmosphere(oc, {**RUN_COUPLED_ATMOS,
+                          "Combined Forcing": cfg.start_params["Combined Forcing"]})
+    sp = {"FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
+          "FGMRES tolerance": args.tol, "Solver": args.solver, "IDR s": args.idr_s}
+    cm = CoupledModel(oc, atm, sp)
+    L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
+    xo = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
+    with np.load(os.path.join(ROOT, "tests", "golden", "coupled4.npz"), allow_pickle=False) as d:
+        xa = d["xa"].astype(np.float64)
+
+    def step():
+        oc.setState(xo)
+        atm.setState(xa)
+        return cm.newtonStep()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    recs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        recs.append(step())
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    r = recs[-1]
+    out = {"metric": "coupled ocean+atmosphere Newton-step wall time (config C4)",
+           "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": False,
+           "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "data": (f"synthetic ocean state (splitmix64, T,S ~ U(+-{args.amp_ts:g})), atmosphere "
+                    "state of tests/golden/coupled4.npz (idealized profile + seeded noise); "
+                    "Combined Forcing 0.5; states reset from host each step"),
+           "config": {"workload": "coupled4: ocean 96x38x12 (coupled T, Mixing 1) + atmosphere "
+                                  "96x38 (T, q, A, P), one Newton step", "rows": cm.N,
+                      "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
+                      "prec": "forward block Gauss-Seidel: ocean block GS, atmosphere exact"},
+           "newton": r, "roofline": None, "cpu_baseline": None}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "coupled4":
+        return bench_coupled(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -47,6 +47,20 @@ ATMOS_PARAMS = {
     "melt threshold width (deg C)": "epm", "rain/snow threshold width (deg C)": "epr",
     "accumulation threshold width (m/y)": "epa",
 }
+# run/coupled/atmosphere_params.xml (the reference's coupled run) over the defaults
+RUN_COUPLED_ATMOS = {
+    "restoring timescale tauf (in days)": 10.0, "restoring timescale tauc (in days)": 1.0,
+    "radiative flux param A": 216.0, "radiative flux param B": 1.5,
+    "background temperature seaice": -5.0, "atmos reference humidity": 8e-3,
+    "atmos humidity scale": 1e-3, "temperature eddy diffusivity": 3.4e6,
+    "humidity eddy diffusivity": 3.1e6, "reference albedo": 0.3, "albedo excursion": 0.4,
+    "melt temperature threshold (deg C)": 0.0, "melt threshold width (deg C)": 5.0,
+    "accumulation precipitation threshold (m/y)": -100.0,
+    "accumulation threshold width (m/y)": 5.0,
+    "rain/snow temperature threshold (deg C)": 150.0, "rain/snow threshold width (deg C)": 5.0,
+    "Combined Forcing": 1.0, "Solar Forcing": 1.0, "Humidity Forcing": 1.0,
+    "Latent Heat Forcing": 1.0, "Albedo Forcing": 0.0,
+}
 # continuation parameters (AtmosLocal allParameters_)
 ATMOS_PARS = ["Combined Forcing", "Solar Forcing", "Longwave Forcing", "Humidity Forcing",
               "Latent Heat Forcing", "Albedo Forcing", "T Eddy Diffusivity"]
