@@ -35,6 +35,8 @@ DEFAULTS = {
     "give up at minimum step size": True, "enable Newton Chord hybrid solve": False,
     "tangent type": "S", "corrector residual test": "D", "initial tangent type": "E",
     "post processing": "at every point", "predictor bound": 1e3,
+    # Continuation.H:1336-1338
+    "enable backtracking": False, "backtracking steps": 0, "backtracking increase": 0.0,
 }
 
 
@@ -96,6 +98,10 @@ class Continuation:
         self.initialTangent = p["initial tangent type"]
         self.postProcessMode = p["post processing"]
         self.predictorBound = float(p["predictor bound"])
+        self.backTracking = bool(p["enable backtracking"])
+        self.numBackTrackingSteps = int(p["backtracking steps"])
+        self.backTrackIncrease = float(p["backtracking increase"])
+        self.backTrack = 0
         self.destinations = []
         for i in range(999):
             d = p.get(f"destination {i}")
@@ -249,6 +255,10 @@ class Continuation:
             self.normRHStest = self._norm(self.model.getRHS("V"))
             if self.normRHStest > self.predictorBound:
                 return 1
+            # no decrease: backtracking along the Newton direction (Continuation.H:724-731)
+            if self.backTracking and self.normRHS < self.normRHStest:
+                if self.runBackTracking(stateDir, parDir):
+                    return 1
             n0 = self._norm(self.st.state0)
             if self._norm(stateDir) > 1e3 * n0 and n0 > 0:
                 return 1
@@ -261,6 +271,28 @@ class Continuation:
         if not self.chordHybrid and y is not None:
             self.stateDot = y
         if res > self.newtonTol and self.rejectFailed:
+            return 1
+        return 0
+
+    # ---- 816-855 ---------------------------------------------------------------------
+    def runBackTracking(self, stateDir, parDir) -> int:
+        """Halve the step back along (stateDir, parDir) until ||F|| drops below
+        increase * ||F_old|| or the step budget is spent."""
+        reduction = -1.0 / 2
+        increase = self.backTrackIncrease
+        self.backTrack = 0
+        while self.backTrack != self.numBackTrackingSteps:
+            if self.normRHStest < self.normRHS * increase:
+                break
+            self.state = self.model.getState("C") + reduction * stateDir
+            self._set_state(self.state)
+            self.par = self.par + reduction * parDir
+            self.model.setPar(self.parName, self.par)
+            self.model.computeRHS()
+            self.normRHStest = self._norm(self.model.getRHS("V"))
+            reduction /= 2.0
+            self.backTrack += 1
+        if self.normRHStest > self.normRHS * increase and self.numBackTrackingSteps > 0:
             return 1
         return 0
 

@@ -111,3 +111,24 @@ def test_reft_ocean_continuation_matches_reference_h5():
     for var in (0, 1, 4, 5):                # u, v, T, S (reft_ocean.C:58)
         nx, ny = np.linalg.norm(x[var::6]), np.linalg.norm(y[var::6])
         assert abs(nx - ny) <= 1e-3, (var, nx, ny)
+
+
+def test_backtracking_halves_the_step():
+    """Continuation.H:816-855: with no decrease of ||F|| the corrector step is halved back
+    (cumulative reductions -1/2, -1/4, ...) until ||F|| < increase * ||F_old||."""
+    m = ToyModel(lambda x, l: x ** 3 - l, lambda x, l: np.diag(3 * x ** 2), 1, par=1.0)
+    cont = Continuation(m, {"enable backtracking": True, "backtracking steps": 3,
+                            "backtracking increase": 1.0})
+    cont.initialize()
+    m.x = np.array([10.0])
+    cont.state = m.x.copy()
+    m.computeRHS()
+    cont.normRHS = 1.0                      # pretend the old residual was small
+    cont.normRHStest = float(np.linalg.norm(m.computeRHS()))
+    stateDir = np.array([8.0])
+    assert cont.runBackTracking(stateDir, 0.0) == 1     # never below 1.0: fails after 3 steps
+    assert cont.backTrack == 3
+    np.testing.assert_allclose(m.x, [10.0 - 4.0 - 2.0 - 1.0])
+    # a step that already decreases enough is left alone
+    m.x = np.array([1.0]); cont.normRHS = 5.0; cont.normRHStest = 0.0
+    assert cont.runBackTracking(stateDir, 0.0) == 0 and cont.backTrack == 0
