@@ -204,11 +204,40 @@ class CoupledModel:
     def synchronize(self) -> None:
         check(lib().iemic_coupled_synchronize(self._h), "iemic_coupled_synchronize")
 
+    # ---- the Model surface Continuation / Newton drive (Model.H, Combined_MultiVec) ------
+    def getState(self, mode: str = "C") -> np.ndarray:
+        return np.concatenate([self.ocean.getState(), self.atmos.getState()])
+
+    def setState(self, x: np.ndarray) -> None:
+        x = np.asarray(x, dtype=np.float64)
+        self.ocean.setState(x[:self.ocean.N])
+        self.atmos.setState(x[self.ocean.N:])
+
+    def getRHS(self, mode: str = "C") -> np.ndarray:
+        F = getattr(self, "_F", None)
+        if F is None:
+            F = self.computeRHS()
+        return F.copy() if mode == "C" else F
+
+    def getPar(self, name: str) -> float:
+        """CoupledModel::getPar: the first model that knows the parameter."""
+        from .config import PAR_INDEX
+        if name in PAR_INDEX:
+            return self.ocean.getPar(name)
+        return float(self.atmos.getCommPars()[16]) if name == "Combined Forcing" else 0.0
+
+    def preProcess(self) -> None:
+        self.ocean.preProcess()
+
+    def postProcess(self) -> None:
+        pass
+
     def computeRHS(self) -> np.ndarray:
         Fo = np.zeros(self.ocean.N)
         Fa = np.zeros(self.atmos.dim)
         check(lib().iemic_coupled_rhs(self._h, ptr(Fo), ptr(Fa)), "iemic_coupled_rhs")
-        return np.concatenate([Fo, Fa])
+        self._F = np.concatenate([Fo, Fa])
+        return self._F
 
     def computeJacobian(self) -> None:
         check(lib().iemic_coupled_jacobian(self._h), "iemic_coupled_jacobian")

@@ -204,3 +204,22 @@ def test_gpu_coupled_newton_step(coupled4):
     rec = cm.newtonStep()
     print("coupled Newton step", rec)
     assert rec["converged"] and rec["norm_f1"] < rec["norm_f0"]
+
+
+def test_gpu_coupled_continuation(coupled4):
+    """run_coupled's driver: pseudo-arclength continuation (Continuation.H) of the coupled
+    model in Combined Forcing from the rest state of both models, a few steps; every
+    corrector converges and the branch advances."""
+    from iemic.continuation import Continuation
+    c, g, L, oc, atm, cm = coupled4
+    cm.setState(np.zeros(cm.N))
+    cm.setPar("Combined Forcing", 0.0)
+    cont = Continuation(cm, {"continuation parameter": "Combined Forcing",
+                             "initial step size": 1e-2, "maximum step size": 0.05,
+                             "destination 0": 1.0, "maximum number of steps": 3,
+                             "Newton tolerance": 1e-4})
+    cont.run()
+    print("coupled continuation", [(h.par, h.newton_iters, h.norm_f) for h in cont.history])
+    assert len(cont.history) >= 2
+    assert cm.getPar("Combined Forcing") > 0.0
+    assert all(np.isfinite(h.norm_f) for h in cont.history)
