@@ -222,7 +222,7 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     rc |= c->d_frc.alloc(NE);
     rc |= c->d_qcor.alloc(8);
     rc |= c->d_intc.alloc(NE);
-    rc |= c->d_atm.alloc((size_t)3 * n * m);
+    rc |= c->d_atm.alloc((size_t)4 * n * m);
     rc |= c->d_x.alloc(NE);
     rc |= c->d_F.alloc(NE);
     rc |= c->d_B.alloc(NE);
@@ -325,15 +325,14 @@ __global__ void k_ref_to_ext(const double* __restrict__ ref, double* __restrict_
 /* Ocean::synchronize(atmos) (Ocean.C:1443-1472): THCM::setAtmosphereT/Q/A/P (inserted
  * into tatm/qatm/albe/patm, inserts.F90:12-100) and set_atmos_parameters (usrc.F90:237-293:
  * CommPars -> qdim, eta, dqso, eo0, albe0, albed, nus, lvsc; then forcing and lin).  The
- * fields are n*m surface vectors, (j, i) with i fastest; p (patm) only enters with
- * "Coupled Salinity" = 1, which is not supported. */
+ * fields are n*m surface vectors, (j, i) with i fastest; p (patm, dimensional) enters
+ * the salinity flux with "Coupled Salinity" = 1. */
 extern "C" int iemic_set_atmosphere(iemic_ctx* c, const double* t, const double* q, const double* a,
                                     const double* p, const double* commpars)
 {
     CTX_CHECK(c);
-    (void)p;
-    if (!c->cfg.coupled_t) {
-        set_error("iemic_set_atmosphere: the context was not created with coupled_t = 1");
+    if (!c->cfg.coupled_t && !c->cfg.coupled_s) {
+        set_error("iemic_set_atmosphere: the context was created with coupled_t = coupled_s = 0");
         return IEMIC_EINVAL;
     }
     if (!t || !q || !a || !commpars) return IEMIC_EINVAL;
@@ -341,6 +340,7 @@ extern "C" int iemic_set_atmosphere(iemic_ctx* c, const double* t, const double*
     int rc = h2d(c, c->d_atm.p, t, sizeof(double) * nm);
     if (!rc) rc = h2d(c, c->d_atm.p + nm, q, sizeof(double) * nm);
     if (!rc) rc = h2d(c, c->d_atm.p + 2 * nm, a, sizeof(double) * nm);
+    if (!rc && p) rc = h2d(c, c->d_atm.p + 3 * nm, p, sizeof(double) * nm);
     if (rc) return rc;
     c->su.set_atmos(commpars);
     c->jac_valid = 0;

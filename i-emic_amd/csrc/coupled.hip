@@ -460,6 +460,9 @@ struct CplPar {
     double dTFQ;           /* nuq tdim/qdim dqso (1 - M)  (Atmosphere.C:547)        */
     double pfac;           /* (1/A)(tdim/qdim) dqso        (Atmosphere.C:596-597)   */
     double Ooa, aft, dqft; /* Ocean.C:1613-1627: Ooa, -comb sunp albed, lvsc eta qdim */
+    int ct, cs;            /* coupled_T, coupled_S                                  */
+    double nus;            /* Ocean.C:1639-1651: -dQFS = nus, -dPFS = nus Pd        */
+    int64_t sint_row;      /* packed row of the ocean's integral condition, or -1   */
 };
 
 /* SST of the ocean state: T at (i, j, l-1) (Ocean::interfaceT -> Atmosphere::synchronize) */
@@ -471,19 +474,23 @@ __global__ void k_sst(CplPar K, const double* __restrict__ xo_ext, double* __res
     const int64_t cell = ((int64_t)(j + HALO) * K.l + (K.l - 1)) * K.n + i;
     sst[q] = xo_ext[NUN * cell + TT];
 }
-/* Atmosphere::interfaceT/Q/A (449-493): the surface fields the ocean needs */
-__global__ void k_atm_fields(const double* __restrict__ xa, double* __restrict__ out, int nm)
+/* Atmosphere::interfaceT/Q/A/P (449-493, getP 1160-1225): the surface fields the ocean
+ * needs; P dimensional, Pdist (Eo0 + eta qdim P) over water */
+__global__ void k_atm_fields(AtmPar P, AtmGeo G, const double* __restrict__ xa, double* __restrict__ out, int nm)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nm) return;
     out[q] = xa[ANUN * q + AT];
     out[nm + q] = xa[ANUN * q + AQ];
     out[2 * nm + q] = xa[ANUN * q + AA];
+    out[3 * nm + q] = G.surf[q] == 0 ? G.pdist[q] * (P.Eo0 + P.eta * P.qdim * xa[G.rowP]) : 0.0;
 }
 
-/* y_o(surface T rows) += C_oa x_a  (Ocean::getBlock(atmos): -dTFT, -dAFT, -dQFT) */
+/* y_o(surface T rows) += C_oa x_a  (Ocean::getBlock(atmos): -dTFT, -dAFT, -dQFT; with
+ * coupled_S the surface S rows: -dQFS, -dPFS) */
 __global__ void k_cpl_oa(CplPar K, const int* __restrict__ surf, const double* __restrict__ suno,
-                         const double* __restrict__ xa, double* __restrict__ yo_packed)
+                         const double* __restrict__ pdist, int rowP, const double* __restrict__ xa,
+                         double* __restrict__ yo_packed)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= K.n * K.m) return;
@@ -494,11 +501,21 @@ __global__ void k_cpl_oa(CplPar K, const int* __restrict__ surf, const double* _
     const double dTFT = K.Ooa * (1.0 - 0.0);
     const double dAFT = K.aft * S * (1.0 - 0.0);
     const double dQFT = K.dqft * (1.0 - 0.0);
-    double z = 0.0;
-    z += -dTFT * xa[ANUN * q + AT];
-    z += -dAFT * xa[ANUN * q + AA];
-    z += -dQFT * xa[ANUN * q + AQ];
-    yo_packed[NUN * lc + TT] += z;
+    if (K.ct) {
+        double z = 0.0;
+        z += -dTFT * xa[ANUN * q + AT];
+        z += -dAFT * xa[ANUN * q + AA];
+        z += -dQFT * xa[ANUN * q + AQ];
+        yo_packed[NUN * lc + TT] += z;
+    }
+    if (K.cs && NUN * lc + SS != K.sint_row) {
+        const double dQFS = -K.nus * (1.0 - 0.0);
+        const double dPFS = -K.nus * pdist[q] * (1.0 - 0.0);
+        double z = 0.0;
+        z += -dQFS * xa[ANUN * q + AQ];
+        z += -dPFS * xa[rowP];
+        yo_packed[NUN * lc + SS] += z;
+    }
 }
 /* y_a += C_ao x_o on the T and q rows (Atmosphere::getBlock(ocean)) */
 __global__ void k_cpl_ao(CplPar K, AtmGeo G, const double* __restrict__ xo_packed, double* __restrict__ ya)
@@ -648,8 +665,8 @@ int coupled_check(iemic_ctx* c)
         set_error("coupled model: one process only (the coupled grid is 4 degrees)");
         return IEMIC_EINVAL;
     }
-    if (!c->cfg.coupled_t) {
-        set_error("coupled model: the ocean context needs coupled_t = 1");
+    if (!c->cfg.coupled_t && !c->cfg.coupled_s) {
+        set_error("coupled model: the ocean context needs coupled_t = 1 (or coupled_s = 1)");
         return IEMIC_EINVAL;
     }
     return 0;
@@ -1071,6 +1088,10 @@ CplPar cpl_par(const iemic_coupled* cm)
     K.Ooa = su.Ooa;
     K.aft = -su.par[P_COMB] * su.par[P_SUNP] * P.da;
     K.dqft = su.lvsc * su.eta_a * su.qdim_a;
+    K.ct = oc->cfg.coupled_t;
+    K.cs = oc->cfg.coupled_s;
+    K.nus = su.nus;
+    K.sint_row = oc->rowintcon >= 0 ? oc->rowintcon - NUN * oc->own0 : -1;
     return K;
 }
 
@@ -1082,7 +1103,8 @@ int cpl_sync(iemic_coupled* cm)
     iemic_atmos* a = cm->at;
     const int nm = a->n * a->m;
     hipStream_t s = oc->stream;
-    hipLaunchKernelGGL(k_atm_fields, dim3((nm + 255) / 256), dim3(256), 0, s, (const double*)a->d_x.p, oc->d_atm.p, nm);
+    hipLaunchKernelGGL(k_atm_fields, dim3((nm + 255) / 256), dim3(256), 0, s, a->P, atm_geo(a), (const double*)a->d_x.p,
+                       oc->d_atm.p, nm);
     double pars[18];
     iemic_atmos_commpars(a, pars);
     /* the ocean Jacobian depends on the CommPars only through lin's latent-heat term */
@@ -1113,7 +1135,8 @@ int cpl_apply(iemic_coupled* cm, const double* x, double* y)
     HIP_OK(hipMemcpyAsync(y, cm->yo.p + o, sizeof(double) * NL, hipMemcpyDeviceToDevice, s));
     if ((rc = atm_spmv_dev(a, x + NL, y + NL))) return rc;
     hipLaunchKernelGGL(k_cpl_oa, dim3((nm + 255) / 256), dim3(256), 0, s, K, (const int*)a->d_surf.p,
-                       (const double*)(oc->d_tab.p + 9 * (oc->m + 2) + 2 * (oc->l + 2)), x + NL, y);
+                       (const double*)(oc->d_tab.p + 9 * (oc->m + 2) + 2 * (oc->l + 2)), (const double*)a->d_pdist.p,
+                       a->rowP, x + NL, y);
     hipLaunchKernelGGL(k_cpl_ao, dim3((nm + 255) / 256), dim3(256), 0, s, K, atm_geo(a), x, y + NL);
     hipLaunchKernelGGL(k_cpl_pdot, dim3(AR_BLOCKS), dim3(256), 0, s, K, (const double*)a->d_pint.p, x,
                        a->d_red.p + 3 * AR_BLOCKS);

@@ -413,6 +413,9 @@ struct Setup {
         g.rho_mixing = cfg.rho_mixing;
         g.alphaT = cfg.alpha_t;
         g.coupled_t = cfg.coupled_t;
+        g.coupled_s = cfg.coupled_s;
+        g.dedt_s = qdim_a != 0.0 ? nus * (1.0 / qdim_a) * dqso : 0.0;
+        g.qsnd = qsnd;
         g.Ooa = Ooa;
         g.dedt = qdim_a != 0.0 ? dedt() : 0.0;
         g.lvsc = lvsc;

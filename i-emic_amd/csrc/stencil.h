@@ -137,10 +137,11 @@ struct Geo {
     /* coupled atmosphere ("Coupled Temperature" = 1; usrc.F90:726-736, forcing.F90:75-95,
      * m_atm after atmos_coef 1183-1223 and set_atmos_parameters 237-293).  No sea ice:
      * the mask msi is zero, so its terms vanish */
-    int coupled_t;
+    int coupled_t, coupled_s;
     double Ooa, dedt, lvsc, eta_a, qdim_a, eo0, albe0, albed;
+    double dedt_s, qsnd;            /* coupled_S: nus (deltat/qdim) dqso; QSnd          */
     const double* suno;             /* suno(j), j = 0..m+1 (atmos_coef)                 */
-    const double* atm;              /* tatm | qatm | albe, each (j-1)*n + (i-1), n*m    */
+    const double* atm;              /* tatm | qatm | albe | patm, (j-1)*n + (i-1), n*m  */
 };
 
 HD int LM(const Geo& g, int i, int j, int k)
@@ -446,6 +447,11 @@ template <int R> HD double lin_val(const Geo& g, const CellCtx& c, int pos, int 
             return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
                    g.tres * bi * at_tc(g, c, pos);
     } else if (R == SS) {
+        /* coupled_S: no restoring; the evaporation's SST dependence (usrc.F90:753-766;
+         * the sea-ice terms, mc = 0, add zeros) */
+        if (col == SS && g.coupled_s)
+            return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos);
+        if (col == TT && g.coupled_s) return -g.dedt_s * at_tc(g, c, pos);
         if (col == SS)
             return -ph * (at_txx(g, c, pos) + at_tyy(g, c, pos)) - pv * at_tzz(g, c, pos) +
                    g.sres * bi * at_tc(g, c, pos);
@@ -1219,10 +1225,20 @@ HD void forcing_cell(const Geo& g, const double* ftab, const double* qcor, int i
         }
         const double gamma = par[P_COMB] * par[P_SALT] * ((double)(1 - SRES) + SRES * par[P_BIOT]);
         const double emip = salf[j] * (1 - LM(g, i, j, l));
-        f[SS] = gamma * (1 - par[P_HMTP]) * (emip - qcor[1]) +
-                gamma * par[P_HMTP] * (0.0 - qcor[2]) +
-                par[P_SPER] * ((double)(1 - SRES) + SRES * par[P_BIOT]) *
-                    (spert[(j - 1) * n + (i - 1)] - qcor[3]);
+        if (g.coupled_s) {
+            /* E - P salinity flux (forcing.F90:162-182): QSoa = pQSnd (eo0 - eta qdim q - P);
+             * no sea ice (msi = gsi = 0) */
+            const int64_t q = (int64_t)(j - 1) * n + (i - 1);
+            const int64_t nm = (int64_t)n * m;
+            const double pQSnd = par[P_COMB] * par[P_SALT] * g.qsnd;
+            const double QSoa = pQSnd * (g.eo0 - g.eta_a * g.qdim_a * g.atm[nm + q] - g.atm[3 * nm + q]);
+            f[SS] = QSoa * (double)(1 - LM(g, i, j, l));
+        } else {
+            f[SS] = gamma * (1 - par[P_HMTP]) * (emip - qcor[1]) +
+                    gamma * par[P_HMTP] * (0.0 - qcor[2]) +
+                    par[P_SPER] * ((double)(1 - SRES) + SRES * par[P_BIOT]) *
+                        (spert[(j - 1) * n + (i - 1)] - qcor[3]);
+        }
     }
     if (k <= l - 1)
         f[WW] = -par[P_COMB] * (1 - LM(g, i, j, k)) * par[P_RAYL] *

@@ -27,7 +27,8 @@ class Grid(C.Structure):
                 ("coriolis_on", C.c_int), ("alpha_t", C.c_double), ("alpha_s", C.c_double),
                 ("int_sign", C.c_int), ("int_i", C.c_int), ("int_j", C.c_int),
                 ("analyze_jacobian", C.c_int), ("max_mask_fixes", C.c_int),
-                ("device", C.c_int), ("rho_mixing", C.c_int), ("coupled_t", C.c_int)]
+                ("device", C.c_int), ("rho_mixing", C.c_int), ("coupled_t", C.c_int),
+                ("coupled_s", C.c_int)]
 
 
 class Dist(C.Structure):
@@ -71,7 +72,8 @@ def grid_from_config(cfg, device: int = 0, analyze_jacobian: bool = True) -> Gri
                 cfg.hdim, cfg.qz, cfg.tres, cfg.sres, cfg.forcing_type,
                 cfg.inhomogeneous_mixing, cfg.mixing, cfg.coriolis, cfg.alpha_t, cfg.alpha_s,
                 cfg.int_sign, cfg.integral_i, cfg.integral_j, int(analyze_jacobian), 5, device,
-                int(cfg.rho_mixing), int(getattr(cfg, "coupled_t", 0)))
+                int(cfg.rho_mixing), int(getattr(cfg, "coupled_t", 0)),
+                int(getattr(cfg, "coupled_s", 0)))
 
 
 _lib = None

@@ -74,6 +74,7 @@ class THCMConfig:
     integral_i: int = -1
     integral_j: int = -1
     coupled_t: int = 0            # "Coupled Temperature" (coupled_T, THCM.C:232)
+    coupled_s: int = 0            # "Coupled Salinity" (coupled_S)
     refine: int = 1               # synthetic horizontal refinement of the mask
     refine_l: int = 0             # target layer count for vertical remap (0: none)
     start_params: Dict[str, float] = dataclasses.field(default_factory=dict)
@@ -110,7 +111,7 @@ class THCMConfig:
             hdim=self.hdim, qz=self.qz, itopo=self.topography, flat=int(self.flat),
             rd_mask=int(self.read_land_mask), maskfile=self.land_mask, tres=self.tres,
             sres=self.sres, iza=self.wind_forcing_type, ite=self.levitus_t,
-            its=self.levitus_s, rd_spertm=0, coupled_T=self.coupled_t, coupled_S=0,
+            its=self.levitus_s, rd_spertm=0, coupled_T=self.coupled_t, coupled_S=self.coupled_s,
             forcing_type=self.forcing_type, ih=self.inhomogeneous_mixing, vmix=self.mixing,
             tap=self.taper, rho_mixing=int(self.rho_mixing), coriolis_on=self.coriolis,
             alphaT=self.alpha_t, alphaS=self.alpha_s, int_sign=self.int_sign,
@@ -303,6 +304,9 @@ def preset(name: str, mixing: Optional[int] = None) -> THCMConfig:
                                      "Salinity Forcing": 1.0, "Wind Forcing": 1.0,
                                      "Temperature Forcing": 1.0, "SPL1": 2.0e3,
                                      "SPL2": 0.01, "Horizontal Ekman-Number": 0.0027037})
+    elif name == "coupled_natl8s":
+        # coupled_natl8 with "Coupled Salinity" = 1 as well (E - P salinity flux)
+        c = preset("coupled_natl8").with_(name=name, coupled_s=1)
     elif name in ("coupled4", "coupled_natl8"):
         # run/coupled/ocean_params.xml: the global 4-degree ocean with Coupled Temperature 1,
         # Coupled Salinity 0, qz 1.5 (config C4); coupled_natl8: the same physics on the
@@ -322,4 +326,4 @@ def preset(name: str, mixing: Optional[int] = None) -> THCMConfig:
 
 
 PRESETS = ("test6x6x4", "natl8", "gateway16", "2dmoc", "2dmoc_run", "global4", "global2",
-           "global1", "coupled4", "coupled_natl8")
+           "global1", "coupled4", "coupled_natl8", "coupled_natl8s")

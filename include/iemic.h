@@ -65,6 +65,7 @@ typedef struct {
     int rho_mixing;              /* "Rho mixing" (vmix_fun: mix T and S as density)  */
     int coupled_t;               /* "Coupled Temperature" (THCM.C:232): surface heat    */
                                  /* flux from an atmosphere (iemic_set_atmosphere)      */
+    int coupled_s;               /* "Coupled Salinity": E - P salinity flux (same)      */
 } iemic_grid;
 
 /* Krylov settings (Ocean.C:961-1020, getDefaultInitParameters 2232-2237). */
@@ -151,7 +152,7 @@ int  iemic_get_par(iemic_ctx* ctx, int idx, double* value);
  * P on the n*m surface ((j, i), i fastest) and the 18 AtmosLocal::CommPars
  * (AtmosLocal.H:40-60) -> THCM::setAtmosphereT/Q/A/P + set_atmos_parameters_
  * (usrc.F90:237-293).  Refreshes the forcing; the next iemic_jacobian uses the new
- * latent-heat coefficient. */
+ * latent-heat coefficient.  p (patm) enters with coupled_s = 1. */
 int  iemic_set_atmosphere(iemic_ctx* ctx, const double* t, const double* q, const double* a,
                           const double* p, const double* commpars);
 /* getdeps_ (usrc.F90:201-219, called by AtmosLocal::setup and Ocean::getBlock):

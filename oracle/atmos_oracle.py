@@ -428,11 +428,12 @@ class AtmosOracle:
                 rows.append(self.rowP); cols.append(oc); vals.append(dTFP)
         return sp.csr_matrix((vals, (rows, cols)), shape=(self.dim, N_o))
 
-    def block_to_ocean(self, l, ocean_surf, deps, comb, sunp) -> sp.csr_matrix:
-        """Ocean::getBlock(atmos) (Ocean.C:1538-1667), coupled_T = 1, coupled_S = 0.
+    def block_to_ocean(self, l, ocean_surf, deps, comb, sunp, coupled_s=False,
+                       rowintcon=-1) -> sp.csr_matrix:
+        """Ocean::getBlock(atmos) (Ocean.C:1538-1667), coupled_T = 1 (and coupled_S).
         deps = getdeps (Ooa, Os, nus, eta, lvsc, qdim, pQSnd); comb/sunp: the ocean's."""
         n, m, P = self.n, self.m, self.P
-        Ooa, _, _, eta, lvsc, qdim, _ = [float(v) for v in deps]
+        Ooa, _, nus, eta, lvsc, qdim, _ = [float(v) for v in deps]
         N_o = 6 * n * m * l
         rows, cols, vals = [], [], []
         osurf = np.asarray(ocean_surf).reshape(m, n)
@@ -450,6 +451,12 @@ class AtmosOracle:
                 for c, v in ((self.row(i, j, TT), -dTFT), (self.row(i, j, AA), -dAFT),
                              (self.row(i, j, QQ), -dQFT)):
                     rows.append(r); cols.append(c); vals.append(v)
+                rs = r + 1                          # the surface S row
+                if coupled_s and rs != rowintcon:
+                    dQFS = -nus * (1.0 - M)
+                    dPFS = -nus * self.pdist[sr] * (1.0 - M)
+                    for c, v in ((self.row(i, j, QQ), -dQFS), (self.rowP, -dPFS)):
+                        rows.append(rs); cols.append(c); vals.append(v)
         return sp.csr_matrix((vals, (rows, cols)), shape=(N_o, self.dim))
 
 

@@ -160,7 +160,7 @@ static void do_init(void* p)
     double* spert = (double*)calloc(nm, sizeof(double));
     /* iza==2, ite==1, its==1 (idealized) give zero fields (global.F90:432-563); so does
      * coupled_T = 1 (get_temforcing puts tatm = 0, global.F90:472-510) */
-    if (iza != 2 || ite != 1 || its != 1 || cT < 0 || cT > 1 || cS != 0) {
+    if (iza != 2 || ite != 1 || its != 1 || cT < 0 || cT > 1 || cS < 0 || cS > 1) {
         fprintf(stderr, "thcm_ref: only idealized ocean-only forcing is supported\n");
         a->rc = -1;
         return;

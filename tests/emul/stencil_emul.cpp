@@ -59,11 +59,12 @@ void* emul_create_band(const iemic_grid* grid, const int* landm, int jb0, int jb
     Emul* e = new Emul();
     e->su.init(*grid, landm, jb0, jb1);
     e->su.vmix_init();
-    e->atm.assign((size_t)3 * e->su.n * e->su.m, 0.0);
+    e->atm.assign((size_t)4 * e->su.n * e->su.m, 0.0);
     return e;
 }
 /* iemic_set_atmosphere (capi.hip) on the CPU */
-void emul_set_atmosphere(void* h, const double* t, const double* q, const double* a, const double* pars)
+void emul_set_atmosphere(void* h, const double* t, const double* q, const double* a, const double* p,
+                         const double* pars)
 {
     Emul* e = (Emul*)h;
     const size_t nm = (size_t)e->su.n * e->su.m;
@@ -71,6 +72,7 @@ void emul_set_atmosphere(void* h, const double* t, const double* q, const double
         e->atm[r] = t[r];
         e->atm[nm + r] = q[r];
         e->atm[2 * nm + r] = a[r];
+        e->atm[3 * nm + r] = p ? p[r] : 0.0;
     }
     e->su.set_atmos(pars);
 }

@@ -8,7 +8,7 @@ AtmosLocal::CommPars of the atmosphere restatement oracle/atmos_oracle.py), and 
 Fortran Jacobian and right-hand side (matrix_/rhs_, usrc.F90:432-586) plus getdeps
 (usrc.F90:201-219: Ooa, Os, nus, eta, lvsc, qdim, pQSnd).
 
-coupled_natl8 keeps full arrays; coupled4 (96x38x12, the C4 ocean) keeps SHA-256 digests.
+coupled_natl8 (and coupled_natl8s, with "Coupled Salinity" = 1 too) keep full arrays; coupled4 (96x38x12, the C4 ocean) keeps SHA-256 digests.
 The atmosphere state and fields are regenerated from the seeds below by the tests.
 
 Usage (this container only):  python tests/golden/make_golden_coupled.py
@@ -31,7 +31,7 @@ from oracle import oracle as orc  # noqa: E402
 from oracle import atmos_oracle as ao  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
-NAMES = ["coupled_natl8", "coupled4"]
+NAMES = ["coupled_natl8", "coupled_natl8s", "coupled4"]
 SEED_ATM = 20261017
 
 
@@ -113,7 +113,7 @@ def main() -> None:
                 if a.dtype.kind == "f":
                     st[f + "_norm"] = float(np.linalg.norm(a))
             entry["states"][k] = st
-            if name == "coupled_natl8":
+            if name.startswith("coupled_natl8"):
                 for f in ("beg", "jco", "co", "coB", "B"):
                     arrays[f"{k}_{f}"] = r[f"{f}{s}"]
                 arrays[f"{k}_x"] = states[k]

@@ -149,11 +149,12 @@ class Emul:
         return self.to_ref(Fe)
 
 
-def emul_set_atmosphere(e: "Emul", t, q, a, pars) -> None:
+def emul_set_atmosphere(e: "Emul", t, q, a, pars, p=None) -> None:
     """iemic_set_atmosphere on the CPU emulation of the device assembly."""
     lib = e.lib
-    lib.emul_set_atmosphere.argtypes = [C.c_void_p] + [P(C.c_double)] * 4
-    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (t, q, a, pars)]
+    lib.emul_set_atmosphere.argtypes = [C.c_void_p] + [P(C.c_double)] * 5
+    p = np.zeros_like(np.asarray(t, dtype=np.float64)) if p is None else p
+    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (t, q, a, p, pars)]
     lib.emul_set_atmosphere(e.h, *[_lib.ptr(v) for v in arrs])
 
 

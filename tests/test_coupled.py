@@ -45,14 +45,15 @@ def fortran_placed(oracle_lib, rowptr, col, g, kind):
                                        g[f"{kind}_co"], -1)
 
 
+@pytest.mark.parametrize("name", ["coupled_natl8", "coupled_natl8s"])
 @pytest.mark.parametrize("kind", ["zero", "synthetic"])
-def test_emulated_coupled_ocean_bitexact(oracle_lib, emul, kind):
-    """coupled_natl8: the device assembly code (CPU emulation) == reference Fortran."""
-    name = "coupled_natl8"
+def test_emulated_coupled_ocean_bitexact(oracle_lib, emul, name, kind):
+    """coupled_natl8 (coupled T) and coupled_natl8s (coupled T and S): the device assembly
+    code (CPU emulation) == reference Fortran, bitwise."""
     c = cf.preset(name)
     g = golden(name)
     e = Emul(c, landm_of(name))
-    emul_set_atmosphere(e, *atm_args(g))
+    emul_set_atmosphere(e, *atm_args(g), p=g["atm_p"])
     np.testing.assert_array_equal(bits(emul_get_deps(e)), bits(g["deps"]))
     x = g[f"{kind}_x"]
     rowptr, col, val, B = e.jacobian_csr(x)
@@ -109,13 +110,14 @@ def test_atmos_oracle_fd_jacobian():
         assert not np.any(C[:, mask])
 
 
-def test_ocean_block_matches_fortran_fd(oracle_lib):
+@pytest.mark.parametrize("name", ["coupled_natl8", "coupled_natl8s"])
+def test_ocean_block_matches_fortran_fd(oracle_lib, name):
+    """Ocean::getBlock(atmos) (Ocean.C:1538-1667) == the derivative of the reference
+    Fortran's residual w.r.t. the inserted atmosphere T, q, albedo (and, with coupled S,
+    P) fields (forcing.F90:75-94, 162-182 are linear in them: a unit perturbation gives
+    the entry up to rounding)."""
     if not oracle_lib.reference_available():
         pytest.skip("reference Fortran library not built (this container only)")
-    """Ocean::getBlock(atmos) (Ocean.C:1538-1667) == the derivative of the reference
-    Fortran's residual w.r.t. the inserted atmosphere T, q, albedo fields (forcing.F90:75-94
-    is linear in them: a unit perturbation gives the entry up to rounding)."""
-    name = "coupled_natl8"
     c = cf.preset(name)
     g = golden(name)
     L = cf.landmask(c)
@@ -128,23 +130,31 @@ def test_ocean_block_matches_fortran_fd(oracle_lib):
                                 "Combined Forcing": c.start_params["Combined Forcing"]})
     at.suno_ocean = np.array(at.suno[1:])
     Cb = at.block_to_ocean(c.l, at.surf, g["deps"], c.start_params["Combined Forcing"],
-                           c.start_params["Solar Forcing"]).toarray()
+                           c.start_params["Solar Forcing"], coupled_s=bool(c.coupled_s)).toarray()
     x = g["synthetic_x"]
+    p0 = g["atm_p"]
     runs = {}
     h = 1.0
     sel = [(3, 2), (5, 4)]          # a few surface points (i, j), 0-based
     for (i, j) in sel:
-        for fld, col in (("t", ao.TT), ("q", ao.QQ), ("a", ao.AA)):
-            f2 = dict(t=t.copy(), q=q.copy(), a=a.copy(), p=np.zeros_like(t), pars=pars)
+        for fld in ("t", "q", "a"):
+            f2 = dict(t=t.copy(), q=q.copy(), a=a.copy(), p=p0.copy(), pars=pars)
             f2[fld][j * c.n + i] += h
             runs[(i, j, fld)] = f2
+    if c.coupled_s:
+        # the P anomaly column: the dimensional field moves by Pdist * eta qdim per unit
+        f2 = dict(t=t, q=q, a=a, p=p0 + at.pdist * at.P.eta * at.P.qdim, pars=pars)
+        runs[(0, 0, "P")] = f2
     keys = list(runs)
     base = oracle_lib.run_reference(c.ref_dict(), L, c.par_list(), [x], use_landm=False,
-                                    atmos=dict(t=t, q=q, a=a, p=np.zeros_like(t), pars=pars))
+                                    atmos=dict(t=t, q=q, a=a, p=p0, pars=pars))
     for k in keys:
         r = oracle_lib.run_reference(c.ref_dict(), L, c.par_list(), [x], use_landm=False,
                                      atmos=runs[k])
         dF = (-r["B0"]) - (-base["B0"])
         i, j, fld = k
-        col = at.row(i, j, {"t": ao.TT, "q": ao.QQ, "a": ao.AA}[fld])
-        np.testing.assert_allclose(dF, Cb[:, col], rtol=1e-9, atol=1e-9 * np.abs(Cb).max())
+        if fld == "P":
+            col = at.rowP                   # the perturbation above is one unit of P
+        else:
+            col = at.row(i, j, {"t": ao.TT, "q": ao.QQ, "a": ao.AA}[fld])
+        np.testing.assert_allclose(dF, Cb[:, col], rtol=1e-6, atol=1e-9 * np.abs(Cb).max())

@@ -37,7 +37,7 @@ def setup(name):
     L = landm_of(name)
     oc = Ocean(c, landm=L, analyze_jacobian=False)
     t, q, a, pars = atm_args(g)
-    oc.setAtmosphere(t, q, a, np.zeros_like(t), pars)
+    oc.setAtmosphere(t, q, a, g["atm_p"], pars)
     return c, g, L, oc
 
 
@@ -51,9 +51,10 @@ def atmos_oracle(c, g, L):
     return at
 
 
+@pytest.mark.parametrize("name", ["coupled_natl8", "coupled_natl8s"])
 @pytest.mark.parametrize("kind", ["zero", "synthetic"])
-def test_gpu_coupled_ocean_natl8_bitexact(oracle_lib, kind):
-    c, g, L, oc = setup("coupled_natl8")
+def test_gpu_coupled_ocean_natl8_bitexact(oracle_lib, name, kind):
+    c, g, L, oc = setup(name)
     np.testing.assert_array_equal(bits(oc.getDeps()), bits(g["deps"]))
     x = g[f"{kind}_x"]
     oc.setState(x)
@@ -139,8 +140,35 @@ def assembled(cm, c, g, L, oc):
     Ja = at.jacobian(xa)
     Cao = at.block_from_ocean(c.l)
     Coa = at.block_to_ocean(c.l, at.surf, oc.getDeps(), oc.getPar("Combined Forcing"),
-                            oc.getPar("Solar Forcing"))
+                            oc.getPar("Solar Forcing"), coupled_s=bool(c.coupled_s))
     return sp.bmat([[Jo, Coa], [Cao, Ja]]).tocsr()
+
+
+def make_coupled(name, **sp):
+    from iemic.coupled import Atmosphere, CoupledModel
+    c, g, L, oc = setup(name)
+    atm = Atmosphere(oc, {**ao.COUPLED_RUN_PARAMS,
+                          "Combined Forcing": c.start_params["Combined Forcing"]})
+    return c, g, L, oc, atm, CoupledModel(oc, atm, sp or None)
+
+
+def test_gpu_coupled_salinity_spmv_and_solve():
+    """coupled T and S (E - P salinity flux) on natl8: applyMatrix against the assembled
+    block matrix and an FGMRES solve to 1e-8."""
+    c, g, L, oc, atm, cm = make_coupled("coupled_natl8s", **{"FGMRES iterations": 200,
+                                                            "FGMRES restarts": 4})
+    oc.setState(g["synthetic_x"])
+    atm.setState(g["xa"])
+    cm.computeJacobian()
+    A = assembled(cm, c, g, L, oc)
+    v = np.random.default_rng(2).standard_normal(cm.N)
+    y = cm.applyMatrix(v)
+    scale = abs(A) @ np.abs(v)
+    assert np.max(np.abs(y - A @ v) / np.maximum(scale, 1e-300)) <= 1e-12
+    F = cm.computeRHS()
+    dx = cm.solve(-F)
+    r = np.linalg.norm(A @ dx + F) / np.linalg.norm(F)
+    assert cm.last_solve.converged and r <= 1e-7, (cm.last_solve.iters, r)
 
 
 def test_gpu_coupled_spmv(coupled4):
