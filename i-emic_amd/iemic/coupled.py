@@ -86,6 +86,7 @@ class Atmosphere:
         h = C.c_void_p()
         check(lib().iemic_atmos_create(C.byref(h), ocean._h, C.byref(p)), "iemic_atmos_create")
         self._h = h
+        self._par = {name: float(p.par[i]) for i, name in enumerate(ATMOS_PARS)}
         self.ocean = ocean
         self.dim = lib().iemic_atmos_dim(h)
         self.n, self.m = ocean.cfg.n, ocean.cfg.m
@@ -104,6 +105,10 @@ class Atmosphere:
     def setPar(self, name, value: float) -> None:
         idx = ATMOS_PARS.index(name) if isinstance(name, str) else int(name)
         check(lib().iemic_atmos_set_par(self._h, idx, float(value)), "iemic_atmos_set_par")
+        self._par[ATMOS_PARS[idx]] = float(value)
+
+    def getPar(self, name) -> float:
+        return self._par[name if isinstance(name, str) else ATMOS_PARS[int(name)]]
 
     def setState(self, x: np.ndarray) -> None:
         x = np.ascontiguousarray(x, dtype=np.float64)
@@ -138,6 +143,68 @@ class Atmosphere:
         z = np.zeros(self.dim)
         check(lib().iemic_atmos_prec_apply(self._h, ptr(r), ptr(z)), "iemic_atmos_prec_apply")
         return z
+
+    # ---- state files (Model::saveStateToFile + Atmosphere::additionalExports 1679-1714) ----
+    def _sst(self) -> np.ndarray:
+        """the ocean's surface temperature the atmosphere currently sees (interfaceT)."""
+        oc = self.ocean
+        c = oc.cfg
+        x = oc.getState()
+        return x.reshape(c.l, c.m, c.n, 6)[c.l - 1, :, :, 4].reshape(-1).copy()
+
+    def saveStateToFile(self, filename: str, sst: Optional[np.ndarray] = None) -> None:
+        """HDF5 in the reference's layout: State (Epetra_MultiVector), Parameters (the
+        AtmosLocal continuation names), Grid, and the additional exports E and P
+        (dimensional), sst and MaskGlobal/Surface.  Written by iemic.h5."""
+        import math
+        from . import h5
+        c = self.ocean.cfg
+        x = self.getState()
+        cp = self.getCommPars()
+        tdim, qdim, nuq, eta, dqso, Eo0 = cp[0], cp[1], cp[2], cp[3], cp[4], cp[7]
+        sst = self._sst() if sst is None else np.asarray(sst, dtype=np.float64)
+        pint, _, _, _ = self.integral_coeff()
+        water = pint != 0.0
+        q = x[1:3 * self.n * self.m:3]
+        E = np.where(water, Eo0 + eta * qdim * ((tdim / qdim) * dqso * sst - q), 0.0)
+        P = np.where(water, self.getPdist() * (Eo0 + eta * qdim * x[-1]), 0.0)
+        xmin, xmax = math.radians(c.xmin), math.radians(c.xmax)
+        ymin, ymax = math.radians(c.ymin), math.radians(c.ymax)
+        dx, dy = (xmax - xmin) / c.n, (ymax - ymin) / c.m
+        tree = {
+            "State": {"Values": x.reshape(1, -1), "GlobalLength": np.array(len(x), dtype=np.int32),
+                      "NumVectors": np.array(1, dtype=np.int32),
+                      "__type__": np.array([b"Epetra_MultiVector"], dtype="S19")},
+            "Parameters": {name: np.array(self._par[name]) for name in ATMOS_PARS},
+            "Grid": {"n": np.array(c.n, dtype=np.int32), "m": np.array(c.m, dtype=np.int32),
+                     "l": np.array(1, dtype=np.int32), "nun": np.array(3, dtype=np.int32),
+                     "aux": np.array(1, dtype=np.int32), "xmin": np.array(xmin), "xmax": np.array(xmax),
+                     "ymin": np.array(ymin), "ymax": np.array(ymax),
+                     "x": xmin + dx * (np.arange(c.n) + 0.5), "y": ymin + dy * (np.arange(c.m) + 0.5)},
+            "E": {"Values": E.reshape(1, -1)},
+            "P": {"Values": P.reshape(1, -1)},
+            "sst": {"Values": sst.reshape(1, -1)},
+            "MaskGlobal": {"Surface": (~water).astype(np.int32)},
+        }
+        h5.write(filename, tree)
+
+    def loadStateFromFile(self, filename: str) -> int:
+        """Model::loadStateFromFile: the state and the known parameters; 1 if no file."""
+        import os
+        from . import h5
+        if not os.path.exists(filename):
+            return 1
+        t = h5.read(filename)
+        if "/State/Values" not in t:
+            raise _lib.IemicError(f"The group <State> is not contained in hdf5 {filename}")
+        x = np.asarray(t["/State/Values"][0], dtype=np.float64).reshape(-1)
+        if x.size != self.dim:
+            raise _lib.IemicError(f"{filename}: state of length {x.size}, this model has {self.dim}")
+        self.setState(x)
+        for path, (v, _) in t.items():
+            if path.startswith("/Parameters/") and path.split("/", 2)[2] in ATMOS_PARS:
+                self.setPar(path.split("/", 2)[2], float(np.asarray(v).reshape(-1)[0]))
+        return 0
 
     def getCommPars(self) -> np.ndarray:
         out = np.zeros(18)

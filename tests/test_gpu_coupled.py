@@ -251,3 +251,25 @@ def test_gpu_coupled_continuation(coupled4):
     assert len(cont.history) >= 2
     assert cm.getPar("Combined Forcing") > 0.0
     assert all(np.isfinite(h.norm_f) for h in cont.history)
+
+
+def test_gpu_atmosphere_state_file(coupled4, tmp_path):
+    """Atmosphere state files (Model::saveStateToFile + additionalExports): the written
+    file reads back through the HDF5 reader, and loadStateFromFile restores state and
+    parameters."""
+    from iemic import h5
+    c, g, L, oc, atm, cm = coupled4
+    atm.setState(g["xa"])
+    atm.setPar("Humidity Forcing", 0.75)
+    f = str(tmp_path / "atmos.h5")
+    atm.saveStateToFile(f)
+    t = h5.read(f)
+    np.testing.assert_array_equal(t["/State/Values"][0][0], g["xa"])
+    assert float(np.asarray(t["/Parameters/Humidity Forcing"][0]).reshape(-1)[0]) == 0.75
+    assert t["/E/Values"][0].size == c.n * c.m and t["/P/Values"][0].size == c.n * c.m
+    atm.setState(np.zeros(atm.dim))
+    atm.setPar("Humidity Forcing", 1.0)
+    assert atm.loadStateFromFile(f) == 0
+    np.testing.assert_array_equal(atm.getState(), g["xa"])
+    assert atm.getPar("Humidity Forcing") == 0.75
+    atm.setPar("Humidity Forcing", 1.0)
