@@ -58,8 +58,7 @@ struct iemic_atmos {
     std::vector<double> tab;             /* per j (1..m): datc*cosdx2i, t4, t6, cosdx2i, q4, */
                                          /* q6, suna, suno (8 (m+1))                         */
     std::vector<double> pdist, pint;     /* n*m                                              */
-    std::vector<double> Ai;
-    DevBuf<double> d_tab, d_pdist, d_pint, d_x, d_sst, d_F, d_val, d_red, d_tmp;
+    DevBuf<double> d_tab, d_pdist, d_pint, d_x, d_sst, d_F, d_val, d_red, d_tmp, d_y;
     DevBuf<int> d_surf, d_col;
     /* preconditioner: 9-point T and q operators, their cyclic reductions, work vectors */
     DevBuf<double> d_s9t, d_s9q, d_bt, d_bq, d_zt, d_zq;
@@ -716,8 +715,6 @@ extern "C" int iemic_atmos_create(iemic_atmos** out, iemic_ctx* oc, const iemic_
     const double muoa = p.rhoa * p.ch * p.cpa * p.uw;
     P.amua = (p.arad + p.brad * p.t0a) / muoa;
     P.bmua = p.brad / muoa;
-    const double Ai = p.rhoa * p.hdima * p.cpa * p.udim / (p.r0dim * muoa);
-    a->Ai.assign(1, Ai);
     P.Ad = p.rhoa * p.hdima * p.cpa * p.D0 / (muoa * p.r0dim * p.r0dim);
     const double As = p.sun0 * (1 - p.c0) / (4 * muoa);
     P.eta = (p.rhoa / p.rhoo) * p.ce * p.uw;
@@ -805,6 +802,7 @@ extern "C" int iemic_atmos_create(iemic_atmos** out, iemic_ctx* oc, const iemic_
     rc |= a->d_x.alloc(a->dim);
     rc |= a->d_sst.alloc((size_t)n * m);
     rc |= a->d_F.alloc(a->dim);
+    rc |= a->d_y.alloc(a->dim);
     rc |= a->d_val.alloc((size_t)(a->dim - 1) * ASL);
     rc |= a->d_col.alloc((size_t)(a->dim - 1) * ASL);
     rc |= a->d_red.alloc(4 * AR_BLOCKS);
@@ -1048,13 +1046,9 @@ extern "C" int iemic_atmos_spmv(iemic_atmos* a, const double* x, double* y)
     if (hipSetDevice(a->oc->device) != hipSuccess) return IEMIC_EDEVICE;
     if (!a->jac_valid) return IEMIC_ESTATE;
     double* dx = a->d_tmp.p;                      /* dim <= tmp size */
-    double* dy = a->d_F.p;
-    std::vector<double> keep(a->dim);
-    int rc = d2h(a->oc, keep.data(), a->d_F.p, sizeof(double) * a->dim);
-    if (!rc) rc = h2d(a->oc, dx, x, sizeof(double) * a->dim);
-    if (!rc) rc = atm_spmv_dev(a, dx, dy);
-    if (!rc) rc = d2h(a->oc, y, dy, sizeof(double) * a->dim);
-    if (!rc) rc = h2d(a->oc, a->d_F.p, keep.data(), sizeof(double) * a->dim);
+    int rc = h2d(a->oc, dx, x, sizeof(double) * a->dim);
+    if (!rc) rc = atm_spmv_dev(a, dx, a->d_y.p);
+    if (!rc) rc = d2h(a->oc, y, a->d_y.p, sizeof(double) * a->dim);
     return rc;
 }
 extern "C" int iemic_atmos_prec_apply(iemic_atmos* a, const double* r, double* z)
