@@ -2164,9 +2164,20 @@ static int mg_smooth(iemic_ctx* c, int q, int nu, bool post)
         const int P = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : 64);
         const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
         const unsigned gp = (unsigned)(((int64_t)((np + 1) / 2) * V.mb * P + 255) / 256);
+        /* IEMIC_MG_HALF: 1 -- on the coarse levels the pre-smoother relaxes the first half of
+         * the colours and the post-smoother the second half (backward), so every column is
+         * relaxed once per visit; 2 -- on every level */
+        static const int half_mode = [] {
+            const char* e = getenv("IEMIC_MG_HALF");
+            return e ? atoi(e) : 0;
+        }();
+        const bool half = half_mode == 2 || (half_mode == 1 && q > 0);
+        const int c0 = half && post ? ncolour / 2 : 0;
+        const int nc = half ? ncolour / 2 : ncolour;
         for (int sw = 0; sw < nu; sw++)
-            for (int h = 0; h < ncolour; h++) {
-                const int col = post ? ncolour - 1 - h : h;
+            for (int hh = 0; hh < nc; hh++) {
+                const int h = c0 + hh;
+                const int col = half ? (post ? ncolour - 1 - hh : h) : (post ? ncolour - 1 - h : h);
                 if ((rc = mg_halo(c, V))) return rc;
                 if (P == 16)
                     hipLaunchKernelGGL(k_mg_zline_pcr<16>, dim3(gp), dim3(256), 0, s, V, col);
