@@ -141,7 +141,9 @@ def bench_coupled(args):
     cm = CoupledModel(oc, atm, sp)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     xo = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
-    with np.load(os.path.join(ROOT, "tests", "golden", "coupled4.npz"), allow_pickle=False) as d:
+    # the atmosphere state of the coupled fixture (idealized profile + seeded noise,
+    # tests/golden/make_golden_coupled.py atmos_state)
+    with np.load(os.path.join(ROOT, "bench_data", "coupled4_atmos.npz"), allow_pickle=False) as d:
         xa = d["xa"].astype(np.float64)
 
     def step():
@@ -164,7 +166,7 @@ def bench_coupled(args):
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": False,
            "scaling": "none", "vs_baseline": None, "dtype": "f64",
            "data": (f"synthetic ocean state (splitmix64, T,S ~ U(+-{args.amp_ts:g})), atmosphere "
-                    "state of tests/golden/coupled4.npz (idealized profile + seeded noise); "
+                    "state bench_data/coupled4_atmos.npz (idealized profile + seeded noise); "
                     "Combined Forcing 0.5; states reset from host each step"),
            "config": {"workload": "coupled4: ocean 96x38x12 (coupled T, Mixing 1) + atmosphere "
                                   "96x38 (T, q, A, P), one Newton step", "rows": cm.N,
