@@ -78,6 +78,7 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic);
 int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij);
 int cr_check(iemic_ctx* c, SchurCR& cr);
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s);
+int cr_inverse_dev(hipStream_t s, int m, const double* src, double* dst, int* info);
 
 /* Preconditioner state (prec.hip: block Jacobi, prec_gs.hip: block Gauss-Seidel). */
 struct BlockGS {
@@ -127,6 +128,8 @@ struct BlockGS {
     int mg_glob = 0, mg_gN = 0, mg_g0 = 0;
     DevBuf<double> mg_gX, mg_gband, mg_gvec, mg_gtmp, mg_glpan;
     DevBuf<int> mg_gpiv, mg_ginfo, mg_gcols;
+    DevBuf<double> mg_cdense;        /* coarsest dense operator (device assembly)        */
+    DevBuf<int> mg_cinfo;            /* its Gauss-Jordan pivot flag                      */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */
 };

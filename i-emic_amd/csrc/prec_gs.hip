@@ -2055,6 +2055,47 @@ __global__ void k_mg_gget(const double* __restrict__ y, int64_t ncl, int nc, int
     z[ncl + t] = y[q + 1];
 }
 
+/* the coarsest level's dense operator, row-major A[row * N + col] (one thread per row; the
+ * same entries as the host assembly below), inactive rows -> identity rows */
+__global__ void k_mg_coarse_dense(const double* __restrict__ off, const double* __restrict__ dg, int64_t ncl,
+                                  int cn, int cm, int l, int periodic, double* __restrict__ A)
+{
+    const int64_t rowq = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rowq >= 2 * ncl) return;
+    const int R = (int)(rowq / ncl);
+    const int64_t t = rowq % ncl;
+    const int64_t N = 2 * ncl;
+    double* Ar = A + rowq * N;
+    const int i = (int)(t % cn), k = (int)((t / cn) % l), jl = (int)(t / ((int64_t)cn * l));
+    Ar[R * ncl + t] += dg[(3 * R) * ncl + t];
+    Ar[(1 - R) * ncl + t] += dg[(1 + R) * ncl + t];
+    for (int qq = 0; qq < 8; qq++) {
+        const double v = off[(8 * R + qq) * ncl + t];
+        if (v == 0.0) continue;
+        int ii = i, jj = jl, kk = k;
+        const int dir = qq < 6 ? qq : qq - 2;
+        switch (dir) {
+        case 0: ii--; break;
+        case 1: ii++; break;
+        case 2: jj--; break;
+        case 3: jj++; break;
+        case 4: kk--; break;
+        default: kk++; break;
+        }
+        if (jj < 0 || jj >= cm || kk < 0 || kk >= l) continue;
+        if (ii < 0 || ii >= cn) {
+            if (!periodic) continue;
+            ii = (ii + cn) % cn;
+        }
+        const int64_t nb = ((int64_t)jj * l + kk) * cn + ii;
+        const int var = qq < 6 ? R : 1 - R;
+        Ar[var * ncl + nb] += v;
+    }
+    bool any = false;
+    for (int64_t c = 0; c < N; c++) any |= Ar[c] != 0.0;
+    if (!any) Ar[rowq] = 1.0;
+}
+
 /* coarse levels, Galerkin operators and the coarsest inverse (once per Jacobian) */
 static int mg_setup(iemic_ctx* c)
 {
@@ -2099,12 +2140,34 @@ static int mg_setup(iemic_ctx* c)
                            gs.mg_off[q].p, gs.mg_diag[q].p, gs.mg_dinv[q].p);
     }
     HIP_OK(hipGetLastError());
-    /* coarsest level: dense operator on the host, inverted, back to the device */
+    /* coarsest level: its dense operator assembled and inverted on the device (Gauss-Jordan
+     * with pivoting in one workgroup, schur_cr.hip, up to 192 unknowns); larger coarsest
+     * levels and the bands' global coarsest problem go through the host */
     const int qc = gs.mg_nlev - 1;
     const int64_t ncl = (int64_t)gs.mg_n[qc] * gs.mg_m[qc] * l;
     const int N = (int)(2 * ncl);
-    std::vector<double> off(16 * ncl), dg(4 * ncl);
     int rc;
+    if (N <= 192 && c->nranks <= 1) {
+        DevBuf<double>& A = gs.mg_cdense;
+        if (A.n < (size_t)N * N && A.alloc((size_t)N * N)) return IEMIC_ENOMEM;
+        if (!gs.mg_cinfo.p && gs.mg_cinfo.alloc(1)) return IEMIC_ENOMEM;
+        HIP_OK(hipMemsetAsync(A.p, 0, sizeof(double) * N * N, s));
+        HIP_OK(hipMemsetAsync(gs.mg_cinfo.p, 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_mg_coarse_dense, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s,
+                           (const double*)gs.mg_off[qc].p, (const double*)gs.mg_diag[qc].p, ncl,
+                           gs.mg_n[qc], gs.mg_m[qc], l, c->cfg.periodic, A.p);
+        /* k_cr_inv reads column-major: it inverts A^T and writes the result column-major,
+         * which is A^-1 row-major -- the layout k_gemv applies */
+        if ((rc = cr_inverse_dev(s, N, A.p, gs.mg_cinv.p, gs.mg_cinfo.p))) return rc;
+        int info = 0;
+        if ((rc = d2h(c, &info, gs.mg_cinfo.p, sizeof(int)))) return rc;
+        if (info) {
+            set_error("block GS: singular coarsest T/S operator");
+            return IEMIC_EINVAL;
+        }
+        return 0;
+    }
+    std::vector<double> off(16 * ncl), dg(4 * ncl);
     if ((rc = d2h(c, off.data(), gs.mg_off[qc].p, sizeof(double) * off.size()))) return rc;
     if ((rc = d2h(c, dg.data(), gs.mg_diag[qc].p, sizeof(double) * dg.size()))) return rc;
     std::vector<double> A((size_t)N * N, 0.0), X;

@@ -596,6 +596,13 @@ static int cr_inverse(hipStream_t s, int m, int count, const double* src, int s0
     return 0;
 }
 
+/* the inverse of one m x m column-major block (m <= 192) on the device; *info set on a
+ * zero pivot */
+int cr_inverse_dev(hipStream_t s, int m, const double* src, double* dst, int* info)
+{
+    return cr_inverse(s, m, 1, src, 0, 1, dst, info);
+}
+
 /* set-up from the 9-point rows (stream-ordered, no host synchronisation) */
 int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
 {
