@@ -753,7 +753,8 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
                                                     const double* __restrict__ pbar,
                                                     const double* __restrict__ crhs,
                                                     double* __restrict__ z, Lay L,
-                                                    const double* __restrict__ rr)
+                                                    const double* __restrict__ rr,
+                                                    double* __restrict__ zo, double omega)
 {
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
@@ -794,6 +795,11 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
     if (k < L.l) {
         if (pa) z[NUN * cell + PP] += pbar[c];
         if (wa) z[NUN * cell + WW] = pa ? A : 0.0;
+        /* defect-correction passes: z_out += omega z on the final W/P rows (k_dyn_add fused) */
+        if (zo) {
+            if (pa) zo[NUN * cell + PP] += omega * z[NUN * cell + PP];
+            if (wa) zo[NUN * cell + WW] += omega * z[NUN * cell + WW];
+        }
     }
 }
 
@@ -1054,7 +1060,8 @@ __global__ void k_mr_update(const uint8_t* __restrict__ known, const double* __r
 /* 4. uv = uv* - D^-1 Guv Mz1^T pbar */
 __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __restrict__ known,
                            const double* __restrict__ uvinv, const int* __restrict__ col_of_ij,
-                           const double* __restrict__ pbar, double* __restrict__ z, Lay L)
+                           const double* __restrict__ pbar, double* __restrict__ z, Lay L,
+                           double* __restrict__ zo, double omega)
 {
     OWNED_CELL;
     const bool ua = !known[NUN * cell + UU], va = !known[NUN * cell + VV];
@@ -1066,6 +1073,11 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
     const double* D = uvinv + 4 * cell;
     if (ua) z[NUN * cell + UU] -= D[0] * gu + D[1] * gv;
     if (va) z[NUN * cell + VV] -= D[2] * gu + D[3] * gv;
+    /* defect-correction passes: z_out += omega z on the final U/V rows (k_dyn_add fused) */
+    if (zo) {
+        if (ua) zo[NUN * cell + UU] += omega * z[NUN * cell + UU];
+        if (va) zo[NUN * cell + VV] += omega * z[NUN * cell + VV];
+    }
 }
 
 /* 4b/5. p = ptil + pbar; continuity rows bottom-up for w (top P row excluded) */
@@ -2466,7 +2478,9 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
 }
 
 /* dynamics block: z(U/V/W/P) from the right-hand side rr (steps 1-5 of the header) */
-static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
+/* zo: when given, zo += omega z on the active U/V/W/P rows once z is final (the defect
+ * correction's update, fused into the pass's last kernels where the column scans run) */
+static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -2520,8 +2534,9 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
         sb = gs.colv.p;
     }
     if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
+    double* zf = Pl == 0 ? nullptr : zo;      /* fused only with the column-scan kernels */
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.col_of_ij.p, gs.colv2.p, z, L);
+                       gs.col_of_ij.p, gs.colv2.p, z, L, zf, omega);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
     if (Pl == 0) {
         hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
@@ -2532,13 +2547,15 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z)
                            gs.colv2.p, gs.tcell.p, z, L);
     else if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
     else if (Pl == 32)
         hipLaunchKernelGGL(k_gs_pw_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
     else
         hipLaunchKernelGGL(k_gs_pw_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr);
+                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
+    if (zo && !zf)
+        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, z, zo, L, omega);
     return 0;
 }
 
@@ -2624,8 +2641,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     for (int it = 1; !gs.dyn_mr && it < gs.dyn_iters; it++) {
         if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* w, p of the neighbours */
         if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
-        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
-        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zc.p, z, L, gs.dyn_omega);
+        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, z, gs.dyn_omega))) return rc;     /* z += w zc */
         if (early && it + 1 == ts_at && (rc = ts_rhs())) return rc;
     }
     if (!early && (rc = ts_rhs())) return rc;
