@@ -62,7 +62,7 @@ def parse():
                    help="untimed Newton iterations from the benchmark state, reported as the "
                         "residual sequence")
     p.add_argument("--tol", type=float, default=1e-8)
-    p.add_argument("--krylov", type=int, default=100)
+    p.add_argument("--krylov", type=int, default=90)
     p.add_argument("--restarts", type=int, default=20)
     p.add_argument("--ts-sweeps", type=int, default=12)
     p.add_argument("--orth", default="DCGS2", choices=["DCGS2", "DGKS"])
