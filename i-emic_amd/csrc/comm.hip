@@ -222,12 +222,22 @@ int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
     return run_ops(c, ops);
 }
 
-int halo_exchange_pair(iemic_ctx* c, double* a, double* b)
+/* one row of two arrays of whole rows (slab doubles each; owned rows [first, first + count)),
+ * e.g. the level-0 T/S multigrid iterate, in one communication group */
+int halo_exchange_slab2(iemic_ctx* c, double* a, double* b, int64_t first, int64_t count, int64_t slab)
 {
     if (c->nranks <= 1) return 0;
     std::vector<P2P> ops;
-    halo_ops(c, a, 1, 1, ops);
-    halo_ops(c, b, 1, 1, ops);
+    for (double* v : {a, b}) {
+        if (c->rank > 0) {
+            ops.push_back({true, v + first, slab, c->rank - 1});
+            ops.push_back({false, v + first - slab, slab, c->rank - 1});
+        }
+        if (c->rank < c->nranks - 1) {
+            ops.push_back({true, v + first + count - slab, slab, c->rank + 1});
+            ops.push_back({false, v + first + count, slab, c->rank + 1});
+        }
+    }
     return run_ops(c, ops);
 }
 

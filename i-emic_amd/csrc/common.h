@@ -112,16 +112,15 @@ struct BlockGS {
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
     int ts_at = 0;                   /* T/S rhs after this many passes (0: after all)     */
-    hipGraphExec_t mg_exec = nullptr; /* the ts_mg V-cycles captured once (fixed buffers)  */
-    /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local):
-     * level 0 is the fine T/S block (tsoff/tsdiag/tsinv, ext cells); coarse level q has
-     * mg_n[q] x mg_m[q] x l cells with 16 couplings, 2x2 block and inverse, rhs, iterate */
+    /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local): level q
+     * has mg_n[q] x mg_m[q] x l cells in the k-contiguous level layout (prec_gs.hip TsLev;
+     * level 0 packed from tsoff/tsdiag) with 16 couplings, the 2x2 block, the z-line
+     * factors (12), rhs and iterate */
     static constexpr int MG_MAX = 12;
     int ts_mg = 1, mg_sweeps = 1, mg_nlev = 0;
-    int ts_halo = 1;                 /* bands: level-0 T/S smoothing across band edges  */
     int mg_n[MG_MAX] = {}, mg_m[MG_MAX] = {};
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
-    DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_dinv[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
+    DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_fac[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
     DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
     /* bands: the coarsest T/S level solved globally (all bands' coarsest cells plus the
      * cross-band couplings; band LU + inverse on the device, redundant on every rank) */
@@ -150,8 +149,6 @@ struct iemic_ctx {
     iemic_grid cfg;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;      /* second stream: block GS T/S solve (one rank)      */
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n = 0, m = 0, l = 0;
     int64_t ncell = 0, nrows = 0;    /* global cells / rows                               */
     /* latitude-band decomposition (stencil.h ext layout): owned band [jb0, jb1) */
@@ -218,8 +215,8 @@ struct StreamGuard {
 int allreduce_sum(iemic_ctx* c, double* dev, int count);
 int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
 int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int rows_j);
-/* one row of two per-cell arrays (width 1) in one communication group */
-int halo_exchange_pair(iemic_ctx* c, double* a, double* b);
+/* one halo row of two arrays laid out in whole rows of slab doubles, owned [first, first+count) */
+int halo_exchange_slab2(iemic_ctx* c, double* a, double* b, int64_t first, int64_t count, int64_t slab);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
 int comm_unique_id(unsigned char* id128);
 void* local_group_new(int nranks);

@@ -1346,26 +1346,46 @@ __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __
  * sweeps barely touch.  Its coarse spaces aggregate 2x2 horizontal neighbours over the
  * full depth (each level is again an n x m x l grid with the fine coupling pattern:
  * 6 same-variable face couplings, T<->S at k-1/k+1, a 2x2 cell block), built by Galerkin
- * summation with piecewise-constant transfers.  Aggregates stay inside a latitude band
- * (block-Jacobi across GPUs, like the fine T/S sweeps).  One V-cycle: symmetric red-black
- * smoothing on every level, a one-workgroup solve on the coarsest. */
+ * summation with piecewise-constant transfers.  Aggregates stay inside a latitude band.
+ * One V-cycle: z-line relaxation by horizontal colour on every level (colours forward
+ * before the coarse correction, backward after it), a dense inverse on the coarsest.
+ *
+ * Level layout (level 0 included, packed once per Jacobian): columns k-contiguous,
+ *     cell = ((jl + hj) * n + i) * l + k,
+ * so the P lanes of a column (lane = level k) read one contiguous run of every array and
+ * a horizontal neighbour is again one whole run (one 128-B line per array at l = 16);
+ * hj = 1 halo row on each side on level 0 of a band group (refreshed by exchanges).
+ * The z-lines are factorised at set-up (block Thomas, k_mg_fac: F = -A'^-1 B, A'^-1,
+ * Cp = A'^-1 C per cell), so a relaxation is two affine parallel scans over the lanes
+ * without a division.  Launch fusion (the apply is latency-bound):
+ *   - the T/S right-hand side and the first colour of level 0 (k_mg_entry),
+ *   - each restriction and the first colour of the coarse level (k_mg_rc): from a zero
+ *     iterate that colour's lines see zero neighbours,
+ *   - the prolongation into the first post-smoothing colour (k_mg_zl, corr): a line solve
+ *     never reads its own old value, so the coarse correction is only needed on the
+ *     neighbours not yet relaxed, and it is added where they are read,
+ *   - after one forward sweep from zero with two colours, the residual of the last colour
+ *     is zero and that of the first is -H z(last colour) (restriction shortcut: 16 instead
+ *     of 72 doubles per fine-cell pair),
+ *   - the last colour launches of the final level-0 sweep write z(T, S) straight into the
+ *     preconditioner output. */
 struct TsLev {
     int n, mb, l, periodic;
-    int64_t base, cstr;              /* cell index = base + (jl*l + k)*n + i; array stride */
-    const double* off;               /* 16 x cstr: T row q 0..7, S row q 8..15          */
-    const double* diag;              /* 4 x cstr: 2x2 block (TT, TS, ST, SS)           */
-    const double* dinv;              /* 4 x cstr (level 0: packed per cell, 4*cell)     */
-    int dinv_aos;                    /* 1: dinv[4*cell + e] (level 0: tsinv)            */
-    const double* bt; const double* bs; int bstr;
-    double* zt; double* zs;
-    int halo_j;                      /* 1: the latitude rows jl = -1 and mb (level 0 of a   */
-                                     /* band, refreshed by halo exchanges) are neighbours  */
+    int hj;                          /* halo rows of the layout (level 0 of a band group)  */
+    int vis;                         /* halo rows the smoother / residual read (0 or hj)   */
+    int jpar;                        /* colour parity of jl = 0 (global j parity, level 0) */
+    int64_t cstr;                    /* array stride (mb + 2 hj) n l                       */
+    const double* off;               /* 16 x cstr: T row q 0..7, S row q 8..15            */
+    const double* diag;              /* 4 x cstr: 2x2 block (TT, TS, ST, SS)              */
+    const double* fac;               /* 12 x cstr: line factors F | A'^-1 | Cp            */
+    double* b;                       /* 2 x cstr: right-hand side (T, S)                  */
+    double* z;                       /* 2 x cstr: iterate (T, S)                          */
 };
-__device__ __forceinline__ int64_t mg_cell(const TsLev& V, int i, int jl, int k)
+__host__ __device__ __forceinline__ int64_t mg_cell(const TsLev& V, int i, int jl, int k)
 {
-    return V.base + ((int64_t)jl * V.l + k) * V.n + i;
+    return (((int64_t)jl + V.hj) * V.n + i) * V.l + k;
 }
-/* neighbour q (-i,+i,-j,+j,-k,+k) of (i,jl,k): false outside the level's band */
+/* neighbour q (-i,+i,-j,+j,-k,+k) of (i,jl,k): false outside the level's (visible) band */
 __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, int& k)
 {
     switch (q) {
@@ -1376,7 +1396,7 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
     case 4: k--; break;
     default: k++; break;
     }
-    if (jl < -V.halo_j || jl >= V.mb + V.halo_j || k < 0 || k >= V.l) return false;
+    if (jl < -V.vis || jl >= V.mb + V.vis || k < 0 || k >= V.l) return false;
     if (i < 0 || i >= V.n) {
         if (!V.periodic) return false;
         i = (i + V.n) % V.n;
@@ -1387,217 +1407,329 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
 __device__ __forceinline__ void mg_offmul(const TsLev& V, int i, int jl, int k, int64_t c,
                                           double& at, double& as)
 {
+    const int64_t cs = V.cstr;
     at = as = 0.0;
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         int ii = i, jj = jl, kk = k;
         if (!mg_nb(V, q, ii, jj, kk)) continue;
         const int64_t nc = mg_cell(V, ii, jj, kk);
-        at += V.off[(int64_t)q * V.cstr + c] * V.zt[nc];
-        as += V.off[(int64_t)(8 + q) * V.cstr + c] * V.zs[nc];
+        at += V.off[(int64_t)q * cs + c] * V.z[nc];
+        as += V.off[(int64_t)(8 + q) * cs + c] * V.z[cs + nc];
         if (q == 4) {
-            at += V.off[(int64_t)6 * V.cstr + c] * V.zs[nc];
-            as += V.off[(int64_t)14 * V.cstr + c] * V.zt[nc];
+            at += V.off[6 * cs + c] * V.z[cs + nc];
+            as += V.off[14 * cs + c] * V.z[nc];
         } else if (q == 5) {
-            at += V.off[(int64_t)7 * V.cstr + c] * V.zs[nc];
-            as += V.off[(int64_t)15 * V.cstr + c] * V.zt[nc];
+            at += V.off[7 * cs + c] * V.z[cs + nc];
+            as += V.off[15 * cs + c] * V.z[nc];
         }
     }
 }
-__device__ __forceinline__ int mg_colour(const TsLev& V, int i, int jl, int k)
-{
-    if (V.periodic && (V.n & 1) && i == V.n - 1) return 2 + ((jl + k) & 1);
-    return (i + jl + k) & 1;
-}
-__device__ __forceinline__ void mg_relax(const TsLev& V, int i, int jl, int k)
-{
-    const int64_t c = mg_cell(V, i, jl, k);
-    double at, as;
-    mg_offmul(V, i, jl, k, c, at, as);
-    const double rt = V.bt[c * V.bstr] - at, rs = V.bs[c * V.bstr] - as;
-    double d0, d1, d2, d3;
-    if (V.dinv_aos) {
-        d0 = V.dinv[4 * c]; d1 = V.dinv[4 * c + 1]; d2 = V.dinv[4 * c + 2]; d3 = V.dinv[4 * c + 3];
-    } else {
-        d0 = V.dinv[c]; d1 = V.dinv[V.cstr + c]; d2 = V.dinv[2 * V.cstr + c]; d3 = V.dinv[3 * V.cstr + c];
-    }
-    V.zt[c] = d0 * rt + d1 * rs;
-    V.zs[c] = d2 * rt + d3 * rs;
-}
-/* one colour of a red-black sweep on a coarse level (all cells launched, one colour acts) */
-__global__ void k_mg_half(TsLev V, int colour)
-{
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t ncl = (int64_t)V.n * V.mb * V.l;
-    if (t >= ncl) return;
-    const int i = (int)(t % V.n), k = (int)((t / V.n) % V.l), jl = (int)(t / ((int64_t)V.n * V.l));
-    if (mg_colour(V, i, jl, k) != colour) return;
-    mg_relax(V, i, jl, k);
-}
-/* z-line relaxation: every water column (i, jl) of one horizontal colour solves its
- * 2x2-block tridiagonal T/S system along k exactly (block Thomas), with the horizontal
- * couplings to the neighbouring columns taken from the current iterate.  Strong vertical
- * coupling (the convective mixing of Mixing = 1/2, vertical diffusion on stretched
- * layers) is then handled by the smoother, the horizontal smooth modes by the coarse
- * levels.  Inactive unknowns (zero diagonal) are identity rows with zero right-hand side.
- * Colour of a column: (i + jl) & 1, with 2/3 for i = n-1 on an odd periodic level. */
+/* colour of water column (i, jl): parity of i + j (global j on level 0); on a periodic
+ * level with odd n the wrap pair (n-1, 0) would share a colour, so column n-1 gets 2 / 3 */
+__host__ __device__ __forceinline__ int mg_ncolour(const TsLev& V) { return (V.periodic && (V.n & 1)) ? 4 : 2; }
 __device__ __forceinline__ int mg_lcolour(const TsLev& V, int i, int jl)
 {
-    if (V.periodic && (V.n & 1) && i == V.n - 1) return 2 + (jl & 1);
-    return (i + jl) & 1;
+    if (V.periodic && (V.n & 1) && i == V.n - 1) return 2 + ((jl + V.jpar) & 1);
+    return (i + jl + V.jpar) & 1;
 }
-/* One column per P lanes (lane = level k, P >= l): every lane loads its level (right-hand side minus horizontal couplings, 2x2 diagonal block,
- * couplings to k-1 and k+1) at once, and the block-tridiagonal system is solved by
- * parallel cyclic reduction over the lanes (log2 P shuffle steps of 2x2 block algebra)
- * instead of a serial block Thomas sweep. */
-struct B2 { double a, b, c, d; };            /* [[a b] [c d]] */
-__device__ __forceinline__ B2 b2mul(const B2& x, const B2& y)
+/* g-th owned column of a colour: row jl holds i = 2h + ((colour + jl + jpar) & 1), h <
+ * ceil(n'/2), n' = n - 1 on an odd periodic level (whose last column has colour 2 or 3) */
+__device__ __forceinline__ bool mg_column(const TsLev& V, int colour, int g, int& i, int& jl)
 {
-    return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+    const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
+    if (colour < 2) {
+        const int per_row = (np + 1) / 2;
+        if (g >= per_row * V.mb) return false;
+        jl = g / per_row;
+        i = 2 * (g % per_row) + ((colour + jl + V.jpar) & 1);
+        return i < np;
+    }
+    if (g >= V.mb) return false;
+    jl = g;
+    i = V.n - 1;
+    return ((jl + V.jpar) & 1) == colour - 2;
 }
-__device__ __forceinline__ B2 b2inv(const B2& x)
+__host__ __device__ __forceinline__ int64_t mg_columns_of(const TsLev& V, int colour)
 {
-    const double det = x.a * x.d - x.b * x.c;
-    const double q = det != 0.0 ? 1.0 / det : 0.0;
-    return {x.d * q, -x.b * q, -x.c * q, x.a * q};
+    const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
+    return colour < 2 ? (int64_t)((np + 1) / 2) * V.mb : V.mb;
 }
+
+/* Line solve of one column, lane = level k (< l when on): g = A'^-1 r, then the forward
+ * recurrence dp_k = F_k dp_{k-1} + g_k and the backward x_k = dp_k - Cp_k x_{k+1} as affine
+ * Hillis-Steele scans over the P lanes (log2 P shuffle steps of 2x2 algebra each, no
+ * division: the pivots were inverted at set-up).  The factor loads are issued first. */
 template <int P>
-__device__ __forceinline__ B2 shfl_b2(const B2& x, int src)
+__device__ __forceinline__ void line_solve(const double* __restrict__ f, int64_t cs, bool on, int k,
+                                           double rt, double rs, double& xt, double& xs)
 {
-    return {__shfl(x.a, src, P), __shfl(x.b, src, P), __shfl(x.c, src, P), __shfl(x.d, src, P)};
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, i0 = 0.0, i1 = 0.0, i2 = 0.0, i3 = 0.0;
+    double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+    if (on) {
+        a0 = f[0]; a1 = f[cs]; a2 = f[2 * cs]; a3 = f[3 * cs];
+        i0 = f[4 * cs]; i1 = f[5 * cs]; i2 = f[6 * cs]; i3 = f[7 * cs];
+        q0 = -f[8 * cs]; q1 = -f[9 * cs]; q2 = -f[10 * cs]; q3 = -f[11 * cs];
+    }
+    double ct = i0 * rt + i1 * rs, cv = i2 * rt + i3 * rs;
+#pragma unroll
+    for (int d = 1; d < P; d <<= 1) {
+        const double b0 = __shfl_up(a0, d, P), b1 = __shfl_up(a1, d, P);
+        const double b2 = __shfl_up(a2, d, P), b3 = __shfl_up(a3, d, P);
+        const double dt = __shfl_up(ct, d, P), dv = __shfl_up(cv, d, P);
+        if (k >= d) {
+            const double nt = ct + (a0 * dt + a1 * dv), nv = cv + (a2 * dt + a3 * dv);
+            const double n0 = a0 * b0 + a1 * b2, n1 = a0 * b1 + a1 * b3;
+            const double n2 = a2 * b0 + a3 * b2, n3 = a2 * b1 + a3 * b3;
+            ct = nt; cv = nv; a0 = n0; a1 = n1; a2 = n2; a3 = n3;
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < P; d <<= 1) {
+        const double b0 = __shfl_down(q0, d, P), b1 = __shfl_down(q1, d, P);
+        const double b2 = __shfl_down(q2, d, P), b3 = __shfl_down(q3, d, P);
+        const double dt = __shfl_down(ct, d, P), dv = __shfl_down(cv, d, P);
+        if (k + d < P) {
+            const double nt = ct + (q0 * dt + q1 * dv), nv = cv + (q2 * dt + q3 * dv);
+            const double n0 = q0 * b0 + q1 * b2, n1 = q0 * b1 + q1 * b3;
+            const double n2 = q2 * b0 + q3 * b2, n3 = q2 * b1 + q3 * b3;
+            ct = nt; cv = nv; q0 = n0; q1 = n1; q2 = n2; q3 = n3;
+        }
+    }
+    xt = ct;
+    xs = cv;
 }
-/* launched over the columns of one colour only: row jl holds the columns
- * i = 2h + ((colour + jl) & 1), h < ceil(n'/2) (n' = n - 1 on an odd periodic level, whose
- * last column has colour 2 or 3 by row parity, see mg_lcolour) */
+
+/* z-line relaxation of one colour: every column of it solves its 2x2-block tridiagonal T/S
+ * system along k with the horizontal couplings taken from the current iterate.  corr: the
+ * first post-smoothing colour launch, neighbours not yet relaxed in this sweep (smaller
+ * colour) read with their aggregate's coarse correction C.z added.  zout (level 0, final
+ * sweep): the active T/S rows of the preconditioner output (ext layout) get the result. */
 template <int P>
-__global__ void __launch_bounds__(256) k_mg_zline_pcr(TsLev V, int colour)
+__global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int corr,
+                                              double* __restrict__ zout)
 {
     const int g = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
-    const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
-    const int per_row = colour < 2 ? (np + 1) / 2 : 1;
-    if (g >= per_row * V.mb) return;                   /* whole column groups exit */
-    const int jl = g / per_row;
-    int i;
-    if (colour < 2) {
-        i = 2 * (g % per_row) + ((colour + jl) & 1);
-        if (i >= np) return;
-    } else {
-        i = V.n - 1;
-        if ((jl & 1) != colour - 2) return;
-    }
+    int i, jl;
+    if (!mg_column(V, colour, g, i, jl)) return;           /* whole column groups exit */
     const int64_t cs = V.cstr;
-    B2 A{1.0, 0.0, 0.0, 1.0}, Bm{0.0, 0.0, 0.0, 0.0}, Cm{0.0, 0.0, 0.0, 0.0};
-    double d0 = 0.0, d1 = 0.0;
+    const bool on = k < V.l;
     int64_t c = 0;
-    if (k < V.l) {
+    double rt = 0.0, rs = 0.0;
+    if (on) {
         c = mg_cell(V, i, jl, k);
-        double rt = V.bt[c * V.bstr], rs = V.bs[c * V.bstr];
+        rt = V.b[c];
+        rs = V.b[cs + c];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int ii = i, jj = jl, kk = k;
             if (!mg_nb(V, q, ii, jj, kk)) continue;
             const int64_t nc = mg_cell(V, ii, jj, kk);
-            rt -= V.off[(int64_t)q * cs + c] * V.zt[nc];
-            rs -= V.off[(int64_t)(8 + q) * cs + c] * V.zs[nc];
+            double zt = V.z[nc], zs = V.z[cs + nc];
+            if (corr && mg_lcolour(V, ii, jj) < colour) {
+                const int64_t p = mg_cell(C, ii >> 1, jj >> 1, k);
+                zt += C.z[p];
+                zs += C.z[C.cstr + p];
+            }
+            rt -= V.off[(int64_t)q * cs + c] * zt;
+            rs -= V.off[(int64_t)(8 + q) * cs + c] * zs;
         }
-        const bool at = V.diag[c] != 0.0, as = V.diag[3 * cs + c] != 0.0;
-        A = {V.diag[c], V.diag[cs + c], V.diag[2 * cs + c], V.diag[3 * cs + c]};
-        Bm = {V.off[4 * cs + c], V.off[6 * cs + c], V.off[14 * cs + c], V.off[12 * cs + c]};
-        Cm = {V.off[5 * cs + c], V.off[7 * cs + c], V.off[15 * cs + c], V.off[13 * cs + c]};
-        d0 = rt;
-        d1 = rs;
-        if (!at) { A.a = 1.0; A.b = A.c = 0.0; Bm.a = Bm.b = 0.0; Cm.a = Cm.b = 0.0; d0 = 0.0; }
-        if (!as) { A.d = 1.0; A.b = A.c = 0.0; Bm.c = Bm.d = 0.0; Cm.c = Cm.d = 0.0; d1 = 0.0; }
     }
-#pragma unroll
-    for (int s = 1; s < P; s <<= 1) {
-        const int lo = k - s, hi = k + s;
-        const B2 Alo = shfl_b2<P>(A, lo < 0 ? k : lo), Ahi = shfl_b2<P>(A, hi >= P ? k : hi);
-        const B2 Blo = shfl_b2<P>(Bm, lo < 0 ? k : lo), Bhi = shfl_b2<P>(Bm, hi >= P ? k : hi);
-        const B2 Clo = shfl_b2<P>(Cm, lo < 0 ? k : lo), Chi = shfl_b2<P>(Cm, hi >= P ? k : hi);
-        const double dlo0 = __shfl(d0, lo < 0 ? k : lo, P), dlo1 = __shfl(d1, lo < 0 ? k : lo, P);
-        const double dhi0 = __shfl(d0, hi >= P ? k : hi, P), dhi1 = __shfl(d1, hi >= P ? k : hi, P);
-        B2 al{0.0, 0.0, 0.0, 0.0}, ga{0.0, 0.0, 0.0, 0.0};
-        if (lo >= 0) {
-            al = b2mul(Bm, b2inv(Alo));
-            al = {-al.a, -al.b, -al.c, -al.d};
-        }
-        if (hi < P) {
-            ga = b2mul(Cm, b2inv(Ahi));
-            ga = {-ga.a, -ga.b, -ga.c, -ga.d};
-        }
-        const B2 t1 = b2mul(al, Clo), t2 = b2mul(ga, Bhi);
-        A = {A.a + t1.a + t2.a, A.b + t1.b + t2.b, A.c + t1.c + t2.c, A.d + t1.d + t2.d};
-        const double nd0 = d0 + (al.a * dlo0 + al.b * dlo1) + (ga.a * dhi0 + ga.b * dhi1);
-        const double nd1 = d1 + (al.c * dlo0 + al.d * dlo1) + (ga.c * dhi0 + ga.d * dhi1);
-        Bm = lo >= 0 ? b2mul(al, Blo) : B2{0.0, 0.0, 0.0, 0.0};
-        Cm = hi < P ? b2mul(ga, Chi) : B2{0.0, 0.0, 0.0, 0.0};
-        d0 = nd0;
-        d1 = nd1;
-    }
-    if (k < V.l) {
-        const B2 Ai = b2inv(A);
-        V.zt[c] = Ai.a * d0 + Ai.b * d1;
-        V.zs[c] = Ai.c * d0 + Ai.d * d1;
+    double xt, xs;
+    line_solve<P>(V.fac + c, cs, on, k, rt, rs, xt, xs);
+    if (!on) return;
+    V.z[c] = xt;
+    V.z[cs + c] = xs;
+    if (zout) {
+        const int64_t e = NUN * ((((int64_t)jl + HALO) * V.l + k) * V.n + i);
+        if (V.diag[c] != 0.0) zout[e + TT] = xt;
+        if (V.diag[3 * cs + c] != 0.0) zout[e + SS] = xs;
     }
 }
 
-/* coarse rhs = sum of the children's residuals b - A z; coarse iterate = 0.  Four lanes
- * per coarse cell, one child each (the residual loads of the children run in parallel),
- * summed by two shuffle steps ((c00 + c10) + (c01 + c11), a fixed order). */
-__global__ void k_mg_restrict(TsLev F, TsLev C, double* __restrict__ bc, double* __restrict__ zc)
+/* Restriction F -> C (coarse rhs = sum of the children's residuals, fixed order
+ * (c00 + c10) + (c01 + c11)) and, when relax, the coarse level's colour-0 lines from the
+ * zero iterate (zero neighbours), the other coarse cells' iterate set to 0.  P lanes per
+ * coarse column (lane = level k), every lane reads its four children's level k.
+ * shortcut: F was relaxed once, colour 0 then 1, from a zero iterate, so the residual of
+ * colour 1 is 0 and that of colour 0 is -H z (its horizontal neighbours). */
+template <int P>
+__global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, int relax)
 {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t ncl = (int64_t)C.n * C.mb * C.l;
-    const int64_t t = g >> 2;
-    const int ch = (int)(g & 3);
-    if (t >= ncl) return;                     /* whole 4-lane groups exit together */
-    const int I = (int)(t % C.n), k = (int)((t / C.n) % C.l), J = (int)(t / ((int64_t)C.n * C.l));
-    const int i = 2 * I + (ch & 1), jl = 2 * J + (ch >> 1);
-    double st = 0.0, ss = 0.0;
-    if (i < F.n && jl < F.mb) {
-        const int64_t c = mg_cell(F, i, jl, k);
-        double at, as;
-        mg_offmul(F, i, jl, k, c, at, as);
-        const double zt = F.zt[c], zs = F.zs[c];
-        at += F.diag[c] * zt + F.diag[F.cstr + c] * zs;
-        as += F.diag[2 * F.cstr + c] * zt + F.diag[3 * F.cstr + c] * zs;
-        st = F.bt[c * F.bstr] - at;
-        ss = F.bs[c * F.bstr] - as;
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+    const int k = threadIdx.x % P;
+    if (g >= C.n * C.mb) return;
+    const int I = g % C.n, J = g / C.n;
+    const bool on = k < C.l;
+    const int64_t fs = F.cstr, cs = C.cstr;
+    double r[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+    int64_t t = 0;
+    if (on) {
+        t = mg_cell(C, I, J, k);
+#pragma unroll
+        for (int ch = 0; ch < 4; ch++) {
+            const int i = 2 * I + (ch & 1), jl = 2 * J + (ch >> 1);
+            if (i >= F.n || jl >= F.mb) continue;
+            const int64_t c = mg_cell(F, i, jl, k);
+            if (shortcut) {
+                if (mg_lcolour(F, i, jl) != 0) continue;
+                double at = 0.0, as = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    int ii = i, jj = jl, kk = k;
+                    if (!mg_nb(F, q, ii, jj, kk)) continue;
+                    const int64_t nc = mg_cell(F, ii, jj, kk);
+                    at += F.off[(int64_t)q * fs + c] * F.z[nc];
+                    as += F.off[(int64_t)(8 + q) * fs + c] * F.z[fs + nc];
+                }
+                r[ch][0] = -at;
+                r[ch][1] = -as;
+            } else {
+                double at, as;
+                mg_offmul(F, i, jl, k, c, at, as);
+                const double zt = F.z[c], zs = F.z[fs + c];
+                at += F.diag[c] * zt + F.diag[fs + c] * zs;
+                as += F.diag[2 * fs + c] * zt + F.diag[3 * fs + c] * zs;
+                r[ch][0] = F.b[c] - at;
+                r[ch][1] = F.b[fs + c] - as;
+            }
+        }
     }
-    st += __shfl_xor(st, 1, 64);
-    ss += __shfl_xor(ss, 1, 64);
-    st += __shfl_xor(st, 2, 64);
-    ss += __shfl_xor(ss, 2, 64);
-    if (ch == 0) {
-        bc[t] = st;
-        bc[ncl + t] = ss;
-        zc[t] = 0.0;
-        zc[ncl + t] = 0.0;
+    const double bt = (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
+    const double bs = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
+    if (on) {
+        C.b[t] = bt;
+        C.b[cs + t] = bs;
+    }
+    if (!relax) return;
+    if (mg_lcolour(C, I, J) == 0) {
+        double xt, xs;
+        line_solve<P>(C.fac + t, cs, on, k, bt, bs, xt, xs);
+        if (on) {
+            C.z[t] = xt;
+            C.z[cs + t] = xs;
+        }
+    } else if (on) {
+        C.z[t] = 0.0;
+        C.z[cs + t] = 0.0;
     }
 }
-/* fine iterate += coarse correction of its aggregate (active unknowns only) */
+
+/* Level-0 entry: the T/S right-hand side rr_TS - A_TS,D z_D of a tile of TI columns of one
+ * latitude row (Jacobian slots read along i, coalesced; identity-row columns skipped by
+ * the slot bitmask), transposed through LDS into the k-contiguous level layout, then the
+ * tile's colour-0 lines relaxed from the zero iterate and the other columns' iterate set
+ * to 0 (one launch instead of rhs + first colour). */
+constexpr int MG_TI = 32;
+template <int P>
+__global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                                                 const uint64_t* __restrict__ kmask,
+                                                 const double* __restrict__ rr, const double* __restrict__ z,
+                                                 Lay L, TsLev V)
+{
+    LAY_ALIASES;
+    __shared__ double sb[2][64][MG_TI + 1];
+    const int tiles = (n + MG_TI - 1) / MG_TI;
+    const int jl = blockIdx.x / tiles, i0 = (blockIdx.x % tiles) * MG_TI;
+    const int j = L.jb0 + jl;
+    for (int e = threadIdx.x; e < 2 * l * MG_TI; e += blockDim.x) {
+        const int R = TT + e / (l * MG_TI);
+        const int k = (e / MG_TI) % l, ii = e % MG_TI, i = i0 + ii;
+        double acc = 0.0;
+        if (i < n) {
+            const int64_t lc = ((int64_t)jl * l + k) * n + i;
+            const int64_t cell = L.own0 + lc;
+            const int64_t row = NUN * cell + R;
+            if (!known[row]) {
+                int ix[3] = {i - 1, i, i + 1};
+                if (ix[0] < 0) ix[0] = periodic ? n - 1 : i;
+                if (ix[2] >= n) ix[2] = periodic ? 0 : i;
+                const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
+                const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
+                int rb[9];
+#pragma unroll
+                for (int a = 0; a < 3; a++)
+#pragma unroll
+                    for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - L.jb0 + HALO) * l + kk[a]) * n;
+                const uint64_t kb = kmask[2 * cell + 1];
+                acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, rb, ix, kb, rr[row])
+                              : bts_row<SS>(val, z, lc, L.nloc, rb, ix, kb, rr[row]);
+            }
+        }
+        sb[R - TT][k][ii] = acc;
+    }
+    __syncthreads();
+    const int grp = threadIdx.x / P, k = threadIdx.x % P, ng = blockDim.x / P;
+    const bool on = k < l;
+    for (int ii = grp; ii < MG_TI; ii += ng) {
+        const int i = i0 + ii;
+        if (i >= n) break;
+        const int64_t c = on ? mg_cell(V, i, jl, k) : 0;
+        const double bt = on ? sb[0][k][ii] : 0.0, bs = on ? sb[1][k][ii] : 0.0;
+        if (on) {
+            V.b[c] = bt;
+            V.b[V.cstr + c] = bs;
+        }
+        if (mg_lcolour(V, i, jl) == 0) {
+            double xt, xs;
+            line_solve<P>(V.fac + c, V.cstr, on, k, bt, bs, xt, xs);
+            if (on) {
+                V.z[c] = xt;
+                V.z[V.cstr + c] = xs;
+            }
+        } else if (on) {
+            V.z[c] = 0.0;
+            V.z[V.cstr + c] = 0.0;
+        }
+    }
+}
+
+/* fine iterate += coarse correction of its aggregate (active unknowns; level 0 of a band
+ * group only, where the first post-smoothing colour reads neighbours across the band edge) */
 __global__ void k_mg_prolong(TsLev F, TsLev C)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nfl = (int64_t)F.n * F.mb * F.l;
-    if (t >= nfl) return;
-    const int i = (int)(t % F.n), k = (int)((t / F.n) % F.l), jl = (int)(t / ((int64_t)F.n * F.l));
-    const int64_t c = mg_cell(F, i, jl, k);
-    const int64_t p = mg_cell(C, i >> 1, jl >> 1, k);
-    if (F.diag[c] != 0.0) F.zt[c] += C.zt[p];
-    if (F.diag[3 * F.cstr + c] != 0.0) F.zs[c] += C.zs[p];
+    if (t >= (int64_t)F.n * F.mb * F.l) return;
+    const int k = (int)(t % F.l), i = (int)((t / F.l) % F.n), jl = (int)(t / ((int64_t)F.l * F.n));
+    const int64_t c = mg_cell(F, i, jl, k), p = mg_cell(C, i >> 1, jl >> 1, k);
+    if (F.diag[c] != 0.0) F.z[c] += C.z[p];
+    if (F.diag[3 * F.cstr + c] != 0.0) F.z[F.cstr + c] += C.z[C.cstr + p];
 }
-/* Galerkin coarse operator: sum of the children's blocks and couplings; couplings inside
- * the aggregate go to the coarse 2x2 block */
-__global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double* __restrict__ diag,
-                              double* __restrict__ dinv)
+
+/* level-0 iterate -> z(T, S) of the preconditioner output on the active rows (when the
+ * T/S block was solved before the last dynamics pass, whose defects see z(T, S) = 0) */
+__global__ void k_mg_out(TsLev V, double* __restrict__ zout)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t ncl = (int64_t)C.n * C.mb * C.l;
-    if (t >= ncl) return;
-    const int I = (int)(t % C.n), k = (int)((t / C.n) % C.l), J = (int)(t / ((int64_t)C.n * C.l));
+    if (t >= (int64_t)V.n * V.mb * V.l) return;
+    const int k = (int)(t % V.l), i = (int)((t / V.l) % V.n), jl = (int)(t / ((int64_t)V.l * V.n));
+    const int64_t c = mg_cell(V, i, jl, k);
+    const int64_t e = NUN * ((((int64_t)jl + HALO) * V.l + k) * V.n + i);
+    if (V.diag[c] != 0.0) zout[e + TT] = V.z[c];
+    if (V.diag[3 * V.cstr + c] != 0.0) zout[e + SS] = V.z[V.cstr + c];
+}
+
+/* level 0: the compact T/S couplings and 2x2 blocks (ext layout) into the level layout */
+__global__ void k_mg_pack0(const double* __restrict__ tsoff, const double* __restrict__ tsdiag, Lay L,
+                           int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag)
+{
+    OWNED_CELL;
+    const int64_t c = mg_cell(V, i, j - L.jb0, k);
+#pragma unroll
+    for (int e = 0; e < 16; e++) off[(int64_t)e * V.cstr + c] = tsoff[(int64_t)e * next + cell];
+#pragma unroll
+    for (int e = 0; e < 4; e++) diag[(int64_t)e * V.cstr + c] = tsdiag[(int64_t)e * next + cell];
+}
+
+/* Galerkin coarse operator: sum of the children's blocks and couplings; couplings inside
+ * the aggregate go to the coarse 2x2 block */
+__global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double* __restrict__ diag)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)C.n * C.mb * C.l) return;
+    const int k = (int)(t % C.l), I = (int)((t / C.l) % C.n), J = (int)(t / ((int64_t)C.l * C.n));
+    const int64_t fs = F.cstr;
     double o[16], d[4] = {0.0, 0.0, 0.0, 0.0};
     for (int e = 0; e < 16; e++) o[e] = 0.0;
     for (int b = 0; b < 2; b++)
@@ -1605,10 +1737,10 @@ __global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double
             const int i = 2 * I + a, jl = 2 * J + b;
             if (i >= F.n || jl >= F.mb) continue;
             const int64_t c = mg_cell(F, i, jl, k);
-            for (int e = 0; e < 4; e++) d[e] += F.diag[(int64_t)e * F.cstr + c];
+            for (int e = 0; e < 4; e++) d[e] += F.diag[(int64_t)e * fs + c];
             for (int R = 0; R < 2; R++)
                 for (int q = 0; q < 8; q++) {
-                    const double v = F.off[(int64_t)(8 * R + q) * F.cstr + c];
+                    const double v = F.off[(int64_t)(8 * R + q) * fs + c];
                     if (v == 0.0) continue;
                     int ii = i, jj = jl, kk = k;
                     if (!mg_nb(F, q < 6 ? q : q - 2, ii, jj, kk)) continue;
@@ -1621,40 +1753,50 @@ __global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double
     const bool at = d[0] != 0.0, as = d[3] != 0.0;
     if (!at) { d[1] = d[2] = 0.0; for (int q = 0; q < 8; q++) o[q] = 0.0; }
     if (!as) { d[1] = d[2] = 0.0; for (int q = 8; q < 16; q++) o[q] = 0.0; }
-    for (int e = 0; e < 16; e++) off[(int64_t)e * ncl + t] = o[e];
-    for (int e = 0; e < 4; e++) diag[(int64_t)e * ncl + t] = d[e];
-    double inv[4];
-    inv2(d[0], d[1], d[2], d[3], at, as, inv);
-    for (int e = 0; e < 4; e++) dinv[(int64_t)e * ncl + t] = inv[e];
-}
-/* coarsest level: `sweeps` symmetric red-black sweeps in one workgroup, iterate in LDS */
-constexpr int MG_COARSE_MAX = 2048;
-__global__ void __launch_bounds__(1024) k_mg_coarsest(TsLev V, int sweeps)
-{
-    __shared__ double zl[2 * MG_COARSE_MAX];
-    const int ncl = V.n * V.mb * V.l;
-    TsLev W = V;
-    W.zt = zl;
-    W.zs = zl + ncl;
-    W.base = 0;
-    for (int t = threadIdx.x; t < 2 * ncl; t += blockDim.x) zl[t] = 0.0;
-    __syncthreads();
-    const int ncol = (V.periodic && (V.n & 1)) ? 4 : 2;
-    for (int sw = 0; sw < sweeps; sw++)
-        for (int h = 0; h < 2 * ncol; h++) {
-            const int colour = h < ncol ? h : 2 * ncol - 1 - h;
-            for (int t = threadIdx.x; t < ncl; t += blockDim.x) {
-                const int i = t % V.n, k = (t / V.n) % V.l, jl = t / (V.n * V.l);
-                if (mg_colour(W, i, jl, k) == colour) mg_relax(W, i, jl, k);
-            }
-            __syncthreads();
-        }
-    for (int t = threadIdx.x; t < ncl; t += blockDim.x) {
-        V.zt[t] = zl[t];
-        V.zs[t] = zl[ncl + t];
-    }
+    const int64_t cs = C.cstr;
+    for (int e = 0; e < 16; e++) off[(int64_t)e * cs + t] = o[e];
+    for (int e = 0; e < 4; e++) diag[(int64_t)e * cs + t] = d[e];
 }
 
+/* z-line factors of every owned column (one thread each, serial block Thomas along k, the
+ * CPU twin's mg_zline arithmetic): A'_k = A_k - B_k Cp_{k-1}, F_k = -A'_k^-1 B_k, Cp_k =
+ * A'_k^-1 C_k; inactive unknowns (zero diagonal) are identity rows whose A'^-1 and F rows
+ * are zeroed, so their line values come out 0 whatever the right-hand side */
+__global__ void k_mg_fac(TsLev V, double* __restrict__ fac)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= V.n * V.mb) return;
+    const int i = t % V.n, jl = t / V.n;
+    const int64_t cs = V.cstr;
+    double P0 = 0.0, P1 = 0.0, P2 = 0.0, P3 = 0.0;
+    for (int k = 0; k < V.l; k++) {
+        const int64_t c = mg_cell(V, i, jl, k);
+        double Am[4] = {V.diag[c], V.diag[cs + c], V.diag[2 * cs + c], V.diag[3 * cs + c]};
+        double Bm[4] = {V.off[4 * cs + c], V.off[6 * cs + c], V.off[14 * cs + c], V.off[12 * cs + c]};
+        double Cm[4] = {V.off[5 * cs + c], V.off[7 * cs + c], V.off[15 * cs + c], V.off[13 * cs + c]};
+        const bool at = Am[0] != 0.0, as = Am[3] != 0.0;
+        if (!at) { Am[0] = 1.0; Am[1] = Am[2] = 0.0; Bm[0] = Bm[1] = 0.0; Cm[0] = Cm[1] = 0.0; }
+        if (!as) { Am[3] = 1.0; Am[1] = Am[2] = 0.0; Bm[2] = Bm[3] = 0.0; Cm[2] = Cm[3] = 0.0; }
+        if (k == 0) Bm[0] = Bm[1] = Bm[2] = Bm[3] = 0.0;
+        else {
+            const double a0 = Am[0] - (Bm[0] * P0 + Bm[1] * P2), a1 = Am[1] - (Bm[0] * P1 + Bm[1] * P3);
+            const double a2 = Am[2] - (Bm[2] * P0 + Bm[3] * P2), a3 = Am[3] - (Bm[2] * P1 + Bm[3] * P3);
+            Am[0] = a0; Am[1] = a1; Am[2] = a2; Am[3] = a3;
+        }
+        const double det = Am[0] * Am[3] - Am[1] * Am[2];
+        const double qd = det != 0.0 ? 1.0 / det : 0.0;
+        double I0 = Am[3] * qd, I1 = -Am[1] * qd, I2 = -Am[2] * qd, I3 = Am[0] * qd;
+        P0 = I0 * Cm[0] + I1 * Cm[2]; P1 = I0 * Cm[1] + I1 * Cm[3];
+        P2 = I2 * Cm[0] + I3 * Cm[2]; P3 = I2 * Cm[1] + I3 * Cm[3];
+        double F0 = -(I0 * Bm[0] + I1 * Bm[2]), F1 = -(I0 * Bm[1] + I1 * Bm[3]);
+        double F2 = -(I2 * Bm[0] + I3 * Bm[2]), F3 = -(I2 * Bm[1] + I3 * Bm[3]);
+        if (!at) { I0 = I1 = F0 = F1 = 0.0; }
+        if (!as) { I2 = I3 = F2 = F3 = 0.0; }
+        const double v[12] = {F0, F1, F2, F3, I0, I1, I2, I3, P0, P1, P2, P3};
+#pragma unroll
+        for (int e = 0; e < 12; e++) fac[(int64_t)e * cs + c] = v[e];
+    }
+}
 /* ---- host: structure from the identity-row pattern ------------------------------ */
 
 /* flags[j*n+i] = 1 for an active water column (any active P), flags[n*m + j*n+i] = 1
@@ -1818,45 +1960,37 @@ static TsLev mg_view(iemic_ctx* c, int q)
     TsLev V{};
     V.l = c->l;
     V.periodic = c->cfg.periodic;
-    if (q == 0) {
-        V.n = c->n;
-        V.mb = c->jb1 - c->jb0;
-        /* bands: the level-0 z-line smoother and residual see the neighbour bands' rows */
-        V.halo_j = (c->nranks > 1 && c->l <= 64 && gs.ts_halo) ? 1 : 0;
-        V.base = c->own0;
-        V.cstr = c->next;
-        V.off = gs.tsoff.p;
-        V.diag = gs.tsdiag.p;
-        V.dinv = gs.tsinv.p;
-        V.dinv_aos = 1;
-        V.bt = gs.bts.p + TT;
-        V.bs = gs.bts.p + SS;
-        V.bstr = NUN;
-        V.zt = gs.zt.p;
-        V.zs = gs.zs.p;
-    } else {
-        V.n = gs.mg_n[q];
-        V.mb = gs.mg_m[q];
-        const int64_t ncl = (int64_t)V.n * V.mb * V.l;
-        V.base = 0;
-        V.cstr = ncl;
-        V.off = gs.mg_off[q].p;
-        V.diag = gs.mg_diag[q].p;
-        V.dinv = gs.mg_dinv[q].p;
-        V.dinv_aos = 0;
-        V.bt = gs.mg_b[q].p;
-        V.bs = gs.mg_b[q].p + ncl;
-        V.bstr = 1;
-        V.zt = gs.mg_z[q].p;
-        V.zs = gs.mg_z[q].p + ncl;
-    }
+    V.n = gs.mg_n[q];
+    V.mb = gs.mg_m[q];
+    /* bands: the level-0 smoother and residual see the neighbour bands' rows (halo rows in
+     * the layout, exchanged before every relaxation), colours by the global j parity so
+     * that all bands relax the same colour in the same launch; coarse levels band-local */
+    V.hj = (q == 0 && c->nranks > 1) ? 1 : 0;
+    V.vis = V.hj;
+    V.jpar = q == 0 ? (c->jb0 & 1) : 0;
+    V.cstr = (int64_t)(V.mb + 2 * V.hj) * V.n * V.l;
+    V.off = gs.mg_off[q].p;
+    V.diag = gs.mg_diag[q].p;
+    V.fac = gs.mg_fac[q].p;
+    V.b = gs.mg_b[q].p;
+    V.z = gs.mg_z[q].p;
     return V;
 }
 
 static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
-/* Gauss-Jordan inverse with partial pivoting (host, the coarsest level: <= 256 unknowns);
- * unknowns without any coupling (inactive) get an identity row */
+/* lanes per z-line (one per level, a power of two >= l; the smoother needs l <= 64) */
+static int mg_lanes(int l) { return l <= 16 ? 16 : (l <= 32 ? 32 : 64); }
+
+#define MG_LAUNCH_P(P, KERNEL, GRID, ...)                                                  \
+    do {                                                                                   \
+        if ((P) == 16) hipLaunchKernelGGL(KERNEL<16>, dim3(GRID), dim3(256), 0, s, __VA_ARGS__); \
+        else if ((P) == 32) hipLaunchKernelGGL(KERNEL<32>, dim3(GRID), dim3(256), 0, s, __VA_ARGS__); \
+        else hipLaunchKernelGGL(KERNEL<64>, dim3(GRID), dim3(256), 0, s, __VA_ARGS__);     \
+    } while (0)
+
+/* Gauss-Jordan inverse with partial pivoting (host, large coarsest levels); unknowns
+ * without any coupling (inactive) get an identity row */
 static void dense_inverse(std::vector<double>& A, int N, std::vector<double>& X)
 {
     X.assign((size_t)N * N, 0.0);
@@ -1893,6 +2027,14 @@ static void dense_inverse(std::vector<double>& A, int N, std::vector<double>& X)
     }
 }
 
+/* decode of a coarse-level cell index t = (jl n + i) l + k */
+static inline void mg_decode(int64_t t, int n, int l, int& i, int& jl, int& k)
+{
+    k = (int)(t % l);
+    i = (int)((t / l) % n);
+    jl = (int)(t / ((int64_t)l * n));
+}
+
 /* Bands: the coarsest T/S level as one global problem.  Unknown (J, i, k, var) of the
  * stacked bands' coarsest grids (J = band row offset + local row) is 2((J nc + i) l + k)
  * + var, a band matrix of half-width 2 l nc + 1.  Every rank writes its own rows — its
@@ -1904,11 +2046,7 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
 {
     BlockGS& gs = c->gs;
     gs.mg_glob = 0;
-    static const int enabled = [] {
-        const char* e = getenv("IEMIC_TS_GLOBAL");
-        return e ? atoi(e) : 1;
-    }();
-    if (c->nranks <= 1 || !enabled || c->l > 64) return 0;
+    if (c->nranks <= 1 || c->l > 64) return 0;
     const int P = c->nranks, me = c->rank, l = c->l, qc = gs.mg_nlev - 1;
     const int nc = gs.mg_n[qc], cm = gs.mg_m[qc], mb = c->jb1 - c->jb0;
     const int64_t ncl = (int64_t)nc * cm * l;
@@ -1944,7 +2082,8 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
     };
     bool ok = true;
     for (int64_t t = 0; t < ncl; t++) {
-        const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+        int i, jl, k;
+        mg_decode(t, nc, l, i, jl, k);
         const int J = joff[me] + jl;
         for (int R = 0; R < 2; R++) {
             const int row = gidx(J, i, k, R);
@@ -2040,7 +2179,6 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
     gs.mg_gN = NG;
     gs.mg_g0 = g0;
     gs.mg_glob = 1;
-    (void)ncl;
     return 0;
 }
 
@@ -2050,7 +2188,7 @@ __global__ void k_mg_gput(const double* __restrict__ b, int64_t ncl, int nc, int
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ncl) return;
-    const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+    const int k = (int)(t % l), i = (int)((t / l) % nc), jl = (int)(t / ((int64_t)l * nc));
     const int64_t q = g0 + 2 * (((int64_t)jl * nc + i) * l + k);
     g[q] = b[t];
     g[q + 1] = b[ncl + t];
@@ -2061,7 +2199,7 @@ __global__ void k_mg_gget(const double* __restrict__ y, int64_t ncl, int nc, int
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ncl) return;
-    const int i = (int)(t % nc), k = (int)((t / nc) % l), jl = (int)(t / ((int64_t)nc * l));
+    const int k = (int)(t % l), i = (int)((t / l) % nc), jl = (int)(t / ((int64_t)l * nc));
     const int64_t q = 2 * (((int64_t)jl * nc + i) * l + k);
     z[t] = y[q];
     z[ncl + t] = y[q + 1];
@@ -2078,7 +2216,7 @@ __global__ void k_mg_coarse_dense(const double* __restrict__ off, const double* 
     const int64_t t = rowq % ncl;
     const int64_t N = 2 * ncl;
     double* Ar = A + rowq * N;
-    const int i = (int)(t % cn), k = (int)((t / cn) % l), jl = (int)(t / ((int64_t)cn * l));
+    const int k = (int)(t % l), i = (int)((t / l) % cn), jl = (int)(t / ((int64_t)l * cn));
     Ar[R * ncl + t] += dg[(3 * R) * ncl + t];
     Ar[(1 - R) * ncl + t] += dg[(1 + R) * ncl + t];
     for (int qq = 0; qq < 8; qq++) {
@@ -2099,7 +2237,7 @@ __global__ void k_mg_coarse_dense(const double* __restrict__ off, const double* 
             if (!periodic) continue;
             ii = (ii + cn) % cn;
         }
-        const int64_t nb = ((int64_t)jj * l + kk) * cn + ii;
+        const int64_t nb = ((int64_t)jj * cn + ii) * l + kk;
         const int var = qq < 6 ? R : 1 - R;
         Ar[var * ncl + nb] += v;
     }
@@ -2108,24 +2246,26 @@ __global__ void k_mg_coarse_dense(const double* __restrict__ off, const double* 
     if (!any) Ar[rowq] = 1.0;
 }
 
-/* coarse levels, Galerkin operators and the coarsest inverse (once per Jacobian) */
+/* levels, Galerkin operators, z-line factors and the coarsest inverse (once per Jacobian) */
 static int mg_setup(iemic_ctx* c)
 {
     BlockGS& gs = c->gs;
     const int l = c->l;
-    int n = c->n, m = c->jb1 - c->jb0, q = 0;
+    if (l > 64) {                /* the z-line smoother runs one lane per level */
+        gs.ts_mg = 0;
+        return 0;
+    }
     if (gs.mg_nlev == 0) {
         /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns) */
+        int n = c->n, m = c->jb1 - c->jb0, q = 0;
+        gs.mg_n[0] = n;
+        gs.mg_m[0] = m;
         while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)n * m * l > 128) && (n > 1 || m > 1)) {
             n = (n + 1) / 2;
             m = (m + 1) / 2;
             q++;
             gs.mg_n[q] = n;
             gs.mg_m[q] = m;
-            const size_t ncl = (size_t)n * m * l;
-            if (gs.mg_off[q].alloc(16 * ncl) || gs.mg_diag[q].alloc(4 * ncl) ||
-                gs.mg_dinv[q].alloc(4 * ncl) || gs.mg_b[q].alloc(2 * ncl) || gs.mg_z[q].alloc(2 * ncl))
-                return IEMIC_ENOMEM;
         }
         if (q == 0) {
             gs.ts_mg = 0;            /* a single water column per band: plain sweeps */
@@ -2135,21 +2275,34 @@ static int mg_setup(iemic_ctx* c)
             set_error("block GS: T/S multigrid coarsest level too large");
             return IEMIC_EINVAL;
         }
+        for (int lv = 0; lv <= q; lv++) {
+            const size_t cs = (size_t)mg_view(c, lv).cstr;
+            if (gs.mg_off[lv].alloc(16 * cs) || gs.mg_diag[lv].alloc(4 * cs) || gs.mg_fac[lv].alloc(12 * cs) ||
+                gs.mg_b[lv].alloc(2 * cs) || gs.mg_z[lv].alloc(2 * cs))
+                return IEMIC_ENOMEM;
+            for (DevBuf<double>* bptr : {&gs.mg_off[lv], &gs.mg_diag[lv], &gs.mg_fac[lv], &gs.mg_b[lv], &gs.mg_z[lv]})
+                HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
+        }
         gs.mg_nlev = q + 1;
         const size_t N = (size_t)2 * n * m * l;
         if (gs.mg_cinv.alloc(N * N)) return IEMIC_ENOMEM;
     }
-    if (gs.mg_nlev < 2) {
-        gs.ts_mg = 0;
-        return 0;
-    }
     hipStream_t s = c->stream;
-    for (q = 1; q < gs.mg_nlev; q++) {
+    {
+        const TsLev V0 = mg_view(c, 0);
+        hipLaunchKernelGGL(k_mg_pack0, dim3(blocks_for(c->nloc)), dim3(256), 0, s, gs.tsoff.p, gs.tsdiag.p,
+                           lay_of(c), c->next, V0, gs.mg_off[0].p, gs.mg_diag[0].p);
+    }
+    for (int q = 1; q < gs.mg_nlev; q++) {
         TsLev F = mg_view(c, q - 1);
         const TsLev C = mg_view(c, q);
-        F.halo_j = 0;                /* aggregates and coarse operators stay band-local */
-        hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for(C.cstr)), dim3(256), 0, s, F, C,
-                           gs.mg_off[q].p, gs.mg_diag[q].p, gs.mg_dinv[q].p);
+        F.vis = 0;                   /* aggregates and coarse operators stay band-local */
+        hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for((int64_t)C.n * C.mb * C.l)), dim3(256), 0, s, F, C,
+                           gs.mg_off[q].p, gs.mg_diag[q].p);
+    }
+    for (int q = 0; q + 1 < gs.mg_nlev; q++) {
+        const TsLev V = mg_view(c, q);
+        hipLaunchKernelGGL(k_mg_fac, dim3(blocks_for((int64_t)V.n * V.mb)), dim3(256), 0, s, V, gs.mg_fac[q].p);
     }
     HIP_OK(hipGetLastError());
     /* coarsest level: its dense operator assembled and inverted on the device (Gauss-Jordan
@@ -2185,7 +2338,8 @@ static int mg_setup(iemic_ctx* c)
     std::vector<double> A((size_t)N * N, 0.0), X;
     const int cn = gs.mg_n[qc], cm = gs.mg_m[qc];
     for (int64_t t = 0; t < ncl; t++) {
-        const int i = (int)(t % cn), k = (int)((t / cn) % l), jl = (int)(t / ((int64_t)cn * l));
+        int i, jl, k;
+        mg_decode(t, cn, l, i, jl, k);
         for (int R = 0; R < 2; R++) {
             const int64_t row = R * ncl + t;
             A[row * N + R * ncl + t] += dg[(3 * R) * ncl + t];
@@ -2208,7 +2362,7 @@ static int mg_setup(iemic_ctx* c)
                     if (!c->cfg.periodic) continue;
                     ii = (ii + cn) % cn;
                 }
-                const int64_t nb = ((int64_t)jj * l + kk) * cn + ii;
+                const int64_t nb = ((int64_t)jj * cn + ii) * l + kk;
                 const int var = qq < 6 ? R : 1 - R;
                 A[row * N + var * ncl + nb] += v;
             }
@@ -2222,110 +2376,141 @@ static int mg_setup(iemic_ctx* c)
 /* refresh the level-0 iterate's latitude halo rows (bands coupled in the T/S smoother) */
 static int mg_halo(iemic_ctx* c, const TsLev& V)
 {
-    if (!V.halo_j) return 0;
-    return halo_exchange_pair(c, V.zt, V.zs);
+    if (!V.vis) return 0;
+    const int64_t slab = (int64_t)V.n * V.l;
+    return halo_exchange_slab2(c, V.z, V.z + V.cstr, V.hj * slab, (int64_t)V.mb * slab, slab);
 }
 
-static int mg_smooth(iemic_ctx* c, int q, int nu, bool post)
+/* one colour launch of the z-line smoother (C: first post-smoothing sweep, zout: final) */
+static int mg_zl(iemic_ctx* c, const TsLev& V, int colour, const TsLev* C, double* zout)
+{
+    hipStream_t s = c->stream;
+    const int P = mg_lanes(V.l);
+    const unsigned g = blocks_for(mg_columns_of(V, colour) * P);
+    if (!g) return 0;
+    const TsLev Cv = C ? *C : V;
+    const int corr = C ? 1 : 0;
+    MG_LAUNCH_P(P, k_mg_zl, g, V, colour, Cv, corr, zout);
+    return 0;
+}
+
+/* the coarsest level: z = A^-1 b (dense), or the bands' global coarsest problem */
+static int mg_coarsest(iemic_ctx* c, int q)
 {
     BlockGS& gs = c->gs;
     hipStream_t s = c->stream;
-    const Lay L = lay_of(c);
     int rc;
-    if (c->l <= 64) {
-        /* z-line relaxation: colours forward before the coarse correction, backward after */
-        const TsLev V = mg_view(c, q);
-        const int ncolour = (V.periodic && (V.n & 1)) ? 4 : 2;
-        const int P = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : 64);
-        const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
-        const unsigned gp = (unsigned)(((int64_t)((np + 1) / 2) * V.mb * P + 255) / 256);
-        /* IEMIC_MG_HALF: 1 -- on the coarse levels the pre-smoother relaxes the first half of
-         * the colours and the post-smoother the second half (backward), so every column is
-         * relaxed once per visit; 2 -- on every level */
-        static const int half_mode = [] {
-            const char* e = getenv("IEMIC_MG_HALF");
-            return e ? atoi(e) : 0;
-        }();
-        const bool half = half_mode == 2 || (half_mode == 1 && q > 0);
-        const int c0 = half && post ? ncolour / 2 : 0;
-        const int nc = half ? ncolour / 2 : ncolour;
-        for (int sw = 0; sw < nu; sw++)
-            for (int hh = 0; hh < nc; hh++) {
-                const int h = c0 + hh;
-                const int col = half ? (post ? ncolour - 1 - hh : h) : (post ? ncolour - 1 - h : h);
-                if ((rc = mg_halo(c, V))) return rc;
-                if (P == 16)
-                    hipLaunchKernelGGL(k_mg_zline_pcr<16>, dim3(gp), dim3(256), 0, s, V, col);
-                else if (P == 32)
-                    hipLaunchKernelGGL(k_mg_zline_pcr<32>, dim3(gp), dim3(256), 0, s, V, col);
-                else
-                    hipLaunchKernelGGL(k_mg_zline_pcr<64>, dim3(gp), dim3(256), 0, s, V, col);
-            }
+    const int N = 2 * gs.mg_n[q] * gs.mg_m[q] * c->l;
+    if (gs.mg_glob) {
+        /* gather the bands' right-hand sides, own rows of X b */
+        const int64_t ncl = N / 2;
+        HIP_OK(hipMemsetAsync(gs.mg_gvec.p, 0, sizeof(double) * gs.mg_gN, s));
+        hipLaunchKernelGGL(k_mg_gput, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_b[q].p, ncl,
+                           gs.mg_n[q], c->l, gs.mg_g0, gs.mg_gvec.p);
+        if ((rc = allreduce_sum(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
+        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s,
+                           gs.mg_gX.p + (int64_t)gs.mg_g0 * gs.mg_gN, N, gs.mg_gN, gs.mg_gvec.p,
+                           gs.mg_gtmp.p);
+        hipLaunchKernelGGL(k_mg_gget, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_gtmp.p, ncl,
+                           gs.mg_n[q], c->l, gs.mg_z[q].p);
         return 0;
     }
-    if (q == 0 && (c->n & 1) == 0) {
-        const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
-        const int seq[4] = {0, 1, 1, 0};
-        for (int sw = 0; sw < nu; sw++)
-            for (int h = 0; h < 4; h++)
-                hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
-                                   gs.zt.p, gs.zs.p, L, seq[h]);
-        return 0;
-    }
+    hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
+                       gs.mg_b[q].p, gs.mg_z[q].p);
+    return 0;
+}
+
+/* One V-cycle from level q.  first: the level's iterate started at 0 and its colour-0 lines
+ * were relaxed by the launch that formed its right-hand side (k_mg_entry / k_mg_rc).
+ * zout: the last level-0 sweep writes z(T, S) into the preconditioner output. */
+static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
+{
+    BlockGS& gs = c->gs;
+    hipStream_t s = c->stream;
+    int rc;
     const TsLev V = mg_view(c, q);
-    const int64_t ncl = (int64_t)V.n * V.mb * V.l;
-    const bool four = V.periodic && (V.n & 1);
-    const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
-    const int* seq = four ? seq4 : seq2;
-    int ns = four ? 8 : 4, h0 = 0;
-    /* coarse levels: forward colour order before the coarse correction, backward after
-     * it (the V-cycle as a whole stays symmetric; half the launches of full sweeps) */
-    if (q > 0) {
-        ns /= 2;
-        h0 = post ? ns : 0;
-    }
+    const int nc = mg_ncolour(V), nu = std::max(1, gs.mg_sweeps);
     for (int sw = 0; sw < nu; sw++)
-        for (int h = 0; h < ns; h++) {
+        for (int h = (sw == 0 && first) ? 1 : 0; h < nc; h++) {
             if ((rc = mg_halo(c, V))) return rc;
-            hipLaunchKernelGGL(k_mg_half, dim3(blocks_for(ncl)), dim3(256), 0, s, V, seq[h0 + h]);
+            if ((rc = mg_zl(c, V, h, nullptr, nullptr))) return rc;
+        }
+    const int qc = gs.mg_nlev - 1;
+    const TsLev C = mg_view(c, q + 1);
+    if ((rc = mg_halo(c, V))) return rc;
+    {
+        const int P = mg_lanes(V.l);
+        const int shortcut = (first && nu == 1 && nc == 2) ? 1 : 0;
+        const int relax = q + 1 < qc ? 1 : 0;
+        MG_LAUNCH_P(P, k_mg_rc, blocks_for((int64_t)C.n * C.mb * P), V, C, shortcut, relax);
+    }
+    if (q + 1 == qc) {
+        if ((rc = mg_coarsest(c, q + 1))) return rc;
+    } else if ((rc = mg_vcycle(c, q + 1, true, nullptr))) {
+        return rc;
+    }
+    /* coarse correction: added where the first post-smoothing colours read it, or (level 0
+     * of a band group, whose lines also read the neighbour bands' rows) explicitly */
+    const bool corr = V.hj == 0;
+    if (!corr)
+        hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)V.n * V.mb * V.l)), dim3(256), 0, s, V, C);
+    for (int sw = 0; sw < nu; sw++)
+        for (int h = nc - 1; h >= 0; h--) {
+            if ((rc = mg_halo(c, V))) return rc;
+            if ((rc = mg_zl(c, V, h, corr && sw == 0 ? &C : nullptr, sw + 1 == nu ? zout : nullptr))) return rc;
         }
     return 0;
 }
 
-static int mg_vcycle(iemic_ctx* c, int q)
+/* the T/S block solve: right-hand side rr_TS - A_TS,D z_D from the dynamics iterate z, then
+ * ts_mg V-cycles (or ts_sweeps symmetric red-black sweeps), result into z(T, S) -- for the
+ * multigrid only when out (else later by ts_out) */
+static int ts_solve(iemic_ctx* c, double* z, bool out)
 {
     BlockGS& gs = c->gs;
+    const Lay L = lay_of(c);
+    const int n = c->n;
     hipStream_t s = c->stream;
+    const unsigned gc = (unsigned)((c->nloc + 255) / 256);
     int rc;
-    if (q == gs.mg_nlev - 1) {
-        const int N = 2 * gs.mg_n[q] * gs.mg_m[q] * c->l;
-        if (gs.mg_glob) {
-            /* global coarsest: gather the bands' right-hand sides, own rows of X b */
-            const int64_t ncl = N / 2;
-            HIP_OK(hipMemsetAsync(gs.mg_gvec.p, 0, sizeof(double) * gs.mg_gN, s));
-            hipLaunchKernelGGL(k_mg_gput, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_b[q].p, ncl,
-                               gs.mg_n[q], c->l, gs.mg_g0, gs.mg_gvec.p);
-            if ((rc = allreduce_sum(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
-            hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s,
-                               gs.mg_gX.p + (int64_t)gs.mg_g0 * gs.mg_gN, N, gs.mg_gN, gs.mg_gvec.p,
-                               gs.mg_gtmp.p);
-            hipLaunchKernelGGL(k_mg_gget, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_gtmp.p, ncl,
-                               gs.mg_n[q], c->l, gs.mg_z[q].p);
-            return 0;
-        }
-        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
-                           gs.mg_b[q].p, gs.mg_z[q].p);
+    if (gs.ts_mg > 0) {
+        const TsLev V0 = mg_view(c, 0);
+        const int P = mg_lanes(c->l);
+        const unsigned ge = (unsigned)(((n + MG_TI - 1) / MG_TI) * V0.mb);
+        MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.known.p, gs.kmask.p, gs.rr.p, z, L, V0);
+        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
+            if ((rc = mg_vcycle(c, 0, cyc == 0, out && cyc + 1 == gs.ts_mg ? z : nullptr))) return rc;
+        HIP_OK(hipGetLastError());
         return 0;
     }
-    const int nu = std::max(1, gs.mg_sweeps);
-    if ((rc = mg_smooth(c, q, nu, false))) return rc;
-    const TsLev F = mg_view(c, q), C = mg_view(c, q + 1);
-    if ((rc = mg_halo(c, F))) return rc;
-    hipLaunchKernelGGL(k_mg_restrict, dim3(blocks_for(4 * C.cstr)), dim3(256), 0, s, F, C, gs.mg_b[q + 1].p,
-                       gs.mg_z[q + 1].p);
-    if ((rc = mg_vcycle(c, q + 1))) return rc;
-    hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)F.n * F.mb * F.l)), dim3(256), 0, s, F, C);
-    return mg_smooth(c, q, nu, true);
+    const int nsw = std::max(1, gs.ts_sweeps);
+    if ((n & 1) == 0) {
+        /* colour-compacted symmetric red-black sweeps */
+        const int nblk = (int)((c->nloc + 63) / 64);
+        hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, c->d_val.p,
+                           gs.known.p, gs.kmask.p, gs.rr.p, z, gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p, nblk);
+        const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
+        const int seq[4] = {0, 1, 1, 0};
+        for (int sw = 0; sw < nsw; sw++)
+            for (int h = 0; h < 4; h++)
+                hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
+                                   gs.zt.p, gs.zs.p, L, seq[h]);
+        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
+    } else {
+        /* symmetric sweeps: colours forward then backward */
+        hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+                           gs.bts.p, L);
+        const bool four = c->cfg.periodic && (n & 1);
+        const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
+        const int* seq = four ? seq4 : seq2;
+        const int ns = four ? 8 : 4;
+        for (int sw = 0; sw < nsw; sw++)
+            for (int h = 0; h < ns; h++)
+                hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
+                                   gs.tsinv.p, gs.bts.p, z, L, c->next, seq[h]);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
 }
 
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
@@ -2421,10 +2606,6 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     if ((rc = allreduce_sum(c, gs.S9.p, 9 * NC))) return rc;
     if ((rc = cr_factor(c, gs.cr, gs.S9.p, gs.col_of_ij.p))) return rc;
     if ((rc = cr_check(c, gs.cr))) return rc;
-    {
-        const char* e = getenv("IEMIC_TS_HALO");
-        gs.ts_halo = e ? atoi(e) : 1;
-    }
     gs.ts_mg = opt ? std::max(0, opt->ts_mg) : 0;
     gs.mg_sweeps = opt ? std::max(1, opt->mg_sweeps) : 1;
     if (gs.ts_mg > 0 && (rc = mg_setup(c))) return rc;
@@ -2432,39 +2613,6 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.dyn_mr = opt ? (opt->dyn_mr != 0) : 0;
     gs.dyn_omega = opt && opt->dyn_omega > 0.0 ? opt->dyn_omega : 1.0;
     gs.ts_at = opt ? std::max(0, opt->ts_at) : 0;
-    /* one rank, early T/S right-hand side: the ts_mg V-cycles (fixed buffers and arguments)
-     * captured once as a graph, so the fork costs the host one launch instead of ~40 while
-     * the main stream waits for its next passes (IEMIC_GRAPH=0: plain launches).  Measured
-     * at 2 degrees (scripts/prec_probe.py): the side-stream V-cycle contends with the passes
-     * for HBM (apply 849 -> 739 us with ts_at = 2, not the 560 us of a full overlap) and
-     * FGMRES needs 240 instead of 208 iterations, so the default stays ts_at = 0. */
-    static const int use_graph = [] {
-        const char* e = getenv("IEMIC_GRAPH");
-        return e ? atoi(e) : 1;
-    }();
-    if (gs.mg_exec) {
-        HIP_OK(hipGraphExecDestroy(gs.mg_exec));
-        gs.mg_exec = nullptr;
-    }
-    if (use_graph && gs.ts_mg > 0 && gs.mg_nlev >= 2 && c->nranks == 1 && c->side && !gs.dyn_mr &&
-        gs.ts_at >= 1 && gs.ts_at < gs.dyn_iters) {
-        HIP_OK(hipStreamSynchronize(c->stream));
-        hipStream_t s0 = c->stream;
-        c->stream = c->side;
-        hipGraph_t g = nullptr;
-        HIP_OK(hipStreamBeginCapture(c->side, hipStreamCaptureModeThreadLocal));
-        for (int cyc = 0; cyc < gs.ts_mg && !rc; cyc++) rc = mg_vcycle(c, 0);
-        const hipError_t ec = hipStreamEndCapture(c->side, &g);
-        c->stream = s0;
-        if (rc) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
-        }
-        HIP_OK(ec);
-        const hipError_t ei = hipGraphInstantiate(&gs.mg_exec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        HIP_OK(ei);
-    }
     if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
         if (gs.dres.alloc(NE) || gs.zc.alloc(NE) || gs.dq.alloc(NE) || gs.dzero.alloc(NE) ||
             gs.dmr.alloc(2 * MR_NB + 2))
@@ -2565,53 +2713,17 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
-    const int n = c->n;
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
     int rc = 0;
-    /* the T/S right-hand side rr_TS - A_TS,D z_D is formed after ts_at dynamics passes (the
-     * CPU twin: orc_gs_apply); before the last pass, the T/S multigrid depends on nothing
-     * the remaining passes write and runs beside them on the side stream (one rank) */
+    /* the T/S block is solved with the right-hand side rr_TS - A_TS,D z_D of the dynamics
+     * iterate after ts_at passes (default: after the last; the CPU twin: orc_gs_apply); the
+     * later passes neither read nor write the T/S rows */
     const int ts_at = (!gs.dyn_mr && gs.ts_at >= 1 && gs.ts_at < gs.dyn_iters) ? gs.ts_at : gs.dyn_iters;
-    const bool early = ts_at < gs.dyn_iters;
-    const bool par = early && !band && gs.ts_mg > 0 && c->side;
-    auto mg_cycles = [&]() -> int {
-        if (gs.mg_exec) {
-            HIP_OK(hipGraphLaunch(gs.mg_exec, c->stream));
-            return 0;
-        }
-        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
-            if ((rc = mg_vcycle(c, 0))) return rc;
-        return 0;
-    };
-    auto ts_rhs = [&]() -> int {
-        if (band && (early || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
-        if ((n & 1) == 0) {
-            const int nblk = (int)((c->nloc + 63) / 64);
-            hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, c->d_val.p,
-                               gs.known.p, gs.kmask.p, gs.rr.p, z, gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p, nblk);
-        } else {
-            hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
-                               gs.bts.p, L);
-            if (gs.ts_mg > 0) {
-                HIP_OK(hipMemsetAsync(gs.zt.p, 0, sizeof(double) * c->next, s));
-                HIP_OK(hipMemsetAsync(gs.zs.p, 0, sizeof(double) * c->next, s));
-            }
-        }
-        if (par) {
-            /* fork: the side stream runs the V-cycles on (bts, zt, zs, mg_*), which the
-             * remaining dynamics passes neither read nor write (one graph launch, so the
-             * host's work for it never holds up the main stream) */
-            HIP_OK(hipEventRecord(c->ev_fork, s));
-            HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-            c->stream = c->side;
-            rc = mg_cycles();
-            c->stream = s;
-            if (rc) return rc;
-            HIP_OK(hipEventRecord(c->ev_join, c->side));
-        }
-        return 0;
+    auto ts = [&]() -> int {
+        if (band && (ts_at < gs.dyn_iters || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
+        return ts_solve(c, z, ts_at == gs.dyn_iters);
     };
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
@@ -2619,7 +2731,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
     if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;
-    if (early && ts_at == 1 && (rc = ts_rhs())) return rc;
+    if (ts_at == 1 && gs.dyn_iters > 1 && (rc = ts())) return rc;
     /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
      * minimal-residual w (dyn_mr) or the fixed w = dyn_omega */
     if (gs.dyn_mr && gs.dyn_iters > 1) {
@@ -2642,39 +2754,12 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
         if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* w, p of the neighbours */
         if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
         if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, z, gs.dyn_omega))) return rc;     /* z += w zc */
-        if (early && it + 1 == ts_at && (rc = ts_rhs())) return rc;
+        if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;
     }
-    if (!early && (rc = ts_rhs())) return rc;
-    if (gs.ts_mg > 0) {
-        /* T/S by aggregation-multigrid V-cycles on (zt, zs) with rhs bts */
-        if (par)
-            HIP_OK(hipStreamWaitEvent(s, c->ev_join, 0));   /* join */
-        else if ((rc = mg_cycles()))
-            return rc;
-        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
-        HIP_OK(hipGetLastError());
-        return 0;
-    }
-    const int nsw = std::max(1, gs.ts_sweeps);
-    if ((n & 1) == 0) {
-        /* colour-compacted symmetric red-black sweeps */
-        const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
-        const int seq[4] = {0, 1, 1, 0};
-        for (int sw = 0; sw < nsw; sw++)
-            for (int h = 0; h < 4; h++)
-                hipLaunchKernelGGL(k_gs_ts_half_c, dim3(gh), dim3(256), 0, s, gs.tsc.p, gs.tic.p, gs.bc.p,
-                                   gs.zt.p, gs.zs.p, L, seq[h]);
-        hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
-    } else {
-        /* symmetric sweeps: colours forward then backward */
-        const bool four = c->cfg.periodic && (n & 1);
-        const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
-        const int* seq = four ? seq4 : seq2;
-        const int ns = four ? 8 : 4;
-        for (int sw = 0; sw < nsw; sw++)
-            for (int h = 0; h < ns; h++)
-                hipLaunchKernelGGL(k_gs_ts_half, dim3(gc), dim3(256), 0, s, gs.tsoff.p, gs.known.p,
-                                   gs.tsinv.p, gs.bts.p, z, L, c->next, seq[h]);
+    if (ts_at == gs.dyn_iters && (rc = ts())) return rc;
+    if (ts_at < gs.dyn_iters && gs.ts_mg > 0) {
+        const TsLev V0 = mg_view(c, 0);
+        hipLaunchKernelGGL(k_mg_out, dim3(blocks_for((int64_t)V0.n * V0.mb * V0.l)), dim3(256), 0, s, V0, z);
     }
     HIP_OK(hipGetLastError());
     return 0;
