@@ -41,8 +41,12 @@ iemic_ctx::~iemic_ctx()
     if (stream) (void)hipStreamSynchronize(stream);
     if (h_red) (void)hipHostFree(h_red);
     h_red = nullptr;
+    if (side) (void)hipStreamSynchronize(side);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
-    stream = nullptr;
+    stream = side = nullptr;
     /* device buffers are members: released after this body, with the stream drained */
 }
 
@@ -179,7 +183,10 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     iemic_ctx* c = new iemic_ctx();
     c->cfg = *grid;
     c->device = std::min(std::max(grid->device, 0), ndev - 1);
-    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         set_error("iemic_create: cannot initialise the HIP device");
         delete c;
         return IEMIC_EDEVICE;

@@ -92,6 +92,8 @@ struct BlockGS {
     int ncol = 0;                    /* active water columns                            */
     DevBuf<int> own_pos;             /* Schur index -> itself for this band's active     */
                                      /* columns, -1 otherwise                           */
+    DevBuf<int> ocol;                /* (j*n+i) -> this band's Schur rhs entry, -2 - entry */
+                                     /* for a pinned column (written 0), -1 for none     */
     DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8), halo-filled */
     DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
     DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index i*m+j, or -1 (no water)   */
@@ -149,6 +151,8 @@ struct iemic_ctx {
     iemic_grid cfg;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;      /* second stream: the early T/S V-cycles (one rank)  */
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n = 0, m = 0, l = 0;
     int64_t ncell = 0, nrows = 0;    /* global cells / rows                               */
     /* latitude-band decomposition (stencil.h ext layout): owned band [jb0, jb1) */

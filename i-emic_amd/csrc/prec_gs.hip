@@ -712,26 +712,27 @@ __global__ void __launch_bounds__(256) k_gs_ptil_scan(const double* __restrict__
                                                       const double* __restrict__ rr,
                                                       double* __restrict__ z, Lay L)
 {
+    (void)col_of_ij;
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;                  /* whole column groups exit */
     const int ij = L.jb0 * L.n + t_;
-    if (col_of_ij[ij] < 0) return;
     const int i = ij % L.n, j = ij / L.n;
     const int64_t ncell = L.nloc;
     double A = 0.0, B = 0.0;
     bool pa = false;
     int64_t cell = 0;
     if (k < L.l) {
+        /* every load of the level at once (no gating on the flags: one memory round) */
         cell = ecell(L, i, j, k);
-        pa = !known[NUN * cell + PP];
-        if (pa && k < L.l - 1 && !known[NUN * cell + WW]) {
-            const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
-            const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
-            if (g0 != 0.0) {
-                A = rr[NUN * cell + WW] / g0;
-                B = -g1 / g0;
-            }
+        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
+        const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
+        const double rw = rr[NUN * cell + WW];
+        pa = !kp;
+        if (pa && k < L.l - 1 && !kw && g0 != 0.0) {
+            A = rw / g0;
+            B = -g1 / g0;
         }
     }
     /* suffix composition from the top: p_k = A_k + B_k p_{k+1}, p_l = 0 */
@@ -756,31 +757,32 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
                                                     const double* __restrict__ rr,
                                                     double* __restrict__ zo, double omega)
 {
+    (void)col_of_ij;
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;
     const int ij = L.jb0 * L.n + t_;
-    const int c = col_of_ij[ij];
-    if (c < 0) return;
     const int i = ij % L.n, j = ij / L.n;
     const int64_t ncell = L.nloc;
-    double A = 0.0, B = 0.0;
+    double A = 0.0, B = 0.0, pb = 0.0, zp = 0.0;
     bool pa = false, wa = false;
     int64_t cell = 0;
     if (k < L.l) {
+        /* pbar by Schur index i*m + j (0 on columns without water); every load at once */
         cell = ecell(L, i, j, k);
-        pa = !known[NUN * cell + PP];
-        wa = !known[NUN * cell + WW];
-        if (pa && wa) {
-            const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
-            const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
-            if (a != 0.0) {
-                /* continuity right-hand side rr_p - Duv uv, evaluated in place */
-                const double rhs = crhs ? crhs[cell]
-                                        : rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
-                A = rhs / a;
-                B = -b / a;
-            }
+        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
+        const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
+        /* continuity right-hand side rr_p - Duv uv, evaluated in place */
+        const double rhs = crhs ? crhs[cell]
+                                : rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
+        pb = pbar[(int64_t)i * L.m + j];
+        zp = z[NUN * cell + PP];
+        pa = !kp;
+        wa = !kw;
+        if (pa && wa && a != 0.0) {
+            A = rhs / a;
+            B = -b / a;
         }
     }
     /* prefix composition from the bottom: w_k = A_k + B_k w_{k-1}, w_{-1} = 0 */
@@ -793,51 +795,42 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
         }
     }
     if (k < L.l) {
-        if (pa) z[NUN * cell + PP] += pbar[c];
-        if (wa) z[NUN * cell + WW] = pa ? A : 0.0;
+        const double pn = zp + pb, wn = pa ? A : 0.0;
+        if (pa) z[NUN * cell + PP] = pn;
+        if (wa) z[NUN * cell + WW] = wn;
         /* defect-correction passes: z_out += omega z on the final W/P rows (k_dyn_add fused) */
         if (zo) {
-            if (pa) zo[NUN * cell + PP] += omega * z[NUN * cell + PP];
-            if (wa) zo[NUN * cell + WW] += omega * z[NUN * cell + WW];
+            if (pa) zo[NUN * cell + PP] += omega * pn;
+            if (wa) zo[NUN * cell + WW] += omega * wn;
         }
     }
 }
 
-template <int P>
-__global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__ val,
-                                                      const uint8_t* __restrict__ known,
-                                                      const double* __restrict__ pw,
-                                                      const double* __restrict__ rr,
-                                                      const double* __restrict__ z,
-                                                      const int* __restrict__ col_of_ij,
-                                                      const uint8_t* __restrict__ pinned,
-                                                      const int* __restrict__ own_pos,
-                                                      double* __restrict__ colv_own, Lay L);
 /* sum over the 4 P corners of a U/V point of G * p(P)  (U row slots 20..23 / V 42..45) */
 __device__ __forceinline__ void guv_p(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                       const double* __restrict__ pv, int64_t pstride, int i, int j,
                                       int k, int64_t lc, const Lay& L, double& gu, double& gv,
-                                      const int* __restrict__ col_of_ij)
+                                      bool colmode)
 {
+    /* branch-free: a corner outside the domain reads the cell itself with weight 0; with
+     * colmode the values are the column values pbar indexed i*m + j (0 without water) */
     const int n = L.n, m = L.m, periodic = L.periodic;
     const int64_t ncell = L.nloc;
     const int64_t cell = lc;
     gu = gv = 0.0;
+#pragma unroll
     for (int g4 = 0; g4 < 4; g4++) {
         int pi = i + (g4 & 1), pj = j + ((g4 >> 1) & 1);
-        if (!hnb(pi, pj, n, m, periodic)) continue;
+        const bool in = hnb(pi, pj, n, m, periodic);
+        if (!in) { pi = i; pj = j; }
         const int64_t pc = ecell(L, pi, pj, k);
-        if (known[NUN * pc + PP]) continue;
-        double p;
-        if (col_of_ij) {            /* column value (pbar) */
-            const int c = col_of_ij[pj * n + pi];
-            if (c < 0) continue;
-            p = pv[c];
-        } else {
-            p = pv[pstride * pc + PP];
-        }
-        gu += val[(int64_t)(S_UP + g4) * ncell + cell] * p;
-        gv += val[(int64_t)(S_VP + g4) * ncell + cell] * p;
+        const uint8_t kp = known[NUN * pc + PP];
+        const double p = colmode ? pv[(int64_t)pi * m + pj] : pv[pstride * pc + PP];
+        const double au = val[(int64_t)(S_UP + g4) * ncell + cell];
+        const double av = val[(int64_t)(S_VP + g4) * ncell + cell];
+        const bool use = in && !kp;
+        gu += use ? au * p : 0.0;
+        gv += use ? av * p : 0.0;
     }
 }
 
@@ -847,15 +840,18 @@ __global__ void k_gs_uvs(const double* __restrict__ val, const uint8_t* __restri
                          double* __restrict__ z, Lay L)
 {
     OWNED_CELL;
-    const bool ua = !known[NUN * cell + UU], va = !known[NUN * cell + VV];
-    if (!ua && !va) return;
+    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
     double gu, gv;
-    guv_p(val, known, z, NUN, i, j, k, lc, L, gu, gv, nullptr);
-    const double ru = ua ? rr[NUN * cell + UU] - gu : 0.0;
-    const double rv = va ? rr[NUN * cell + VV] - gv : 0.0;
+    guv_p(val, known, z, NUN, i, j, k, lc, L, gu, gv, false);
     const double* D = uvinv + 4 * cell;
-    if (ua) z[NUN * cell + UU] = D[0] * ru + D[1] * rv;
-    if (va) z[NUN * cell + VV] = D[2] * ru + D[3] * rv;
+    const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
+    const double r0 = rr[NUN * cell + UU], r1 = rr[NUN * cell + VV];
+    const bool ua = !ku, va = !kv;
+    if (!ua && !va) return;
+    const double ru = ua ? r0 - gu : 0.0;
+    const double rv = va ? r1 - gv : 0.0;
+    if (ua) z[NUN * cell + UU] = d0 * ru + d1 * rv;
+    if (va) z[NUN * cell + VV] = d2 * ru + d3 * rv;
 }
 
 /* Duv uv at a P cell: sum over the 4 U/V corners (P row slots 54..61) */
@@ -864,15 +860,21 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
                                          const double* __restrict__ z, int i, int j, int k,
                                          int64_t pl, const Lay& L)
 {
+    /* branch-free: a corner outside the domain reads the cell itself with weight 0 */
     const int n = L.n, m = L.m, periodic = L.periodic;
     const int64_t ncell = L.nloc, pc = pl;
     double acc = 0.0;
+#pragma unroll
     for (int q4 = 0; q4 < 4; q4++) {
         int qi = i - (q4 & 1), qj = j - ((q4 >> 1) & 1);
-        if (!hnb(qi, qj, n, m, periodic)) continue;
+        const bool in = hnb(qi, qj, n, m, periodic);
+        if (!in) { qi = i; qj = j; }
         const int64_t qc = ecell(L, qi, qj, k);
-        if (!known[NUN * qc + UU]) acc += val[(int64_t)(S_PU + q4) * ncell + pc] * z[NUN * qc + UU];
-        if (!known[NUN * qc + VV]) acc += val[(int64_t)(S_PV + q4) * ncell + pc] * z[NUN * qc + VV];
+        const uint8_t ku = known[NUN * qc + UU], kv = known[NUN * qc + VV];
+        const double au = val[(int64_t)(S_PU + q4) * ncell + pc], av = val[(int64_t)(S_PV + q4) * ncell + pc];
+        const double zu = z[NUN * qc + UU], zv = z[NUN * qc + VV];
+        acc += (in && !ku) ? au * zu : 0.0;
+        acc += (in && !kv) ? av * zv : 0.0;
     }
     return acc;
 }
@@ -911,29 +913,30 @@ __global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__
                                                       const double* __restrict__ pw,
                                                       const double* __restrict__ rr,
                                                       const double* __restrict__ z,
-                                                      const int* __restrict__ col_of_ij,
-                                                      const uint8_t* __restrict__ pinned,
-                                                      const int* __restrict__ own_pos,
+                                                      const int* __restrict__ ocol,
                                                       double* __restrict__ colv_own, Lay L)
 {
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;
     const int ij = L.jb0 * L.n + t_;
-    const int c = col_of_ij[ij];
-    if (c < 0) return;
     const int i = ij % L.n, j = ij / L.n;
+    /* ocol: this band's entry of the column (pinned: -2 - entry, written 0; -1: none),
+     * loaded with the rest (no gating round) */
+    const int q = ocol[ij];
     double v = 0.0;
     if (k < L.l) {
         const int64_t cell = ecell(L, i, j, k);
-        if (!known[NUN * cell + PP])
-            v = pw[cell] * (duv_uv(val, known, z, i, j, k, cell - L.own0, L) - rr[NUN * cell + PP]);
+        const uint8_t kp = known[NUN * cell + PP];
+        const double w = pw[cell], rp = rr[NUN * cell + PP];
+        const double d = duv_uv(val, known, z, i, j, k, cell - L.own0, L);
+        v = kp ? 0.0 : w * (d - rp);
     }
 #pragma unroll
     for (int o = P / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, P);
-    if (k == 0) {
-        const int q = own_pos[c];
-        if (q >= 0) colv_own[q] = pinned[c] ? 0.0 : v;
+    if (k == 0 && q != -1) {
+        if (q >= 0) colv_own[q] = v;
+        else colv_own[-2 - q] = 0.0;
     }
 }
 
@@ -1063,20 +1066,25 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
                            const double* __restrict__ pbar, double* __restrict__ z, Lay L,
                            double* __restrict__ zo, double omega)
 {
+    (void)col_of_ij;
     OWNED_CELL;
-    const bool ua = !known[NUN * cell + UU], va = !known[NUN * cell + VV];
-    if (!ua && !va) return;
+    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
     double gu, gv;
-    guv_p(val, known, pbar, 0, i, j, k, lc, L, gu, gv, col_of_ij);
+    guv_p(val, known, pbar, 0, i, j, k, lc, L, gu, gv, true);
+    const double* D = uvinv + 4 * cell;
+    const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
+    const double zu = z[NUN * cell + UU], zv = z[NUN * cell + VV];
+    const bool ua = !ku, va = !kv;
+    if (!ua && !va) return;
     if (!ua) gu = 0.0;
     if (!va) gv = 0.0;
-    const double* D = uvinv + 4 * cell;
-    if (ua) z[NUN * cell + UU] -= D[0] * gu + D[1] * gv;
-    if (va) z[NUN * cell + VV] -= D[2] * gu + D[3] * gv;
+    const double nu = zu - (d0 * gu + d1 * gv), nv = zv - (d2 * gu + d3 * gv);
+    if (ua) z[NUN * cell + UU] = nu;
+    if (va) z[NUN * cell + VV] = nv;
     /* defect-correction passes: z_out += omega z on the final U/V rows (k_dyn_add fused) */
     if (zo) {
-        if (ua) zo[NUN * cell + UU] += omega * z[NUN * cell + UU];
-        if (va) zo[NUN * cell + VV] += omega * z[NUN * cell + VV];
+        if (ua) zo[NUN * cell + UU] += omega * nu;
+        if (va) zo[NUN * cell + VV] += omega * nv;
     }
 }
 
@@ -1214,9 +1222,11 @@ __device__ __forceinline__ double bts_row(const double* __restrict__ val, const 
     for (int s = 0; s < NS; s++) {
         const Slot sl = SLOTS[B + s];
         if (sl.var == TT || sl.var == SS) continue;
-        if ((kbits >> (B + s - 64)) & 1) continue;
+        /* identity-row columns (coupling already in rr) weigh 0: no branch, so the loads of
+         * all the row's slots issue together */
+        const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : val[(int64_t)(B + s) * nloc + lc];
         const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
-        acc -= val[(int64_t)(B + s) * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+        acc -= v * z[NUN * (int64_t)cidx + sl.var];
     }
     return acc;
 }
@@ -1403,6 +1413,20 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
     }
     return true;
 }
+/* the same neighbour, branch-free for the apply: outside the level's (visible) band the
+ * cell itself (every coupling to outside is 0: k_ts_compact / k_mg_galerkin), so the loads
+ * of all neighbours issue together */
+__device__ __forceinline__ void mg_nbc(const TsLev& V, int q, int& i, int& jl, int& k)
+{
+    switch (q) {
+    case 0: i = i > 0 ? i - 1 : (V.periodic ? V.n - 1 : i); break;
+    case 1: i = i < V.n - 1 ? i + 1 : (V.periodic ? 0 : i); break;
+    case 2: jl = jl > -V.vis ? jl - 1 : jl; break;
+    case 3: jl = jl < V.mb - 1 + V.vis ? jl + 1 : jl; break;
+    case 4: k = k > 0 ? k - 1 : k; break;
+    default: k = k < V.l - 1 ? k + 1 : k; break;
+    }
+}
 /* off-diagonal part of row (T, S) of cell (i,jl,k) applied to the iterate */
 __device__ __forceinline__ void mg_offmul(const TsLev& V, int i, int jl, int k, int64_t c,
                                           double& at, double& as)
@@ -1412,7 +1436,7 @@ __device__ __forceinline__ void mg_offmul(const TsLev& V, int i, int jl, int k, 
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         int ii = i, jj = jl, kk = k;
-        if (!mg_nb(V, q, ii, jj, kk)) continue;
+        mg_nbc(V, q, ii, jj, kk);
         const int64_t nc = mg_cell(V, ii, jj, kk);
         at += V.off[(int64_t)q * cs + c] * V.z[nc];
         as += V.off[(int64_t)(8 + q) * cs + c] * V.z[cs + nc];
@@ -1506,11 +1530,9 @@ __device__ __forceinline__ void line_solve(const double* __restrict__ f, int64_t
  * colour) read with their aggregate's coarse correction C.z added.  zout (level 0, final
  * sweep): the active T/S rows of the preconditioner output (ext layout) get the result. */
 template <int P>
-__global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int corr,
-                                              double* __restrict__ zout)
+__device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k, const TsLev& C, int corr,
+                                       double* __restrict__ zout)
 {
-    const int g = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-    const int k = threadIdx.x % P;
     int i, jl;
     if (!mg_column(V, colour, g, i, jl)) return;           /* whole column groups exit */
     const int64_t cs = V.cstr;
@@ -1524,7 +1546,7 @@ __global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int ii = i, jj = jl, kk = k;
-            if (!mg_nb(V, q, ii, jj, kk)) continue;
+            mg_nbc(V, q, ii, jj, kk);
             const int64_t nc = mg_cell(V, ii, jj, kk);
             double zt = V.z[nc], zs = V.z[cs + nc];
             if (corr && mg_lcolour(V, ii, jj) < colour) {
@@ -1547,6 +1569,12 @@ __global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int
         if (V.diag[3 * cs + c] != 0.0) zout[e + SS] = xs;
     }
 }
+template <int P>
+__global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int corr,
+                                              double* __restrict__ zout)
+{
+    zl_one<P>(V, colour, (blockIdx.x * blockDim.x + threadIdx.x) / P, threadIdx.x % P, C, corr, zout);
+}
 
 /* Restriction F -> C (coarse rhs = sum of the children's residuals, fixed order
  * (c00 + c10) + (c01 + c11)) and, when relax, the coarse level's colour-0 lines from the
@@ -1555,49 +1583,58 @@ __global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int
  * shortcut: F was relaxed once, colour 0 then 1, from a zero iterate, so the residual of
  * colour 1 is 0 and that of colour 0 is -H z (its horizontal neighbours). */
 template <int P>
-__global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, int relax)
+__device__ __forceinline__ void rc_one(const TsLev& F, const TsLev& C, int g, int k, int shortcut, int relax)
 {
-    const int g = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-    const int k = threadIdx.x % P;
     if (g >= C.n * C.mb) return;
     const int I = g % C.n, J = g / C.n;
     const bool on = k < C.l;
     const int64_t fs = F.cstr, cs = C.cstr;
-    double r[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-    int64_t t = 0;
-    if (on) {
-        t = mg_cell(C, I, J, k);
+    const int64_t t = on ? mg_cell(C, I, J, k) : 0;
+    double bt = 0.0, bs = 0.0;
+    if (shortcut) {
+        /* the two colour-0 children (a + b + jpar even), clamped into the level and weighted
+         * 0 outside it, so that all their loads issue at once; (c00 + c10) + (c01 + c11)
+         * with the colour-1 terms 0 is their plain sum */
+        double rr[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int a = h ? 1 - F.jpar : F.jpar, b = h;
+            const int i0 = 2 * I + a, j0 = 2 * J + b;
+            const bool in = on && i0 < F.n && j0 < F.mb;
+            const int i = min(i0, F.n - 1), jl = min(j0, F.mb - 1), kc = on ? k : 0;
+            const int64_t c = mg_cell(F, i, jl, kc);
+            double at = 0.0, as = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int ii = i, jj = jl, kk = kc;
+                mg_nbc(F, q, ii, jj, kk);
+                const int64_t nc = mg_cell(F, ii, jj, kk);
+                at += F.off[(int64_t)q * fs + c] * F.z[nc];
+                as += F.off[(int64_t)(8 + q) * fs + c] * F.z[fs + nc];
+            }
+            rr[h][0] = in ? -at : 0.0;
+            rr[h][1] = in ? -as : 0.0;
+        }
+        bt = rr[0][0] + rr[1][0];
+        bs = rr[0][1] + rr[1][1];
+    } else if (on) {
+        double r[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
 #pragma unroll
         for (int ch = 0; ch < 4; ch++) {
             const int i = 2 * I + (ch & 1), jl = 2 * J + (ch >> 1);
             if (i >= F.n || jl >= F.mb) continue;
             const int64_t c = mg_cell(F, i, jl, k);
-            if (shortcut) {
-                if (mg_lcolour(F, i, jl) != 0) continue;
-                double at = 0.0, as = 0.0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    int ii = i, jj = jl, kk = k;
-                    if (!mg_nb(F, q, ii, jj, kk)) continue;
-                    const int64_t nc = mg_cell(F, ii, jj, kk);
-                    at += F.off[(int64_t)q * fs + c] * F.z[nc];
-                    as += F.off[(int64_t)(8 + q) * fs + c] * F.z[fs + nc];
-                }
-                r[ch][0] = -at;
-                r[ch][1] = -as;
-            } else {
-                double at, as;
-                mg_offmul(F, i, jl, k, c, at, as);
-                const double zt = F.z[c], zs = F.z[fs + c];
-                at += F.diag[c] * zt + F.diag[fs + c] * zs;
-                as += F.diag[2 * fs + c] * zt + F.diag[3 * fs + c] * zs;
-                r[ch][0] = F.b[c] - at;
-                r[ch][1] = F.b[fs + c] - as;
-            }
+            double at, as;
+            mg_offmul(F, i, jl, k, c, at, as);
+            const double zt = F.z[c], zs = F.z[fs + c];
+            at += F.diag[c] * zt + F.diag[fs + c] * zs;
+            as += F.diag[2 * fs + c] * zt + F.diag[3 * fs + c] * zs;
+            r[ch][0] = F.b[c] - at;
+            r[ch][1] = F.b[fs + c] - as;
         }
+        bt = (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
+        bs = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
     }
-    const double bt = (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
-    const double bs = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
     if (on) {
         C.b[t] = bt;
         C.b[cs + t] = bs;
@@ -1615,13 +1652,18 @@ __global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, i
         C.z[cs + t] = 0.0;
     }
 }
+template <int P>
+__global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, int relax)
+{
+    rc_one<P>(F, C, (blockIdx.x * blockDim.x + threadIdx.x) / P, threadIdx.x % P, shortcut, relax);
+}
 
 /* Level-0 entry: the T/S right-hand side rr_TS - A_TS,D z_D of a tile of TI columns of one
  * latitude row (Jacobian slots read along i, coalesced; identity-row columns skipped by
  * the slot bitmask), transposed through LDS into the k-contiguous level layout, then the
  * tile's colour-0 lines relaxed from the zero iterate and the other columns' iterate set
  * to 0 (one launch instead of rhs + first colour). */
-constexpr int MG_TI = 32;
+constexpr int MG_TI = 16;
 template <int P>
 __global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                                  const uint64_t* __restrict__ kmask,
@@ -1911,10 +1953,13 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
             }
         }
     }
-    std::vector<int> own(NC, -1);
+    std::vector<int> own(NC, -1), ocol((size_t)n * m, -1);
     for (int q = 0; q < ncol; q++) {
         const int ij = ord[q].second;
-        if (ij / n >= c->jb0 && ij / n < c->jb1) own[colid[ij]] = colid[ij];
+        if (ij / n >= c->jb0 && ij / n < c->jb1) {
+            own[colid[ij]] = colid[ij];
+            ocol[ij] = pin[colid[ij]] ? -2 - colid[ij] : colid[ij];
+        }
     }
     gs.ncol = ncol;
     int rc = 0;
@@ -1926,6 +1971,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     rc |= gs.colv_own.alloc(NC);
     rc |= gs.colv.alloc(NC);
     rc |= gs.own_pos.alloc(NC);
+    rc |= gs.ocol.alloc((size_t)n * m);
     if (rc) {
         set_error("block GS: out of device memory");
         return IEMIC_ENOMEM;
@@ -1934,6 +1980,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * NC))) return rc;
     if ((rc = h2d(c, gs.pinned.p, pin.data(), NC))) return rc;
     if ((rc = h2d(c, gs.own_pos.p, own.data(), sizeof(int) * NC))) return rc;
+    if ((rc = h2d(c, gs.ocol.p, ocol.data(), sizeof(int) * ocol.size()))) return rc;
     /* entries of inactive and foreign columns stay 0 (the rhs of the reduced solve) */
     HIP_OK(hipMemsetAsync(gs.colv_own.p, 0, sizeof(double) * NC, c->stream));
     HIP_OK(hipMemsetAsync(gs.colv2.p, 0, sizeof(double) * NC, c->stream));
@@ -2464,8 +2511,11 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
 
 /* the T/S block solve: right-hand side rr_TS - A_TS,D z_D from the dynamics iterate z, then
  * ts_mg V-cycles (or ts_sweeps symmetric red-black sweeps), result into z(T, S) -- for the
- * multigrid only when out (else later by ts_out) */
-static int ts_solve(iemic_ctx* c, double* z, bool out)
+ * multigrid only when out (else later by k_mg_out).  side: the V-cycles (which read and
+ * write only the multigrid's own buffers once the entry kernel has formed the right-hand
+ * side) run on the side stream, forked after the entry kernel; gs_apply joins before
+ * k_mg_out. */
+static int ts_solve(iemic_ctx* c, double* z, bool out, bool side = false)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -2478,8 +2528,20 @@ static int ts_solve(iemic_ctx* c, double* z, bool out)
         const int P = mg_lanes(c->l);
         const unsigned ge = (unsigned)(((n + MG_TI - 1) / MG_TI) * V0.mb);
         MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.known.p, gs.kmask.p, gs.rr.p, z, L, V0);
-        for (int cyc = 0; cyc < gs.ts_mg; cyc++)
-            if ((rc = mg_vcycle(c, 0, cyc == 0, out && cyc + 1 == gs.ts_mg ? z : nullptr))) return rc;
+        if (side) {
+            HIP_OK(hipEventRecord(c->ev_fork, s));
+            HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+            c->stream = c->side;
+        }
+        rc = 0;
+        for (int cyc = 0; cyc < gs.ts_mg && !rc; cyc++)
+            rc = mg_vcycle(c, 0, cyc == 0, out && cyc + 1 == gs.ts_mg ? z : nullptr);
+        if (side) {
+            c->stream = s;
+            if (rc) return rc;
+            HIP_OK(hipEventRecord(c->ev_join, c->side));
+        }
+        if (rc) return rc;
         HIP_OK(hipGetLastError());
         return 0;
     }
@@ -2663,13 +2725,13 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
                            gs.pinned.p, gs.colv_own.p, L);
     } else if (Pl == 16) {
         hipLaunchKernelGGL(k_gs_pcol_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
     } else if (Pl == 32) {
         hipLaunchKernelGGL(k_gs_pcol_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
     } else {
         hipLaunchKernelGGL(k_gs_pcol_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.col_of_ij.p, gs.pinned.p, gs.own_pos.p, gs.colv_own.p, L);
+                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
     }
     /* pbar = S^-1 b: the bands' entries of b summed, then the cyclic-reduction solve
      * (redundant on every rank: O(n m^2) bytes) */
@@ -2721,9 +2783,12 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
      * iterate after ts_at passes (default: after the last; the CPU twin: orc_gs_apply); the
      * later passes neither read nor write the T/S rows */
     const int ts_at = (!gs.dyn_mr && gs.ts_at >= 1 && gs.ts_at < gs.dyn_iters) ? gs.ts_at : gs.dyn_iters;
+    /* early T/S on one rank: its V-cycles run on the side stream beside the remaining
+     * dynamics passes (both chains are latency-bound, so they overlap) */
+    const bool par = ts_at < gs.dyn_iters && !band && gs.ts_mg > 0;
     auto ts = [&]() -> int {
         if (band && (ts_at < gs.dyn_iters || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
-        return ts_solve(c, z, ts_at == gs.dyn_iters);
+        return ts_solve(c, z, ts_at == gs.dyn_iters, par);
     };
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
@@ -2758,6 +2823,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     }
     if (ts_at == gs.dyn_iters && (rc = ts())) return rc;
     if (ts_at < gs.dyn_iters && gs.ts_mg > 0) {
+        if (par) HIP_OK(hipStreamWaitEvent(s, c->ev_join, 0));   /* join */
         const TsLev V0 = mg_view(c, 0);
         hipLaunchKernelGGL(k_mg_out, dim3(blocks_for((int64_t)V0.n * V0.mb * V0.l)), dim3(256), 0, s, V0, z);
     }
