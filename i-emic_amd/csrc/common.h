@@ -49,6 +49,19 @@ template <typename T> struct DevBuf {
         p = nullptr;
         n = 0;
     }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept
+    {
+        if (this != &o) {
+            free();
+            p = o.p; n = o.n;
+            o.p = nullptr; o.n = 0;
+        }
+        return *this;
+    }
     ~DevBuf() { free(); }
 };
 
@@ -59,8 +72,36 @@ struct CrGemm {                      /* C = C0 + C0b + s1 A1 B1 + s2 A2 B2      
     const double *C0, *C0b, *A1, *B1, *A2, *B2;
     double s1, s2;
 };
+/* one output block of a (composite) cyclic-reduction apply step: y = sum_t s_t A_t v_t
+ * (A_t null: identity); vectors and output addressed as (base, offset) with base 0 the
+ * solve's right-hand side b, 1 its solution x, 2 / 3 the internal level vectors bv / xv */
+constexpr int CR_MT = 8;
+struct CrOut {
+    int yb, nt;
+    int64_t yo;
+    double s[CR_MT];
+    const double* A[CR_MT];
+    int vb[CR_MT];
+    int64_t vo[CR_MT];
+};
+/* C = sum_k s_k A_k B_k (B_k null: s_k A_k; A_k null: s_k I), a composite operator */
+struct CrComp {
+    double* C;
+    int nt;
+    const double* A[4];
+    const double* B[4];
+    double s[4];
+};
+struct CrStep {                      /* one apply launch: its output descriptors         */
+    DevBuf<CrOut> d;
+    int nout = 0;
+};
 struct SchurCR {
     int n = 0, m = 0, periodic = 0, nlev = 0;
+    std::vector<CrStep> down, up;    /* apply steps above the tail: one or two levels each */
+    DevBuf<double> cmat;             /* composite operators                              */
+    DevBuf<CrComp> cdesc;            /* their products (set-up)                          */
+    int ncomp = 0;
     std::vector<int> N, per, merge;  /* blocks, periodic coupling, periodic pair merged   */
     std::vector<size_t> dlr_off;     /* level l: D, L, R blocks (3 N[l])                  */
     std::vector<size_t> ap_off;      /* level l: XL, XR (evens), Dinv, YL, YR (odds);      */

@@ -27,6 +27,8 @@
  * Every m x m block is stored column-major: a(r, c) at [r + c*m].
  */
 #include <algorithm>
+#include <map>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -424,6 +426,118 @@ __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv
     if (lane == 0) x[r] = v;
 }
 
+/* Apply step: one (output block, row chunk of CR_RC rows) per workgroup,
+ * y = sum_t s_t A_t v_t over up to CR_MT terms (the composite of two levels: 7 terms down,
+ * 4 up).  The term vectors are staged in LDS while the matrix rows are loaded into
+ * registers; per row the column groups' partial sums meet in LDS in a fixed order. */
+template <int CPT>
+__global__ void __launch_bounds__(256) k_cr_multi(const CrOut* __restrict__ outs, int m, int nch,
+                                                  const double* __restrict__ b, double* __restrict__ x,
+                                                  double* __restrict__ bv, double* __restrict__ xv)
+{
+    __shared__ double vs[CR_MT][CR_MAXM];
+    __shared__ double red[256];
+    const CrOut& o = outs[blockIdx.x / nch];
+    const int r0 = (blockIdx.x % nch) * CR_RC;
+    const int t = threadIdx.x, g = t / CR_RC, r = r0 + t % CR_RC;
+    const int nt = o.nt;
+    const double* base[4] = {b, x, bv, xv};
+    double a[CR_MT][CPT];
+#pragma unroll
+    for (int q = 0; q < CR_MT; q++)
+#pragma unroll
+        for (int u = 0; u < CPT; u++) {
+            const int c = g + CR_G * u;
+            a[q][u] = (q < nt && o.A[q] && r < m && c < m) ? o.A[q][r + (size_t)c * m] : 0.0;
+        }
+    for (int e = t; e < nt * m; e += 256) {
+        const int q = e / m, c = e - q * m;
+        vs[q][c] = base[o.vb[q]][o.vo[q] + c];
+    }
+    __syncthreads();
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < CR_MT; q++) {
+        if (q >= nt) break;
+        double p = 0.0;
+        if (o.A[q]) {
+#pragma unroll
+            for (int u = 0; u < CPT; u++) {
+                const int c = g + CR_G * u;
+                if (c < m) p += a[q][u] * vs[q][c];
+            }
+        } else if (g == 0 && r < m) {
+            p = vs[q][r];
+        }
+        acc += o.s[q] * p;
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (t < CR_RC && r < m) {
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < CR_G; q++) sum += red[q * CR_RC + t];
+        double* const ys[4] = {nullptr, x, bv, xv};
+        ys[o.yb][o.yo + r] = sum;
+    }
+}
+
+/* composite operators C = sum_k s_k A_k B_k: one 32x32 tile of one descriptor per workgroup */
+__global__ void __launch_bounds__(256) k_cr_comp(const CrComp* __restrict__ dd, int m)
+{
+    const CrComp d = dd[blockIdx.y];
+    const int T = (m + 31) / 32;
+    const int r0 = (blockIdx.x % T) * 32, c0 = (blockIdx.x / T) * 32;
+    const int t = threadIdx.x, tr = t & 31, tc = t >> 5;
+    __shared__ double As[32][33], Bs[32][33];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int term = 0; term < d.nt; term++) {
+        const double* A = d.A[term];
+        const double* B = d.B[term];
+        const double sc = d.s[term];
+        if (!A) {                                           /* identity */
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (r0 + tr == c0 + tc + 8 * q && r0 + tr < m) acc[q] += sc;
+            continue;
+        }
+        if (!B) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int rr = r0 + tr, cc = c0 + tc + 8 * q;
+                if (rr < m && cc < m) acc[q] += sc * A[rr + (size_t)cc * m];
+            }
+            continue;
+        }
+        double pa[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < m; k0 += 32) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int e = t + 256 * q;
+                const int rr = e & 31, kk = e >> 5;
+                As[kk][rr] = (r0 + rr < m && k0 + kk < m) ? A[(r0 + rr) + (size_t)(k0 + kk) * m] : 0.0;
+                const int kb = e & 31, cc = e >> 5;
+                Bs[cc][kb] = (k0 + kb < m && c0 + cc < m) ? B[(k0 + kb) + (size_t)(c0 + cc) * m] : 0.0;
+            }
+            __syncthreads();
+#pragma unroll 8
+            for (int kk = 0; kk < 32; kk++) {
+                const double av = As[kk][tr];
+#pragma unroll
+                for (int q = 0; q < 4; q++) pa[q] += av * Bs[tc + 8 * q][kk];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[q] += sc * pa[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int rr = r0 + tr, cc = c0 + tc + 8 * q;
+        if (rr < m && cc < m) d.C[rr + (size_t)cc * m] = acc[q];
+    }
+}
+
 }  // namespace
 
 /* one level down / up for nrhs right-hand sides (level vectors N[l] m apart) */
@@ -443,6 +557,228 @@ static void cr_up(const SchurCR& cr, int l, const double* bl, const double* xn, 
     hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch, nrhs), dim3(256), 0, s, bl, xn, xl, ap + (size_t)2 * ne * mm,
                        ap + (size_t)(2 * ne + no) * mm, ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch,
                        (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m);
+}
+
+/* ---- apply steps: the level operations as block expressions, composed two levels at a
+ * time.  A quantity (a block of a level vector) is a sum over leaves -- blocks of the
+ * right-hand sides b_l or solutions x_l of other levels -- of coefficient matrices, each a
+ * signed product of at most two level operators.  Composing level l with level l + 1 (the
+ * down step b_l -> b_{l+2}, the up step x_{l+2} -> x_l) halves the apply launches; the
+ * merged coefficients are materialised once per factorisation (k_cr_comp). */
+namespace {
+using Leaf = std::tuple<int, int, int>;          /* (0: b / 1: x, level, block) */
+struct Prod {
+    double s;
+    const double* A;                             /* null: identity */
+    const double* B;                             /* null: none     */
+};
+using Expr = std::map<Leaf, std::vector<Prod>>;
+
+struct CrLevel {                                 /* level l operators (cr.ap) */
+    const SchurCR& cr;
+    int l;
+    const double* op(int which, int idx) const
+    {
+        const size_t mm = (size_t)cr.m * cr.m;
+        const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
+        const double* ap = cr.ap.p + cr.ap_off[l];
+        switch (which) {
+        case 0: return ap + (size_t)idx * mm;                        /* XL_q */
+        case 1: return ap + (size_t)(ne + idx) * mm;                 /* XR_q */
+        case 2: return ap + (size_t)(2 * ne + idx) * mm;             /* Dinv_p */
+        case 3: return ap + (size_t)(2 * ne + no + idx) * mm;        /* YL_p */
+        default: return ap + (size_t)(2 * ne + 2 * no + idx) * mm;   /* YR_p */
+        }
+    }
+};
+
+/* b_{l+1}[q] over b_l (k_cr_fwd) */
+Expr fwd_expr(const SchurCR& cr, int l, int q)
+{
+    const CrLevel L{cr, l};
+    const int Nl = cr.N[l], per = cr.per[l], e = 2 * q;
+    const bool lex = e > 0 || per, rex = e + 1 < Nl || per;
+    const int lnb = e > 0 ? e - 1 : Nl - 1, rnb = (e + 1) % Nl;
+    Expr E;
+    E[Leaf{0, l, e}].push_back({1.0, nullptr, nullptr});
+    if (lex && (lnb & 1)) E[Leaf{0, l, lnb}].push_back({-1.0, L.op(0, q), nullptr});
+    if (rex && (rnb & 1)) E[Leaf{0, l, rnb}].push_back({-1.0, L.op(1, q), nullptr});
+    return E;
+}
+/* x_l[t] over x_{l+1} and b_l (k_cr_bwd; even blocks are copies) */
+Expr bwd_expr(const SchurCR& cr, int l, int t)
+{
+    Expr E;
+    if ((t & 1) == 0) {
+        E[Leaf{1, l + 1, t / 2}].push_back({1.0, nullptr, nullptr});
+        return E;
+    }
+    const CrLevel L{cr, l};
+    const int Nl = cr.N[l], per = cr.per[l], p = t / 2;
+    const bool rex = t + 1 < Nl || per;
+    const int rn = (t + 1) % Nl;
+    E[Leaf{0, l, t}].push_back({1.0, L.op(2, p), nullptr});
+    E[Leaf{1, l + 1, p}].push_back({-1.0, L.op(3, p), nullptr});
+    if (rex) E[Leaf{1, l + 1, rn / 2}].push_back({-1.0, L.op(4, p), nullptr});
+    return E;
+}
+/* dst += s M E  (E's coefficients single operators) */
+void add_mul(Expr& dst, double s, const double* M, const Expr& E)
+{
+    for (const auto& kv : E)
+        for (const Prod& p : kv.second) {
+            Prod q{s * p.s, p.A, nullptr};
+            if (M) {
+                if (p.A) { q.A = M; q.B = p.A; }
+                else q.A = M;
+            }
+            dst[kv.first].push_back(q);
+        }
+}
+/* E with every leaf of (kind, level) replaced by sub(block) */
+template <class F>
+Expr substitute(const Expr& E, int kind, int level, F sub)
+{
+    Expr R;
+    for (const auto& kv : E) {
+        if (std::get<0>(kv.first) != kind || std::get<1>(kv.first) != level) {
+            for (const Prod& p : kv.second) R[kv.first].push_back(p);
+            continue;
+        }
+        const Expr S = sub(std::get<2>(kv.first));
+        for (const Prod& p : kv.second) {
+            if (p.B) return Expr{};              /* not composable (never: single operators) */
+            add_mul(R, p.s, p.A, S);
+        }
+    }
+    return R;
+}
+struct OutSpec {
+    int kind, level, block;                      /* the output quantity */
+    Expr e;
+};
+}  // namespace
+
+/* the outputs of the apply step(s) for levels [l0, l0 + nl) (nl = 1 or 2), down or up */
+static std::vector<OutSpec> step_outputs(const SchurCR& cr, int l0, int nl, bool down)
+{
+    std::vector<OutSpec> out;
+    if (down) {
+        if (nl == 1) {
+            for (int q = 0; q < cr.N[l0 + 1]; q++) out.push_back({0, l0 + 1, q, fwd_expr(cr, l0, q)});
+            return out;
+        }
+        for (int r = 0; r < cr.N[l0 + 2]; r++)
+            out.push_back({0, l0 + 2, r, substitute(fwd_expr(cr, l0 + 1, r), 0, l0 + 1,
+                                                    [&](int q) { return fwd_expr(cr, l0, q); })});
+        for (int q = 1; q < cr.N[l0 + 1]; q += 2) out.push_back({0, l0 + 1, q, fwd_expr(cr, l0, q)});
+        return out;
+    }
+    if (nl == 1) {
+        for (int t = 0; t < cr.N[l0]; t++) out.push_back({1, l0, t, bwd_expr(cr, l0, t)});
+        return out;
+    }
+    for (int t = 0; t < cr.N[l0]; t++)
+        out.push_back({1, l0, t, substitute(bwd_expr(cr, l0, t), 1, l0 + 1,
+                                            [&](int q) { return bwd_expr(cr, l0 + 1, q); })});
+    return out;
+}
+
+/* apply steps (descriptors) and the composite operators they need; two levels per step
+ * where the composed step stays within CR_MT terms */
+static int cr_build_steps(iemic_ctx* c, SchurCR& cr)
+{
+    const int m = cr.m;
+    const size_t mm = (size_t)m * m;
+    const int le = cr.tM ? cr.lt : cr.nlev;
+    struct Plan { int l0, nl; std::vector<OutSpec> dn, up; };
+    std::vector<Plan> plan;
+    for (int l = 0; l < le;) {
+        Plan P{l, std::min(2, le - l), {}, {}};
+        P.dn = step_outputs(cr, l, P.nl, true);
+        P.up = step_outputs(cr, l, P.nl, false);
+        bool ok = true;
+        for (const auto* v : {&P.dn, &P.up})
+            for (const OutSpec& o : *v) {
+                ok &= (int)o.e.size() <= CR_MT;
+                for (const auto& kv : o.e) ok &= kv.second.size() <= 4;
+            }
+        if (!ok && P.nl == 2) {                  /* fall back to one level */
+            P.nl = 1;
+            P.dn = step_outputs(cr, l, 1, true);
+            P.up = step_outputs(cr, l, 1, false);
+        }
+        l += P.nl;
+        plan.push_back(std::move(P));
+    }
+    /* composite operators: coefficients that are not a single signed operator */
+    std::vector<CrComp> comps;
+    auto is_single = [](const std::vector<Prod>& v) { return v.size() == 1 && !v[0].B; };
+    for (const Plan& P : plan)
+        for (const auto* v : {&P.dn, &P.up})
+            for (const OutSpec& o : *v)
+                for (const auto& kv : o.e)
+                    if (!is_single(kv.second)) comps.push_back(CrComp{});
+    cr.ncomp = (int)comps.size();
+    if (cr.ncomp && (cr.cmat.alloc(comps.size() * mm) || cr.cdesc.alloc(comps.size()))) {
+        set_error("Schur cyclic reduction: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    auto vref = [&](int kind, int level, int block, int& base, int64_t& off) {
+        if (level == 0) { base = kind; off = (int64_t)block * m; }
+        else { base = 2 + kind; off = (int64_t)cr.v_off[level] + (int64_t)block * m; }
+    };
+    size_t ic = 0;
+    cr.down.clear();
+    cr.up.clear();
+    cr.down.resize(plan.size());
+    cr.up.resize(plan.size());
+    for (size_t ip = 0; ip < plan.size(); ip++) {
+        const Plan& P = plan[ip];
+        for (int dir = 0; dir < 2; dir++) {
+            const std::vector<OutSpec>& specs = dir == 0 ? P.dn : P.up;
+            std::vector<CrOut> outs;
+            for (const OutSpec& o : specs) {
+                CrOut d{};
+                vref(o.kind, o.level, o.block, d.yb, d.yo);
+                for (const auto& kv : o.e) {
+                    const int t = d.nt++;
+                    vref(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), d.vb[t], d.vo[t]);
+                    if (is_single(kv.second)) {
+                        d.s[t] = kv.second[0].s;
+                        d.A[t] = kv.second[0].A;
+                    } else {
+                        CrComp& cc = comps[ic];
+                        cc.C = cr.cmat.p + ic * mm;
+                        cc.nt = (int)kv.second.size();
+                        for (int k = 0; k < cc.nt; k++) {
+                            cc.A[k] = kv.second[k].A;
+                            cc.B[k] = kv.second[k].B;
+                            cc.s[k] = kv.second[k].s;
+                        }
+                        d.s[t] = 1.0;
+                        d.A[t] = cc.C;
+                        ic++;
+                    }
+                }
+                outs.push_back(d);
+            }
+            /* down steps top-first in plan order; up steps applied bottom-first (reverse) */
+            CrStep& st = dir == 0 ? cr.down[ip] : cr.up[plan.size() - 1 - ip];
+            st.nout = (int)outs.size();
+            int rc;
+            if (st.d.alloc(outs.size())) {
+                set_error("Schur cyclic reduction: out of device memory");
+                return IEMIC_ENOMEM;
+            }
+            if ((rc = h2d(c, st.d.p, outs.data(), sizeof(CrOut) * outs.size()))) return rc;
+        }
+    }
+    if (cr.ncomp) {
+        int rc;
+        if ((rc = h2d(c, cr.cdesc.p, comps.data(), sizeof(CrComp) * comps.size()))) return rc;
+    }
+    return 0;
 }
 
 /* level sizes, storage offsets and the GEMM descriptors (host, once per grid) */
@@ -571,7 +907,7 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
             return IEMIC_ENOMEM;
         }
     }
-    return 0;
+    return cr_build_steps(c, cr);
 }
 
 static int cr_inverse(hipStream_t s, int m, int count, const double* src, int s0, int sstep, double* dst,
@@ -630,6 +966,8 @@ int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
     }
     if ((rc = cr_inverse(s, m, 1, cr.dlr.p + cr.dlr_off[cr.nlev], 0, 1, cr.ap.p + cr.ap_off[cr.nlev], cr.info.p)))
         return rc;
+    if (cr.ncomp)                          /* the composite operators of the apply steps */
+        hipLaunchKernelGGL(k_cr_comp, dim3(T * T, cr.ncomp), dim3(256), 0, s, cr.cdesc.p, m);
     if (cr.tM) {                           /* the tail's inverse, column r = tail solve of e_r */
         const int M = cr.tM;
         auto tb = [&](int l) { return cr.tb.p + cr.tb_off[l - cr.lt]; };
@@ -657,22 +995,37 @@ int cr_check(iemic_ctx* c, SchurCR& cr)
     return 0;
 }
 
-/* x = S^-1 b (b, x: n*m, c = i*m + j): the levels above the tail one launch each way, the
- * tail (levels >= lt, tM = N[lt] m unknowns) one dense GEMV */
+/* x = S^-1 b (b, x: n*m, c = i*m + j): the levels above the tail in apply steps of one or
+ * two levels each way (k_cr_multi), the tail (levels >= lt, tM = N[lt] m unknowns) one
+ * dense GEMV */
+static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double* x, hipStream_t s)
+{
+    const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC;
+    const int need = (m + CR_G - 1) / CR_G;
+    const dim3 g((unsigned)(st.nout * nch));
+    double* bv = const_cast<double*>(cr.bv.p);
+    double* xv = const_cast<double*>(cr.xv.p);
+    if (need <= 3) hipLaunchKernelGGL(k_cr_multi<3>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+    else if (need <= 5) hipLaunchKernelGGL(k_cr_multi<5>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+    else if (need <= 8) hipLaunchKernelGGL(k_cr_multi<8>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+    else if (need <= 10) hipLaunchKernelGGL(k_cr_multi<10>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+    else hipLaunchKernelGGL(k_cr_multi<12>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+}
+
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)
 {
     (void)c;
     auto bvec = [&](int l) { return l == 0 ? b : cr.bv.p + cr.v_off[l]; };
     auto xvec = [&](int l) { return l == 0 ? x : cr.xv.p + cr.v_off[l]; };
     const int le = cr.tM ? cr.lt : cr.nlev;
-    for (int l = 0; l < le; l++) cr_down(cr, l, bvec(l), cr.bv.p + cr.v_off[l + 1], 1, s);
+    for (const CrStep& st : cr.down) cr_step(cr, st, b, x, s);
     if (cr.tM)
         hipLaunchKernelGGL(k_cr_tail, dim3((cr.tM + 3) / 4), dim3(256), 0, s, (const double*)cr.tinv.p, bvec(le),
                            xvec(le), cr.tM);
     else
         hipLaunchKernelGGL(k_cr_final, dim3((cr.m + CR_RC - 1) / CR_RC), dim3(256), 0, s,
                            (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), bvec(le), xvec(le), cr.m);
-    for (int l = le - 1; l >= 0; l--) cr_up(cr, l, bvec(l), xvec(l + 1), xvec(l), 1, s);
+    for (const CrStep& st : cr.up) cr_step(cr, st, b, x, s);
     HIP_OK(hipGetLastError());
     return 0;
 }
