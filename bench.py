@@ -4,13 +4,17 @@ One step = one full Newton step of the 2-degree global ocean (192x76x16, 1,400,8
 unknowns) on the GPU: residual F, Jacobian assembly, preconditioner
 set-up, FGMRES solve of J dx = -F to the relative tolerance 1e-8 (Belos semantics,
 Ocean.C:1060-1137), x += dx and the new residual (transient/Newton.H:92-99).  Every step
-restarts from the same synthetic state (splitmix64 seed 20261015, resident in HBM; the
-reset is a device-to-device copy inside the timed region).
+restarts from the same state, resident in HBM (the reset is a device-to-device copy inside
+the timed region): by default the near-solution branch state bench_data/<config>_cf05.npz
+(the 2-degree model continued from rest to Combined Forcing 0.5, scripts/branch_state.py),
+with --state synthetic SURVEY §8d's splitmix64 state (seed 20261015; a Newton step from it
+diverges).  The state is named in config["state"].
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): the same 2-degree problem is split
-into N latitude bands, one per GPU (halo exchange and Krylov reductions over RCCL,
-block-Jacobi coupling of the preconditioner across bands) -- strong
-scaling; the step time is the max over ranks.
+into N latitude bands, one per GPU (halo exchange and Krylov reductions over RCCL; the
+preconditioner's Schur problem and coarsest T/S level are global, the rest couples across
+band edges through halos) -- strong scaling; the step time is the max over
+ranks.
 
 Prints ONE JSON line (rank 0) with the metric, the SpMV roofline of the same run (HIP
 events on the library's stream) and the CPU baseline (the oracle port, rank 0, N=1).
@@ -311,6 +315,8 @@ def main():
                    "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
                    "schur": "cyclic reduction (fp64, exact)",
+                   "state": (f"branch (bench_data/{args.config}_cf05.npz, CF 0.5)" if state == "branch"
+                             else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
                    "parallelism": f"latitude-bands x{world}" if world > 1 else "single",
                    "band_rows": [lay["jb0"], lay["jb1"]]},

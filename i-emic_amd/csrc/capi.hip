@@ -272,13 +272,18 @@ extern "C" int iemic_create(iemic_ctx** out, const iemic_grid* grid, const int* 
     return iemic_create_dist(out, grid, landm, nullptr);
 }
 
-extern "C" void iemic_destroy(iemic_ctx* c)
+namespace iemic {
+void ctx_release(iemic_ctx* c)
 {
-    if (!c) return;
+    if (!c || --c->refs > 0) return;
     (void)hipSetDevice(c->device);
     comm_destroy(c);
     delete c; /* ~iemic_ctx drains the stream before any buffer is released */
 }
+}  // namespace iemic
+
+/* the context lives on while an atmosphere or coupled model built on it exists */
+extern "C" void iemic_destroy(iemic_ctx* c) { ctx_release(c); }
 
 #define CTX_CHECK(c)                                   \
     if (!(c)) return IEMIC_EINVAL;                     \
@@ -624,9 +629,12 @@ extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
 {
     CTX_CHECK(c);
     if (!c->jac_valid || nrep < 1) return IEMIC_ESTATE;
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
+    EventPair ev;
+    if (ev.create()) {
+        set_error("hipEventCreate failed");
+        return IEMIC_EDEVICE;
+    }
+    hipEvent_t e0 = ev.a, e1 = ev.b;
     int rc = spmv(c, c->d_x.p, c->d_tmp2.p, c->stream); /* warm, fills the halo */
     if (rc) return rc;
     HIP_OK(hipEventRecord(e0, c->stream));
@@ -639,8 +647,6 @@ extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     *ms_per_launch = ms / nrep;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     return 0;
 }
 
@@ -648,9 +654,12 @@ extern "C" int iemic_time_prec(iemic_ctx* c, int nrep, double* ms_per_apply, dou
 {
     CTX_CHECK(c);
     if (!c->gs.ready || nrep < 1 || !ms_per_apply || !host_ms_per_apply) return IEMIC_ESTATE;
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
+    EventPair ev;
+    if (ev.create()) {
+        set_error("hipEventCreate failed");
+        return IEMIC_EDEVICE;
+    }
+    hipEvent_t e0 = ev.a, e1 = ev.b;
     HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, c->stream));
     int rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);   /* warm */
     if (rc) return rc;
@@ -666,8 +675,6 @@ extern "C" int iemic_time_prec(iemic_ctx* c, int nrep, double* ms_per_apply, dou
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     *ms_per_apply = ms / nrep;
     *host_ms_per_apply = host / nrep;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     return 0;
 }
 
@@ -693,9 +700,12 @@ extern "C" int iemic_time_spmv_cold(iemic_ctx* c, int nrep, void* flush, int64_t
 {
     CTX_CHECK(c);
     if (!c->jac_valid || nrep < 1 || !flush || flush_bytes <= 0) return IEMIC_EINVAL;
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
+    EventPair ev;
+    if (ev.create()) {
+        set_error("hipEventCreate failed");
+        return IEMIC_EDEVICE;
+    }
+    hipEvent_t e0 = ev.a, e1 = ev.b;
     int rc = spmv(c, c->d_x.p, c->d_tmp2.p, c->stream);
     if (rc) return rc;
     double tot = 0.0;
@@ -711,7 +721,5 @@ extern "C" int iemic_time_spmv_cold(iemic_ctx* c, int nrep, void* flush, int64_t
         tot += ms;
     }
     *ms_per_launch = tot / nrep;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     return 0;
 }

@@ -223,6 +223,7 @@ struct iemic_ctx {
     iemic::DevBuf<double> d_part, d_hbuf;
     double* h_red = nullptr;
     int jac_valid = 0;
+    int refs = 1;                    /* the handle + dependents (atmosphere, coupled model) */
     iemic::BlockGS gs;
     iemic::Krylov kr;
     iemic::Geo geo() const;
@@ -249,6 +250,20 @@ inline int d2h(iemic_ctx* c, void* dst, const void* src, size_t bytes)
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
 }
+/* two timing events, destroyed on every return path */
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int create()
+    {
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return IEMIC_EDEVICE;
+        return 0;
+    }
+    ~EventPair()
+    {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
 /* Drains the stream when an entry point returns, also on error paths, so no kernel of
  * this context is still in flight when control goes back to the caller. */
 struct StreamGuard {
@@ -263,6 +278,9 @@ int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int rows_j);
 /* one halo row of two arrays laid out in whole rows of slab doubles, owned [first, first+count) */
 int halo_exchange_slab2(iemic_ctx* c, double* a, double* b, int64_t first, int64_t count, int64_t slab);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
+/* drop one reference to the context (iemic_destroy, a dependent's destroy); the last one
+ * frees it */
+void ctx_release(iemic_ctx* c);
 int comm_unique_id(unsigned char* id128);
 void* local_group_new(int nranks);
 void local_group_free(void* g);

@@ -50,6 +50,7 @@ struct AtmPar {
 
 struct iemic_atmos {
     iemic_ctx* oc = nullptr;             /* the ocean context: device, stream, surface mask  */
+    int refs = 1;                        /* the handle + coupled models built on it          */
     iemic_atmos_params prm{};
     int n = 0, m = 0, periodic = 0, dim = 0, rowint = 0, rowP = 0;
     AtmPar P{};
@@ -606,7 +607,8 @@ struct LinC {
     double c[16];
     const double* X[16];
 };
-__global__ void __launch_bounds__(256) k_clincomb(LinC L, double* __restrict__ y, int64_t N)
+/* y may also be one of the X (IDR's U(:,k) update): no __restrict__ */
+__global__ void __launch_bounds__(256) k_clincomb(LinC L, double* y, int64_t N)
 {
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x) {
         double acc = L.a == 0.0 ? 0.0 : L.a * y[q];
@@ -839,17 +841,24 @@ extern "C" int iemic_atmos_create(iemic_atmos** out, iemic_ctx* oc, const iemic_
     (void)hipMemsetAsync(a->d_x.p, 0, sizeof(double) * a->dim, oc->stream);
     (void)hipMemsetAsync(a->d_sst.p, 0, sizeof(double) * n * m, oc->stream);
     (void)hipStreamSynchronize(oc->stream);
+    oc->refs++;
     *out = a;
     return 0;
 }
 
-extern "C" void iemic_atmos_destroy(iemic_atmos* a)
+/* the atmosphere lives on while a coupled model built on it exists; its last reference
+ * releases the ocean context's */
+static void atmos_release(iemic_atmos* a)
 {
-    if (!a) return;
-    (void)hipSetDevice(a->oc->device);
-    (void)hipStreamSynchronize(a->oc->stream);
+    if (!a || --a->refs > 0) return;
+    iemic_ctx* oc = a->oc;
+    (void)hipSetDevice(oc->device);
+    (void)hipStreamSynchronize(oc->stream);
     delete a;
+    ctx_release(oc);
 }
+
+extern "C" void iemic_atmos_destroy(iemic_atmos* a) { atmos_release(a); }
 
 extern "C" int iemic_atmos_dim(const iemic_atmos* a) { return a ? a->dim : -1; }
 
@@ -1205,6 +1214,8 @@ extern "C" int iemic_coupled_create(iemic_coupled** out, iemic_ctx* oc, iemic_at
     for (DevBuf<double>* b : {&cm->xo, &cm->yo, &cm->ro, &cm->zo})
         (void)hipMemsetAsync(b->p, 0, sizeof(double) * b->n, oc->stream);
     (void)hipStreamSynchronize(oc->stream);
+    oc->refs++;
+    a->refs++;
     *out = cm;
     return 0;
 }
@@ -1212,9 +1223,13 @@ extern "C" int iemic_coupled_create(iemic_coupled** out, iemic_ctx* oc, iemic_at
 extern "C" void iemic_coupled_destroy(iemic_coupled* cm)
 {
     if (!cm) return;
-    (void)hipSetDevice(cm->oc->device);
-    (void)hipStreamSynchronize(cm->oc->stream);
+    iemic_ctx* oc = cm->oc;
+    iemic_atmos* a = cm->at;
+    (void)hipSetDevice(oc->device);
+    (void)hipStreamSynchronize(oc->stream);
     delete cm;
+    atmos_release(a);
+    ctx_release(oc);
 }
 
 extern "C" int iemic_coupled_synchronize(iemic_coupled* cm)

@@ -1,10 +1,12 @@
 /*
  * krylov.hip -- stencil-ELL SpMV and the flexible GMRES driver.
  *
- *  - k_spmv replaces Epetra_CrsMatrix::Apply (Ocean::applyMatrix, src/ocean/Ocean.C:1352-1357)
- *    on the maximal graph: one thread per cell computes its 6 rows from 104 slot-major
- *    values (coalesced) and implicit neighbour columns.  The dense integral-condition row
- *    (SRES = 0, THCM.C:2121-2198) is a separate fused dot.
+ *  - k_spmv7 replaces Epetra_CrsMatrix::Apply (Ocean::applyMatrix, src/ocean/Ocean.C:1352-1357)
+ *    on the maximal graph: one workgroup per 64-cell tile of a grid row stages the x values
+ *    of the tile's neighbourhood in LDS and four waves share the 104 slot-major coefficient
+ *    rows (read non-temporally); columns are implicit in the cell index and slot.  The dense
+ *    integral-condition row (SRES = 0, THCM.C:2121-2198) is a separate fused dot.
+ *  - k_spmv_dyn: the U/V/W/P rows only (the dynamics defect of the block GS).
  *  - fgmres restates Belos BlockGmresSolMgr as configured by Ocean::initializeBelos
  *    (Ocean.C:961-1020): flexible (right) preconditioning, x0 = 0, residual relative to
  *    ||b|| (the preconditioned initial residual for right preconditioning), classical
@@ -22,130 +24,9 @@
 namespace iemic {
 
 /* ---- SpMV ------------------------------------------------------------------------ */
+/* row R of one cell: slot-major coefficients (coalesced over adjacent cells) times the
+ * implicit-column gathers; rb / ii are the (dk, dj) row bases and the i offsets */
 template <int R>
-__device__ __forceinline__ double row_dot(const double* __restrict__ val, const double* __restrict__ x,
-                                          int64_t lc, int64_t nloc, const int64_t* nb)
-{
-    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
-    double acc = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const Slot sl = SLOTS[B + s];
-        const int o = (sl.dk + 1) * 9 + (sl.dj + 1) * 3 + (sl.di + 1);
-        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * nb[o] + sl.var];
-    }
-    return acc;
-}
-
-/* ext cell of the 27 neighbours of owned cell (i, j, k) (0-based, j global); outside the
- * domain -> the cell itself (those slots hold 0).  The j +- 1 rows of a band edge are
- * halo rows, filled by halo_exchange before the launch. */
-__device__ __forceinline__ void neighbours(int n, int m, int l, int periodic, int jb0, int i, int j,
-                                           int k, int64_t* nb)
-{
-    int ii[3], jj[3], kk[3];
-    ii[0] = i - 1; ii[1] = i; ii[2] = i + 1;
-    if (periodic) {
-        if (ii[0] < 0) ii[0] = n - 1;
-        if (ii[2] >= n) ii[2] = 0;
-    } else {
-        if (ii[0] < 0) ii[0] = i;
-        if (ii[2] >= n) ii[2] = i;
-    }
-    jj[0] = j > 0 ? j - 1 : j; jj[1] = j; jj[2] = j < m - 1 ? j + 1 : j;
-    kk[0] = k > 0 ? k - 1 : k; kk[1] = k; kk[2] = k < l - 1 ? k + 1 : k;
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++)
-#pragma unroll
-            for (int d = 0; d < 3; d++)
-                nb[a * 9 + b * 3 + d] = (((int64_t)jj[b] - jb0 + HALO) * l + kk[a]) * n + ii[d];
-}
-
-__global__ void __launch_bounds__(256) k_spmv(int n, int m, int l, int periodic, int jb0,
-                                              const double* __restrict__ val,
-                                              const double* __restrict__ x,
-                                              double* __restrict__ y, int64_t nloc)
-{
-    const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (lc >= nloc) return;
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
-    int64_t nb[27];
-    neighbours(n, m, l, periodic, jb0, i, j, k, nb);
-    double r0 = row_dot<UU>(val, x, lc, nloc, nb);
-    double r1 = row_dot<VV>(val, x, lc, nloc, nb);
-    double r2 = row_dot<WW>(val, x, lc, nloc, nb);
-    double r3 = row_dot<PP>(val, x, lc, nloc, nb);
-    double r4 = row_dot<TT>(val, x, lc, nloc, nb);
-    double r5 = row_dot<SS>(val, x, lc, nloc, nb);
-    double* yc = y + NUN * ((int64_t)HALO * l * n + lc);
-    yc[0] = r0; yc[1] = r1; yc[2] = r2; yc[3] = r3; yc[4] = r4; yc[5] = r5;
-}
-
-/* Two cells per thread (even n): the pair (lc, lc+1) shares its (j, k) row, so the slot
- * values load as one 16-B double2 per slot and the 27-point neighbourhoods overlap in
- * four i columns (i-1 .. i+2).  Blocks are dealt to the 8 XCDs in contiguous runs
- * (blockIdx b runs on XCD b % 8), so each XCD's L2 serves the x neighbourhood of one
- * contiguous slab of latitude rows instead of every XCD fetching all of x. */
-template <int R>
-__device__ __forceinline__ void row_dot2(const double* __restrict__ val, const double* __restrict__ x,
-                                         int64_t lc, int64_t nloc, const int* rb, const int* iu,
-                                         double& a0, double& a1)
-{
-    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
-    double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const Slot sl = SLOTS[B + s];
-        const int r = rb[(sl.dk + 1) * 3 + (sl.dj + 1)];
-        const double2 v = *reinterpret_cast<const double2*>(val + (int64_t)(B + s) * nloc + lc);
-        s0 += v.x * x[NUN * (int64_t)(r + iu[sl.di + 1]) + sl.var];
-        s1 += v.y * x[NUN * (int64_t)(r + iu[sl.di + 2]) + sl.var];
-    }
-    a0 = s0;
-    a1 = s1;
-}
-
-__global__ void __launch_bounds__(256) k_spmv2(int n, int m, int l, int periodic, int jb0,
-                                               const double* __restrict__ val,
-                                               const double* __restrict__ x,
-                                               double* __restrict__ y, int64_t nloc, int nblk)
-{
-    const int per = (nblk + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile >= nblk) return;
-    const int64_t lc = 2 * ((int64_t)tile * blockDim.x + threadIdx.x);
-    if (lc >= nloc) return;
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
-    int iu[4] = {i - 1, i, i + 1, i + 2};
-    if (iu[0] < 0) iu[0] = periodic ? n - 1 : 0;
-    if (iu[3] >= n) iu[3] = periodic ? 0 : n - 1;
-    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
-    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
-    int rb[9];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
-    double r[12];
-    row_dot2<UU>(val, x, lc, nloc, rb, iu, r[0], r[6]);
-    row_dot2<VV>(val, x, lc, nloc, rb, iu, r[1], r[7]);
-    row_dot2<WW>(val, x, lc, nloc, rb, iu, r[2], r[8]);
-    row_dot2<PP>(val, x, lc, nloc, rb, iu, r[3], r[9]);
-    row_dot2<TT>(val, x, lc, nloc, rb, iu, r[4], r[10]);
-    row_dot2<SS>(val, x, lc, nloc, rb, iu, r[5], r[11]);
-    double2* yc = reinterpret_cast<double2*>(y + NUN * ((int64_t)HALO * l * n + lc));
-#pragma unroll
-    for (int q = 0; q < 6; q++) yc[q] = make_double2(r[2 * q], r[2 * q + 1]);
-}
-
-/* One wavefront per (64 cells, equation): a 384-thread block covers 64 consecutive cells
- * and wave R computes their row R (U, V, W, P, T, S).  Loads stay coalesced (lanes read
- * adjacent cells of one slot), the per-lane work is one row (7-24 slots), and the grid
- * has 6x more wavefronts than a thread-per-cell launch, enough to keep HBM busy at the
- * 2-degree size (233k cells per GPU).  Blocks are dealt to the XCDs in contiguous runs. */
-template <int R, bool NT = false>
 __device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, const double* __restrict__ x,
                                              int64_t lc, int64_t nloc, const int* rb, const int* ii)
 {
@@ -155,46 +36,10 @@ __device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, con
     for (int s = 0; s < NS; s++) {
         const Slot sl = SLOTS[B + s];
         const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
-        const double* vp = val + (int64_t)(B + s) * nloc + lc;
-        acc += (NT ? __builtin_nontemporal_load(vp) : *vp) * x[NUN * (int64_t)cidx + sl.var];
+        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * (int64_t)cidx + sl.var];
     }
     return acc;
 }
-
-__global__ void __launch_bounds__(384) k_spmv6(int n, int m, int l, int periodic, int jb0,
-                                               const double* __restrict__ val,
-                                               const double* __restrict__ x,
-                                               double* __restrict__ y, int64_t nloc, int nblk)
-{
-    const int per = (nblk + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile >= nblk) return;
-    const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
-    if (lc >= nloc) return;
-    const int R = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
-    int ii[3] = {i - 1, i, i + 1};
-    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
-    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
-    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
-    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
-    int rb[9];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
-    double acc;
-    switch (R) {
-    case UU: acc = row_dot_rb<UU>(val, x, lc, nloc, rb, ii); break;
-    case VV: acc = row_dot_rb<VV>(val, x, lc, nloc, rb, ii); break;
-    case WW: acc = row_dot_rb<WW>(val, x, lc, nloc, rb, ii); break;
-    case PP: acc = row_dot_rb<PP>(val, x, lc, nloc, rb, ii); break;
-    case TT: acc = row_dot_rb<TT>(val, x, lc, nloc, rb, ii); break;
-    default: acc = row_dot_rb<SS>(val, x, lc, nloc, rb, ii); break;
-    }
-    y[NUN * ((int64_t)HALO * l * n + lc) + R] = acc;
-}
-
 
 /* ---- k_spmv7: LDS-staged x, slot-balanced waves ----------------------------------------
  * One workgroup (4 waves) per tile of up to 64 cells along i of one (j, k) grid row.  The
@@ -213,14 +58,15 @@ __host__ __device__ constexpr int sp7_combo(int dj, int dk)
 {
     return dk == 0 ? (dj + 1) : (dk == -1 ? (dj == 0 ? 3 : 5) : 4);  /* (-1,0)0 (0,0)1 (1,0)2 (0,-1)3 (0,1)4 (1,-1)5 */
 }
-template <int S0, int S1, bool NT = false>
+/* the coefficient stream is read once per SpMV: non-temporal loads (in-solve 43.4 us vs
+ * 45.9 us with the default policy at 2 degrees) */
+template <int S0, int S1>
 __device__ __forceinline__ void sp7_load(const double* __restrict__ val, int64_t nloc, int64_t lc, bool act,
                                          double* v)
 {
 #pragma unroll
     for (int s = S0; s < S1; s++)
-        v[s - S0] = !act ? 0.0 : NT ? __builtin_nontemporal_load(val + (int64_t)s * nloc + lc)
-                                    : val[(int64_t)s * nloc + lc];
+        v[s - S0] = !act ? 0.0 : __builtin_nontemporal_load(val + (int64_t)s * nloc + lc);
 }
 template <int S0, int S1>
 __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, int c, double* acc)
@@ -232,7 +78,6 @@ __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, i
         acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
     }
 }
-template <bool NT>
 __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic, int jb0,
                                                const double* __restrict__ val,
                                                const double* __restrict__ x,
@@ -269,10 +114,10 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
     double acc[3] = {0.0, 0.0, 0.0};
     double v[26];
     /* the coefficient loads are issued before the barrier, overlapping the x staging */
-    if (g == 0) sp7_load<0, 26, NT>(val, nloc, lc, act, v);
-    else if (g == 1) sp7_load<26, 52, NT>(val, nloc, lc, act, v);
-    else if (g == 2) sp7_load<52, 78, NT>(val, nloc, lc, act, v);
-    else sp7_load<78, 104, NT>(val, nloc, lc, act, v);
+    if (g == 0) sp7_load<0, 26>(val, nloc, lc, act, v);
+    else if (g == 1) sp7_load<26, 52>(val, nloc, lc, act, v);
+    else if (g == 2) sp7_load<52, 78>(val, nloc, lc, act, v);
+    else sp7_load<78, 104>(val, nloc, lc, act, v);
     __syncthreads();
     if (g == 0) sp7_compute<0, 26>(v, xs, c, acc);
     else if (g == 1) sp7_compute<26, 52>(v, xs, c, acc);
@@ -298,76 +143,10 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
 }
 
 
-/* the dynamics defect (see k_spmv_dyn below) with k_spmv7's LDS staging: the U/V/W/P rows
- * only (slots 0..63), four 16-slot waves (U | U+V | V+W | W+P) */
-__global__ void __launch_bounds__(256) k_spmv7_dyn(int n, int m, int l, int periodic, int jb0,
-                                                   const double* __restrict__ val,
-                                                   const double* __restrict__ z,
-                                                   const double* __restrict__ r,
-                                                   const uint8_t* __restrict__ known,
-                                                   double* __restrict__ d, int nloc, int ntile, int tpr)
-{
-    __shared__ double xs[6 * (SP7_T + 2) * NUN];
-    __shared__ double red[4][2][SP7_T];
-    const int per = (ntile + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile >= ntile) return;
-    const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
-    const int k = row % l, jl = row / l, j = jb0 + jl;
-    const int nc = min(SP7_T, n - i0);
-    const int lc0 = row * n + i0;
-    const int t = threadIdx.x, c = t & 63, g = t >> 6;
-    {
-        const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
-        const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
-        const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
-        const int il = i0 > 0 ? i0 - 1 : (periodic ? n - 1 : 0);
-        const int ir = i0 + nc < n ? i0 + nc : (periodic ? 0 : n - 1);
-        const int per_row = (nc + 2) * NUN;
-        for (int e = t; e < 6 * per_row; e += 256) {
-            const int q = e / per_row, w = e - q * per_row;
-            const int p = w / NUN, var = w - p * NUN;
-            const int i = p == 0 ? il : (p == nc + 1 ? ir : i0 + p - 1);
-            const int64_t cell = ((int64_t)(rj[q] - jb0 + HALO) * l + rk[q]) * n + i;
-            xs[(q * (SP7_T + 2) + p) * NUN + var] = z[NUN * cell + var];
-        }
-    }
-    const bool act = c < nc;
-    const int64_t lc = lc0 + c;
-    double acc[3] = {0.0, 0.0, 0.0};
-    double v[16];
-    if (g == 0) sp7_load<0, 16>(val, nloc, lc, act, v);
-    else if (g == 1) sp7_load<16, 32>(val, nloc, lc, act, v);
-    else if (g == 2) sp7_load<32, 48>(val, nloc, lc, act, v);
-    else sp7_load<48, 64>(val, nloc, lc, act, v);
-    __syncthreads();
-    if (g == 0) sp7_compute<0, 16>(v, xs, c, acc);
-    else if (g == 1) sp7_compute<16, 32>(v, xs, c, acc);
-    else if (g == 2) sp7_compute<32, 48>(v, xs, c, acc);
-    else sp7_compute<48, 64>(v, xs, c, acc);
-    red[g][0][c] = acc[0];
-    red[g][1][c] = acc[1];
-    __syncthreads();
-    /* g0 {U} g1 {U,V} g2 {V,W} g3 {W,P} */
-    for (int o = t; o < nc * 4; o += 256) {
-        const int cc = o >> 2, R = o & 3;
-        double a;
-        switch (R) {
-        case 0: a = red[0][0][cc] + red[1][0][cc]; break;
-        case 1: a = red[1][1][cc] + red[2][0][cc]; break;
-        case 2: a = red[2][1][cc] + red[3][0][cc]; break;
-        default: a = red[3][1][cc]; break;
-        }
-        const int64_t rw = NUN * ((int64_t)HALO * l * n + lc0 + cc) + R;
-        d[rw] = known[rw] ? 0.0 : r[rw] - a;
-    }
-}
-
 /* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
  * full rows of the SpMV are used: one wavefront per (64 cells, dynamics equation). */
-template <bool NT>
 __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int periodic, int jb0,
                                                   const double* __restrict__ val,
                                                   const double* __restrict__ z,
@@ -399,36 +178,20 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int perio
     }
     double acc;
     switch (R) {
-    case UU: acc = row_dot_rb<UU, NT>(val, z, lc, nloc, rb, ii); break;
-    case VV: acc = row_dot_rb<VV, NT>(val, z, lc, nloc, rb, ii); break;
-    case WW: acc = row_dot_rb<WW, NT>(val, z, lc, nloc, rb, ii); break;
-    default: acc = row_dot_rb<PP, NT>(val, z, lc, nloc, rb, ii); break;
+    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, rb, ii); break;
+    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, rb, ii); break;
+    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, rb, ii); break;
+    default: acc = row_dot_rb<PP>(val, z, lc, nloc, rb, ii); break;
     }
     d[row] = r[row] - acc;
 }
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d)
 {
-    static const int variant = [] {
-        const char* e = getenv("IEMIC_SPMV_DYN");
-        return e ? atoi(e) : 6;      /* measured in-solve: 29.6 us (6) vs 35.5 us (7) at 2 degrees */
-    }();
-    if (variant == 7 && c->nloc < INT32_MAX) {
-        const int tpr = (c->n + SP7_T - 1) / SP7_T;
-        const int ntile = (int)(c->nloc / c->n) * tpr;
-        const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-        hipLaunchKernelGGL(k_spmv7_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l, c->cfg.periodic,
-                           c->jb0, c->d_val.p, z, r, known, d, (int)c->nloc, ntile, tpr);
-        return 0;
-    }
     const int nblk = (int)((c->nloc + 63) / 64);
     const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-    if (variant == 8)          /* 8: the coefficient stream read non-temporally */
-        hipLaunchKernelGGL(k_spmv_dyn<true>, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
-                           c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
-    else
-        hipLaunchKernelGGL(k_spmv_dyn<false>, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l,
-                           c->cfg.periodic, c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
+    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l, c->cfg.periodic,
+                       c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
     return 0;
 }
 
@@ -447,20 +210,22 @@ __device__ __forceinline__ double block_sum(double v, double* sm)
 }
 
 /* partial[i * gridDim.x + blk] = sum over the block's range of V_i . w, i < nvec;
- * with extra != null, row i == nvec is extra . w (the norm of w in the same launch) */
+ * with extra != null, row i == nvec is extra . w (or extra . extra_w) in the same launch */
 __global__ void __launch_bounds__(256) k_mdot(const double* __restrict__ V, int64_t ldv, int nvec,
                                               const double* __restrict__ w, int64_t N,
                                               double* __restrict__ partial,
-                                              const double* __restrict__ extra = nullptr)
+                                              const double* __restrict__ extra = nullptr,
+                                              const double* __restrict__ extra_w = nullptr)
 {
     __shared__ double sm[8];
     const int i = blockIdx.y;
     if (i > nvec || (i == nvec && !extra)) return;
     const double* vi = i == nvec ? extra : V + (int64_t)i * ldv;
+    const double* wi = (i == nvec && extra_w) ? extra_w : w;
     double s = 0.0;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
          q += (int64_t)gridDim.x * blockDim.x)
-        s += vi[q] * w[q];
+        s += vi[q] * wi[q];
     double t = block_sum(s, sm);
     if (threadIdx.x == 0) partial[(int64_t)i * gridDim.x + blockIdx.x] = t;
 }
@@ -683,35 +448,15 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
         return IEMIC_ESTATE;
     }
     hipStream_t s = c->stream;
-    static const int variant = [] {
-        const char* e = getenv("IEMIC_SPMV");
-        return e ? atoi(e) : 8;       /* 8: in-solve 43.4 us vs 45.9 us (7) at 2 degrees */
-    }();
-    if ((variant == 7 || variant == 8) && c->nloc < INT32_MAX) {
-        /* 8: the coefficient stream read non-temporally */
-        const int tpr = (c->n + SP7_T - 1) / SP7_T;
-        const int ntile = (int)(c->nloc / c->n) * tpr;
-        const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-        if (variant == 8)
-            hipLaunchKernelGGL(k_spmv7<true>, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
-                               c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
-        else
-            hipLaunchKernelGGL(k_spmv7<false>, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
-                               c->jb0, c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
-    } else if (variant == 6 || variant == 7) {
-        const int nblk = (int)((c->nloc + 63) / 64);
-        const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-        hipLaunchKernelGGL(k_spmv6, dim3(grid), dim3(384), 0, s, c->n, c->m, c->l, c->cfg.periodic,
-                           c->jb0, c->d_val.p, x, y, c->nloc, nblk);
-    } else if (variant == 2 && (c->n & 1) == 0 && c->n >= 4) {
-        const int nblk = (int)((c->nloc / 2 + 255) / 256);
-        const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-        hipLaunchKernelGGL(k_spmv2, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic,
-                           c->jb0, c->d_val.p, x, y, c->nloc, nblk);
-    } else {
-        hipLaunchKernelGGL(k_spmv, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, s, c->n,
-                           c->m, c->l, c->cfg.periodic, c->jb0, c->d_val.p, x, y, c->nloc);
+    if (c->nloc >= INT32_MAX) {
+        set_error("spmv: more than 2^31 cells per rank");
+        return IEMIC_EINVAL;
     }
+    const int tpr = (c->n + SP7_T - 1) / SP7_T;
+    const int ntile = (int)(c->nloc / c->n) * tpr;
+    const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
+    hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic, c->jb0,
+                       c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
     if (c->su.rowintcon_ref >= 0) {
         /* dense intcond row: y[rowintcon] = intSign * coeff . x (summed over the ranks) */
         const int64_t o = NUN * c->own0;
@@ -736,22 +481,24 @@ int spmv(iemic_ctx* c, double* x, double* y, hipStream_t)
     return spmv_kernel(c, x, y);
 }
 
-/* dot products of nvec vectors V_i (stride ldv) with w; result on host in out[] */
-/* V, w point at the first owned row; length nlrows; sums over the ranks */
+/* dot products of nvec vectors V_i (stride ldv) with w, and (ea != null) ea . eb as
+ * out[nvec], in one launch pair and one host synchronisation */
+/* V, w, ea, eb point at the first owned row; length nlrows; sums over the ranks */
 static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const double* w,
-                     double* out)
+                     double* out, const double* ea = nullptr, const double* eb = nullptr)
 {
     const int64_t N = c->nlrows;
-    hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nvec), dim3(256), 0, c->stream, V, ldv, nvec, w, N,
-                       c->d_part.p);
-    hipLaunchKernelGGL(k_mdot_final, dim3(nvec), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS,
-                       nvec, c->d_hbuf.p);
-    int rc = allreduce_sum(c, c->d_hbuf.p, nvec);
+    const int nout = nvec + (ea ? 1 : 0);
+    hipLaunchKernelGGL(k_mdot, dim3(RED_BLOCKS, nout), dim3(256), 0, c->stream, V, ldv, nvec, w, N,
+                       c->d_part.p, ea, eb);
+    hipLaunchKernelGGL(k_mdot_final, dim3(nout), dim3(256), 0, c->stream, c->d_part.p, RED_BLOCKS,
+                       nout, c->d_hbuf.p);
+    int rc = allreduce_sum(c, c->d_hbuf.p, nout);
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * nvec, hipMemcpyDeviceToHost,
+    HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * nout, hipMemcpyDeviceToHost,
                           c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < nvec; i++) out[i] = c->h_red[i];
+    for (int i = 0; i < nout; i++) out[i] = c->h_red[i];
     return 0;
 }
 
@@ -1113,7 +860,8 @@ struct LinComb {
     double c[16];
     const double* X[16];
 };
-__global__ void __launch_bounds__(256) k_lincomb(LinComb L, double* __restrict__ y, int64_t N)
+/* y may also be one of the X (the IDR update of U(:,k) reads U(:,k)): no __restrict__ */
+__global__ void __launch_bounds__(256) k_lincomb(LinComb L, double* y, int64_t N)
 {
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
          q += (int64_t)gridDim.x * blockDim.x) {
@@ -1236,20 +984,35 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
         HIP_OK(hipEventRecord(e1, c->stream));
         return r2;
     };
+    /* one host synchronisation per inner step: the multi-dot after the matvec also returns
+     * r.r of the previous update, whose convergence check therefore comes one matvec late
+     * (wasted only on the final step: the pending step's updates are not applied) */
     auto matvec = [&](double* in, double* out) -> int {
         int r2 = spmv(c, in, out, c->stream);
         HIP_OK(hipEventRecord(e2, c->stream));
-        HIP_OK(hipEventSynchronize(e2));
+        return r2;
+    };
+    auto times = [&]() {                          /* after a synchronisation: e2 is done */
         float a1 = 0.f, a2 = 0.f;
         (void)hipEventElapsedTime(&a1, e0, e1);
         (void)hipEventElapsedTime(&a2, e1, e2);
         inf.t_prec_ms += a1;
         inf.t_spmv_ms += a2;
         inf.n_spmv++;
-        return r2;
     };
-    while (normr > tolb && iter < maxit) {
-        if ((rc = mdot_host(c, P + o, NE, s, r + o, f.data()))) return rc;      /* f = P' r */
+    auto set_normr = [&](double rr) -> int {
+        normr = sqrt0(rr);
+        return std::isfinite(normr) ? 0 : nonfinite();
+    };
+    bool done = false;
+    while (!done && iter < maxit) {
+        {
+            std::vector<double> fr(s + 1);
+            if ((rc = mdot_host(c, P + o, NE, s, r + o, fr.data(), r + o, r + o))) return rc;  /* f = P' r */
+            for (int k = 0; k < s; k++) f[k] = fr[k];
+            if ((rc = set_normr(fr[s]))) return rc;
+            if (normr <= tolb) break;
+        }
         for (int k = 0; k < s; k++) {
             if (jj > 0) {
                 /* gamma from the lower-triangular M(k:s, k:s); v = r - G(:, k:s) gamma */
@@ -1277,8 +1040,17 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
             }
             if ((rc = matvec(Ui(k), Gi(k)))) return rc;                          /* G(:,k) = A U(:,k) */
             /* bi-orthogonalise against P(:, 0:k) (the modified Gram-Schmidt of the reference
-             * restated as one multi-dot + forward substitution) and the new column of M */
-            if ((rc = mdot_host(c, P + o, NE, s, Gi(k) + o, d.data()))) return rc;
+             * restated as one multi-dot + forward substitution) and the new column of M; the
+             * same launch returns r.r after the previous step's update */
+            if ((rc = mdot_host(c, P + o, NE, s, Gi(k) + o, d.data(), r + o, r + o))) return rc;
+            times();
+            if (k > 0) {
+                if ((rc = set_normr(d[s]))) return rc;
+                if (normr <= tolb) {
+                    done = true;
+                    break;
+                }
+            }
             std::vector<double> al(k, 0.0);
             for (int i = 0; i < k; i++) {
                 double a = d[i];
@@ -1305,20 +1077,24 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
             const double beta = f[k] / M[k][k];
             lincomb(c, 1.0, r, {{-beta, Gi(k)}}, o, NL);                         /* r -= beta G */
             lincomb(c, 1.0, x, {{beta, Ui(k)}}, o, NL);                          /* x += beta U */
-            normr = sqrt0(dot(c, r, r, 0));
-            if (!std::isfinite(normr)) return nonfinite();
-            if (opt->idr_replace && normr > tolb / mp) trueres = true;
+            if (opt->idr_replace) {
+                if ((rc = set_normr(dot(c, r, r, 0)))) return rc;
+                if (normr > tolb / mp) trueres = true;
+            }
             for (int i = k + 1; i < s; i++) f[i] -= beta * M[i][k];
             iter++;
-            if (normr < tolb || iter >= maxit) break;
+            if (iter >= maxit) break;
         }
-        if (normr < tolb || iter >= maxit) break;
+        if (done || iter >= maxit) break;
         jj++;
         /* first residual of G_{j+1}: v = M^-1 r, t = A v, omega, r -= om t, x += om v */
         if ((rc = prec(r, v))) return rc;
         if ((rc = matvec(v, t))) return rc;
-        double tt_tr[2];
-        if ((rc = mdot_host(c, t + o, NE, 2, t + o, tt_tr))) return rc;       /* t.t, r.t */
+        double tt_tr[3];
+        if ((rc = mdot_host(c, t + o, NE, 2, t + o, tt_tr, r + o, r + o))) return rc;   /* t.t, r.t, r.r */
+        times();
+        if ((rc = set_normr(tt_tr[2]))) return rc;
+        if (normr <= tolb) break;
         const double nt = sqrt0(tt_tr[0]), ts = tt_tr[1];
         if (!(nt > 0.0) || !std::isfinite(ts)) return nonfinite();
         const double rho = std::fabs(ts / (nt * normr));
@@ -1326,19 +1102,20 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
         if (rho < angle) om = om * angle / rho;                                 /* calc_omega */
         lincomb(c, 1.0, r, {{-om, t}}, o, NL);
         lincomb(c, 1.0, x, {{om, v}}, o, NL);
-        normr = sqrt0(dot(c, r, r, 0));
-        if (!std::isfinite(normr)) return nonfinite();
-        if (opt->idr_replace && normr > tolb / mp) trueres = true;
-        if (trueres && normr < normb) {
-            /* residual replacement: r = b - A x */
-            if ((rc = spmv(c, x, r, c->stream))) return rc;
-            hipLaunchKernelGGL(k_axpby, dim3(GR), dim3(256), 0, c->stream, 1.0, b + o, -1.0, r + o, r + o, NL);
-            normr = sqrt0(dot(c, r, r, 0));
-            trueres = false;
-            inf.reorth++;
+        if (opt->idr_replace) {
+            if ((rc = set_normr(dot(c, r, r, 0)))) return rc;
+            if (normr > tolb / mp) trueres = true;
+            if (trueres && normr < normb) {
+                /* residual replacement: r = b - A x */
+                if ((rc = spmv(c, x, r, c->stream))) return rc;
+                hipLaunchKernelGGL(k_axpby, dim3(GR), dim3(256), 0, c->stream, 1.0, b + o, -1.0, r + o, r + o, NL);
+                trueres = false;
+                inf.reorth++;
+            }
         }
         iter++;
     }
+    if (!done && (rc = set_normr(dot(c, r, r, 0)))) return rc;                  /* the final r */
     /* explicit residual */
     if ((rc = spmv(c, x, t, c->stream))) return rc;
     hipLaunchKernelGGL(k_axpby, dim3(GR), dim3(256), 0, c->stream, 1.0, b + o, -1.0, t + o, t + o, NL);

@@ -158,11 +158,15 @@ class Ocean {
     iemic_krylov& solverParameters() { return krylov_; }
     const iemic_solve_info& lastSolve() const { return lastSolve_; }
 
-    /* device-resident Newton step (transient/Newton.H:92-99 shape) */
+    /* device-resident Newton step (transient/Newton.H:92-99 shape).  The update is applied
+     * even when the linear solve missed its tolerance (IEMIC_ENOCONV, a warning), as the
+     * reference's Newton / Continuation go on with the unconverged correction unless
+     * rejectFailedNewton is set: the caller reads info.solve.converged.  Errors throw. */
     iemic_newton_info newtonStep()
     {
         iemic_newton_info info{};
-        check(iemic_newton_step(ctx_, &krylov_, &info), "newtonStep");
+        const int rc = iemic_newton_step(ctx_, &krylov_, &info);
+        if (rc != IEMIC_ENOCONV) check(rc, "newtonStep");
         return info;
     }
 

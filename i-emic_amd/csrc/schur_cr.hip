@@ -880,13 +880,10 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
         return IEMIC_ENOMEM;
     }
     if (!g.empty() && (rc = h2d(c, cr.gd.p, g.data(), sizeof(CrGemm) * g.size()))) return rc;
-    /* dense tail: the first level of at most IEMIC_CR_TAIL (default 1024) unknowns and its
+    /* dense tail: the first level of at most 1024 unknowns (2048: no gain) and its
      * descendants become one explicit inverse (built at set-up by solving the tail for the
      * identity), so the apply spends one GEMV launch instead of 2 (nlev - lt) + 1 */
-    static const int tail_max = [] {
-        const char* e = getenv("IEMIC_CR_TAIL");
-        return std::min(e ? atoi(e) : 1024, CR_TAIL_MAX);
-    }();
+    constexpr int tail_max = 1024;
     cr.lt = cr.nlev;
     cr.tM = 0;
     for (int l = 0; l < cr.nlev; l++)

@@ -881,7 +881,14 @@ HD void boundaries_row(const Geo& g, const CellCtx& c, double* A, bool& frc_zero
  * the device mixing matches the reference's Fortran bit for bit: its forward-difference
  * Jacobian (mix_imp.f:729-815, eps = 1e-8) would amplify a last-bit difference of tanh by
  * 1/eps.  Checked bitwise against the host libm over 1.3e7 arguments in [2^-60, 2^7]
- * (tests/test_mixing.py).  Needs -ffp-contract=off like the rest of this header. */
+ * (tests/test_mixing.py).  Needs -ffp-contract=off like the rest of this header.
+ *
+ * libm_expm1 / libm_tanh below follow fdlibm's s_expm1.c / s_tanh.c (as carried by glibc),
+ * whose notice is preserved here:
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this software is freely granted,
+ *   provided that this notice is preserved. */
 HD int64_t f64_bits(double x)
 {
     int64_t u;

@@ -315,10 +315,12 @@ class CoupledModel:
         check(lib().iemic_coupled_spmv(self._h, ptr(x), ptr(y)), "iemic_coupled_spmv")
         return y
 
-    def newtonStep(self) -> dict:
+    def newtonStep(self, allow_unconverged: bool = False) -> dict:
         """One Newton iteration of the coupled model as the reference's Newton /
         Continuation drives it (src/newton/Newton.H:76-123): F(x), J(x), solve J dx = -F,
-        x += dx, F(x + dx).  Returns the residual norms and the solve record."""
+        x += dx, F(x + dx).  Returns the residual norms and the solve record.  The update
+        is applied either way; a solve that missed its tolerance raises IemicError (as
+        Ocean.newtonStep does) unless allow_unconverged."""
         F0 = self.computeRHS()
         self.computeJacobian()
         dx = self.solve(-F0)
@@ -327,6 +329,13 @@ class CoupledModel:
         self.ocean.setState(xo)
         self.atmos.setState(xa)
         F1 = self.computeRHS()
+        if not self.last_solve.converged and not allow_unconverged:
+            sp = self.solver_params
+            method = (f"IDR({int(sp.get('IDR s', 4))})" if str(sp.get("Solver", "FGMRES")).upper() == "IDR"
+                      else "FGMRES")
+            raise _lib.IemicError(
+                f"coupled Newton step: {method} did not converge ({self.last_solve.iters} steps, "
+                f"relative residual {self.last_solve.explicit_rel_res:.3e}); the update was applied")
         return dict(norm_f0=float(np.linalg.norm(F0)), norm_f1=float(np.linalg.norm(F1)),
                     iters=int(self.last_solve.iters), converged=bool(self.last_solve.converged),
                     explicit_rel_res=float(self.last_solve.explicit_rel_res))

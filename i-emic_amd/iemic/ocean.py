@@ -290,8 +290,9 @@ class Ocean:
         if rc == _lib.IEMIC_ENOCONV and allow_unconverged:
             rc = 0
         if rc == _lib.IEMIC_ENOCONV:
+            method = f"IDR({k.idr_s})" if k.method == 1 else "FGMRES"
             raise _lib.IemicError(
-                f"iemic_newton_step: FGMRES did not converge ({info.solve.iters} steps, "
+                f"iemic_newton_step: {method} did not converge ({info.solve.iters} steps, "
                 f"relative residual {info.solve.explicit_rel_res:.3e})")
         check(rc, "iemic_newton_step")
         return info

@@ -133,6 +133,8 @@ void* iemic_local_group_new(int nranks);
 void  iemic_local_group_free(void* group);
 int   iemic_create_local(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
                          void* group, int rank, int nranks);
+/* releases the handle; the context itself is freed once no atmosphere or coupled model
+ * built on it remains (each holds a reference, dropped by its own destroy) */
 void iemic_destroy(iemic_ctx* ctx);
 int  iemic_device_count(void);
 const char* iemic_last_error(void);
@@ -176,7 +178,7 @@ int  iemic_atmos_default_params(iemic_atmos_params* p);
  * ocean's top layer (AtmosLocal::setSurfaceMask 1722-1756), Ooa/Os from getdeps.  The
  * ocean context must have coupled_t = 1 and one rank. */
 int  iemic_atmos_create(iemic_atmos** a, iemic_ctx* ocean, const iemic_atmos_params* p);
-void iemic_atmos_destroy(iemic_atmos* a);
+void iemic_atmos_destroy(iemic_atmos* a);                       /* refcounted like the ocean */
 int  iemic_atmos_dim(const iemic_atmos* a);                    /* 3 n m + 1               */
 int  iemic_atmos_set_par(iemic_atmos* a, int idx, double v);   /* AtmosLocal::setPar      */
 int  iemic_atmos_set_state(iemic_atmos* a, const double* x);
