@@ -465,6 +465,128 @@ extern "C" int iemic_get_state(iemic_ctx* c, double* x)
     return get_ref(c, c->d_x.p, x);
 }
 
+/* ---- diagnostics of the state (host side, as in the reference) --------------------- */
+/* THCM::getIntCondCoeff (THCM.C:2549-2577): the integral-condition coefficients */
+extern "C" int iemic_get_intcond_coeff(iemic_ctx* c, double* out)
+{
+    CTX_CHECK(c);
+    if (!out) return IEMIC_EINVAL;
+    return get_ref(c, c->d_intc.p, out);
+}
+
+namespace {
+/* the current state on the host in the ext layout with its HALO rows refreshed (the
+ * reference's Solve2Assembly import before usol) */
+int host_state(iemic_ctx* c, std::vector<double>& x)
+{
+    int rc = halo_exchange(c, c->d_x.p, HALO);
+    if (rc) return rc;
+    x.assign((size_t)c->nerows, 0.0);
+    return d2h(c, x.data(), c->d_x.p, sizeof(double) * x.size());
+}
+/* sum of a host array over the ranks */
+int host_sum(iemic_ctx* c, std::vector<double>& v)
+{
+    if (c->nranks <= 1) return 0;
+    DevBuf<double> d;
+    if (d.alloc(v.size())) return IEMIC_ENOMEM;
+    int rc = h2d(c, d.p, v.data(), sizeof(double) * v.size());
+    if (!rc) rc = allreduce_sum(c, d.p, (int)v.size());
+    if (!rc) rc = d2h(c, v.data(), d.p, sizeof(double) * v.size());
+    return rc;
+}
+}  // namespace
+
+/* Ocean::getPsiM (Ocean.C:872-886): the meridional overturning streamfunction of the
+ * state, OceanGrid::recomputePsiM (OceanGrid.C:270-346: v of usol integrated over x, times
+ * dx) and m_thcm_utils::compute_psim (thcm_utils.F90:95-118: -cos(yv) vs dz dfzT summed up
+ * from the bottom below 500 m), its extrema over (0:m, 0:l), in Sv (r0dim hdim udim 1e-6).
+ * psim (optional): PsiM(j, k) at [(m+1) k + j]. */
+extern "C" int iemic_psim(iemic_ctx* c, double* psim_min, double* psim_max, double* psim)
+{
+    CTX_CHECK(c);
+    if (!psim_min || !psim_max) return IEMIC_EINVAL;
+    std::vector<double> x;
+    int rc = host_state(c, x);
+    if (rc) return rc;
+    const auto& su = c->su;
+    const Geo g = su.geo(su.landm.data(), su.tab.data());
+    const int n = c->n, m = c->m, l = c->l;
+    std::vector<double> ps((size_t)(m + 1) * (l + 1), 0.0);
+    for (int j = c->jb0 + 1; j <= c->jb1 && j <= m; j++) {          /* 1-based, owned */
+        const double cs = std::cos(su.yv[j]);
+        for (int k = 1; k <= l; k++) {
+            double sum = 0.0;
+            for (int i = 1; i <= n; i++) sum += uv_arr(g, x.data(), VV, i, j, k);
+            const double vs = sum * su.dx;
+            const double zk = host::fz(((double)k - 0.5) * su.dz + host::zmin, su.cfg.qz);
+            if (zk * su.cfg.hdim < -500.0)
+                ps[(size_t)(m + 1) * k + j] = -cs * vs * su.dz * su.dfzT[k] + ps[(size_t)(m + 1) * (k - 1) + j];
+        }
+    }
+    if ((rc = host_sum(c, ps))) return rc;
+    const double transc = host::r0dim * su.cfg.hdim * host::udim * 1e-6;
+    double mn = ps[0], mx = ps[0];
+    for (double v : ps) {
+        mn = std::min(mn, v);
+        mx = std::max(mx, v);
+    }
+    *psim_min = mn * transc;
+    *psim_max = mx * transc;
+    if (psim)
+        for (size_t q = 0; q < ps.size(); q++) psim[q] = ps[q] * transc;
+    return 0;
+}
+
+/* Ocean::integralChecks (Ocean.C:1841-1848 -> THCM.C:2042-2118): the volume integrals of
+ * the salt advection and salt diffusion operators of the state (m_integrals,
+ * integrals.F90:17-89, over usol's padded fields; the advection sum covers the columns whose
+ * top cell is ocean, as there).  Discrete conservation makes both vanish. */
+extern "C" int iemic_integral_checks(iemic_ctx* c, double* salt_advection, double* salt_diffusion)
+{
+    CTX_CHECK(c);
+    if (!salt_advection || !salt_diffusion) return IEMIC_EINVAL;
+    std::vector<double> x;
+    int rc = host_state(c, x);
+    if (rc) return rc;
+    const auto& su = c->su;
+    const Geo g = su.geo(su.landm.data(), su.tab.data());
+    const int n = c->n, m = c->m, l = c->l;
+    const double dx = su.dx, dy = su.dy, dz = su.dz;
+    const double* xs = x.data();
+    auto u = [&](int i, int j, int k) { return uv_arr(g, xs, UU, i, j, k); };
+    auto v = [&](int i, int j, int k) { return uv_arr(g, xs, VV, i, j, k); };
+    auto w = [&](int i, int j, int k) { return w_arr(g, xs, i, j, k); };
+    auto sa = [&](int i, int j, int k) { return ts_arr(g, xs, SS, i, j, k); };
+    std::vector<double> sums(2, 0.0);
+    for (int k = 1; k <= l; k++) {
+        const double h1 = 1.0 / (su.dfzT[k] * su.dfzW[k]), h2 = 1.0 / (su.dfzT[k] * su.dfzW[k - 1]);
+        for (int j = c->jb0 + 1; j <= c->jb1 && j <= m; j++) {
+            const double cay = std::cos(su.y[j]), c1 = std::cos(su.yv[j]), c2 = std::cos(su.yv[j - 1]);
+            for (int i = 1; i <= n; i++) {
+                if (LM(g, i, j, l) == OCEAN)
+                    sums[0] += (u(i, j, k) + u(i, j - 1, k)) * (sa(i + 1, j, k) + sa(i, j, k)) / (4 * dx) -
+                               (u(i - 1, j, k) + u(i - 1, j - 1, k)) * (sa(i, j, k) + sa(i - 1, j, k)) / (4 * dx) +
+                               (v(i, j, k) + v(i - 1, j, k)) * (sa(i, j + 1, k) + sa(i, j, k)) * std::cos(su.yv[j]) / (4 * dy) -
+                               (v(i, j - 1, k) + v(i - 1, j - 1, k)) * (sa(i, j, k) + sa(i, j - 1, k)) *
+                                   std::cos(su.yv[j - 1]) / (4 * dy) +
+                               w(i, j, k) * (sa(i, j, k + 1) + sa(i, j, k)) * std::cos(su.y[j]) / (2 * dz * su.dfzW[k]) -
+                               w(i, j, k - 1) * (sa(i, j, k) + sa(i, j, k - 1)) * std::cos(su.y[j]) /
+                                   (2 * dz * su.dfzW[k - 1]);
+                if (LM(g, i, j, k) == OCEAN)
+                    sums[1] += std::cos(su.y[j]) * su.dfzT[k] *
+                               ((sa(i + 1, j, k) + sa(i - 1, j, k) - 2 * sa(i, j, k)) / (dx * dx * cay * cay) +
+                                (c1 * sa(i, j + 1, k) + c2 * sa(i, j - 1, k) - (c1 + c2) * sa(i, j, k)) / (dy * dy * cay) +
+                                (h1 * sa(i, j, k + 1) + h2 * sa(i, j, k - 1) - (h1 + h2) * sa(i, j, k)) / (dz * dz));
+            }
+        }
+    }
+    if ((rc = host_sum(c, sums))) return rc;
+    *salt_advection = sums[0];
+    *salt_diffusion = sums[1];
+    return 0;
+}
+
 extern "C" int iemic_jacobian(iemic_ctx* c)
 {
     CTX_CHECK(c);

@@ -131,6 +131,9 @@ def lib():
         "iemic_time_spmv_cold": (C.c_int, [vp, C.c_int, vp, C.c_int64, PD]),
         "iemic_set_intcond_correction": (C.c_int, [vp, PD]),
         "iemic_get_intcond_correction": (C.c_int, [vp, PD]),
+        "iemic_get_intcond_coeff": (C.c_int, [vp, PD]),
+        "iemic_psim": (C.c_int, [vp, PD, PD, PD]),
+        "iemic_integral_checks": (C.c_int, [vp, PD, PD]),
         "iemic_ilu_create": (C.c_int, [P(vp), C.c_int, C.c_int, C.c_int64, P64, PI, PD, C.c_int]),
         "iemic_ilu_compute": (C.c_int, [vp]),
         "iemic_ilu_apply": (C.c_int, [vp, PD, PD]),
@@ -176,7 +179,8 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",
             "iemic_set_par", "iemic_get_par", "iemic_set_intcond_correction",
-            "iemic_get_intcond_correction", "iemic_nrows", "iemic_graph_nnz",
+            "iemic_get_intcond_correction", "iemic_get_intcond_coeff", "iemic_psim",
+            "iemic_integral_checks", "iemic_nrows", "iemic_graph_nnz",
             "iemic_rowintcon", "iemic_landm", "iemic_set_state", "iemic_get_state",
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",

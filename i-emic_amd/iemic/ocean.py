@@ -279,6 +279,60 @@ class Ocean:
     def postProcess(self) -> None:
         pass
 
+    # ---- diagnostics (Ocean.C; host side as in the reference) ---------------------------
+    def getIntCondCoeff(self) -> np.ndarray:
+        """THCM::getIntCondCoeff (THCM.C:2549-2577), reference row order."""
+        out = np.zeros(self.N)
+        check(lib().iemic_get_intcond_coeff(self._h, ptr(out)), "iemic_get_intcond_coeff")
+        return out
+
+    def getPsiM(self, field: bool = False):
+        """Ocean::getPsiM (Ocean.C:872-886): (psiMin, psiMax) of the meridional overturning
+        streamfunction of the current state in Sv; with field=True also PsiM(0:m, 0:l) as
+        an (l+1, m+1) array."""
+        mn, mx = C.c_double(), C.c_double()
+        ps = np.zeros((self.cfg.m + 1) * (self.cfg.l + 1))
+        check(lib().iemic_psim(self._h, C.byref(mn), C.byref(mx), ptr(ps)), "iemic_psim")
+        if field:
+            return mn.value, mx.value, ps.reshape(self.cfg.l + 1, self.cfg.m + 1)
+        return mn.value, mx.value
+
+    def integralChecks(self):
+        """Ocean::integralChecks (Ocean.C:1841-1848): (salt_advection, salt_diffusion)."""
+        a, d = C.c_double(), C.c_double()
+        check(lib().iemic_integral_checks(self._h, C.byref(a), C.byref(d)), "iemic_integral_checks")
+        return a.value, d.value
+
+    def getMassMat(self) -> np.ndarray:
+        """Ocean::getMassMat: the diagonal mass matrix B (fillcolB; state independent, so
+        a Jacobian is assembled first when none is current)."""
+        try:
+            return self.diagB()
+        except _lib.IemicError:
+            self.computeJacobian()
+            return self.diagB()
+
+    def applyMassMat(self, v: np.ndarray) -> np.ndarray:
+        """Ocean::applyMassMat: B v (B diagonal)."""
+        return self.getMassMat() * np.asarray(v, dtype=np.float64)
+
+    def getColumnIntegral(self, use_sres: bool = True) -> np.ndarray:
+        """Ocean::getColumnIntegral (Ocean.C:1851-1895): for every S column of the last
+        Jacobian the integral-condition-weighted column sum sum_r coeff_r J[r, c] (the
+        intcond row's own coefficient dropped when SRES = 0 and use_sres), 0 elsewhere.
+        Host side, from the exported CSR, as the reference's Epetra computation."""
+        rowptr, col, val = self.exportCSR()
+        coef = self.getIntCondCoeff()
+        ri = self.rowintcon
+        if use_sres and ri >= 0:
+            coef[ri] = 0.0
+        rows = np.repeat(np.arange(self.N), np.diff(rowptr))
+        sums = np.zeros(self.N)
+        np.add.at(sums, col, coef[rows] * val)
+        sel = np.zeros(self.N)
+        sel[5::6] = 1.0
+        return sums * sel
+
     # ---- fused device-resident Newton step -------------------------------------------
     def newtonStep(self, allow_unconverged: bool = False) -> _lib.NewtonInfo:
         """F, J, preconditioner, J dx = -F, x += dx, F (transient/Newton.H:92-99).  The

@@ -139,6 +139,18 @@ void iemic_destroy(iemic_ctx* ctx);
 int  iemic_device_count(void);
 const char* iemic_last_error(void);
 
+/* ---- diagnostics of the state (host side, as the reference computes them) --------- */
+/* THCM::getIntCondCoeff (THCM.C:2549-2577): integral-condition coefficients, global row
+ * order (each rank fills its own rows) */
+int iemic_get_intcond_coeff(iemic_ctx* ctx, double* coeff);
+/* Ocean::getPsiM (Ocean.C:872-886, OceanGrid::recomputePsiM OceanGrid.C:270-346,
+ * compute_psim thcm_utils.F90:95-118): extrema of the meridional overturning streamfunction
+ * in Sv; psim (optional) = PsiM(j, k) at [(m+1) k + j], j = 0..m, k = 0..l */
+int iemic_psim(iemic_ctx* ctx, double* psim_min, double* psim_max, double* psim);
+/* Ocean::integralChecks (Ocean.C:1841-1848, THCM.C:2042-2118, integrals.F90:17-89): volume
+ * integrals of the salt advection / diffusion operators of the state */
+int iemic_integral_checks(iemic_ctx* ctx, double* salt_advection, double* salt_diffusion);
+
 /* ---- parameters (setparcs_/getparcs_, usrc.F90:163-198; index 1..30 = par2int) --- */
 int  iemic_set_par(iemic_ctx* ctx, int idx, double value);
 /* THCM::setIntCondCorrection (THCM.C:2020-2038, called by Ocean at Ocean.C:144-148 for a
