@@ -306,6 +306,59 @@ def fortran_to_graph(rowptr, col, beg, jco, co, rowintcon=-1):
     return val
 
 
+def graph_to_fortran(n, m, l, periodic, rowptr, col, val, rowintcon=-1, chunk=16384):
+    """The inverse of fortran_to_graph: the Fortran CSR (beg, jco, co; 1-based, int32 /
+    float64) that assemble.F90's fillcolA (assemble.F90:57-139) writes for the same
+    coefficients -- per row the 27 stencil positions kk outer (kk 1..9 at level k, 10..18
+    at k-1, 19..27 at k+1; within a level (i-1+(kk-1)//3, j-1+(kk+2)%3), shift's periodic
+    wrap in i, assemble.F90:142-179), the 6 unknowns inner, entries with |v| > 1e-10 only.
+    The integral-condition row (SRES = 0) is not a Fortran row (assemble.F90:198-199)."""
+    N = len(rowptr) - 1
+    di = np.empty(27, np.int64)
+    dj = np.empty(27, np.int64)
+    dk = np.empty(27, np.int64)
+    for kk in range(1, 28):
+        q = (kk - 1) % 9 + 1
+        di[kk - 1] = (q - 1) // 3 - 1
+        dj[kk - 1] = (q + 2) % 3 - 1
+        dk[kk - 1] = 0 if kk <= 9 else (-1 if kk <= 18 else 1)
+    rows_of = np.repeat(np.arange(N, dtype=np.int64), np.diff(rowptr))
+    gkey = rows_of * N + np.asarray(col, dtype=np.int64)          # sorted (rows, then cols)
+    val = np.asarray(val)
+    begs, jcos, cos = [np.zeros(1, np.int64)], [], []
+    for r0 in range(0, N, chunk):
+        r = np.arange(r0, min(N, r0 + chunk), dtype=np.int64)
+        cell = r // 6
+        i, j, k = cell % n, (cell // n) % m, cell // (n * m)
+        ii = i[:, None, None] + di[None, :, None]
+        jj = j[:, None, None] + dj[None, :, None]
+        kc = k[:, None, None] + dk[None, :, None]
+        if periodic:
+            ii = np.where(ii < 0, ii + n, np.where(ii >= n, ii - n, ii))
+        inside = np.broadcast_to((ii >= 0) & (ii < n) & (jj >= 0) & (jj < m) & (kc >= 0) & (kc < l),
+                                 (len(r), 27, 6))
+        cc = 6 * ((kc * m + jj) * n + ii) + np.arange(6)[None, None, :]
+        cc = np.where(inside, cc, 0).reshape(len(r), 162)
+        key = r[:, None] * N + cc
+        pos = np.minimum(np.searchsorted(gkey, key), len(gkey) - 1)
+        hit = (gkey[pos] == key) & inside.reshape(len(r), 162)
+        v = np.where(hit, val[pos], 0.0)
+        keep = np.abs(v) > 1e-10
+        if rowintcon >= 0:
+            keep[r == rowintcon] = False
+        cnt = keep.sum(axis=1)
+        begs.append(np.cumsum(cnt))
+        jcos.append(cc[keep])
+        cos.append(v[keep])
+    bl = [begs[0]]
+    off = 0
+    for b in begs[1:]:
+        bl.append(b + off)
+        off += b[-1] if len(b) else 0
+    beg = np.concatenate(bl).astype(np.int32) + 1
+    return beg, (np.concatenate(jcos) + 1).astype(np.int32), np.concatenate(cos).astype(np.float64)
+
+
 # ------------------------------------------------------------------------------------
 # CPU linear solve (krylov_oracle.c)
 
