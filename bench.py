@@ -11,10 +11,11 @@ with --state synthetic SURVEY §8d's splitmix64 state (seed 20261015; a Newton s
 diverges).  The state is named in config["state"].
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): the same 2-degree problem is split
-into N latitude bands, one per GPU (halo exchange and Krylov reductions over RCCL; the
-preconditioner's Schur problem and coarsest T/S level are global, the rest couples across
-band edges through halos) -- strong scaling; the step time is the max over
-ranks.
+into N subdomains by the reference's Decomp2D rule (TRIOS_Domain.C:88-109; 8 GPUs: 4 x 2,
+48 x 38 columns each; ``--npx 1`` latitude bands), one per GPU: halo exchanges and Krylov
+reductions over RCCL; the preconditioner's Schur problem and coarsest T/S level are
+global, the rest couples across subdomain edges through halos -- strong
+scaling; the step time is the max over ranks.
 
 Prints ONE JSON line (rank 0) with the metric, the SpMV roofline of the same run (HIP
 events on the library's stream) and the CPU baseline (the oracle port, rank 0, N=1).
@@ -50,6 +51,8 @@ def stencil_ell_bytes(ncell: int, nslot: int, n: int) -> int:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--npx", type=int, default=0,
+                   help="x parts of the process grid (0: the reference's Decomp2D rule, 1: bands)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="global2")
@@ -215,7 +218,8 @@ def main():
             idt.copy_(torch.frombuffer(bytearray(Ocean.unique_id()), dtype=torch.uint8))
         dist.broadcast(idt, 0)
         comm_id = bytes(idt.cpu().numpy().tobytes())
-    oc = Ocean(cfg, device=local, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id)
+    oc = Ocean(cfg, device=local, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id,
+               npx=args.npx)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
     state = args.state if (args.state == "synthetic" or os.path.exists(fix)) else "synthetic"
@@ -318,8 +322,8 @@ def main():
                    "state": (f"branch (bench_data/{args.config}_cf05.npz, CF 0.5)" if state == "branch"
                              else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
-                   "parallelism": f"latitude-bands x{world}" if world > 1 else "single",
-                   "band_rows": [lay["jb0"], lay["jb1"]]},
+                   "parallelism": (f"decomp2d {lay['npx']}x{lay['npy']}" if world > 1 else "single"),
+                   "subdomain_rank0": {"cols": [lay["ib0"], lay["ib1"]], "rows": [lay["jb0"], lay["jb1"]]}},
         "newton": {"iters": s.iters, "converged": s.converged,
                    "explicit_rel_res": s.explicit_rel_res, "norm_f0": last.norm_f0,
                    "norm_f1": last.norm_f1, "t_rhs_ms": last.t_rhs_ms,

@@ -132,26 +132,66 @@ extern "C" int iemic_comm_unique_id(unsigned char* id128)
     return comm_unique_id(id128);
 }
 
-static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm,
-                       const iemic_dist* dist, void* group, int grank, int granks);
+extern "C" int iemic_decomp2d(int n, int m, int nranks, int* npx, int* npy)
+{
+    if (nranks < 1 || !npx || !npy) return IEMIC_EINVAL;
+    decomp2d(n, m, nranks, *npx, *npy);
+    return 0;
+}
+
+struct CreateArgs {
+    const iemic_dist* dist = nullptr;       /* RCCL                                       */
+    void* group = nullptr;                  /* in-process rank group                      */
+    const iemic_transport* tp = nullptr;    /* host transport                             */
+    int rank = 0, nranks = 1, npx = 1;
+};
+static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm, const CreateArgs& a);
 
 extern "C" int iemic_create_dist(iemic_ctx** out, const iemic_grid* grid, const int* landm,
                                  const iemic_dist* dist)
 {
-    return create_impl(out, grid, landm, dist, nullptr, 0, 1);
+    CreateArgs a;
+    if (dist) {
+        a.dist = dist;
+        a.rank = dist->rank;
+        a.nranks = dist->nranks;
+        a.npx = dist->npx;
+    }
+    return create_impl(out, grid, landm, a);
+}
+
+extern "C" int iemic_create_transport(iemic_ctx** out, const iemic_grid* grid, const int* landm, int rank,
+                                      int nranks, int npx, const iemic_transport* tp)
+{
+    if (!tp || !tp->send || !tp->recv || !tp->allreduce_sum) return IEMIC_EINVAL;
+    CreateArgs a;
+    a.tp = tp;
+    a.rank = rank;
+    a.nranks = nranks;
+    a.npx = npx;
+    return create_impl(out, grid, landm, a);
 }
 
 extern "C" void* iemic_local_group_new(int nranks) { return local_group_new(nranks); }
 extern "C" void iemic_local_group_free(void* group) { local_group_free(group); }
+extern "C" int iemic_create_local_2d(iemic_ctx** out, const iemic_grid* grid, const int* landm,
+                                     void* group, int rank, int nranks, int npx)
+{
+    if (!group) return IEMIC_EINVAL;
+    CreateArgs a;
+    a.group = group;
+    a.rank = rank;
+    a.nranks = nranks;
+    a.npx = npx;
+    return create_impl(out, grid, landm, a);
+}
 extern "C" int iemic_create_local(iemic_ctx** out, const iemic_grid* grid, const int* landm,
                                   void* group, int rank, int nranks)
 {
-    if (!group) return IEMIC_EINVAL;
-    return create_impl(out, grid, landm, nullptr, group, rank, nranks);
+    return iemic_create_local_2d(out, grid, landm, group, rank, nranks, 1);
 }
 
-static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm,
-                       const iemic_dist* dist, void* group, int grank, int granks)
+static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm, const CreateArgs& a)
 {
     if (!out || !grid || !landm) return IEMIC_EINVAL;
     *out = nullptr;
@@ -168,16 +208,9 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
         set_error("iemic_create: grid too small");
         return IEMIC_EINVAL;
     }
-    const int rank = group ? grank : dist ? dist->rank : 0;
-    const int nranks = group ? granks : dist ? dist->nranks : 1;
-    if (nranks < 1 || rank < 0 || rank >= nranks) {
-        set_error("iemic_create: bad rank / nranks");
-        return IEMIC_EINVAL;
-    }
-    /* latitude bands: rows split evenly; each band must cover the halo depth */
-    const int jb0 = (int)((int64_t)rank * grid->m / nranks), jb1 = (int)((int64_t)(rank + 1) * grid->m / nranks);
-    if (jb1 - jb0 < HALO) {
-        set_error("iemic_create: too many ranks for the latitude rows (need >= 2 rows per rank)");
+    Sub sub;
+    if (const char* why = sub_init(sub, grid->n, grid->m, grid->l, grid->periodic, a.rank, a.nranks, a.npx)) {
+        set_error(std::string("iemic_create: ") + why);
         return IEMIC_EINVAL;
     }
     iemic_ctx* c = new iemic_ctx();
@@ -194,13 +227,27 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     c->n = grid->n; c->m = grid->m; c->l = grid->l;
     c->ncell = (int64_t)c->n * c->m * c->l;
     c->nrows = NUN * c->ncell;
-    c->rank = rank;
-    c->nranks = nranks;
-    c->jb0 = jb0;
-    c->jb1 = jb1;
+    c->sub = sub;
+    c->rank = sub.rank;
+    c->nranks = sub.nranks;
+    c->npx = sub.npx;
+    c->npy = sub.npy;
+    c->px = sub.px;
+    c->py = sub.py;
+    c->ib0 = sub.ib0;
+    c->ib1 = sub.ib1;
+    c->jb0 = sub.jb0;
+    c->jb1 = sub.jb1;
+    for (int d = 0; d < 4; d++) c->nb[d] = sub.nb[d];
     const int n = c->n, m = c->m, l = c->l;
     const size_t nl = (size_t)(n + 2) * (m + 2) * (l + 2);
-    c->su.init(*grid, landm, jb0, jb1);
+    {
+        const int s0[2] = {c->ib0, c->jb0}, s1[2] = {c->ib1, c->jb1};
+        c->su.init(*grid, landm, s0, s1, sub.npx > 1 ? 1 : 0);
+    }
+    c->nx = c->su.nx;
+    c->hx = c->su.hx;
+    c->xb = c->su.xb;
     c->su.vmix_init();
     c->nloc = c->su.nloc;
     c->nlrows = NUN * c->nloc;
@@ -209,8 +256,9 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     c->own0 = c->su.own0();
     c->rowintcon = c->su.rowintcon;
     int rc = 0;
-    if (group) local_group_join(c, group);
-    else if (nranks > 1 && (rc = comm_init(c, dist->id, rank, nranks))) {
+    if (a.group) local_group_join(c, a.group);
+    else if (a.tp) c->tp = *a.tp;
+    else if (sub.nranks > 1 && (rc = comm_init(c, a.dist->id, sub.rank, sub.nranks))) {
         delete c;
         return rc;
     }
@@ -315,12 +363,12 @@ int get_ref(iemic_ctx* c, const double* dev, double* ref)
 namespace iemic {
 /* reference-ordered global device vector -> ext layout (owned rows) */
 __global__ void k_ref_to_ext(const double* __restrict__ ref, double* __restrict__ ext, int n, int m,
-                             int l, int jb0, int64_t nloc)
+                             int l, int jb0, int ib0, int nx, int64_t nloc)
 {
     const int64_t lc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lc >= nloc) return;
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
-    const int64_t e = NUN * ((int64_t)HALO * l * n + lc), r = NUN * (((int64_t)k * m + j) * n + i);
+    const int i = ib0 + (int)(lc % nx), k = (int)((lc / nx) % l), j = jb0 + (int)(lc / ((int64_t)nx * l));
+    const int64_t e = NUN * ((int64_t)HALO * l * nx + lc), r = NUN * (((int64_t)k * m + j) * n + i);
     for (int v = 0; v < NUN; v++) ext[e + v] = ref[r + v];
 }
 }  // namespace iemic
@@ -412,6 +460,11 @@ extern "C" int iemic_layout(const iemic_ctx* c, int64_t* out)
     out[4] = c->jb1;
     out[5] = c->rank;
     out[6] = c->nranks;
+    out[7] = c->ib0;
+    out[8] = c->ib1;
+    out[9] = c->npx;
+    out[10] = c->npy;
+    out[11] = c->hx;
     return 0;
 }
 
@@ -454,7 +507,7 @@ extern "C" int iemic_set_state_dev(iemic_ctx* c, const double* x_dev)
     CTX_CHECK(c);
     if (!x_dev) return IEMIC_EINVAL;
     hipLaunchKernelGGL(k_ref_to_ext, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, c->stream,
-                       x_dev, c->d_x.p, c->n, c->m, c->l, c->jb0, c->nloc);
+                       x_dev, c->d_x.p, c->n, c->m, c->l, c->jb0, c->ib0, c->nx, c->nloc);
     HIP_OK(hipGetLastError());
     c->jac_valid = 0;
     return 0;
@@ -517,7 +570,7 @@ extern "C" int iemic_psim(iemic_ctx* c, double* psim_min, double* psim_max, doub
         const double cs = std::cos(su.yv[j]);
         for (int k = 1; k <= l; k++) {
             double sum = 0.0;
-            for (int i = 1; i <= n; i++) sum += uv_arr(g, x.data(), VV, i, j, k);
+            for (int i = c->ib0 + 1; i <= c->ib1; i++) sum += uv_arr(g, x.data(), VV, i, j, k);
             const double vs = sum * su.dx;
             const double zk = host::fz(((double)k - 0.5) * su.dz + host::zmin, su.cfg.qz);
             if (zk * su.cfg.hdim < -500.0)
@@ -563,7 +616,7 @@ extern "C" int iemic_integral_checks(iemic_ctx* c, double* salt_advection, doubl
         const double h1 = 1.0 / (su.dfzT[k] * su.dfzW[k]), h2 = 1.0 / (su.dfzT[k] * su.dfzW[k - 1]);
         for (int j = c->jb0 + 1; j <= c->jb1 && j <= m; j++) {
             const double cay = std::cos(su.y[j]), c1 = std::cos(su.yv[j]), c2 = std::cos(su.yv[j - 1]);
-            for (int i = 1; i <= n; i++) {
+            for (int i = c->ib0 + 1; i <= c->ib1; i++) {
                 if (LM(g, i, j, l) == OCEAN)
                     sums[0] += (u(i, j, k) + u(i, j - 1, k)) * (sa(i + 1, j, k) + sa(i, j, k)) / (4 * dx) -
                                (u(i - 1, j, k) + u(i - 1, j - 1, k)) * (sa(i, j, k) + sa(i - 1, j, k)) / (4 * dx) +

@@ -1,12 +1,15 @@
 /*
- * comm.hip -- RCCL over xGMI for the latitude-band decomposition.
+ * comm.hip -- halo exchanges and sums of the Decomp2D subdomains over
+ * RCCL (xGMI), an in-process group (tests on one GPU) or a caller's host transport.
  *
- * Replaces the Epetra/MPI communication of the reference path: the Import of ghost rows
+ * Replaces the Epetra/MPI communication of the reference path: the Import of ghost cells
  * before matrix_/rhs_ and Apply (TRIOS_Domain.C Solve2Assembly, Epetra_CrsMatrix::Apply)
  * and the MPI_Allreduce inside Belos' dots and norms and THCM's intcond/forcing sums.
- * In the j-major ext layout every halo is a contiguous slab of whole latitude rows, so an
- * exchange is one ncclSend/ncclRecv pair per neighbour straight from the vector, grouped
- * and enqueued on the context stream.  One rank: all calls are no-ops.
+ * In the ext layout (stencil.h) a latitude halo is a contiguous slab of the main block
+ * plus one of the x-halo block, so a y exchange goes straight from the vector; an x halo
+ * is one short run per (j, k) row, packed by a 2-D copy on the stream.  An exchange runs
+ * in two phases, x then y, and the y messages carry the x halo of the rows they send, so
+ * the diagonal neighbours arrive too.  One rank: all calls are no-ops.
  */
 #include <rccl/rccl.h>
 
@@ -59,6 +62,18 @@ struct LocalGroup {
         }
     }
 };
+
+static int host_allreduce(iemic_ctx* c, double* dev, int count)
+{
+    std::vector<double> h(count);
+    int rc = d2h(c, h.data(), dev, sizeof(double) * count);
+    if (rc) return rc;
+    if (c->tp.allreduce_sum(c->tp.user, h.data(), count)) {
+        set_error("host transport: allreduce failed");
+        return IEMIC_EDEVICE;
+    }
+    return h2d(c, dev, h.data(), sizeof(double) * count);
+}
 
 static int local_allreduce(iemic_ctx* c, double* dev, int count)
 {
@@ -113,77 +128,133 @@ int allreduce_sum(iemic_ctx* c, double* dev, int count)
 {
     if (c->nranks <= 1 || count <= 0) return 0;
     if (c->group) return local_allreduce(c, dev, count);
+    if (c->tp.send) return host_allreduce(c, dev, count);
     NCCL_OK(ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)c->comm,
                           c->stream));
     return 0;
 }
 
-/* One batch of point-to-point messages.  The halo exchanges build their batch once
- * (halo_ops) and hand it to the transport: RCCL (one ncclGroupStart/End, messages to the
- * same peer matched in order, as NCCL requires) or, for in-process band groups, the host
- * mailbox below, which pairs the k-th send of rank a to b with the k-th receive of b from
- * a -- the same pairing rule, so the batches the tests run are the ones RCCL runs. */
-struct P2P {
-    bool send;
-    double* buf;
-    int64_t cnt;
-    int peer;
-};
+/* ---- messages ----------------------------------------------------------------------
+ * Pairing rule (RCCL's, and that of the in-process mailbox and the host transport): the
+ * k-th message rank a sends to rank b is the k-th message b receives from a (the plans of
+ * decomp.h are built for it). */
 
-/* rows_j (<= HALO) latitude rows of a per-cell array (width doubles per ext cell) to and
- * from the neighbouring bands */
-static void halo_ops(const iemic_ctx* c, double* v, int width, int rows_j, std::vector<P2P>& ops)
+static size_t seg_count(const Seg& g) { return (size_t)(g.nblk * g.len); }
+
+/* strided message <-> contiguous buffer (device or host), stream-ordered */
+static int seg_copy(iemic_ctx* c, const Seg& g, double* buf, bool to_buf, hipMemcpyKind kind)
 {
-    const int64_t slab = (int64_t)width * c->l * c->n;        /* doubles per latitude row */
-    const int64_t cnt = slab * rows_j;
-    const int64_t own_first = (int64_t)width * c->own0;        /* first owned cell         */
-    const int64_t own_end = own_first + (int64_t)width * c->nloc; /* one past the last     */
-    if (c->rank > 0) {
-        ops.push_back({true, v + own_first, cnt, c->rank - 1});
-        ops.push_back({false, v + own_first - cnt, cnt, c->rank - 1});
-    }
-    if (c->rank < c->nranks - 1) {
-        ops.push_back({true, v + own_end - cnt, cnt, c->rank + 1});
-        ops.push_back({false, v + own_end, cnt, c->rank + 1});
-    }
+    if (!g.nblk || !g.len) return 0;
+    double* p = g.base + g.off;
+    const size_t w = sizeof(double) * g.len, sp = sizeof(double) * g.stride;
+    if (to_buf) HIP_OK(hipMemcpy2DAsync(buf, w, p, sp, w, g.nblk, kind, c->stream));
+    else HIP_OK(hipMemcpy2DAsync(p, sp, buf, w, w, g.nblk, kind, c->stream));
+    return 0;
 }
+static bool seg_contig(const Seg& g) { return g.nblk == 1 || g.len == g.stride; }
 
-static int run_local(iemic_ctx* c, const std::vector<P2P>& ops)
+static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
 {
     LocalGroup* g = (LocalGroup*)c->group;
     std::map<int, int> ksend, krecv;
-    for (const P2P& op : ops) {
+    for (const Msg& op : ops) {
         if (!op.send) continue;
-        std::vector<double> h((size_t)op.cnt);
-        int rc = d2h(c, h.data(), op.buf, sizeof(double) * h.size());
+        std::vector<double> h(seg_count(op.s));
+        int rc = seg_copy(c, op.s, h.data(), true, hipMemcpyDeviceToHost);
         if (rc) return rc;
+        HIP_OK(hipStreamSynchronize(c->stream));
         std::lock_guard<std::mutex> lk(g->mu);
         g->box[std::make_tuple(c->rank, op.peer, ksend[op.peer]++)] = std::move(h);
     }
     g->barrier();
-    for (const P2P& op : ops) {
+    for (const Msg& op : ops) {
         if (op.send) continue;
         std::vector<double> h;
         {
             std::lock_guard<std::mutex> lk(g->mu);
             auto it = g->box.find(std::make_tuple(op.peer, c->rank, krecv[op.peer]++));
-            if (it == g->box.end() || (int64_t)it->second.size() != op.cnt) {
-                set_error("band group: unmatched receive");
+            if (it == g->box.end() || it->second.size() != seg_count(op.s)) {
+                set_error("rank group: unmatched receive");
                 return IEMIC_EINVAL;
             }
             h = std::move(it->second);
             g->box.erase(it);
         }
-        int rc = h2d(c, op.buf, h.data(), sizeof(double) * h.size());
+        int rc = seg_copy(c, op.s, h.data(), false, hipMemcpyHostToDevice);
         if (rc) return rc;
+        HIP_OK(hipStreamSynchronize(c->stream));
     }
     g->barrier();
     return 0;
 }
 
-static int run_ops(iemic_ctx* c, const std::vector<P2P>& ops)
+/* the caller's host transport: all sends (staged), all receives, wait, unpack */
+static int run_host(iemic_ctx* c, const std::vector<Msg>& ops)
 {
-    if (c->group) return run_local(c, ops);
+    size_t tot = 0;
+    for (const Msg& op : ops) tot += seg_count(op.s);
+    if (c->h_stage.size() < tot) c->h_stage.resize(tot);
+    double* h = c->h_stage.data();
+    size_t o = 0;
+    int rc;
+    for (const Msg& op : ops) {
+        if (op.send && (rc = seg_copy(c, op.s, h + o, true, hipMemcpyDeviceToHost))) return rc;
+        o += seg_count(op.s);
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    o = 0;
+    for (const Msg& op : ops) {
+        if (op.send && c->tp.send(c->tp.user, op.peer, h + o, (int64_t)seg_count(op.s))) {
+            set_error("host transport: send failed");
+            return IEMIC_EDEVICE;
+        }
+        o += seg_count(op.s);
+    }
+    o = 0;
+    for (const Msg& op : ops) {
+        if (!op.send && c->tp.recv(c->tp.user, op.peer, h + o, (int64_t)seg_count(op.s))) {
+            set_error("host transport: recv failed");
+            return IEMIC_EDEVICE;
+        }
+        o += seg_count(op.s);
+    }
+    if (c->tp.wait && c->tp.wait(c->tp.user)) {
+        set_error("host transport: wait failed");
+        return IEMIC_EDEVICE;
+    }
+    o = 0;
+    for (const Msg& op : ops) {
+        if (!op.send && (rc = seg_copy(c, op.s, h + o, false, hipMemcpyHostToDevice))) return rc;
+        o += seg_count(op.s);
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+/* RCCL: contiguous messages straight from / into the vector, strided ones through the
+ * device staging buffer (packed before the group, unpacked after it, stream-ordered) */
+static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
+{
+    size_t tot = 0;
+    for (const Msg& op : ops)
+        if (!seg_contig(op.s)) tot += seg_count(op.s);
+    if (c->d_stage.n < tot && c->d_stage.alloc(tot)) {
+        set_error("halo exchange: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    std::vector<double*> buf(ops.size());
+    size_t o = 0;
+    int rc;
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
+        if (seg_contig(op.s)) {
+            buf[q] = op.s.base + op.s.off;
+            continue;
+        }
+        buf[q] = c->d_stage.p + o;
+        o += seg_count(op.s);
+        if (op.send && (rc = seg_copy(c, op.s, buf[q], true, hipMemcpyDeviceToDevice))) return rc;
+    }
     ncclComm_t comm = (ncclComm_t)c->comm;
     ncclResult_t first = ncclSuccess;
     std::string what;
@@ -192,9 +263,11 @@ static int run_ops(iemic_ctx* c, const std::vector<P2P>& ops)
         set_error(std::string("ncclGroupStart: ") + ncclGetErrorString(r));
         return IEMIC_EDEVICE;
     }
-    for (const P2P& op : ops) {
-        r = op.send ? ncclSend(op.buf, (size_t)op.cnt, ncclDouble, op.peer, comm, c->stream)
-                    : ncclRecv(op.buf, (size_t)op.cnt, ncclDouble, op.peer, comm, c->stream);
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
+        const size_t cnt = seg_count(op.s);
+        r = op.send ? ncclSend(buf[q], cnt, ncclDouble, op.peer, comm, c->stream)
+                    : ncclRecv(buf[q], cnt, ncclDouble, op.peer, comm, c->stream);
         if (r != ncclSuccess && first == ncclSuccess) {
             first = r;
             what = op.send ? "ncclSend" : "ncclRecv";
@@ -211,37 +284,43 @@ static int run_ops(iemic_ctx* c, const std::vector<P2P>& ops)
         set_error(what + ": " + ncclGetErrorString(first));
         return IEMIC_EDEVICE;
     }
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
+        if (!op.send && !seg_contig(op.s) && (rc = seg_copy(c, op.s, buf[q], false, hipMemcpyDeviceToDevice)))
+            return rc;
+    }
     return 0;
 }
 
-int halo_exchange_w(iemic_ctx* c, double* v, int width, int rows_j)
+int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops)
 {
-    if (c->nranks <= 1) return 0;
-    std::vector<P2P> ops;
-    halo_ops(c, v, width, rows_j, ops);
-    return run_ops(c, ops);
+    if (c->nranks <= 1 || ops.empty()) return 0;
+    if (c->group) return run_local(c, ops);
+    if (c->tp.send) return run_host(c, ops);
+    return run_rccl(c, ops);
 }
 
-/* one row of two arrays of whole rows (slab doubles each; owned rows [first, first + count)),
- * e.g. the level-0 T/S multigrid iterate, in one communication group */
-int halo_exchange_slab2(iemic_ctx* c, double* a, double* b, int64_t first, int64_t count, int64_t slab)
+/* the plan of decomp.h on this context's subdomain, as messages on v */
+void halo_plan_ext(const iemic_ctx* c, double* v, int width, int depth, std::vector<Msg>& x,
+                   std::vector<Msg>& y)
+{
+    std::vector<MsgD> px, py;
+    plan_ext(c->sub, width, depth, px, py);
+    for (const MsgD& q : px) x.push_back({q.send != 0, q.peer, Seg{v, q.s.off, q.s.nblk, q.s.len, q.s.stride}});
+    for (const MsgD& q : py) y.push_back({q.send != 0, q.peer, Seg{v, q.s.off, q.s.nblk, q.s.len, q.s.stride}});
+}
+
+int halo_exchange_w(iemic_ctx* c, double* v, int width, int depth)
 {
     if (c->nranks <= 1) return 0;
-    std::vector<P2P> ops;
-    for (double* v : {a, b}) {
-        if (c->rank > 0) {
-            ops.push_back({true, v + first, slab, c->rank - 1});
-            ops.push_back({false, v + first - slab, slab, c->rank - 1});
-        }
-        if (c->rank < c->nranks - 1) {
-            ops.push_back({true, v + first + count - slab, slab, c->rank + 1});
-            ops.push_back({false, v + first + count, slab, c->rank + 1});
-        }
-    }
-    return run_ops(c, ops);
+    std::vector<Msg> x, y;
+    halo_plan_ext(c, v, width, depth, x, y);
+    int rc = run_msgs(c, x);
+    if (rc) return rc;
+    return run_msgs(c, y);
 }
 
 /* state-vector halo (NUN doubles per cell) */
-int halo_exchange(iemic_ctx* c, double* v, int rows_j) { return halo_exchange_w(c, v, NUN, rows_j); }
+int halo_exchange(iemic_ctx* c, double* v, int depth) { return halo_exchange_w(c, v, NUN, depth); }
 
 }  // namespace iemic

@@ -14,6 +14,7 @@
 #include "../../include/iemic.h"
 #include "stencil.h"
 #include "host_setup.h"
+#include "decomp.h"
 
 namespace iemic {
 
@@ -165,9 +166,9 @@ struct BlockGS {
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
     DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_fac[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
     DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
-    /* bands: the coarsest T/S level solved globally (all bands' coarsest cells plus the
-     * cross-band couplings; band LU + inverse on the device, redundant on every rank) */
-    int mg_glob = 0, mg_gN = 0, mg_g0 = 0;
+    /* subdomains: the coarsest T/S level solved globally (all ranks' coarsest cells plus
+     * the cross-subdomain couplings; band LU + inverse on the device, on every rank) */
+    int mg_glob = 0, mg_gN = 0, mg_gGX = 0, mg_gI0 = 0, mg_gJ0 = 0;
     DevBuf<double> mg_gX, mg_gband, mg_gvec, mg_gtmp, mg_glpan;
     DevBuf<int> mg_gpiv, mg_ginfo, mg_gcols;
     DevBuf<double> mg_cdense;        /* coarsest dense operator (device assembly)        */
@@ -196,16 +197,25 @@ struct iemic_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n = 0, m = 0, l = 0;
     int64_t ncell = 0, nrows = 0;    /* global cells / rows                               */
-    /* latitude-band decomposition (stencil.h ext layout): owned band [jb0, jb1) */
+    /* Decomp2D subdomain (TRIOS_Domain.C:81-195; stencil.h ext layout): process grid
+     * npx x npy, rank = py * npx + px, owned columns [ib0, ib1) and rows [jb0, jb1); hx x-halo
+     * columns when npx > 1; neighbours nb[W, E, S, N] (-1: none; W/E wrap when periodic) */
+    iemic::Sub sub;                  /* the same, as decomp.h computed it                  */
     int rank = 0, nranks = 1;
-    int jb0 = 0, jb1 = 0;
+    int npx = 1, npy = 1, px = 0, py = 0;
+    int jb0 = 0, jb1 = 0, ib0 = 0, ib1 = 0, nx = 0, hx = 0;
+    int64_t xb = 0;                  /* first x-halo cell of an ext vector                */
+    int nb[4] = {-1, -1, -1, -1};
     int64_t nloc = 0, nlrows = 0;    /* owned cells / rows                                */
-    int64_t next = 0, nerows = 0;    /* cells / rows of an ext vector (band + 2 HALO)     */
+    int64_t next = 0, nerows = 0;    /* cells / rows of an ext vector (+ halo rows/columns) */
     int64_t own0 = 0;                /* ext cell of the first owned cell                  */
     int64_t rowintcon = -1;          /* ext row of the integral condition if owned        */
     double int_correction = 0.0;     /* THCM::intCorrection_ (setIntCondCorrection)      */
-    void* comm = nullptr;            /* ncclComm_t when nranks > 1                        */
-    void* group = nullptr;           /* in-process band group (test facility), else null  */
+    void* comm = nullptr;            /* ncclComm_t when nranks > 1 over RCCL              */
+    void* group = nullptr;           /* in-process rank group (test facility), else null  */
+    iemic_transport tp{};            /* host transport (tp.send != null), else RCCL/group  */
+    iemic::DevBuf<double> d_stage;   /* packed strided messages (RCCL)                    */
+    std::vector<double> h_stage;     /* host-staged messages (group / host transport)     */
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
     iemic::DevBuf<int> d_landm;
@@ -271,12 +281,36 @@ struct StreamGuard {
     ~StreamGuard() { if (c && c->stream) (void)hipStreamSynchronize(c->stream); }
 };
 
-/* comm.hip: sums over the ranks (no-op for one rank) and halo exchange of the ext layout */
+/* the subdomain layout handed to the structured-grid kernels */
+inline SubLay sub_lay(const iemic_ctx* c)
+{
+    SubLay X;
+    X.n = c->n; X.m = c->m; X.l = c->l; X.periodic = c->cfg.periodic;
+    X.jb0 = c->jb0; X.ib0 = c->ib0; X.nx = c->nx; X.hx = c->hx; X.xb = c->xb;
+    return X;
+}
+
+/* comm.hip: sums over the ranks (no-op for one rank) and halo exchanges.  A message is
+ * nblk blocks of len doubles, stride doubles apart, from base + off; one exchange is a
+ * list of messages in two phases (x, then y: the y messages carry the x halo, so the
+ * corner cells arrive too), each run as one batch by the transport. */
+struct Seg {
+    double* base;
+    int64_t off, nblk, len, stride;
+};
+struct Msg {
+    bool send;
+    int peer;
+    Seg s;
+};
 int allreduce_sum(iemic_ctx* c, double* dev, int count);
-int halo_exchange(iemic_ctx* c, double* ext_vec, int rows_j);
-int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int rows_j);
-/* one halo row of two arrays laid out in whole rows of slab doubles, owned [first, first+count) */
-int halo_exchange_slab2(iemic_ctx* c, double* a, double* b, int64_t first, int64_t count, int64_t slab);
+/* depth latitude rows and x columns of the ext layout (width doubles per cell) */
+int halo_exchange(iemic_ctx* c, double* ext_vec, int depth);
+int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int depth);
+/* the two phases of an exchange of arrays of the ext layout (appended to x / y) */
+void halo_plan_ext(const iemic_ctx* c, double* v, int width, int depth, std::vector<Msg>& x,
+                   std::vector<Msg>& y);
+int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
 /* drop one reference to the context (iemic_destroy, a dependent's destroy); the last one
  * frees it */

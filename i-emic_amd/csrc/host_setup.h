@@ -103,25 +103,47 @@ struct Setup {
     double dedt() const { return lvsc * eta_a * qdim_a * (1.0 / qdim_a) * dqso; }
     int rowintcon_ref = -1;          /* reference (global) row of the integral condition */
     int64_t rowintcon = -1;          /* its ext row when this band owns it, else -1       */
-    int jb0 = 0, jb1 = 0;            /* owned latitude band [jb0, jb1)                    */
-    int64_t nloc = 0, next = 0;      /* owned cells, cells incl. HALO rows each side      */
+    /* owned subdomain [ib0, ib1) x [jb0, jb1) of the Decomp2D process grid, full depth;
+     * hx = HALO x-halo columns when the x direction is split (stencil.h ext layout) */
+    int jb0 = 0, jb1 = 0, ib0 = 0, ib1 = 0, nx = 0, hx = 0;
+    int64_t xb = 0;                  /* first x-halo cell                                 */
+    int64_t nloc = 0, next = 0;      /* owned cells, cells of an ext vector               */
 
     /* ---- layout helpers (see the ext layout in stencil.h) ------------------------- */
-    int64_t ext_cell(int i, int j, int k) const { return (((int64_t)j - jb0 + HALO) * l + k) * n + i; }
+    /* ext cell of 0-based global (i, j, k), j within the halo rows, i within the x halo
+     * (after the global wrap) */
+    int64_t ext_cell(int i, int j, int k) const
+    {
+        const int64_t r = ((int64_t)j - jb0 + HALO) * l + k;
+        return xcell(r, xlocal(i, n, ib0, nx, hx, hx ? cfg.periodic : 0), nx, hx, xb);
+    }
     int64_t ref_cell(int i, int j, int k) const { return ((int64_t)k * m + j) * n + i; }
-    int64_t own0() const { return (int64_t)HALO * l * n; }        /* first owned ext cell  */
+    int64_t own0() const { return (int64_t)HALO * l * nx; }       /* first owned ext cell  */
     /* owned-local index lc -> 0-based (i, j, k) */
     void owned_ijk(int64_t lc, int& i, int& j, int& k) const
     {
-        i = (int)(lc % n);
-        k = (int)((lc / n) % l);
-        j = jb0 + (int)(lc / ((int64_t)n * l));
+        i = ib0 + (int)(lc % nx);
+        k = (int)((lc / nx) % l);
+        j = jb0 + (int)(lc / ((int64_t)nx * l));
     }
+    /* ext cell -> 0-based global (i, j, k) (i wrapped into the grid) */
     void ext_ijk(int64_t ec, int& i, int& j, int& k) const
     {
-        i = (int)(ec % n);
-        k = (int)((ec / n) % l);
-        j = jb0 - HALO + (int)(ec / ((int64_t)n * l));
+        int64_t r;
+        int il;
+        if (ec < xb) {
+            r = ec / nx;
+            il = (int)(ec % nx);
+        } else {
+            r = (ec - xb) / (2 * hx);
+            const int h = (int)((ec - xb) % (2 * hx));
+            il = h < hx ? h - hx : nx + h - hx;
+        }
+        k = (int)(r % l);
+        j = jb0 - HALO + (int)(r / l);
+        i = ib0 + il;
+        if (i < 0) i += n;
+        if (i >= n) i -= n;
     }
     int64_t ext_to_ref_row(int64_t er) const
     {
@@ -129,16 +151,24 @@ struct Setup {
         ext_ijk(er / NUN, i, j, k);
         return NUN * ref_cell(i, j, k) + er % NUN;
     }
-    bool owns_j(int j) const { return j >= jb0 && j < jb1; }
+    bool owns(int i, int j) const { return j >= jb0 && j < jb1 && i >= ib0 && i < ib1; }
 
-    void init(const iemic_grid& g, const int* landm_in, int band0 = 0, int band1 = -1)
+    /* sub0/sub1: owned columns [sub0[0], sub1[0]) and rows [sub0[1], sub1[1]); xsplit: the x
+     * direction is split over several ranks (x halo in the layout) */
+    void init(const iemic_grid& g, const int* landm_in, const int* sub0 = nullptr, const int* sub1 = nullptr,
+              int xsplit = 0)
     {
         cfg = g;
         n = g.n; m = g.m; l = g.l;
-        jb0 = band0;
-        jb1 = band1 < 0 ? m : band1;
-        nloc = (int64_t)n * l * (jb1 - jb0);
-        next = (int64_t)n * l * (jb1 - jb0 + 2 * HALO);
+        ib0 = sub0 ? sub0[0] : 0;
+        ib1 = sub1 ? sub1[0] : n;
+        jb0 = sub0 ? sub0[1] : 0;
+        jb1 = sub1 ? sub1[1] : m;
+        nx = ib1 - ib0;
+        hx = xsplit ? HALO : 0;
+        nloc = (int64_t)nx * l * (jb1 - jb0);
+        xb = (int64_t)nx * l * (jb1 - jb0 + 2 * HALO);
+        next = xb + (int64_t)2 * hx * l * (jb1 - jb0 + 2 * HALO);
         xmin = g.xmin * pi_ / 180.0;
         xmax = g.xmax * pi_ / 180.0;
         ymin = g.ymin * pi_ / 180.0;
@@ -159,7 +189,7 @@ struct Setup {
             int Nic = g.int_i == -1 ? n - 1 : g.int_i;
             int Mic = g.int_j == -1 ? m - 1 : g.int_j;
             rowintcon_ref = (int)(NUN * ref_cell(Nic, Mic, l - 1) + SS);
-            if (owns_j(Mic)) rowintcon = NUN * ext_cell(Nic, Mic, l - 1) + SS;
+            if (owns(Nic, Mic)) rowintcon = NUN * ext_cell(Nic, Mic, l - 1) + SS;
         }
         grid();
         stpnt();
@@ -340,14 +370,14 @@ struct Setup {
         int64_t pos = 0, r = 0;
         for (int k = 0; k < l; k++)
             for (int j = jb0; j < jb1; j++)
-                for (int i = 0; i < n; i++)
+                for (int i = ib0; i < ib1; i++)
                     for (int var = 0; var < NUN; var++, r++) {
                         if (rowptr) rowptr[r] = pos;
                         graph_row(i, j, k, var, cols, slot);
                         if (col)
                             for (size_t a = 0; a < cols.size(); a++) col[pos + a] = (int)cols[a];
                         if (val) {
-                            const int64_t lc = (((int64_t)j - jb0) * l + k) * n + i;
+                            const int64_t lc = (((int64_t)j - jb0) * l + k) * nx + (i - ib0);
                             if (NUN * ref_cell(i, j, k) + var == rowintcon_ref)
                                 for (size_t a = 0; a < cols.size(); a++) {
                                     const int64_t q = cols[a] / NUN;
@@ -391,6 +421,10 @@ struct Setup {
         Geo g{};
         g.n = n; g.m = m; g.l = l;
         g.jb0 = jb0;
+        g.ib0 = ib0;
+        g.nx = nx;
+        g.hx = hx;
+        g.xb = xb;
         g.periodic = cfg.periodic;
         g.tres = cfg.tres; g.sres = cfg.sres; g.coriolis_on = cfg.coriolis_on;
         g.dx = dx; g.dy = dy; g.dz = dz;

@@ -25,17 +25,17 @@ namespace iemic {
 
 /* ---- SpMV ------------------------------------------------------------------------ */
 /* row R of one cell: slot-major coefficients (coalesced over adjacent cells) times the
- * implicit-column gathers; rb / ii are the (dk, dj) row bases and the i offsets */
+ * implicit-column gathers; nc: the neighbour cells (nb_cells) */
 template <int R>
 __device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, const double* __restrict__ x,
-                                             int64_t lc, int64_t nloc, const int* rb, const int* ii)
+                                             int64_t lc, int64_t nloc, const int (*nc)[9])
 {
     constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
     double acc = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const Slot sl = SLOTS[B + s];
-        const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
+        const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
         acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * (int64_t)cidx + sl.var];
     }
     return acc;
@@ -78,34 +78,35 @@ __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, i
         acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
     }
 }
-__global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic, int jb0,
-                                               const double* __restrict__ val,
+__global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restrict__ val,
                                                const double* __restrict__ x,
                                                double* __restrict__ y, int nloc, int ntile, int tpr)
 {
     __shared__ double xs[6 * (SP7_T + 2) * NUN];
     __shared__ double red[4][3][SP7_T];
+    const int l = X.l, nx = X.nx;
     const int per = (ntile + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     if (tile >= ntile) return;
     const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
-    const int k = row % l, jl = row / l, j = jb0 + jl;
-    const int nc = min(SP7_T, n - i0);
-    const int lc0 = row * n + i0;
+    const int k = row % l, jl = row / l, j = X.jb0 + jl;
+    const int nc = min(SP7_T, nx - i0);
+    const int lc0 = row * nx + i0;
     const int t = threadIdx.x, c = t & 63, g = t >> 6;
-    /* stage x: 6 grid rows x (nc + 2) cells x 6 unknowns, contiguous runs */
+    /* stage x: 6 grid rows x (nc + 2) cells x 6 unknowns, contiguous runs (the two end
+     * cells: the neighbour columns, from the x halo when the x direction is split) */
     {
-        const int jm = j > 0 ? j - 1 : j, jp = j < m - 1 ? j + 1 : j;
+        const int jm = j > 0 ? j - 1 : j, jp = j < X.m - 1 ? j + 1 : j;
         const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
         const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
-        const int il = i0 > 0 ? i0 - 1 : (periodic ? n - 1 : 0);
-        const int ir = i0 + nc < n ? i0 + nc : (periodic ? 0 : n - 1);
         const int per_row = (nc + 2) * NUN;
         for (int e = t; e < 6 * per_row; e += 256) {
             const int q = e / per_row, w = e - q * per_row;
             const int p = w / NUN, var = w - p * NUN;
-            const int i = p == 0 ? il : (p == nc + 1 ? ir : i0 + p - 1);
-            const int64_t cell = ((int64_t)(rj[q] - jb0 + HALO) * l + rk[q]) * n + i;
+            const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
+            const int64_t cell = (p == 0 || p == nc + 1)
+                                     ? xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb)
+                                     : r * nx + i0 + p - 1;
             xs[(q * (SP7_T + 2) + p) * NUN + var] = x[NUN * cell + var];
         }
     }
@@ -138,7 +139,7 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
         case 4: v = red[2][2][cc] + red[3][0][cc]; break;
         default: v = red[3][1][cc]; break;
         }
-        y[NUN * ((int64_t)HALO * l * n + lc0) + o] = v;
+        y[NUN * ((int64_t)HALO * l * nx + lc0) + o] = v;
     }
 }
 
@@ -147,8 +148,7 @@ __global__ void __launch_bounds__(256) k_spmv7(int n, int m, int l, int periodic
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
  * full rows of the SpMV are used: one wavefront per (64 cells, dynamics equation). */
-__global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int periodic, int jb0,
-                                                  const double* __restrict__ val,
+__global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
                                                   const uint8_t* __restrict__ known,
@@ -160,28 +160,20 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(int n, int m, int l, int perio
     const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
     if (lc >= nloc) return;
     const int R = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
-    int ii[3] = {i - 1, i, i + 1};
-    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
-    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
-    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
-    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
-    int rb[9];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - jb0 + HALO) * l + kk[a]) * n;
-    const int64_t row = NUN * ((int64_t)HALO * l * n + lc) + R;
+    const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
+    int nc[3][9];
+    nb_cells(X, il, j, k, nc);
+    const int64_t row = NUN * ((int64_t)HALO * X.l * X.nx + lc) + R;
     if (known[row]) {
         d[row] = 0.0;
         return;
     }
     double acc;
     switch (R) {
-    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, rb, ii); break;
-    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, rb, ii); break;
-    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, rb, ii); break;
-    default: acc = row_dot_rb<PP>(val, z, lc, nloc, rb, ii); break;
+    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, nc); break;
+    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, nc); break;
+    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, nc); break;
+    default: acc = row_dot_rb<PP>(val, z, lc, nloc, nc); break;
     }
     d[row] = r[row] - acc;
 }
@@ -190,8 +182,8 @@ int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_
 {
     const int nblk = (int)((c->nloc + 63) / 64);
     const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, c->n, c->m, c->l, c->cfg.periodic,
-                       c->jb0, c->d_val.p, z, r, known, d, c->nloc, nblk);
+    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, known, d,
+                       c->nloc, nblk);
     return 0;
 }
 
@@ -452,11 +444,11 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
         set_error("spmv: more than 2^31 cells per rank");
         return IEMIC_EINVAL;
     }
-    const int tpr = (c->n + SP7_T - 1) / SP7_T;
-    const int ntile = (int)(c->nloc / c->n) * tpr;
+    const int tpr = (c->nx + SP7_T - 1) / SP7_T;
+    const int ntile = (int)(c->nloc / c->nx) * tpr;
     const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-    hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, c->n, c->m, c->l, c->cfg.periodic, c->jb0,
-                       c->d_val.p, x, y, (int)c->nloc, ntile, tpr);
+    hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, y, (int)c->nloc, ntile,
+                       tpr);
     if (c->su.rowintcon_ref >= 0) {
         /* dense intcond row: y[rowintcon] = intSign * coeff . x (summed over the ranks) */
         const int64_t o = NUN * c->own0;
@@ -874,14 +866,14 @@ __global__ void __launch_bounds__(256) k_lincomb(LinComb L, double* y, int64_t N
 /* the IDR shadow space P: s vectors uniform in [-1, 1] from splitmix64 over the global
  * row index (identical for every band split), orthonormalised (IDRSolver::createP) */
 __global__ void k_idr_random(double* __restrict__ P, int64_t ldp, int s, int64_t NL, int64_t row0,
-                             int n, int m, int l, int jb0)
+                             int n, int m, int l, int jb0, int ib0, int nx)
 {
     const int64_t lr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lr >= NL) return;
     /* owned row -> global reference row 6((k m + j) n + i) + v */
     const int64_t lc = lr / NUN;
     const int v = (int)(lr % NUN);
-    const int i = (int)(lc % n), k = (int)((lc / n) % l), j = jb0 + (int)(lc / ((int64_t)n * l));
+    const int i = ib0 + (int)(lc % nx), k = (int)((lc / nx) % l), j = jb0 + (int)(lc / ((int64_t)nx * l));
     const uint64_t g = (uint64_t)(NUN * (((int64_t)k * m + j) * n + i) + v);
     for (int q = 0; q < s; q++) {
         uint64_t z = 0x9E3779B97F4A7C15ull * (g * 16 + (uint64_t)q + 1) + 20261015ull;
@@ -943,7 +935,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
     const unsigned GR = grid_for(NL);
     /* shadow space (createP: random, orthonormalised in order) */
     hipLaunchKernelGGL(k_idr_random, dim3((unsigned)((NL + 255) / 256)), dim3(256), 0, c->stream, P, NE, s, NL,
-                       o, c->n, c->m, c->l, c->jb0);
+                       o, c->n, c->m, c->l, c->jb0, c->ib0, c->nx);
     for (int j = 0; j < s; j++) {
         std::vector<double> al(j + 1);
         if (j > 0 && (rc = mdot_host(c, P + o, NE, j, Pi(j) + o, al.data()))) return rc;

@@ -45,21 +45,31 @@ constexpr int S_PW0 = 62, S_PWM = 63;               /* P row: W(k), W(k-1)      
 constexpr int S_TT0 = 64, S_TS0 = 81;               /* T row: T self, S self            */
 constexpr int S_SS0 = 84, S_ST0 = 101;              /* S row: S self, T self            */
 
-/* band layout seen by the kernels (stencil.h ext layout); per-cell arrays are indexed by
- * ext cell, the Jacobian by owned cell (ext cell - own0) */
+/* subdomain layout seen by the kernels (stencil.h ext layout, Decomp2D): n, m global;
+ * owned columns [ib0, ib0 + nx), rows from jb0; per-cell arrays are indexed by ext cell,
+ * the Jacobian by owned cell (ext cell - own0: the owned cells are one slab) */
 struct Lay {
-    int n, m, l, periodic, jb0;
-    int64_t nloc, own0;
+    int n, m, l, periodic, jb0, ib0, nx, hx;
+    int64_t nloc, own0, xb;
 };
+/* ext cell of global (i, j, k) (i in the grid after hnb's wrap; the x halo when split) */
 __device__ __forceinline__ int64_t ecell(const Lay& L, int i, int j, int k)
 {
-    return (((int64_t)j - L.jb0 + HALO) * L.l + k) * L.n + i;
+    const int64_t r = ((int64_t)j - L.jb0 + HALO) * L.l + k;
+    return xcell(r, xlocal(i, L.n, L.ib0, L.nx, L.hx, L.hx ? L.periodic : 0), L.nx, L.hx, L.xb);
 }
 __device__ __forceinline__ void lc_ijk(const Lay& L, int64_t lc, int& i, int& j, int& k)
 {
-    i = (int)(lc % L.n);
-    k = (int)((lc / L.n) % L.l);
-    j = L.jb0 + (int)(lc / ((int64_t)L.n * L.l));
+    i = L.ib0 + (int)(lc % L.nx);
+    k = (int)((lc / L.nx) % L.l);
+    j = L.jb0 + (int)(lc / ((int64_t)L.nx * L.l));
+}
+__device__ __forceinline__ SubLay sub_of(const Lay& L)
+{
+    SubLay X;
+    X.n = L.n; X.m = L.m; X.l = L.l; X.periodic = L.periodic;
+    X.jb0 = L.jb0; X.ib0 = L.ib0; X.nx = L.nx; X.hx = L.hx; X.xb = L.xb;
+    return X;
 }
 #define LAY_ALIASES const int n = L.n, m = L.m, l = L.l, periodic = L.periodic; (void)n; (void)m; (void)l; (void)periodic
 /* thread -> owned cell: lc (Jacobian column), cell (ext), (i, j, k) */
@@ -144,7 +154,7 @@ __global__ void k_cell_factors(const double* __restrict__ val, const uint8_t* __
      * the row's own W (or -1/b_k with b_k that of W(k-1) when the own W is an identity) */
     double w = 0.0;
     if (!kn[PP]) {
-        const int64_t nm = L.n;                 /* k - 1 is one row of n cells back */
+        const int64_t nm = L.nx;                /* k - 1 is one row of nx cells back */
         const bool w_own = !kn[WW];
         const bool w_below = k > 0 && !known[NUN * (cell - nm) + WW];
         if (w_own && V(S_PW0) != 0.0) w = 1.0 / V(S_PW0);
@@ -166,10 +176,10 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
 {
     LAY_ALIASES;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)n * (jb1 - L.jb0) * 9) return;
+    if (t >= (int64_t)L.nx * (jb1 - L.jb0) * 9) return;
     const int q = (int)(t / 9), o = (int)(t % 9);
     const int di = o % 3 - 1, dj = o / 3 - 1;
-    const int i = q % n, j = L.jb0 + q / n;
+    const int i = L.ib0 + q % L.nx, j = L.jb0 + q / L.nx;
     const int c = col_of_ij[j * n + i];
     if (c < 0) return;
     double* row = S9 + (int64_t)c * 9;
@@ -672,8 +682,8 @@ __global__ void k_ts_compact(const double* __restrict__ val, const uint8_t* __re
 #define BAND_COLUMN                                                                      \
     const int t_ = blockIdx.x * blockDim.x + threadIdx.x;                                \
     if (t_ >= (int)(L.nloc / L.l)) return;                                               \
-    const int ij = L.jb0 * L.n + t_;                                                     \
-    const int i = ij % L.n, j = ij / L.n;                                                \
+    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;                              \
+    const int ij = j * L.n + i;                                                          \
     const int64_t ncell = L.nloc
 
 __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restrict__ known,
@@ -716,8 +726,8 @@ __global__ void __launch_bounds__(256) k_gs_ptil_scan(const double* __restrict__
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;                  /* whole column groups exit */
-    const int ij = L.jb0 * L.n + t_;
-    const int i = ij % L.n, j = ij / L.n;
+    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
+    const int ij = j * L.n + i;
     const int64_t ncell = L.nloc;
     double A = 0.0, B = 0.0;
     bool pa = false;
@@ -761,8 +771,8 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;
-    const int ij = L.jb0 * L.n + t_;
-    const int i = ij % L.n, j = ij / L.n;
+    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
+    const int ij = j * L.n + i;
     const int64_t ncell = L.nloc;
     double A = 0.0, B = 0.0, pb = 0.0, zp = 0.0;
     bool pa = false, wa = false;
@@ -919,8 +929,8 @@ __global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__
     const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
     const int k = threadIdx.x % P;
     if (t_ >= (int)(L.nloc / L.l)) return;
-    const int ij = L.jb0 * L.n + t_;
-    const int i = ij % L.n, j = ij / L.n;
+    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
+    const int ij = j * L.n + i;
     /* ocol: this band's entry of the column (pinned: -2 - entry, written 0; -1: none),
      * loaded with the rest (no gating round) */
     const int q = ocol[ij];
@@ -1214,7 +1224,7 @@ __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __rest
  * kmask instead of a byte gather per slot.  Dealt to the XCDs in contiguous runs. */
 template <int R>
 __device__ __forceinline__ double bts_row(const double* __restrict__ val, const double* __restrict__ z,
-                                          int64_t lc, int64_t nloc, const int* rb, const int* ii,
+                                          int64_t lc, int64_t nloc, const int (*nc)[9],
                                           uint64_t kbits, double acc)
 {
     constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
@@ -1225,7 +1235,7 @@ __device__ __forceinline__ double bts_row(const double* __restrict__ val, const 
         /* identity-row columns (coupling already in rr) weigh 0: no branch, so the loads of
          * all the row's slots issue together */
         const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : val[(int64_t)(B + s) * nloc + lc];
-        const int cidx = rb[(sl.dk + 1) * 3 + (sl.dj + 1)] + ii[sl.di + 1];
+        const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
         acc -= v * z[NUN * (int64_t)cidx + sl.var];
     }
     return acc;
@@ -1247,22 +1257,14 @@ __global__ void __launch_bounds__(128) k_gs_bts2(const double* __restrict__ val,
     int i, j, k;
     lc_ijk(L, lc, i, j, k);
     const int64_t cell = L.own0 + lc;
-    int ii[3] = {i - 1, i, i + 1};
-    if (ii[0] < 0) ii[0] = periodic ? n - 1 : i;
-    if (ii[2] >= n) ii[2] = periodic ? 0 : i;
-    const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
-    const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
-    int rb[9];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - L.jb0 + HALO) * l + kk[a]) * n;
+    int nc[3][9];
+    nb_cells(sub_of(L), i - L.ib0, j, k, nc);
     const int64_t row = NUN * cell + R;
     double acc = 0.0;
     if (!known[row]) {
         const uint64_t kb = kmask[2 * cell + 1];
-        acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, rb, ii, kb, rr[row])
-                      : bts_row<SS>(val, z, lc, L.nloc, rb, ii, kb, rr[row]);
+        acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, nc, kb, rr[row])
+                      : bts_row<SS>(val, z, lc, L.nloc, nc, kb, rr[row]);
     }
     const int64_t half = L.nloc / 2;
     const int c = (i + j + k) & 1;
@@ -1316,18 +1318,18 @@ __global__ void __launch_bounds__(256) k_gs_ts_half_c(const double* __restrict__
     const int64_t half = L.nloc / 2;
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= half) return;
-    const int64_t row = (2 * q) / n;                 /* (j - jb0) * l + k */
+    const int nx = L.nx;
+    const int64_t row = (2 * q) / nx;                /* (j - jb0) * l + k */
     const int k = (int)(row % l), j = L.jb0 + (int)(row / l);
-    const int64_t lc = 2 * q + ((j + k + c) & 1);
-    const int i = (int)(lc - row * n);
+    const int64_t lc = 2 * q + ((j + k + c) & 1);    /* ib0 even: local parity = global */
+    const int il = (int)(lc - row * nx);
     const int64_t cell = L.own0 + lc;
-    int im = i - 1, ip = i + 1;
-    if (periodic) { if (im < 0) im = n - 1; if (ip >= n) ip = 0; }
-    else { if (im < 0) im = i; if (ip >= n) ip = i; }
-    const int64_t ln = (int64_t)l * n;
-    const int64_t base = cell - i;
-    const int64_t nb[6] = {base + im, base + ip, j > 0 ? cell - ln : cell, j < m - 1 ? cell + ln : cell,
-                           k > 0 ? cell - n : cell, k < l - 1 ? cell + n : cell};
+    const int64_t r = row + (int64_t)HALO * l;
+    const int64_t ln = (int64_t)l * nx;
+    const int64_t nb[6] = {xnb_cell(r, il - 1, n, L.ib0, nx, L.hx, periodic, L.xb),
+                           xnb_cell(r, il + 1, n, L.ib0, nx, L.hx, periodic, L.xb),
+                           j > 0 ? cell - ln : cell, j < m - 1 ? cell + ln : cell,
+                           k > 0 ? cell - nx : cell, k < l - 1 ? cell + nx : cell};
     const double* a = tsc + (int64_t)(c * TS_NC) * half + q;
     double rt = bc[(int64_t)(c * 2) * half + q], rs = bc[(int64_t)(c * 2 + 1) * half + q];
 #pragma unroll
@@ -1364,7 +1366,8 @@ __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __
  *     cell = ((jl + hj) * n + i) * l + k,
  * so the P lanes of a column (lane = level k) read one contiguous run of every array and
  * a horizontal neighbour is again one whole run (one 128-B line per array at l = 16);
- * hj = 1 halo row on each side on level 0 of a band group (refreshed by exchanges).
+ * with hj = 1 halo row on each side and hi = 1 halo column (the row width is n + 2 hi) on
+ * level 0 when the y / x direction is split over ranks (refreshed by exchanges).
  * The z-lines are factorised at set-up (block Thomas, k_mg_fac: F = -A'^-1 B, A'^-1,
  * Cp = A'^-1 C per cell), so a relaxation is two affine parallel scans over the lanes
  * without a division.  Launch fusion (the apply is latency-bound):
@@ -1380,11 +1383,11 @@ __global__ void k_ts_scatter(const uint8_t* __restrict__ known, const double* __
  *   - the last colour launches of the final level-0 sweep write z(T, S) straight into the
  *     preconditioner output. */
 struct TsLev {
-    int n, mb, l, periodic;
-    int hj;                          /* halo rows of the layout (level 0 of a band group)  */
-    int vis;                         /* halo rows the smoother / residual read (0 or hj)   */
-    int jpar;                        /* colour parity of jl = 0 (global j parity, level 0) */
-    int64_t cstr;                    /* array stride (mb + 2 hj) n l                       */
+    int n, mb, l, periodic;          /* periodic: the level wraps in x (one x part)        */
+    int hj, hi;                      /* halo rows / columns of the layout (level 0, split)  */
+    int vis, visi;                   /* halo rows / columns the smoother / residual read    */
+    int jpar;                        /* colour parity of (0, 0) (global i + j, level 0)     */
+    int64_t cstr;                    /* array stride (mb + 2 hj) (n + 2 hi) l              */
     const double* off;               /* 16 x cstr: T row q 0..7, S row q 8..15            */
     const double* diag;              /* 4 x cstr: 2x2 block (TT, TS, ST, SS)              */
     const double* fac;               /* 12 x cstr: line factors F | A'^-1 | Cp            */
@@ -1393,7 +1396,7 @@ struct TsLev {
 };
 __host__ __device__ __forceinline__ int64_t mg_cell(const TsLev& V, int i, int jl, int k)
 {
-    return (((int64_t)jl + V.hj) * V.n + i) * V.l + k;
+    return (((int64_t)jl + V.hj) * (V.n + 2 * V.hi) + i + V.hi) * V.l + k;
 }
 /* neighbour q (-i,+i,-j,+j,-k,+k) of (i,jl,k): false outside the level's (visible) band */
 __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, int& k)
@@ -1407,7 +1410,7 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
     default: k++; break;
     }
     if (jl < -V.vis || jl >= V.mb + V.vis || k < 0 || k >= V.l) return false;
-    if (i < 0 || i >= V.n) {
+    if (i < -V.visi || i >= V.n + V.visi) {
         if (!V.periodic) return false;
         i = (i + V.n) % V.n;
     }
@@ -1419,8 +1422,8 @@ __device__ __forceinline__ bool mg_nb(const TsLev& V, int q, int& i, int& jl, in
 __device__ __forceinline__ void mg_nbc(const TsLev& V, int q, int& i, int& jl, int& k)
 {
     switch (q) {
-    case 0: i = i > 0 ? i - 1 : (V.periodic ? V.n - 1 : i); break;
-    case 1: i = i < V.n - 1 ? i + 1 : (V.periodic ? 0 : i); break;
+    case 0: i = i > -V.visi ? i - 1 : (V.periodic ? V.n - 1 : i); break;
+    case 1: i = i < V.n - 1 + V.visi ? i + 1 : (V.periodic ? 0 : i); break;
     case 2: jl = jl > -V.vis ? jl - 1 : jl; break;
     case 3: jl = jl < V.mb - 1 + V.vis ? jl + 1 : jl; break;
     case 4: k = k > 0 ? k - 1 : k; break;
@@ -1672,31 +1675,25 @@ __global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val
 {
     LAY_ALIASES;
     __shared__ double sb[2][64][MG_TI + 1];
-    const int tiles = (n + MG_TI - 1) / MG_TI;
+    const int nx = L.nx;
+    const int tiles = (nx + MG_TI - 1) / MG_TI;
     const int jl = blockIdx.x / tiles, i0 = (blockIdx.x % tiles) * MG_TI;
     const int j = L.jb0 + jl;
+    const SubLay X = sub_of(L);
     for (int e = threadIdx.x; e < 2 * l * MG_TI; e += blockDim.x) {
         const int R = TT + e / (l * MG_TI);
         const int k = (e / MG_TI) % l, ii = e % MG_TI, i = i0 + ii;
         double acc = 0.0;
-        if (i < n) {
-            const int64_t lc = ((int64_t)jl * l + k) * n + i;
+        if (i < nx) {
+            const int64_t lc = ((int64_t)jl * l + k) * nx + i;
             const int64_t cell = L.own0 + lc;
             const int64_t row = NUN * cell + R;
             if (!known[row]) {
-                int ix[3] = {i - 1, i, i + 1};
-                if (ix[0] < 0) ix[0] = periodic ? n - 1 : i;
-                if (ix[2] >= n) ix[2] = periodic ? 0 : i;
-                const int jj[3] = {j > 0 ? j - 1 : j, j, j < m - 1 ? j + 1 : j};
-                const int kk[3] = {k > 0 ? k - 1 : k, k, k < l - 1 ? k + 1 : k};
-                int rb[9];
-#pragma unroll
-                for (int a = 0; a < 3; a++)
-#pragma unroll
-                    for (int b = 0; b < 3; b++) rb[a * 3 + b] = ((jj[b] - L.jb0 + HALO) * l + kk[a]) * n;
+                int nc[3][9];
+                nb_cells(X, i, j, k, nc);
                 const uint64_t kb = kmask[2 * cell + 1];
-                acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, rb, ix, kb, rr[row])
-                              : bts_row<SS>(val, z, lc, L.nloc, rb, ix, kb, rr[row]);
+                acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, nc, kb, rr[row])
+                              : bts_row<SS>(val, z, lc, L.nloc, nc, kb, rr[row]);
             }
         }
         sb[R - TT][k][ii] = acc;
@@ -1706,7 +1703,7 @@ __global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val
     const bool on = k < l;
     for (int ii = grp; ii < MG_TI; ii += ng) {
         const int i = i0 + ii;
-        if (i >= n) break;
+        if (i >= nx) break;
         const int64_t c = on ? mg_cell(V, i, jl, k) : 0;
         const double bt = on ? sb[0][k][ii] : 0.0, bs = on ? sb[1][k][ii] : 0.0;
         if (on) {
@@ -1757,7 +1754,7 @@ __global__ void k_mg_pack0(const double* __restrict__ tsoff, const double* __res
                            int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag)
 {
     OWNED_CELL;
-    const int64_t c = mg_cell(V, i, j - L.jb0, k);
+    const int64_t c = mg_cell(V, i - L.ib0, j - L.jb0, k);
 #pragma unroll
     for (int e = 0; e < 16; e++) off[(int64_t)e * V.cstr + c] = tsoff[(int64_t)e * next + cell];
 #pragma unroll
@@ -1848,7 +1845,7 @@ static void band_flags(const iemic_ctx* c, const std::vector<uint8_t>& kn, std::
     const int n = c->n, m = c->m, l = c->l;
     flags.assign((size_t)2 * n * m, 0.0);
     for (int j = c->jb0; j < c->jb1; j++)
-        for (int i = 0; i < n; i++)
+        for (int i = c->ib0; i < c->ib1; i++)
             for (int k = 0; k < l; k++) {
                 const int64_t cc = c->su.ext_cell(i, j, k);
                 if (!kn[NUN * cc + PP]) flags[(size_t)j * n + i] = 1.0;
@@ -1956,7 +1953,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     std::vector<int> own(NC, -1), ocol((size_t)n * m, -1);
     for (int q = 0; q < ncol; q++) {
         const int ij = ord[q].second;
-        if (ij / n >= c->jb0 && ij / n < c->jb1) {
+        if (c->su.owns(ij % n, ij / n)) {
             own[colid[ij]] = colid[ij];
             ocol[ij] = pin[colid[ij]] ? -2 - colid[ij] : colid[ij];
         }
@@ -1995,9 +1992,13 @@ static Lay lay_of(const iemic_ctx* c)
 {
     Lay L;
     L.n = c->n; L.m = c->m; L.l = c->l; L.periodic = c->cfg.periodic; L.jb0 = c->jb0;
+    L.ib0 = c->ib0; L.nx = c->nx; L.hx = c->hx; L.xb = c->xb;
     L.nloc = c->nloc; L.own0 = c->own0;
     return L;
 }
+/* colour-compacted T/S sweeps: the owned cells of one colour are every other cell of a
+ * row (even n, nx and ib0) */
+static bool ts_compact(const iemic_ctx* c) { return (c->n & 1) == 0 && (c->nx & 1) == 0 && (c->ib0 & 1) == 0; }
 
 
 /* ---- T/S multigrid: host side ------------------------------------------------------ */
@@ -2006,16 +2007,19 @@ static TsLev mg_view(iemic_ctx* c, int q)
     BlockGS& gs = c->gs;
     TsLev V{};
     V.l = c->l;
-    V.periodic = c->cfg.periodic;
     V.n = gs.mg_n[q];
     V.mb = gs.mg_m[q];
-    /* bands: the level-0 smoother and residual see the neighbour bands' rows (halo rows in
-     * the layout, exchanged before every relaxation), colours by the global j parity so
-     * that all bands relax the same colour in the same launch; coarse levels band-local */
-    V.hj = (q == 0 && c->nranks > 1) ? 1 : 0;
+    /* subdomains: the level-0 smoother and residual see the neighbours' edge rows and
+     * columns (halo rows / columns in the layout, exchanged before every relaxation),
+     * colours by the global i + j parity so that all subdomains relax the same colour in
+     * the same launch; coarse levels subdomain-local; the x wrap only with one x part */
+    V.periodic = c->cfg.periodic && c->npx == 1;
+    V.hj = (q == 0 && c->npy > 1) ? 1 : 0;
+    V.hi = (q == 0 && c->npx > 1) ? 1 : 0;
     V.vis = V.hj;
-    V.jpar = q == 0 ? (c->jb0 & 1) : 0;
-    V.cstr = (int64_t)(V.mb + 2 * V.hj) * V.n * V.l;
+    V.visi = V.hi;
+    V.jpar = q == 0 ? ((c->jb0 + c->ib0) & 1) : 0;
+    V.cstr = (int64_t)(V.mb + 2 * V.hj) * (V.n + 2 * V.hi) * V.l;
     V.off = gs.mg_off[q].p;
     V.diag = gs.mg_diag[q].p;
     V.fac = gs.mg_fac[q].p;
@@ -2082,44 +2086,50 @@ static inline void mg_decode(int64_t t, int n, int l, int& i, int& jl, int& k)
     jl = (int)(t / ((int64_t)l * n));
 }
 
-/* Bands: the coarsest T/S level as one global problem.  Unknown (J, i, k, var) of the
- * stacked bands' coarsest grids (J = band row offset + local row) is 2((J nc + i) l + k)
- * + var, a band matrix of half-width 2 l nc + 1.  Every rank writes its own rows — its
- * band-local coarsest operator plus the couplings of its edge rows to the neighbour
- * bands' edge aggregates, taken from the level-0 couplings across the band edge (the
- * Galerkin sum of piecewise-constant aggregates) — the rows are summed over the ranks,
+/* Subdomains: the coarsest T/S level as one global problem.  The ranks' coarsest grids
+ * tile a GX x GY coarse grid (rank (px, py) at column offset ioff[px], row offset joff[py]);
+ * unknown (J, I, k, var) is 2((J GX + I) l + k) + var, a band matrix of half-width
+ * 2 l GX + 1 (+ the periodic wrap inside a row).  Every rank writes its own rows -- its
+ * local coarsest operator plus the couplings of its edge aggregates to the neighbours'
+ * edge aggregates, taken from the level-0 couplings across the subdomain edges (the
+ * Galerkin sum of piecewise-constant aggregates) -- the rows are summed over the ranks,
  * and every rank factorises (k_band_lu) and inverts (k_band_inv_pan) the whole matrix. */
 static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const std::vector<double>& dg)
 {
     BlockGS& gs = c->gs;
     gs.mg_glob = 0;
     if (c->nranks <= 1 || c->l > 64) return 0;
-    const int P = c->nranks, me = c->rank, l = c->l, qc = gs.mg_nlev - 1;
+    const int P = c->nranks, l = c->l, qc = gs.mg_nlev - 1;
     const int nc = gs.mg_n[qc], cm = gs.mg_m[qc], mb = c->jb1 - c->jb0;
     const int64_t ncl = (int64_t)nc * cm * l;
     int rc;
-    /* coarsest rows of every band */
-    std::vector<double> rows(P, 0.0);
-    rows[me] = cm;
+    /* coarsest columns / rows of every rank: offsets of its rank column / row */
+    std::vector<double> dims(2 * P, 0.0);
+    dims[2 * c->rank] = nc;
+    dims[2 * c->rank + 1] = cm;
     {
         DevBuf<double> rb;
-        if (rb.alloc(P)) return IEMIC_ENOMEM;
-        if ((rc = h2d(c, rb.p, rows.data(), sizeof(double) * P))) return rc;
-        if ((rc = allreduce_sum(c, rb.p, P))) return rc;
-        if ((rc = d2h(c, rows.data(), rb.p, sizeof(double) * P))) return rc;
+        if (rb.alloc(2 * P)) return IEMIC_ENOMEM;
+        if ((rc = h2d(c, rb.p, dims.data(), sizeof(double) * 2 * P))) return rc;
+        if ((rc = allreduce_sum(c, rb.p, 2 * P))) return rc;
+        if ((rc = d2h(c, dims.data(), rb.p, sizeof(double) * 2 * P))) return rc;
     }
-    std::vector<int> joff(P + 1, 0);
-    for (int r = 0; r < P; r++) joff[r + 1] = joff[r] + (int)rows[r];
-    const int MG = joff[P];
-    const int NG = 2 * nc * MG * l;
-    const int bl = 2 * l * nc + 1, bu = bl, W = 2 * bl + bu + 1;
+    std::vector<int> ioff(c->npx + 1, 0), joff(c->npy + 1, 0);
+    for (int px = 0; px < c->npx; px++) ioff[px + 1] = ioff[px] + (int)dims[2 * px];
+    for (int py = 0; py < c->npy; py++) joff[py + 1] = joff[py] + (int)dims[2 * (py * c->npx) + 1];
+    const int GX = ioff[c->npx], GY = joff[c->npy];
+    const int I0 = ioff[c->px], J0 = joff[c->py];
+    const int NG = 2 * GX * GY * l;
+    const int bl = 2 * l * GX + 1, bu = bl, W = 2 * bl + bu + 1;
     {
         /* LDS of the band kernels (same rules as the Schur band) */
         const size_t lb = sizeof(double) * ((size_t)(NBP + bl) * (NBP + 1) + (size_t)NBP * (bl + bu));
         const size_t li = sizeof(double) * (size_t)(std::max(bl + NBP + 1, bl + bu + 1) + 2 * NBP) * 16;
-        if (lb > 150 * 1024 || li > 150 * 1024 || (int64_t)NG * W > INT32_MAX) return 0;   /* stay band-local */
+        if (lb > 150 * 1024 || li > 150 * 1024 || (int64_t)NG * W > INT32_MAX) return 0;   /* stay local */
     }
-    auto gidx = [&](int J, int i, int k, int var) { return 2 * ((J * nc + i) * l + k) + var; };
+    const bool wrap = c->cfg.periodic != 0;
+    auto gidx = [&](int J, int I, int k, int var) { return 2 * ((J * GX + I) * l + k) + var; };
+    auto gwrap = [&](int I) { return I < 0 ? I + GX : (I >= GX ? I - GX : I); };
     std::vector<double> H((size_t)NG * W, 0.0);
     auto add = [&](int row, int col, double v) {
         const int d = col - row;
@@ -2128,14 +2138,14 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
         return true;
     };
     bool ok = true;
+    const bool lwrap = wrap && c->npx == 1;           /* the local level wraps in x */
     for (int64_t t = 0; t < ncl; t++) {
         int i, jl, k;
         mg_decode(t, nc, l, i, jl, k);
-        const int J = joff[me] + jl;
         for (int R = 0; R < 2; R++) {
-            const int row = gidx(J, i, k, R);
-            ok &= add(row, gidx(J, i, k, R), dg[(3 * R) * ncl + t]);
-            ok &= add(row, gidx(J, i, k, 1 - R), dg[(1 + R) * ncl + t]);
+            const int row = gidx(J0 + jl, I0 + i, k, R);
+            ok &= add(row, gidx(J0 + jl, I0 + i, k, R), dg[(3 * R) * ncl + t]);
+            ok &= add(row, gidx(J0 + jl, I0 + i, k, 1 - R), dg[(1 + R) * ncl + t]);
             for (int qq = 0; qq < 8; qq++) {
                 const double v = off[(8 * R + qq) * ncl + t];
                 if (v == 0.0) continue;
@@ -2150,45 +2160,51 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
                 }
                 if (jj < 0 || jj >= cm || kk < 0 || kk >= l) continue;
                 if (ii < 0 || ii >= nc) {
-                    if (!c->cfg.periodic) continue;
+                    if (!lwrap) continue;
                     ii = (ii + nc) % nc;
                 }
-                ok &= add(row, gidx(joff[me] + jj, ii, kk, qq < 6 ? R : 1 - R), v);
+                ok &= add(row, gidx(J0 + jj, I0 + ii, kk, qq < 6 ? R : 1 - R), v);
             }
         }
     }
-    /* cross-band couplings: level-0 T/S couplings of the band's first (-j) and last (+j)
-     * latitude rows, summed into the edge aggregates */
+    /* cross-subdomain couplings: level-0 T/S couplings of the first / last latitude row (-j /
+     * +j) and the first / last column (-i / +i), summed into the edge aggregates */
     {
-        const int64_t slab = (int64_t)l * c->n;
-        std::vector<double> e(slab);
-        for (int side = 0; side < 2; side++) {
-            if (side == 0 && me == 0) continue;
-            if (side == 1 && me == P - 1) continue;
-            const int jl = side == 0 ? 0 : mb - 1;
-            const int Jsrc = joff[me] + (jl >> qc);
-            const int Jdst = side == 0 ? joff[me] - 1 : joff[me + 1];
+        const int64_t nx = c->nx, slab = (int64_t)l * nx;
+        std::vector<double> e((size_t)slab * mb);
+        for (int dir = 0; dir < 4; dir++) {
+            if (c->nb[dir] < 0) continue;
+            const int q = dir == 0 ? 0 : dir == 1 ? 1 : dir == 2 ? 2 : 3;   /* -i, +i, -j, +j */
             for (int R = 0; R < 2; R++) {
-                const int q = side == 0 ? 2 : 3;
-                const double* src = gs.tsoff.p + (int64_t)(R * 8 + q) * c->next + c->own0 + (int64_t)jl * slab;
-                if ((rc = d2h(c, e.data(), src, sizeof(double) * slab))) return rc;
-                for (int k = 0; k < l; k++)
-                    for (int i = 0; i < c->n; i++) {
-                        const double v = e[(int64_t)k * c->n + i];
-                        if (v != 0.0)
-                            ok &= add(gidx(Jsrc, i >> qc, k, R), gidx(Jdst, i >> qc, k, R), v);
-                    }
+                /* the owned rows of coupling q of row R (ext layout: one slab) */
+                const double* src = gs.tsoff.p + (int64_t)(R * 8 + q) * c->next + c->own0;
+                if ((rc = d2h(c, e.data(), src, sizeof(double) * e.size()))) return rc;
+                for (int jl = 0; jl < mb; jl++)
+                    for (int k = 0; k < l; k++)
+                        for (int il = 0; il < nx; il++) {
+                            const bool edge = dir == 0 ? il == 0 : dir == 1 ? il == nx - 1 : dir == 2 ? jl == 0 : jl == mb - 1;
+                            if (!edge) continue;
+                            const double v = e[((int64_t)jl * l + k) * nx + il];
+                            if (v == 0.0) continue;
+                            const int Is = I0 + (il >> qc), Js = J0 + (jl >> qc);
+                            const int Id = dir == 0 ? gwrap(I0 - 1) : dir == 1 ? gwrap(ioff[c->px + 1]) : Is;
+                            const int Jd = dir == 2 ? J0 - 1 : dir == 3 ? joff[c->py + 1] : Js;
+                            ok &= add(gidx(Js, Is, k, R), gidx(Jd, Id, k, R), v);
+                        }
             }
         }
     }
-    if (!ok) return 0;                        /* outside the assumed band: stay band-local */
+    if (!ok) return 0;                        /* outside the assumed band: stay local */
     /* own rows without entries (inactive unknowns) become identity rows */
-    const int g0 = gidx(joff[me], 0, 0, 0), g1 = gidx(joff[me + 1], 0, 0, 0);
-    for (int row = g0; row < g1; row++) {
-        bool any = false;
-        for (int d = 0; d < W; d++) any |= H[(size_t)row * W + d] != 0.0;
-        if (!any) H[(size_t)row * W + bl] = 1.0;
-    }
+    for (int jl = 0; jl < cm; jl++)
+        for (int i = 0; i < nc; i++)
+            for (int k = 0; k < l; k++)
+                for (int R = 0; R < 2; R++) {
+                    const int row = gidx(J0 + jl, I0 + i, k, R);
+                    bool any = false;
+                    for (int d = 0; d < W; d++) any |= H[(size_t)row * W + d] != 0.0;
+                    if (!any) H[(size_t)row * W + bl] = 1.0;
+                }
     const size_t npan = (size_t)(NG + NBP - 1) / NBP;
     if (gs.mg_gband.n < (size_t)NG * W) {
         if (gs.mg_gband.alloc((size_t)NG * W) || gs.mg_gX.alloc((size_t)NG * NG) ||
@@ -2213,7 +2229,7 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
         int info = 0;
         HIP_OK(hipGetLastError());
         if ((rc = d2h(c, &info, gs.mg_ginfo.p, sizeof(int)))) return rc;
-        if (info != 0) return 0;              /* singular global coarse problem: band-local */
+        if (info != 0) return 0;              /* singular global coarse problem: local */
         const int ring = std::max(bl + NBP + 1, bl + bu + 1);
         const size_t li = (size_t)(ring + 2 * NBP) * 16 * sizeof(double);
         HIP_OK(hipFuncSetAttribute((const void*)k_band_inv_pan<16, false>,
@@ -2224,30 +2240,36 @@ static int mg_global_setup(iemic_ctx* c, const std::vector<double>& off, const s
         HIP_OK(hipGetLastError());
     }
     gs.mg_gN = NG;
-    gs.mg_g0 = g0;
+    gs.mg_gGX = GX;
+    gs.mg_gI0 = I0;
+    gs.mg_gJ0 = J0;
     gs.mg_glob = 1;
     return 0;
 }
 
+/* global index of local coarsest cell t (rank offsets I0, J0 in the GX-wide coarse grid) */
+__device__ __forceinline__ int64_t mg_gq(int64_t t, int nc, int l, int GX, int I0, int J0)
+{
+    const int k = (int)(t % l), i = (int)((t / l) % nc), jl = (int)(t / ((int64_t)l * nc));
+    return 2 * ((((int64_t)J0 + jl) * GX + I0 + i) * l + k);
+}
 /* local coarsest rhs (T block, S block) -> its entries of the global vector */
-__global__ void k_mg_gput(const double* __restrict__ b, int64_t ncl, int nc, int l, int g0,
+__global__ void k_mg_gput(const double* __restrict__ b, int64_t ncl, int nc, int l, int GX, int I0, int J0,
                           double* __restrict__ g)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ncl) return;
-    const int k = (int)(t % l), i = (int)((t / l) % nc), jl = (int)(t / ((int64_t)l * nc));
-    const int64_t q = g0 + 2 * (((int64_t)jl * nc + i) * l + k);
+    const int64_t q = mg_gq(t, nc, l, GX, I0, J0);
     g[q] = b[t];
     g[q + 1] = b[ncl + t];
 }
-/* own rows of the global solution (global order) -> local (T block, S block) */
-__global__ void k_mg_gget(const double* __restrict__ y, int64_t ncl, int nc, int l,
+/* own rows of the global solution -> local (T block, S block) */
+__global__ void k_mg_gget(const double* __restrict__ y, int64_t ncl, int nc, int l, int GX, int I0, int J0,
                           double* __restrict__ z)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ncl) return;
-    const int k = (int)(t % l), i = (int)((t / l) % nc), jl = (int)(t / ((int64_t)l * nc));
-    const int64_t q = 2 * (((int64_t)jl * nc + i) * l + k);
+    const int64_t q = mg_gq(t, nc, l, GX, I0, J0);
     z[t] = y[q];
     z[ncl + t] = y[q + 1];
 }
@@ -2303,11 +2325,16 @@ static int mg_setup(iemic_ctx* c)
         return 0;
     }
     if (gs.mg_nlev == 0) {
-        /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns) */
-        int n = c->n, m = c->jb1 - c->jb0, q = 0;
+        /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns); the
+         * number of levels is that of the largest subdomain, the same on every rank, so the
+         * coarsest grids of the ranks tile the global coarsest problem */
+        int N = (c->n + c->npx - 1) / c->npx, M = (c->m + c->npy - 1) / c->npy, q = 0;
+        int n = c->nx, m = c->jb1 - c->jb0;
         gs.mg_n[0] = n;
         gs.mg_m[0] = m;
-        while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)n * m * l > 128) && (n > 1 || m > 1)) {
+        while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)N * M * l > 128) && (N > 1 || M > 1)) {
+            N = (N + 1) / 2;
+            M = (M + 1) / 2;
             n = (n + 1) / 2;
             m = (m + 1) / 2;
             q++;
@@ -2331,8 +2358,8 @@ static int mg_setup(iemic_ctx* c)
                 HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         }
         gs.mg_nlev = q + 1;
-        const size_t N = (size_t)2 * n * m * l;
-        if (gs.mg_cinv.alloc(N * N)) return IEMIC_ENOMEM;
+        const size_t NC = (size_t)2 * n * m * l;
+        if (gs.mg_cinv.alloc(NC * NC)) return IEMIC_ENOMEM;
     }
     hipStream_t s = c->stream;
     {
@@ -2343,7 +2370,7 @@ static int mg_setup(iemic_ctx* c)
     for (int q = 1; q < gs.mg_nlev; q++) {
         TsLev F = mg_view(c, q - 1);
         const TsLev C = mg_view(c, q);
-        F.vis = 0;                   /* aggregates and coarse operators stay band-local */
+        F.vis = F.visi = 0;          /* aggregates and coarse operators stay local      */
         hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for((int64_t)C.n * C.mb * C.l)), dim3(256), 0, s, F, C,
                            gs.mg_off[q].p, gs.mg_diag[q].p);
     }
@@ -2367,7 +2394,7 @@ static int mg_setup(iemic_ctx* c)
         HIP_OK(hipMemsetAsync(gs.mg_cinfo.p, 0, sizeof(int), s));
         hipLaunchKernelGGL(k_mg_coarse_dense, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s,
                            (const double*)gs.mg_off[qc].p, (const double*)gs.mg_diag[qc].p, ncl,
-                           gs.mg_n[qc], gs.mg_m[qc], l, c->cfg.periodic, A.p);
+                           gs.mg_n[qc], gs.mg_m[qc], l, c->cfg.periodic && c->npx == 1, A.p);
         /* k_cr_inv reads column-major: it inverts A^T and writes the result column-major,
          * which is A^-1 row-major -- the layout k_gemv applies */
         if ((rc = cr_inverse_dev(s, N, A.p, gs.mg_cinv.p, gs.mg_cinfo.p))) return rc;
@@ -2406,7 +2433,7 @@ static int mg_setup(iemic_ctx* c)
                 }
                 if (jj < 0 || jj >= cm || kk < 0 || kk >= l) continue;
                 if (ii < 0 || ii >= cn) {
-                    if (!c->cfg.periodic) continue;
+                    if (!(c->cfg.periodic && c->npx == 1)) continue;
                     ii = (ii + cn) % cn;
                 }
                 const int64_t nb = ((int64_t)jj * cn + ii) * l + kk;
@@ -2420,12 +2447,33 @@ static int mg_setup(iemic_ctx* c)
     return mg_global_setup(c, off, dg);
 }
 
-/* refresh the level-0 iterate's latitude halo rows (bands coupled in the T/S smoother) */
+/* refresh the level-0 iterate's halo columns (phase x, owned rows) and halo rows (phase
+ * y, whole rows with their halo columns) -- the subdomains coupled in the T/S smoother */
 static int mg_halo(iemic_ctx* c, const TsLev& V)
 {
-    if (!V.vis) return 0;
-    const int64_t slab = (int64_t)V.n * V.l;
-    return halo_exchange_slab2(c, V.z, V.z + V.cstr, V.hj * slab, (int64_t)V.mb * slab, slab);
+    if (!V.vis && !V.visi) return 0;
+    const int64_t W = V.n + 2 * V.hi, L = V.l;
+    const int w = c->nb[0], e = c->nb[1], so = c->nb[2], no = c->nb[3];
+    std::vector<Msg> x, y;
+    for (double* z : {V.z, V.z + V.cstr}) {
+        if (V.visi) {
+            auto col = [&](int64_t i) { return Seg{z, (V.hj * W + V.hi + i) * L, V.mb, L, W * L}; };
+            if (w >= 0) x.push_back({true, w, col(0)});
+            if (e >= 0) x.push_back({false, e, col(V.n)});
+            if (e >= 0) x.push_back({true, e, col(V.n - 1)});
+            if (w >= 0) x.push_back({false, w, col(-1)});
+        }
+        if (V.vis) {
+            auto row = [&](int64_t jl) { return Seg{z, (V.hj + jl) * W * L, 1, W * L, W * L}; };
+            if (so >= 0) y.push_back({true, so, row(0)});
+            if (no >= 0) y.push_back({false, no, row(V.mb)});
+            if (no >= 0) y.push_back({true, no, row(V.mb - 1)});
+            if (so >= 0) y.push_back({false, so, row(-1)});
+        }
+    }
+    int rc = run_msgs(c, x);
+    if (rc) return rc;
+    return run_msgs(c, y);
 }
 
 /* one colour launch of the z-line smoother (C: first post-smoothing sweep, zout: final) */
@@ -2453,13 +2501,12 @@ static int mg_coarsest(iemic_ctx* c, int q)
         const int64_t ncl = N / 2;
         HIP_OK(hipMemsetAsync(gs.mg_gvec.p, 0, sizeof(double) * gs.mg_gN, s));
         hipLaunchKernelGGL(k_mg_gput, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_b[q].p, ncl,
-                           gs.mg_n[q], c->l, gs.mg_g0, gs.mg_gvec.p);
+                           gs.mg_n[q], c->l, gs.mg_gGX, gs.mg_gI0, gs.mg_gJ0, gs.mg_gvec.p);
         if ((rc = allreduce_sum(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
-        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s,
-                           gs.mg_gX.p + (int64_t)gs.mg_g0 * gs.mg_gN, N, gs.mg_gN, gs.mg_gvec.p,
-                           gs.mg_gtmp.p);
+        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((gs.mg_gN + 3) / 4)), dim3(256), 0, s, gs.mg_gX.p,
+                           gs.mg_gN, gs.mg_gN, gs.mg_gvec.p, gs.mg_gtmp.p);
         hipLaunchKernelGGL(k_mg_gget, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_gtmp.p, ncl,
-                           gs.mg_n[q], c->l, gs.mg_z[q].p);
+                           gs.mg_n[q], c->l, gs.mg_gGX, gs.mg_gI0, gs.mg_gJ0, gs.mg_z[q].p);
         return 0;
     }
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
@@ -2498,7 +2545,7 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
     }
     /* coarse correction: added where the first post-smoothing colours read it, or (level 0
      * of a band group, whose lines also read the neighbour bands' rows) explicitly */
-    const bool corr = V.hj == 0;
+    const bool corr = V.hj == 0 && V.hi == 0;
     if (!corr)
         hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)V.n * V.mb * V.l)), dim3(256), 0, s, V, C);
     for (int sw = 0; sw < nu; sw++)
@@ -2526,7 +2573,7 @@ static int ts_solve(iemic_ctx* c, double* z, bool out, bool side = false)
     if (gs.ts_mg > 0) {
         const TsLev V0 = mg_view(c, 0);
         const int P = mg_lanes(c->l);
-        const unsigned ge = (unsigned)(((n + MG_TI - 1) / MG_TI) * V0.mb);
+        const unsigned ge = (unsigned)(((c->nx + MG_TI - 1) / MG_TI) * V0.mb);
         MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.known.p, gs.kmask.p, gs.rr.p, z, L, V0);
         if (side) {
             HIP_OK(hipEventRecord(c->ev_fork, s));
@@ -2546,7 +2593,7 @@ static int ts_solve(iemic_ctx* c, double* z, bool out, bool side = false)
         return 0;
     }
     const int nsw = std::max(1, gs.ts_sweeps);
-    if ((n & 1) == 0) {
+    if (ts_compact(c)) {
         /* colour-compacted symmetric red-black sweeps */
         const int nblk = (int)((c->nloc + 63) / 64);
         hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, c->d_val.p,
@@ -2655,12 +2702,12 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                        gs.kmask.p, L, c->jb1);
     hipLaunchKernelGGL(k_ts_compact, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        gs.tsoff.p, L, next, (int64_t)c->rowintcon);
-    if ((c->n & 1) == 0)
+    if (ts_compact(c))
         hipLaunchKernelGGL(k_ts_pack, dim3(gc), dim3(256), 0, c->stream, gs.tsoff.p, gs.tsinv.p,
                            gs.tsc.p, gs.tic.p, L, next);
     const int NC = c->n * c->m;
     HIP_OK(hipMemsetAsync(gs.S9.p, 0, sizeof(double) * 9 * (size_t)NC, c->stream));
-    const int64_t nt = (int64_t)c->n * (c->jb1 - c->jb0) * 9;
+    const int64_t nt = (int64_t)c->nx * (c->jb1 - c->jb0) * 9;
     hipLaunchKernelGGL(k_schur_build, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream,
                        c->d_val.p, gs.known.p, gs.uvinv.p, gs.gslot.p, gs.pw.p, gs.col_of_ij.p,
                        gs.pinned.p, L, c->jb1, gs.S9.p);

@@ -101,17 +101,77 @@ HD constexpr int fortran_rank(int s)
 }
 
 /* ---- per-context geometry (grid.F90, usrc.F90 stpnt/init) ------------------------- */
-/* Internal vector layout ("ext"): cells ordered j-major, (j, k, i) with i fastest, over the
- * owned latitude band [jb0, jb1) plus HALO rows on each side:
- *     cell = ((j - jb0 + HALO) * l + k) * n + i,   row = 6 * cell + var   (0-based i,j,k).
- * A band of j rows is then one contiguous slab, so halo exchanges need no packing, and
- * the reference's row order (k-major, THCMdefs.H:21) is restored only at the C ABI.
- * With one GPU the band is the whole grid. */
+/* Internal vector layout ("ext") of a subdomain [ib0, ib0 + nx) x [jb0, jb0 + mb) of the
+ * TRIOS Decomp2D process grid (TRIOS_Domain.C:81-195), full depth:
+ *   main block: rows r = (j - jb0 + HALO) * l + k for j in [jb0 - HALO, jb0 + mb + HALO),
+ *       each of the nx owned columns:   cell = r * nx + (i - ib0)
+ *   x halo (hx = HALO when the x direction is split, else 0 and the periodic wrap stays
+ *       the kernels'): after the main block, 2 hx cells per row,
+ *       cell = xb + r * 2 hx + (il < 0 ? il + hx : hx + il - nx),  il = i - ib0,
+ *       xb = (mb + 2 HALO) l nx;   row = 6 * cell + var   (0-based i,j,k).
+ * The owned cells are one contiguous slab (rows HALO l .. (HALO + mb) l - 1 of the main
+ * block), so vector reductions run over [6 own0, 6 (own0 + nloc)); a latitude halo is a
+ * contiguous slab of the main block plus one of the x halo; the reference's row order
+ * (k-major, THCMdefs.H:21) is restored only at the C ABI.  One GPU: nx = n, hx = 0, the
+ * subdomain is the whole grid and the layout is the j-major grid with 2 halo rows. */
 constexpr int HALO = 2;
+
+/* column il (-hx .. nx + hx - 1 after the wrap / clamp below) of ext row r -> ext cell */
+HD int64_t xcell(int64_t r, int il, int nx, int hx, int64_t xb)
+{
+    return (il >= 0 && il < nx) ? r * nx + il : xb + r * 2 * hx + (il < 0 ? il + hx : hx + il - nx);
+}
+/* local column of global column gi of a subdomain: the global periodic wrap into the x
+ * halo (split x) or into the grid (one x part) */
+HD int xlocal(int gi, int n, int ib0, int nx, int hx, int periodic)
+{
+    int il = gi - ib0;
+    if (periodic) {
+        if (il < -hx) il += n;
+        else if (il >= nx + hx) il -= n;
+    }
+    return il;
+}
+
+/* ext cell of column lcol of ext row r for a neighbour one column beyond the owned ones
+ * (lcol in -1 .. nx): outside the grid the column is clamped (non-periodic: the coupling
+ * is 0 there) or wrapped (periodic, one x part); a split x direction reads the x halo */
+HD int64_t xnb_cell(int64_t r, int lcol, int n, int ib0, int nx, int hx, int periodic, int64_t xb)
+{
+    int gi = ib0 + lcol;
+    if (gi < 0 || gi >= n) {
+        if (!periodic) gi = gi < 0 ? 0 : n - 1;
+        else if (!hx) gi = gi < 0 ? gi + n : gi - n;
+    }
+    return xcell(r, gi - ib0, nx, hx, xb);
+}
+/* the subdomain's ext layout as the structured-grid kernels see it */
+struct SubLay {
+    int n, m, l, periodic;          /* global grid                                      */
+    int jb0, ib0, nx, hx;           /* first owned row / column, owned columns, x halo   */
+    int64_t xb;                     /* first x-halo cell                                */
+};
+/* neighbour cells of owned cell (il, j, k) in the 3 x 3 (dk, dj) rows: c[di + 1][(dk + 1)
+ * * 3 + (dj + 1)], the row clamped at the top / bottom / north / south of the grid (the
+ * couplings are 0 there) */
+HD void nb_cells(const SubLay& X, int il, int j, int k, int (*c)[9])
+{
+    const int jj[3] = {j > 0 ? j - 1 : j, j, j < X.m - 1 ? j + 1 : j};
+    const int kk[3] = {k > 0 ? k - 1 : k, k, k < X.l - 1 ? k + 1 : k};
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) {
+            const int64_t r = ((int64_t)jj[b] - X.jb0 + HALO) * X.l + kk[a];
+            c[0][a * 3 + b] = (int)xnb_cell(r, il - 1, X.n, X.ib0, X.nx, X.hx, X.periodic, X.xb);
+            c[1][a * 3 + b] = (int)(r * X.nx + il);
+            c[2][a * 3 + b] = (int)xnb_cell(r, il + 1, X.n, X.ib0, X.nx, X.hx, X.periodic, X.xb);
+        }
+}
 
 struct Geo {
     int n, m, l;                    /* global grid                                      */
     int jb0;                        /* first owned j (0-based)                          */
+    int ib0, nx, hx;                /* first owned i, owned columns, x halo width       */
+    int64_t xb;                     /* first x-halo cell                                */
     int periodic;
     int tres, sres, coriolis_on;
     double dx, dy, dz;
@@ -148,21 +208,24 @@ HD int LM(const Geo& g, int i, int j, int k)
 {
     return g.landm[((int64_t)k * (g.m + 2) + j) * (g.n + 2) + i];
 }
-/* internal (ext) row of variable v at 1-based global (i,j,k) */
+/* internal (ext) row of variable v at 1-based global (i,j,k) (i in 1..n: the callers
+ * resolve the grid's own periodic wrap) */
 HD int64_t frow(const Geo& g, int i, int j, int k, int v)
 {
-    return (int64_t)NUN * ((((int64_t)(j - 1) - g.jb0 + HALO) * g.l + (k - 1)) * g.n + (i - 1)) + v;
+    const int64_t r = ((int64_t)(j - 1) - g.jb0 + HALO) * g.l + (k - 1);
+    const int il = xlocal(i - 1, g.n, g.ib0, g.nx, g.hx, g.hx ? g.periodic : 0);
+    return (int64_t)NUN * xcell(r, il, g.nx, g.hx, g.xb) + v;
 }
 
-/* owned-local cell lc (0 .. n*l*(jb1-jb0)-1) -> 1-based global (i,j,k); its ext cell is
- * HALO*l*n + lc */
+/* owned-local cell lc (0 .. nx*l*mb-1) -> 1-based global (i,j,k); its ext cell is
+ * HALO*l*nx + lc */
 HD void owned_cell(const Geo& g, int64_t lc, int& i, int& j, int& k)
 {
-    i = (int)(lc % g.n) + 1;
-    k = (int)((lc / g.n) % g.l) + 1;
-    j = g.jb0 + (int)(lc / ((int64_t)g.n * g.l)) + 1;
+    i = g.ib0 + (int)(lc % g.nx) + 1;
+    k = (int)((lc / g.nx) % g.l) + 1;
+    j = g.jb0 + (int)(lc / ((int64_t)g.nx * g.l)) + 1;
 }
-HD int64_t own0(const Geo& g) { return (int64_t)HALO * g.l * g.n; }
+HD int64_t own0(const Geo& g) { return (int64_t)HALO * g.l * g.nx; }
 
 /* ---- usol (usrc.F90:997-1104): padded staggered state, closed forms ---------------- */
 HD bool land_in(const Geo& g, int i, int j, int k)

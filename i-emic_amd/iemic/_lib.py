@@ -32,8 +32,21 @@ class Grid(C.Structure):
 
 
 class Dist(C.Structure):
-    """iemic_dist: latitude-band decomposition over nranks GPUs (RCCL unique id)."""
-    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("id", C.c_ubyte * 128)]
+    """iemic_dist: Decomp2D decomposition over nranks GPUs (RCCL unique id; npx x parts,
+    0: the reference's factorisation, 1: latitude bands)."""
+    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("id", C.c_ubyte * 128), ("npx", C.c_int)]
+
+
+SEND_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int64)
+RECV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int64)
+WAIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)
+ALLRED_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64)
+
+
+class Transport(C.Structure):
+    """iemic_transport: the caller's host point-to-point and all-reduce."""
+    _fields_ = [("user", C.c_void_p), ("send", SEND_FN), ("recv", RECV_FN), ("wait", WAIT_FN),
+                ("allreduce_sum", ALLRED_FN)]
 
 
 class Krylov(C.Structure):
@@ -103,6 +116,9 @@ def lib():
         "iemic_local_group_new": (vp, [C.c_int]),
         "iemic_local_group_free": (None, [vp]),
         "iemic_create_local": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int]),
+        "iemic_create_local_2d": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int, C.c_int]),
+        "iemic_create_transport": (C.c_int, [P(vp), P(Grid), PI, C.c_int, C.c_int, C.c_int, P(Transport)]),
+        "iemic_decomp2d": (C.c_int, [C.c_int, C.c_int, C.c_int, PI, PI]),
         "iemic_destroy": (None, [vp]),
         "iemic_device_count": (C.c_int, []),
         "iemic_last_error": (C.c_char_p, []),
@@ -177,6 +193,7 @@ def lib():
 
 EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
+            "iemic_create_local_2d", "iemic_create_transport", "iemic_decomp2d",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",
             "iemic_set_par", "iemic_get_par", "iemic_set_intcond_correction",
             "iemic_get_intcond_correction", "iemic_get_intcond_coeff", "iemic_psim",

@@ -31,19 +31,27 @@ class Ocean:
     def __init__(self, cfg: THCMConfig, landm: Optional[np.ndarray] = None, device: int = 0,
                  analyze_jacobian: bool = True, solver_params: Optional[dict] = None,
                  rank: int = 0, nranks: int = 1, comm_id: Optional[bytes] = None,
-                 local_group=None):
-        """rank/nranks/comm_id: latitude-band decomposition (one Ocean per GPU); comm_id is
-        the RCCL unique id of rank 0 (Ocean.unique_id()), shared by the caller."""
+                 local_group=None, npx: Optional[int] = None, transport=None):
+        """rank/nranks: the Decomp2D subdomain of this rank (one Ocean per GPU); comm_id is
+        the RCCL unique id of rank 0 (Ocean.unique_id()), shared by the caller; transport:
+        a host transport instead of RCCL (iemic.transport.GlooTransport); local_group: the
+        in-process test facility.  npx: x parts (0: the reference's Decomp2D factorisation,
+        1: latitude bands; default 0, and 1 for a local group)."""
         self.cfg = cfg
         L = landmask(cfg) if landm is None else landm
         L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
         self._grid = _lib.grid_from_config(cfg, device=device, analyze_jacobian=analyze_jacobian)
         h = C.c_void_p()
+        self._transport = transport
         if local_group is not None:
-            rc = lib().iemic_create_local(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
-                                          local_group, rank, nranks)
+            rc = lib().iemic_create_local_2d(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
+                                             local_group, rank, nranks, 1 if npx is None else npx)
+        elif transport is not None:
+            rc = lib().iemic_create_transport(C.byref(h), C.byref(self._grid), ptr(L, C.c_int), rank,
+                                              nranks, 0 if npx is None else npx, C.byref(transport.c))
         elif nranks > 1:
             d = _lib.Dist(rank, nranks)
+            d.npx = 0 if npx is None else npx
             C.memmove(d.id, comm_id, 128)
             rc = lib().iemic_create_dist(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
                                          C.byref(d))
@@ -77,10 +85,12 @@ class Ocean:
         return bytes(buf)
 
     def layout(self) -> dict:
-        out = np.zeros(7, dtype=np.int64)
+        out = np.zeros(12, dtype=np.int64)
         check(lib().iemic_layout(self._h, ptr(out, C.c_int64)), "iemic_layout")
         return dict(ext_rows=int(out[0]), own_first=int(out[1]), own_rows=int(out[2]),
-                    jb0=int(out[3]), jb1=int(out[4]), rank=int(out[5]), nranks=int(out[6]))
+                    jb0=int(out[3]), jb1=int(out[4]), rank=int(out[5]), nranks=int(out[6]),
+                    ib0=int(out[7]), ib1=int(out[8]), npx=int(out[9]), npy=int(out[10]),
+                    hx=int(out[11]))
 
     # ---- lifecycle -----------------------------------------------------------------
     def close(self):

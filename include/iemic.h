@@ -106,16 +106,35 @@ typedef struct {
     int n_spmv;                  /* SpMV launches inside the Arnoldi loop (t_spmv_ms) */
 } iemic_solve_info;
 
-/* Latitude-band decomposition over several GPUs (one process and one context per GPU,
- * RCCL over xGMI).  `id` is an RCCL unique id from iemic_comm_unique_id on
- * rank 0, broadcast by the caller (e.g. torch.distributed).  Rank r owns latitude rows
- * [r*m/P, (r+1)*m/P) with all columns and levels; vectors passed to the host-pointer entry
- * points are full reference-ordered global vectors of which each rank reads / writes its
- * owned rows. */
+/* Domain decomposition over several GPUs (one process and one context per GPU, RCCL over
+ * xGMI): the TRIOS Decomp2D split (TRIOS_Domain.C:81-195).  nranks =
+ * npx * npy; rank r = py * npx + px owns columns [px*n/npx + min(px, n%npx) ...) and rows
+ * likewise (the reference's remainder rule: the first ranks take one more), all levels.
+ * npx = 0 picks the reference's factorisation (iemic_decomp2d); npx = 1 gives latitude
+ * bands.  `id` is an RCCL unique id from iemic_comm_unique_id on rank 0, broadcast by the
+ * caller (e.g. torch.distributed).  Vectors passed to the host-pointer entry points are
+ * full reference-ordered global vectors of which each rank reads / writes its owned rows. */
 typedef struct {
     int rank, nranks;
     unsigned char id[128];
+    int npx;                     /* x parts (0: Decomp2D rule, 1: latitude bands)    */
 } iemic_dist;
+/* TRIOS::Domain::Decomp2D's factorisation nranks = npx * npy (TRIOS_Domain.C:88-109:
+ * npy = the largest t1 <= nranks dividing it that minimises |m/t1 - n/(nranks/t1)|, ties
+ * to the smaller t1) */
+int iemic_decomp2d(int n, int m, int nranks, int* npx, int* npy);
+/* Host transport (no RCCL): the caller's point-to-point and all-reduce over host memory,
+ * e.g. torch.distributed gloo.  Per exchange batch the library calls send for every
+ * outgoing message in order (it may return before delivery), then recv for every incoming
+ * one in order (blocking), then wait; the k-th message sent from a to b is the k-th b
+ * receives from a.  Return 0 on success. */
+typedef struct {
+    void* user;
+    int (*send)(void* user, int peer, const double* buf, int64_t count);
+    int (*recv)(void* user, int peer, double* buf, int64_t count);
+    int (*wait)(void* user);
+    int (*allreduce_sum)(void* user, double* buf, int64_t count);
+} iemic_transport;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */
 /* landm: (n+2)(m+2)(l+2) ints, i fastest, the global mask m_global::get_landm returns
@@ -126,13 +145,19 @@ int  iemic_create(iemic_ctx** ctx, const iemic_grid* grid, const int* landm);
 int  iemic_create_dist(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
                        const iemic_dist* dist);
 int  iemic_comm_unique_id(unsigned char* id128);
-/* Test facility: the bands of one problem as contexts of one process (one host thread
+/* the subdomain of a rank through a host transport (one process per rank, any device,
+ * e.g. several processes on one GPU, where RCCL refuses duplicate devices) */
+int  iemic_create_transport(iemic_ctx** ctx, const iemic_grid* grid, const int* landm, int rank,
+                            int nranks, int npx, const iemic_transport* tp);
+/* Test facility: the subdomains of one problem as contexts of one process (one host thread
  * each, all on `grid->device`), collectives host-staged through `group`.  Used to check
- * the band decomposition on a single GPU, where RCCL refuses duplicate devices. */
+ * the decomposition on a single GPU.  iemic_create_local: latitude bands (npx = 1). */
 void* iemic_local_group_new(int nranks);
 void  iemic_local_group_free(void* group);
 int   iemic_create_local(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
                          void* group, int rank, int nranks);
+int   iemic_create_local_2d(iemic_ctx** ctx, const iemic_grid* grid, const int* landm,
+                            void* group, int rank, int nranks, int npx);
 /* releases the handle; the context itself is freed once no atmosphere or coupled model
  * built on it remains (each holds a reference, dropped by its own destroy) */
 void iemic_destroy(iemic_ctx* ctx);
@@ -226,8 +251,10 @@ int64_t iemic_graph_nnz(const iemic_ctx* ctx);       /* Epetra maximal-graph nnz
 int     iemic_rowintcon(const iemic_ctx* ctx);       /* -1 when SRES != 0              */
 int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local mask   */
 /* internal vector layout of the _dev entry points: out[0] ext length (rows), out[1] first
- * owned row, out[2] owned rows, out[3..4] owned latitude band [jb0, jb1), out[5] rank,
- * out[6] nranks.  Internally cells are ordered (j, k, i), i fastest, with 2 halo rows. */
+ * owned row, out[2] owned rows, out[3..4] owned rows [jb0, jb1), out[5] rank, out[6]
+ * nranks, out[7..8] owned columns [ib0, ib1), out[9..10] process grid npx, npy, out[11]
+ * x-halo width.  Internally the owned cells are ordered (j, k, i), i fastest, one
+ * contiguous slab between 2 halo rows each side; the x halo (npx > 1) follows them. */
 int     iemic_layout(const iemic_ctx* ctx, int64_t* out);
 
 /* ---- state ------------------------------------------------------------------------ */

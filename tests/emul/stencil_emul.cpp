@@ -2,20 +2,22 @@
 /*
  * stencil_emul.cpp -- TEST HARNESS: runs the device library's per-row assembly code
  * (i-emic_amd/csrc/stencil.h, host_setup.h) on the CPU, loop for loop like the kernels
- * k_jacobian / k_rhs / k_diagB / k_qint / k_forcing, over one latitude band [jb0, jb1) in
- * the library's internal (ext) layout, so the restated arithmetic and the band
- * decomposition can be checked bit-for-bit against the oracle without a GPU.  Never
- * linked into the product.
+ * k_jacobian / k_rhs / k_diagB / k_qint / k_forcing, over one Decomp2D subdomain (or a
+ * latitude band) in the library's internal (ext) layout, so the restated arithmetic and
+ * the decomposition -- partition, neighbours and halo-exchange plans of decomp.h -- can be
+ * checked bit-for-bit against the oracle without a GPU.  Never linked into the product.
  */
 #include <cstring>
 #include <vector>
 
 #include "../../i-emic_amd/csrc/host_setup.h"
+#include "../../i-emic_amd/csrc/decomp.h"
 
 using namespace iemic;
 
 struct Emul {
     host::Setup su;
+    Sub sub;
     std::vector<double> frc, qcor, val;
     std::vector<double> atm;      /* coupled: tatm | qatm | albe (n*m each) */
     const double* atm_p() const { return atm.empty() ? nullptr : atm.data(); }
@@ -57,10 +59,50 @@ void emul_tanh(const double* x, double* y, long n)
 void* emul_create_band(const iemic_grid* grid, const int* landm, int jb0, int jb1)
 {
     Emul* e = new Emul();
-    e->su.init(*grid, landm, jb0, jb1);
+    const int s0[2] = {0, jb0}, s1[2] = {grid->n, jb1 < 0 ? grid->m : jb1};
+    e->su.init(*grid, landm, s0, s1, 0);
     e->su.vmix_init();
     e->atm.assign((size_t)4 * e->su.n * e->su.m, 0.0);
     return e;
+}
+/* the subdomain of rank `rank` of the library's decomposition (npx = 0: Decomp2D rule);
+ * null when the library would refuse it */
+void* emul_create_sub(const iemic_grid* grid, const int* landm, int rank, int nranks, int npx)
+{
+    Sub d;
+    if (sub_init(d, grid->n, grid->m, grid->l, grid->periodic, rank, nranks, npx)) return nullptr;
+    Emul* e = new Emul();
+    e->sub = d;
+    const int s0[2] = {d.ib0, d.jb0}, s1[2] = {d.ib1, d.jb1};
+    e->su.init(*grid, landm, s0, s1, d.npx > 1 ? 1 : 0);
+    e->su.vmix_init();
+    e->atm.assign((size_t)4 * e->su.n * e->su.m, 0.0);
+    return e;
+}
+/* subdomain facts: ib0 ib1 jb0 jb1 npx npy nb[4] */
+void emul_sub_info(void* h, int* out10)
+{
+    const Sub& d = ((Emul*)h)->sub;
+    const int v[10] = {d.ib0, d.ib1, d.jb0, d.jb1, d.npx, d.npy, d.nb[0], d.nb[1], d.nb[2], d.nb[3]};
+    for (int q = 0; q < 10; q++) out10[q] = v[q];
+}
+/* the library's exchange plan (decomp.h plan_ext): phase 0 (x) or 1 (y); up to cap
+ * messages as (send, peer, off, nblk, len, stride); returns the message count */
+int emul_plan(void* h, int width, int depth, int phase, int64_t* out, int cap)
+{
+    std::vector<MsgD> x, y;
+    plan_ext(((Emul*)h)->sub, width, depth, x, y);
+    const std::vector<MsgD>& v = phase == 0 ? x : y;
+    for (size_t q = 0; q < v.size() && (int)q < cap; q++) {
+        const int64_t r[6] = {v[q].send, v[q].peer, v[q].s.off, v[q].s.nblk, v[q].s.len, v[q].s.stride};
+        for (int t = 0; t < 6; t++) out[6 * q + t] = r[t];
+    }
+    return (int)v.size();
+}
+int emul_decomp2d(int n, int m, int P, int* npx, int* npy)
+{
+    decomp2d(n, m, P, *npx, *npy);
+    return 0;
 }
 /* iemic_set_atmosphere (capi.hip) on the CPU */
 void emul_set_atmosphere(void* h, const double* t, const double* q, const double* a, const double* p,
@@ -112,7 +154,7 @@ static void mix_control(Emul* e, const double* x)
     if (su.cfg.vmix != 2 || su.vmix_fix) return;
     double st = 0.0, ss = 0.0;
     for (int64_t lc = 0; lc < su.nloc; lc++) {
-        const int64_t r = NUN * ((int64_t)HALO * su.l * su.n + lc);
+        const int64_t r = NUN * ((int64_t)HALO * su.l * su.nx + lc);
         st += x[r + TT] * x[r + TT];
         ss += x[r + SS] * x[r + SS];
     }

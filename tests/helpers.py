@@ -69,13 +69,19 @@ def emul_lib():
 
 
 class Emul:
-    """ctypes wrapper of tests/emul/stencil_emul.cpp (one latitude band, default: all)."""
+    """ctypes wrapper of tests/emul/stencil_emul.cpp: one latitude band (default: all), or
+    with sub=(rank, nranks, npx) the library's Decomp2D subdomain of that rank."""
 
-    def __init__(self, cfg, landm, jb0: int = 0, jb1: int = -1):
+    def __init__(self, cfg, landm, jb0: int = 0, jb1: int = -1, sub=None):
         lib = C.CDLL(EMUL_LIB)
         vp = C.c_void_p
         lib.emul_create_band.restype = vp
         lib.emul_create_band.argtypes = [P(_lib.Grid), P(C.c_int), C.c_int, C.c_int]
+        lib.emul_create_sub.restype = vp
+        lib.emul_create_sub.argtypes = [P(_lib.Grid), P(C.c_int), C.c_int, C.c_int, C.c_int]
+        lib.emul_sub_info.argtypes = [vp, P(C.c_int)]
+        lib.emul_plan.restype = C.c_int
+        lib.emul_plan.argtypes = [vp, C.c_int, C.c_int, C.c_int, P(C.c_int64), C.c_int]
         lib.emul_destroy.argtypes = [vp]
         lib.emul_set_par.argtypes = [vp, C.c_int, C.c_double]
         lib.emul_ext_rows.restype = C.c_int64
@@ -90,12 +96,27 @@ class Emul:
         self.cfg = cfg
         g = _lib.grid_from_config(cfg, analyze_jacobian=False)
         L = np.ascontiguousarray(landm.reshape(-1), dtype=np.int32)
-        self.h = lib.emul_create_band(C.byref(g), _lib.ptr(L, C.c_int), jb0, jb1)
+        if sub is None:
+            self.h = lib.emul_create_band(C.byref(g), _lib.ptr(L, C.c_int), jb0, jb1)
+            self.ib0, self.ib1, self.jb0, self.jb1 = 0, cfg.n, jb0, cfg.m if jb1 < 0 else jb1
+            self.nb = [-1, -1, -1, -1]
+        else:
+            self.h = lib.emul_create_sub(C.byref(g), _lib.ptr(L, C.c_int), *sub)
+            if not self.h:
+                raise ValueError(f"decomposition {sub} refused")
+            info = (C.c_int * 10)()
+            lib.emul_sub_info(self.h, info)
+            self.ib0, self.ib1, self.jb0, self.jb1, self.npx, self.npy = info[:6]
+            self.nb = list(info[6:10])
         for idx, v in cfg.par_list():
             lib.emul_set_par(self.h, idx, v)
         self.ext_rows = lib.emul_ext_rows(self.h)
-        self.jb0 = jb0
-        self.jb1 = cfg.m if jb1 < 0 else jb1
+
+    def plan(self, width: int, depth: int, phase: int):
+        """the library's halo-exchange plan: [(send, peer, off, nblk, len, stride)]"""
+        out = np.zeros(6 * 64, dtype=np.int64)
+        k = self.lib.emul_plan(self.h, width, depth, phase, _lib.ptr(out, C.c_int64), 64)
+        return [tuple(int(v) for v in out[6 * q:6 * q + 6]) for q in range(k)]
 
     def __del__(self):
         try:
@@ -123,7 +144,7 @@ class Emul:
 
     def csr(self):
         nnz = self.lib.emul_to_csr(self.h, None, None, None)
-        nrow = 6 * self.cfg.n * self.cfg.l * (self.jb1 - self.jb0)
+        nrow = 6 * (self.ib1 - self.ib0) * self.cfg.l * (self.jb1 - self.jb0)
         rowptr = np.zeros(nrow + 1, dtype=np.int64)
         col = np.zeros(nnz, dtype=np.int32)
         val = np.zeros(nnz)

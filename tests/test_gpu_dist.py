@@ -1,11 +1,14 @@
-"""Latitude bands on the GPU.
+"""Decomp2D subdomains on the GPU (TRIOS_Domain.C:81-195): latitude bands
+(npx = 1), x splits and 2-D process grids.
 
-* In-process group (one GPU, one host thread per band, host-staged collectives):
-  every band's Jacobian rows equal the oracle's bit for bit, the residual norm equals the
-  oracle's, and the distributed Newton step solves the linearised system of the whole
-  problem: ||F + J dx|| <= 1e-8 ||F|| with dx gathered from the bands.
-* RCCL across processes: skipped on a one-GPU box (RCCL refuses two ranks on one
-  device); the driver's multi-GPU bench exercises it.
+* In-process group (one GPU, one host thread per subdomain, host-staged collectives):
+  every subdomain's Jacobian rows equal the oracle's bit for bit, the residual norm equals
+  the oracle's, and the distributed Newton step solves the linearised system of the whole
+  problem: ||F + J dx|| <= 1e-8 ||F|| with dx gathered from the subdomains.
+* Across processes: several processes on one GPU through the library's host transport
+  (iemic.transport.GlooTransport over gloo) run the library's own exchange batches
+  (comm.hip run_msgs); RCCL with one GPU per process is skipped on a one-GPU box (RCCL
+  refuses two ranks on one device); the driver's multi-GPU bench exercises it.
 """
 import os
 import threading
@@ -21,9 +24,15 @@ from iemic import config as cf
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name,nranks", [("natl8", 2), ("gateway16", 2), ("gateway16", 3),
-                                         ("global4", 4)])
-def test_bands_in_one_process(oracle_lib, name, nranks):
+def owned_rows(c, lay):
+    return [6 * ((k * c.m + j) * c.n + i) + v for k in range(c.l) for j in range(lay["jb0"], lay["jb1"])
+            for i in range(lay["ib0"], lay["ib1"]) for v in range(6)]
+
+
+@pytest.mark.parametrize("name,nranks,npx", [("natl8", 2, 1), ("gateway16", 2, 1), ("gateway16", 3, 1),
+                                             ("global4", 4, 1), ("natl8", 2, 2), ("gateway16", 2, 2),
+                                             ("gateway16", 4, 2), ("global4", 4, 0), ("global4", 6, 3)])
+def test_subdomains_in_one_process(oracle_lib, name, nranks, npx):
     from iemic import _lib
     from iemic.ocean import Ocean
     c = cf.preset(name, mixing=0)
@@ -39,7 +48,7 @@ def test_bands_in_one_process(oracle_lib, name, nranks):
 
     def work(r):
         try:
-            oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks,
+            oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks, npx=npx,
                        solver_params={"Preconditioner": 2, "FGMRES tolerance": 1e-10,
                                       "FGMRES iterations": 1000})
             oc.setState(x)
@@ -65,10 +74,8 @@ def test_bands_in_one_process(oracle_lib, name, nranks):
     assert not errs, errs
     covered = []
     for r in res:
-        jb0, jb1 = r["lay"]["jb0"], r["lay"]["jb1"]
         rowptr, col, val = r["csr"]
-        rows = [6 * ((k * c.m + j) * c.n + i) + v for k in range(c.l) for j in range(jb0, jb1)
-                for i in range(c.n) for v in range(6)]
+        rows = owned_rows(c, r["lay"])
         covered += rows
         for a, q in enumerate(rows):
             b0, b1 = o.rowptr[q], o.rowptr[q + 1]
@@ -92,11 +99,12 @@ def test_bands_in_one_process(oracle_lib, name, nranks):
     assert abs(res[0]["info"].norm_f1 - f1) <= 1e-9 * f1 + 1e-14 * f0
 
 
-@pytest.mark.parametrize("nranks", [2, 8])
-def test_bands_global2_newton_mixing(oracle_lib, nranks):
+@pytest.mark.parametrize("nranks,npx", [(2, 1), (8, 1), (4, 0), (8, 0)])
+def test_subdomains_global2_newton_mixing(oracle_lib, nranks, npx):
     """The bench workload split as the multi-GPU bench splits it (global 2 deg, Mixing = 1,
-    default solver: block GS with 4 damped defect passes, T/S multigrid per band): the
-    banded Newton step converges and solves the linearised system of the whole problem."""
+    default solver: block GS with 4 damped defect passes, T/S multigrid per subdomain;
+    npx = 0: the reference's Decomp2D, 2 x 2 and 4 x 2): the distributed Newton step
+    converges and solves the linearised system of the whole problem."""
     from iemic.ocean import Ocean
     c = cf.preset("global2", mixing=1)
     L0 = cf.init_landmask(c, cf.landmask(c))
@@ -107,7 +115,7 @@ def test_bands_global2_newton_mixing(oracle_lib, nranks):
 
     def fn(r, group):
         from iemic import _lib
-        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks,
+        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks, npx=npx,
                    solver_params={"FGMRES iterations": 100, "FGMRES restarts": 20})
         oc.setState(x)
         info = oc.newtonStep()
@@ -119,9 +127,7 @@ def test_bands_global2_newton_mixing(oracle_lib, nranks):
 
     res = _run_bands(nranks, fn)
     for r in res:
-        jb0, jb1 = r["lay"]["jb0"], r["lay"]["jb1"]
-        rows = np.array([6 * ((k * c.m + j) * c.n + i) + q for k in range(c.l)
-                         for j in range(jb0, jb1) for i in range(c.n) for q in range(6)])
+        rows = np.array(owned_rows(c, r["lay"]))
         x1[rows] = r["x"][rows]
         assert r["info"].solve.converged == 1
     ov, _ = o.jacobian(x)
@@ -153,11 +159,13 @@ def _run_bands(nranks, fn):
     return res
 
 
-@pytest.mark.parametrize("name,nranks,prec", [("natl8", 2, 1), ("natl8", 2, 2),
-                                              ("gateway16", 3, 2), ("global4", 4, 2)])
-def test_bands_spmv_and_solve(oracle_lib, name, nranks, prec):
-    """Band SpMV equals the oracle's J v on the owned rows; a band FGMRES solve (no
-    preconditioner, block Jacobi, block GS) gives ||b - J x|| <= 1e-8 ||b|| globally."""
+@pytest.mark.parametrize("name,nranks,npx,prec", [("natl8", 2, 1, 1), ("natl8", 2, 1, 2),
+                                                  ("gateway16", 3, 1, 2), ("global4", 4, 1, 2),
+                                                  ("natl8", 2, 2, 2), ("gateway16", 4, 2, 2),
+                                                  ("global4", 4, 2, 1), ("global4", 8, 0, 2)])
+def test_subdomains_spmv_and_solve(oracle_lib, name, nranks, npx, prec):
+    """Subdomain SpMV equals the oracle's J v on the owned rows; a distributed FGMRES solve
+    (block Jacobi, block GS) gives ||b - J x|| <= 1e-8 ||b|| globally."""
     from iemic import _lib
     from iemic.ocean import Ocean
     c = cf.preset(name, mixing=0)
@@ -173,7 +181,7 @@ def test_bands_spmv_and_solve(oracle_lib, name, nranks, prec):
     xs = np.zeros(c.nrows)
 
     def fn(r, group):
-        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks,
+        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks, npx=npx,
                    solver_params={"Preconditioner": prec, "FGMRES tolerance": 1e-10,
                                   "FGMRES iterations": 1000})
         oc.setState(x)
@@ -186,9 +194,7 @@ def test_bands_spmv_and_solve(oracle_lib, name, nranks, prec):
 
     res = _run_bands(nranks, fn)
     for r in res:
-        jb0, jb1 = r["lay"]["jb0"], r["lay"]["jb1"]
-        rows = np.array([6 * ((k * c.m + j) * c.n + i) + q for k in range(c.l)
-                         for j in range(jb0, jb1) for i in range(c.n) for q in range(6)])
+        rows = np.array(owned_rows(c, r["lay"]))
         y[rows] = r["y"][rows]
         xs[rows] = r["sol"][rows]
     scale = np.abs(ov).max() * np.abs(v).max()
@@ -220,7 +226,7 @@ def _rccl_worker(rank, nranks, port, q):
         y = oc.applyMatrix(v)
         sol = oc.solve(y)
         lay = oc.layout()
-        q.put((rank, {"jb": (lay["jb0"], lay["jb1"]), "y": y, "sol": sol, "x": x, "v": v,
+        q.put((rank, {"lay": lay, "y": y, "sol": sol, "x": x, "v": v,
                       "converged": oc.last_solve.converged}))
         oc.close()
     except Exception as e:  # noqa: BLE001
@@ -253,12 +259,86 @@ def test_rccl_ranks(oracle_lib):
     y = np.zeros(c.nrows)
     xs = np.zeros(c.nrows)
     for r in out.values():
-        jb0, jb1 = r["jb"]
-        rows = np.array([6 * ((k * c.m + j) * c.n + i) + qv for k in range(c.l)
-                         for j in range(jb0, jb1) for i in range(c.n) for qv in range(6)])
+        rows = np.array(owned_rows(c, r["lay"]))
         y[rows] = r["y"][rows]
         xs[rows] = r["sol"][rows]
         assert r["converged"] == 1
     assert np.max(np.abs(y - yref)) <= 1e-13 * np.abs(ov).max() * np.abs(v).max()
     lin = np.linalg.norm(yref - o.spmv(ov, xs)) / np.linalg.norm(yref)
+    assert lin <= 1e-8, lin
+
+
+def _transport_worker(rank, nranks, npx, name, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "i-emic_amd"), os.path.join(root, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        from iemic.ocean import Ocean
+        from iemic.transport import GlooTransport
+        c = cf.preset(name, mixing=0)
+        L0 = golden_landm(name)
+        tp = GlooTransport()
+        oc = Ocean(c, landm=L0, device=0, rank=rank, nranks=nranks, npx=npx, transport=tp,
+                   solver_params={"FGMRES tolerance": 1e-10, "FGMRES iterations": 1000})
+        L = oc.landmask().reshape(c.l + 2, c.m + 2, c.n + 2)
+        x = cf.synthetic_state(c, L, amp_ts=1e-3)
+        v = cf.synthetic_vector(c, seed=5)
+        oc.setState(x)
+        oc.computeJacobian()
+        rowptr, col, val = oc.exportCSR()
+        y = oc.applyMatrix(v)
+        info = oc.newtonStep()
+        x1 = oc.getState().copy()
+        lay = oc.layout()
+        q.put((rank, {"lay": lay, "y": y, "x": x, "v": v, "x1": x1, "csr": (rowptr, col, val),
+                      "converged": info.solve.converged, "f0": info.norm_f0, "f1": info.norm_f1}))
+        oc.close()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,nranks,npx", [("gateway16", 2, 2), ("global4", 4, 2)])
+def test_transport_processes(oracle_lib, name, nranks, npx):
+    """One process per subdomain on one GPU, the library's exchange batches and sums over
+    its host transport (gloo): J rows bit-exact, J v to 1e-13, and a Newton step whose
+    gathered update solves the whole linearised system to 1e-8."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_transport_worker, args=(r, nranks, npx, name, 29830 + nranks, q))
+             for r in range(nranks)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert all(isinstance(v, dict) for v in out.values()), out
+    c = cf.preset(name, mixing=0)
+    L = mask_fix(oracle_lib, c, golden_landm(name))
+    o = oracle_lib.Oracle(c.ref_dict(), L, c.par_list())
+    x, v = out[0]["x"], out[0]["v"]
+    ov, _ = o.jacobian(x)
+    yref = o.spmv(ov, v)
+    y = np.zeros(c.nrows)
+    x1 = np.zeros(c.nrows)
+    for r in out.values():
+        rows = owned_rows(c, r["lay"])
+        rowptr, col, val = r["csr"]
+        for a, qr in enumerate(rows):
+            b0, b1 = o.rowptr[qr], o.rowptr[qr + 1]
+            np.testing.assert_array_equal(col[rowptr[a]:rowptr[a + 1]], o.col[b0:b1])
+            np.testing.assert_array_equal(val[rowptr[a]:rowptr[a + 1]], ov[b0:b1])
+        rows = np.array(rows)
+        y[rows] = r["y"][rows]
+        x1[rows] = r["x1"][rows]
+        assert r["converged"] == 1
+    assert np.max(np.abs(y - yref)) <= 1e-13 * np.abs(ov).max() * np.abs(v).max()
+    F0 = o.rhs(x)
+    f0 = np.linalg.norm(F0)
+    assert abs(out[0]["f0"] - f0) <= 1e-12 * f0
+    lin = np.linalg.norm(F0 + o.spmv(ov, x1 - x)) / f0
     assert lin <= 1e-8, lin
