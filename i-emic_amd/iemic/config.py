@@ -249,6 +249,24 @@ def synthetic_state(cfg: THCMConfig, landm: np.ndarray, seed: int = 20261015,
     return np.ascontiguousarray(x.reshape(-1))
 
 
+def prolong_state(cfg_c: THCMConfig, x_c: np.ndarray, cfg_f: THCMConfig, landm_f: np.ndarray) -> np.ndarray:
+    """A state of a coarser global grid on a finer one (an initial guess, e.g. the 1-degree
+    continuation state from the 2-degree branch state): each fine cell takes the values
+    of the coarse cell containing it -- horizontal refinement r = n_f / n_c, layer k' from
+    the coarse layer floor((k' + 1/2) l_c / l_f) (the mask refinement's rule) -- and land
+    cells of the fine mask are 0."""
+    r = cfg_f.n // cfg_c.n
+    assert cfg_f.n == r * cfg_c.n and cfg_f.m == r * cfg_c.m
+    xc = np.asarray(x_c, dtype=np.float64).reshape(cfg_c.l, cfg_c.m, cfg_c.n, NUN)
+    ks = np.floor((np.arange(cfg_f.l) + 0.5) * cfg_c.l / cfg_f.l).astype(np.int64)
+    js = np.arange(cfg_f.m) // r
+    is_ = np.arange(cfg_f.n) // r
+    xf = xc[np.ix_(ks, js, is_)]
+    ocean = landm_f[1:-1, 1:-1, 1:-1] == OCEAN
+    xf = xf * ocean[..., None]
+    return np.ascontiguousarray(xf.reshape(-1))
+
+
 def synthetic_vector(cfg: THCMConfig, seed: int = 7) -> np.ndarray:
     rows = np.arange(cfg.nrows, dtype=np.int64)
     return splitmix64_uniform(seed, rows) * 2.0 - 1.0

@@ -162,7 +162,8 @@ def _run_bands(nranks, fn):
 @pytest.mark.parametrize("name,nranks,npx,prec", [("natl8", 2, 1, 1), ("natl8", 2, 1, 2),
                                                   ("gateway16", 3, 1, 2), ("global4", 4, 1, 2),
                                                   ("natl8", 2, 2, 2), ("gateway16", 4, 2, 2),
-                                                  ("global4", 4, 2, 1), ("global4", 8, 0, 2)])
+                                                  ("global4", 4, 2, 2), ("natl8", 2, 2, 1),
+                                                  ("global4", 8, 0, 2)])
 def test_subdomains_spmv_and_solve(oracle_lib, name, nranks, npx, prec):
     """Subdomain SpMV equals the oracle's J v on the owned rows; a distributed FGMRES solve
     (block Jacobi, block GS) gives ||b - J x|| <= 1e-8 ||b|| globally."""
