@@ -91,6 +91,12 @@ def parse():
     p.add_argument("--cold-reps", type=int, default=0,
                    help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--mode", default="newton", choices=["newton", "continuation"],
+                   help="continuation: config C5, one pseudo-arclength continuation step of the "
+                        "1-degree ocean (run/ocean settings) from bench_data/<config>_cf05.npz")
+    p.add_argument("--ds", type=float, default=0.1, help="continuation step size (--mode continuation)")
+    p.add_argument("--cpu-iters", type=int, default=8,
+                   help="FGMRES iterations of the bounded CPU sample (--mode continuation)")
     return p.parse_args()
 
 
@@ -130,6 +136,135 @@ def cpu_baseline(cfg, L, x, args):
     }
 
 
+RUN_OCEAN_CONT = {                  # run/ocean/continuation_params.xml
+    "continuation parameter": "Combined Forcing", "initial step size": 1.0e-3,
+    "minimum step size": 1.0e-8, "maximum step size": 1.0, "Newton tolerance": 1.0e-2,
+    "destination tolerance": 1.0e-4, "epsilon increment": 1.0e-5, "normalize strategy": "N",
+    "corrector residual test": "D", "state tangent scaling": 1.0,
+    "enable Newton Chord hybrid solve": False, "predictor bound": 3000.0,
+    "post processing": "never"}
+
+
+def bench_continuation(args):
+    """Config C5: one pseudo-arclength continuation step (Continuation.H:230-298: Euler
+    predictor, Newton corrector on the bordered system with two solves per Jacobian,
+    587-813) of the 1-degree global ocean (384x152x32, 11.2 M unknowns) with the
+    reference's run/ocean settings (continuation_params.xml: Newton tolerance 1e-2;
+    solver_params.xml: FGMRES tolerance 1e-4), from the near-solution branch state
+    bench_data/<config>_cf05.npz (the model continued on the GPU from rest to Combined
+    Forcing 0.5, scripts/branch_state.py, fp32-rounded).  The tangent (an Euler tangent: one
+    solve with dF/dpar) is formed once, untimed; every timed step restarts from that state,
+    tangent and step size ds.  One GPU."""
+    import torch
+    from iemic import config as cf
+    from iemic.continuation import Continuation
+    from iemic.ocean import Ocean
+    cfg = cf.preset(args.config, mixing=args.mixing)
+    fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
+    with np.load(fix, allow_pickle=False) as d:
+        x0 = d["x"].astype(np.float64)
+        par0 = float(d["par"])
+    sp = {"FGMRES tolerance": 1e-4, "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
+          "Dyn iterations": args.dyn_iters, "Dyn damping": args.dyn_omega, "TS multigrid cycles": args.ts_mg}
+    oc = Ocean(cfg, solver_params=sp)
+    solves = []
+    orig_solve = oc.solve
+
+    def solve(b):
+        x = orig_solve(b)
+        solves.append(oc.last_solve)
+        return x
+    oc.solve = solve
+    oc.setState(x0)
+    oc.setPar("Combined Forcing", par0)
+    cont = Continuation(oc, {**RUN_OCEAN_CONT, "initial step size": args.ds})
+    cont.initialize()
+    cont.createInitialTangent()
+    saved = (cont.state.copy(), cont.par, cont.stateDot.copy(), cont.parDot)
+
+    def step():
+        st, par, sd, pd = saved
+        oc.setState(st)
+        oc.setPar("Combined Forcing", par)
+        cont.state, cont.par, cont.stateDot, cont.parDot, cont.ds = st.copy(), par, sd.copy(), pd, args.ds
+        cont.store()
+        solves.clear()
+        t = time.perf_counter()
+        rc = cont.step()
+        torch.cuda.synchronize()
+        return rc, time.perf_counter() - t, list(solves)
+
+    for _ in range(args.warmup):
+        step()
+    recs = [step() for _ in range(args.steps)]
+    ms = sum(r[1] for r in recs) / len(recs) * 1e3
+    rc, _, sv = recs[-1]
+    # SpMV roofline of the 1-degree operator: HIP events on the library stream (hot)
+    sp_ms = oc.time_spmv(20)
+    from iemic import _lib
+    nnz = int(_lib.lib().iemic_graph_nnz(oc._h))
+    bsp = spmv_bytes(nnz, cfg.nrows)
+    achieved = bsp / (sp_ms * 1e-3) / 1e9
+    its = [s.iters for s in sv]
+    out = {"metric": "1-degree continuation-step wall time (config C5: predictor + bordered Newton corrector)",
+           "value": round(ms, 1), "unit": "ms/continuation-step", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 1), "higher_is_better": False,
+           "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "data": ("near-solution state: global1 continued on the GPU from rest to Combined Forcing "
+                    f"{par0:.5f} with the reference's run/ocean settings (scripts/branch_state.py; "
+                    "bench_data/global1_cf05.npz, fp32-rounded); Euler tangent formed untimed"),
+           "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing={args.mixing}, one "
+                                  f"continuation step ds={args.ds:g} (Newton tol 1e-2, FGMRES tol 1e-4)",
+                      "rows": cfg.nrows, "nnz": nnz, "krylov_dim": args.krylov, "restarts": args.restarts},
+           "continuation": {"rc": rc, "newton_iters": cont.newtonIter, "par": cont.par,
+                            "norm_f": cont.normRHStest, "fgmres_iters": its,
+                            "solve_ms": [round(s.t_total_ms, 1) for s in sv]},
+           "roofline": {"kernel": "k_spmv7 (1-degree operator, HIP events, 20 back-to-back launches)",
+                        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes": bsp, "launch_us": round(sp_ms * 1e3, 2)},
+           "cpu_baseline": None}
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_continuation_sample(cfg, oc, cont, saved, its, args)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_continuation_sample(cfg, oc, cont, saved, its, args):
+    """Bounded CPU sample of the C5 step on the oracle port (16 threads): F, J, the block
+    GS set-up and args.cpu_iters FGMRES iterations timed at the predicted state, scaled to
+    the GPU step's work (its Newton iterations' F/J/set-up and its FGMRES iterations)."""
+    from oracle import oracle as orc
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
+    o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
+    st, par, sd, pd = saved
+    x = st + args.ds * sd
+    o.set_par(19, par + args.ds * pd)        # Combined Forcing (par2int COMB = 19)
+    t = time.perf_counter()
+    F = o.rhs(x)
+    t_rhs = time.perf_counter() - t
+    t = time.perf_counter()
+    val, _ = o.jacobian(x)
+    t_jac = time.perf_counter() - t
+    t = time.perf_counter()
+    P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
+                    ts_mg=args.ts_mg)
+    t_prec = time.perf_counter() - t
+    t = time.perf_counter()
+    _, k, _, _ = P.fgmres(np.ascontiguousarray(-F), tol=1e-30, m=args.cpu_iters, maxit=args.cpu_iters)
+    t_it = (time.perf_counter() - t) / max(1, k)
+    newton = cont.newtonIter
+    # per Newton iteration: F for dF/dpar (2 F evaluations; the first iteration 3), J,
+    # preconditioner set-up; the predictor's F; the FGMRES iterations of the step's solves
+    est = ((2 * newton + 2) * t_rhs + newton * (t_jac + t_prec) + sum(its) * t_it) * 1e3
+    return {"value": round(est, 1), "unit": "ms/continuation-step", "cores": cores, "kind": "port",
+            "sample": (f"bounded sample on the oracle C port ({cores} threads) at the step's predicted state: "
+                       f"F {t_rhs*1e3:.0f} ms, J {t_jac*1e3:.0f} ms, block GS set-up {t_prec*1e3:.0f} ms, "
+                       f"{k} FGMRES iterations at {t_it*1e3:.0f} ms each; scaled to the GPU step's "
+                       f"{newton} Newton iterations and {sum(its)} FGMRES iterations ({its})"),
+            "timed": True, "extrapolated": True}
+
+
 def bench_coupled(args):
     """Config C4: the coupled ocean + atmosphere model at 4 degrees (run/coupled: ocean
     96x38x12 with Coupled Temperature = 1, Mixing 1; the atmosphere on the same grid),
@@ -140,18 +275,31 @@ def bench_coupled(args):
     from iemic.coupled import RUN_COUPLED_ATMOS, Atmosphere, CoupledModel
     from iemic.ocean import Ocean
     cfg = cf.preset("coupled4")
+    fix = os.path.join(ROOT, "bench_data", "coupled4_cf015.npz")
+    branch = args.state == "branch" and os.path.exists(fix)
+    if branch:
+        # near-solution state of both models: the coupled model continued on the GPU from
+        # rest with run/coupled's settings to Combined Forcing 0.15
+        # (scripts/coupled_branch_state.py), fp32-rounded
+        with np.load(fix, allow_pickle=False) as d:
+            xo_b, xa_b, comb = d["x"].astype(np.float64), d["xa"].astype(np.float64), float(d["par"])
+    else:
+        comb = cfg.start_params["Combined Forcing"]
     oc = Ocean(cfg, solver_params={"Dyn iterations": args.dyn_iters})
-    atm = Atmosphere(oc, {**RUN_COUPLED_ATMOS,
-                          "Combined Forcing": cfg.start_params["Combined Forcing"]})
+    atm = Atmosphere(oc, {**RUN_COUPLED_ATMOS, "Combined Forcing": comb})
     sp = {"FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "FGMRES tolerance": args.tol, "Solver": args.solver, "IDR s": args.idr_s}
     cm = CoupledModel(oc, atm, sp)
+    cm.setPar("Combined Forcing", comb)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
-    xo = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
-    # the atmosphere state of the coupled fixture (idealized profile + seeded noise,
-    # tests/golden/make_golden_coupled.py atmos_state)
-    with np.load(os.path.join(ROOT, "bench_data", "coupled4_atmos.npz"), allow_pickle=False) as d:
-        xa = d["xa"].astype(np.float64)
+    if branch:
+        xo, xa = xo_b, xa_b
+    else:
+        xo = cf.synthetic_state(cfg, L, amp_ts=args.amp_ts)
+        # the atmosphere state of the coupled fixture (idealized profile + seeded noise,
+        # tests/golden/make_golden_coupled.py atmos_state)
+        with np.load(os.path.join(ROOT, "bench_data", "coupled4_atmos.npz"), allow_pickle=False) as d:
+            xa = d["xa"].astype(np.float64)
 
     def step():
         oc.setState(xo)
@@ -168,18 +316,42 @@ def bench_coupled(args):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     r = recs[-1]
+    seq = []
+    if args.newton_seq > 0:
+        oc.setState(xo)
+        atm.setState(xa)
+        for _ in range(args.newton_seq):
+            q = cm.newtonStep()
+            seq.append({k: q[k] for k in ("norm_f0", "norm_f1", "iters", "converged") if k in q})
+    # SpMV roofline: the ocean block's k_spmv7 (HIP events on the library stream, hot)
+    from iemic import _lib
+    oc.setState(xo)
+    oc.computeJacobian()
+    sp_ms = oc.time_spmv(50)
+    nnz = int(_lib.lib().iemic_graph_nnz(oc._h))
+    bsp = spmv_bytes(nnz, cfg.nrows)
+    achieved = bsp / (sp_ms * 1e-3) / 1e9
     out = {"metric": "coupled ocean+atmosphere Newton-step wall time (config C4)",
            "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": False,
            "scaling": "none", "vs_baseline": None, "dtype": "f64",
-           "data": (f"synthetic ocean state (splitmix64, T,S ~ U(+-{args.amp_ts:g})), atmosphere "
-                    "state bench_data/coupled4_atmos.npz (idealized profile + seeded noise); "
-                    "Combined Forcing 0.5; states reset from host each step"),
+           "data": (("near-solution state of both models: coupled4 continued on the GPU from rest with "
+                     "run/coupled's settings to Combined Forcing 0.15 (scripts/coupled_branch_state.py; "
+                     "bench_data/coupled4_cf015.npz, fp32-rounded); states reset from host each step")
+                    if branch else
+                    (f"synthetic ocean state (splitmix64, T,S ~ U(+-{args.amp_ts:g})), atmosphere "
+                     "state bench_data/coupled4_atmos.npz (idealized profile + seeded noise); "
+                     "Combined Forcing 0.5; states reset from host each step")),
            "config": {"workload": "coupled4: ocean 96x38x12 (coupled T, Mixing 1) + atmosphere "
                                   "96x38 (T, q, A, P), one Newton step", "rows": cm.N,
                       "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                       "prec": "forward block Gauss-Seidel: ocean block GS, atmosphere exact"},
-           "newton": r, "roofline": None, "cpu_baseline": None}
+           "newton": {**r, "sequence": seq},
+           "roofline": {"kernel": "k_spmv7 (ocean block, 4 degrees; HIP events, 50 back-to-back launches)",
+                        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes": bsp, "launch_us": round(sp_ms * 1e3, 2)},
+           "cpu_baseline": None}
     print(json.dumps(out), flush=True)
 
 
@@ -187,6 +359,8 @@ def main():
     args = parse()
     if args.config == "coupled4":
         return bench_coupled(args)
+    if args.mode == "continuation":
+        return bench_continuation(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -59,7 +59,8 @@ def main():
         if rc == 0:
             states.append(oc.getState("C").astype(np.float64))
             pars.append(oc.getPar("Combined Forcing"))
-            np.savez_compressed(out, x=states[-1], par=pars[-1], n=len(pars))
+            np.savez_compressed(out, x=states[-1].astype(np.float32), par=pars[-1], n=len(pars),
+                                ds=cont.ds)
         return rc
     cont.step = step
     rc = cont.run()

@@ -17,14 +17,17 @@ from iemic import config as cf  # noqa: E402
 from iemic.ocean import Ocean  # noqa: E402
 
 
-def near_solution(oc, cfg, steps: int, log=print):
-    """prolonged 2-degree branch state -> Newton at the config's Combined Forcing; returns
-    the list of (||F0||, ||F1||, FGMRES its)"""
+def near_solution(oc, cfg, steps: int, log=print, ts_only: bool = False):
+    """prolonged 2-degree branch state (ts_only: T and S only, u, v, w, p = 0) -> Newton at
+    the config's Combined Forcing; returns the list of (||F0||, ||F1||, FGMRES its)"""
     c2 = cf.preset("global2", mixing=1)
     with np.load(os.path.join(ROOT, "bench_data", "global2_cf05.npz"), allow_pickle=False) as d:
         x2 = d["x"].astype(np.float64)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
-    oc.setState(cf.prolong_state(c2, x2, cfg, L))
+    x = cf.prolong_state(c2, x2, cfg, L)
+    if ts_only:
+        x.reshape(-1, 6)[:, :4] = 0.0
+    oc.setState(x)
     seq = []
     for it in range(steps):
         t = time.time()
@@ -42,7 +45,8 @@ def main():
     tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-8
     cfg = cf.preset("global1", mixing=1)
     oc = Ocean(cfg, solver_params={"FGMRES tolerance": tol, "FGMRES iterations": 90, "FGMRES restarts": 20})
-    near_solution(oc, cfg, steps, log=lambda s: print(s, flush=True))
+    near_solution(oc, cfg, steps, log=lambda s: print(s, flush=True),
+                  ts_only=os.environ.get("TS_ONLY", "0") == "1")
     if len(sys.argv) > 3:
         np.savez_compressed(sys.argv[3], x=oc.getState().astype(np.float32), par=0.5)
 

@@ -158,3 +158,40 @@ def test_2dmoc_continuation_chain_psim(Ocean):
     print(f"2dmoc state 2: psiMax {psiMax2:.3e} Sv, psiMin {psiMin2:.6f} Sv")
     assert abs(psiMin1 + psiMax2) <= 1e-4, (psiMin1, psiMax2)
     assert abs(psiMax1 + psiMin2) <= 1e-4, (psiMax1, psiMin2)
+
+
+def test_global1_continuation_step():
+    """Config C5 (run/ocean at 1 degree, 11.2 M unknowns): one pseudo-arclength continuation
+    step (Continuation.H:230-298, 587-813) from the committed near-solution branch state
+    (bench_data/global1_cf05.npz, Combined Forcing 0.5): the Euler predictor, then the
+    bordered Newton corrector converges (update below the Newton tolerance 1e-2 within the
+    iteration limit) and the corrected state's residual is far below the predicted one's."""
+    import os
+    from iemic import config as cf
+    from iemic.continuation import Continuation
+    from iemic.ocean import Ocean
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with np.load(os.path.join(root, "bench_data", "global1_cf05.npz"), allow_pickle=False) as d:
+        x0 = d["x"].astype(np.float64)
+        par0 = float(d["par"])
+    c = cf.preset("global1", mixing=1)
+    oc = Ocean(c, solver_params={"FGMRES tolerance": 1e-4, "FGMRES iterations": 90, "FGMRES restarts": 20})
+    oc.setState(x0)
+    oc.setPar("Combined Forcing", par0)
+    f_start = np.linalg.norm(oc.computeRHS())
+    cont = Continuation(oc, {"continuation parameter": "Combined Forcing", "initial step size": 0.1,
+                             "Newton tolerance": 1e-2, "normalize strategy": "N",
+                             "corrector residual test": "D", "predictor bound": 3000.0,
+                             "post processing": "never"})
+    cont.initialize()
+    cont.createInitialTangent()
+    cont.store()
+    assert cont.eulerPredictor() == 0
+    f_pred = np.linalg.norm(oc.getRHS("V"))
+    assert cont.newtonCorrector() == 0
+    f_corr = cont.normRHStest
+    print(f"C5 step: |F| start {f_start:.3e}, predicted {f_pred:.3e}, corrected {f_corr:.3e} "
+          f"after {cont.newtonIter} Newton iterations, par {cont.par:.5f}")
+    assert cont.par > par0
+    assert f_corr < 0.1 * f_pred
+    oc.close()
