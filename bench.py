@@ -352,6 +352,24 @@ def bench_coupled(args):
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                         "algorithmic_bytes": bsp, "launch_us": round(sp_ms * 1e3, 2)},
            "cpu_baseline": None}
+    if not args.no_cpu:
+        from oracle import atmos_oracle as ao
+        from oracle import oracle as orc
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        cb = orc.coupled_newton_step(cfg, L, xo, xa, comb, ao.COUPLED_RUN_PARAMS, ts_sweeps=args.ts_sweeps,
+                                     dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega, ts_mg=args.ts_mg,
+                                     tol=args.tol, m=args.krylov, maxit=args.krylov * (args.restarts + 1))
+        out["cpu_baseline"] = {
+            "value": round(cb["total"] * 1e3, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
+            "sample": (f"timed, one full coupled Newton step on the CPU restatements ({cores} OpenMP threads "
+                       f"for the ocean): oracle/thcm_oracle.c in coupled mode (bitwise vs the reference "
+                       f"Fortran) + oracle/atmos_oracle.py, forward block GS (ocean prec_oracle.c, "
+                       f"atmosphere sparse LU), FGMRES({args.krylov}) in numpy: F {cb['t_rhs']*1e3:.0f} ms, "
+                       f"J {cb['t_jac']*1e3:.0f} ms, set-up {cb['t_prec']*1e3:.0f} ms, {cb['iters']} iterations "
+                       f"to {cb['rel']:.1e} in {cb['t_solve']:.1f} s"),
+            "iters": cb["iters"]}
+        out["newton"]["norm_f0_cpu"] = cb["norm_f0"]
+        out["newton"]["norm_f1_cpu"] = cb["norm_f1"]
     print(json.dumps(out), flush=True)
 
 

@@ -39,7 +39,8 @@ class _Cfg(C.Structure):
                 ("iza", C.c_int), ("forcing_type", C.c_int), ("ih", C.c_int),
                 ("vmix", C.c_int), ("coriolis_on", C.c_int), ("alphaT", C.c_double),
                 ("alphaS", C.c_double), ("int_sign", C.c_int), ("nic", C.c_int),
-                ("mic", C.c_int), ("rho_mixing", C.c_int)]
+                ("mic", C.c_int), ("rho_mixing", C.c_int), ("coupled_t", C.c_int),
+                ("coupled_s", C.c_int)]
 
 
 def _p(a, t):
@@ -57,6 +58,8 @@ def _load():
         lib = C.CDLL(LIB_ORACLE)
         lib.orc_create.restype = C.c_void_p
         lib.orc_create.argtypes = [C.POINTER(_Cfg), C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        lib.orc_set_atmos.argtypes = [C.c_void_p] + [C.POINTER(C.c_double)] * 5
+        lib.orc_get_deps.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         lib.orc_destroy.argtypes = [C.c_void_p]
         lib.orc_set_par.argtypes = [C.c_void_p, C.c_int, C.c_double]
         lib.orc_get_par.argtypes = [C.c_void_p, C.c_int]
@@ -87,7 +90,7 @@ def cfg_struct(d: dict) -> _Cfg:
                 d["ymax_deg"], d["periodic"], d["hdim"], d["qz"], d["tres"], d["sres"],
                 d["ite"], d["its"], d["iza"], d["forcing_type"], d["ih"], d["vmix"],
                 d["coriolis_on"], d["alphaT"], d["alphaS"], d["int_sign"], d["nic"], d["mic"],
-                d["rho_mixing"])
+                d["rho_mixing"], int(d.get("coupled_T", 0)), int(d.get("coupled_S", 0)))
 
 
 class Oracle:
@@ -118,6 +121,20 @@ class Oracle:
             self.lib.orc_destroy(self.h)
         except Exception:
             pass
+
+    def set_atmos(self, t, q, a, pars, p=None):
+        """Ocean::synchronize(atmos) on the restatement (coupled_T / coupled_S configs)"""
+        arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (t, q, a)]
+        pa = np.ascontiguousarray(pars, dtype=np.float64)
+        pp = None if p is None else np.ascontiguousarray(p, dtype=np.float64)
+        self._atm = (arrs, pa, pp)
+        self.lib.orc_set_atmos(self.h, *[_p(v, C.c_double) for v in arrs],
+                               None if pp is None else _p(pp, C.c_double), _p(pa, C.c_double))
+
+    def get_deps(self) -> np.ndarray:
+        out = np.zeros(7)
+        self.lib.orc_get_deps(self.h, _p(out, C.c_double))
+        return out
 
     def set_par(self, idx, v):
         self.lib.orc_set_par(self.h, int(idx), float(v))
@@ -577,3 +594,100 @@ class BlockILU:
             self.lib.orc_ilu_destroy(self.h)
         except Exception:
             pass
+
+
+# ------------------------------------------------------------------------------------
+# coupled ocean + atmosphere Newton step on the CPU (CoupledModel.C, bench cpu_baseline)
+
+def coupled_newton_step(cfg, landm, xo, xa, comb, atm_params, ts_sweeps=12, dyn_iters=4,
+                        dyn_omega=0.95, ts_mg=1, tol=1e-8, m=100, maxit=600):
+    """One Newton step of CoupledModel (solving scheme 'C', preconditioning 'F') on the CPU
+    restatements: synchronize (Ocean::synchronize(atmos): T, q, A, dimensional P over water,
+    CommPars; Atmosphere: SST), F and J of the ocean (thcm_oracle.c in coupled mode) and of
+    the atmosphere (atmos_oracle.py), the coupling blocks (Ocean::getBlock /
+    Atmosphere::getBlock), FGMRES(m) on [ocean | atmosphere] with the forward block
+    Gauss-Seidel preconditioner (ocean: prec_oracle.c block GS; atmosphere: sparse LU
+    with r_a - C_ao z_o), x += dx, F(x + dx).  Returns timings and norms."""
+    import time
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    from . import atmos_oracle as ao
+    t_all = time.perf_counter()
+    n, mm, l = cfg.n, cfg.m, cfg.l
+    o = Oracle(cfg.ref_dict(), landm, cfg.par_list())
+    o.set_par(19, comb)
+    surf = (landm[l, 1:mm + 1, 1:n + 1] != 0).astype(int)
+    deps0 = o.get_deps()
+    at = ao.AtmosOracle(n, mm, cfg.xmin, cfg.xmax, cfg.ymin, cfg.ymax, cfg.periodic, surf,
+                        Ooa=deps0[0], Os=deps0[1], params={**atm_params, "Combined Forcing": comb})
+    No = 6 * n * mm * l
+    top = 6 * (((l - 1) * mm) * n + np.arange(n * mm)) + 4     # surface T rows
+
+    def sync(xo_, xa_):
+        T, Q, A = xa_[0:3 * n * mm:3], xa_[1:3 * n * mm:3], xa_[2:3 * n * mm:3]
+        P = at.P
+        pf = np.where(surf.reshape(-1) == 0, at.pdist * (P.Eo0 + P.eta * P.qdim * xa_[at.rowP]), 0.0)
+        o.set_atmos(T, Q, A, at.P.commpars(), p=pf if cfg.coupled_s else None)
+        return xo_[top]
+
+    def rhs(xo_, xa_):
+        sst = sync(xo_, xa_)
+        return np.concatenate([o.rhs(xo_), at.rhs(xa_, sst)])
+
+    t = time.perf_counter()
+    F0 = rhs(xo, xa)
+    t_rhs = time.perf_counter() - t
+    t = time.perf_counter()
+    val, _ = o.jacobian(xo)
+    Jo = sp.csr_matrix((val, o.col, o.rowptr), shape=(No, No))
+    Ja = at.jacobian(xa).tocsc()
+    Cao = at.block_from_ocean(l).tocsr()
+    Coa = at.block_to_ocean(l, surf, o.get_deps(), comb, o.get_par(10), coupled_s=bool(cfg.coupled_s),
+                            rowintcon=o.rowintcon).tocsr()
+    A = sp.bmat([[Jo, Coa], [Cao, Ja]]).tocsr()
+    t_jac = time.perf_counter() - t
+    t = time.perf_counter()
+    G = BlockGS(o, val, ts_sweeps, dyn_iters=dyn_iters, dyn_omega=dyn_omega, ts_mg=ts_mg)
+    lu = spla.splu(Ja)
+    t_prec = time.perf_counter() - t
+
+    def prec(r):
+        zo = G.apply(r[:No])
+        return np.concatenate([zo, lu.solve(r[No:] - Cao @ zo)])
+
+    t = time.perf_counter()
+    b = -F0
+    nb = np.linalg.norm(b)
+    x = np.zeros_like(b)
+    its = 0
+    rel = 1.0
+    V = np.zeros((m + 1, len(b)))
+    Z = np.zeros((m, len(b)))
+    while its < maxit and rel > tol:                       # FGMRES(m), x0 = 0, restarts
+        r = b - A @ x
+        beta = np.linalg.norm(r)
+        V[0] = r / beta
+        H = np.zeros((m + 1, m))
+        g = np.zeros(m + 1)
+        g[0] = beta
+        for k in range(m):
+            Z[k] = prec(V[k])
+            w = A @ Z[k]
+            for rep in range(2):                            # CGS2
+                h = V[:k + 1] @ w
+                w -= h @ V[:k + 1]
+                H[:k + 1, k] += h
+            H[k + 1, k] = np.linalg.norm(w)
+            V[k + 1] = w / H[k + 1, k]
+            its += 1
+            y = np.linalg.lstsq(H[:k + 2, :k + 1], g[:k + 2], rcond=None)[0]
+            rel = np.linalg.norm(H[:k + 2, :k + 1] @ y - g[:k + 2]) / nb
+            if rel <= tol or its >= maxit:
+                break
+        x = x + y @ Z[:len(y)]
+        rel = np.linalg.norm(b - A @ x) / nb
+    t_solve = time.perf_counter() - t
+    F1 = rhs(xo + x[:No], xa + x[No:])
+    total = time.perf_counter() - t_all
+    return dict(total=total, t_rhs=t_rhs, t_jac=t_jac, t_prec=t_prec, t_solve=t_solve, iters=its,
+                rel=rel, norm_f0=float(np.linalg.norm(F0)), norm_f1=float(np.linalg.norm(F1)))

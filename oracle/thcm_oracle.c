@@ -7,9 +7,9 @@
  * restatement reproduces the reference to the last bit or within a few ulps; this file
  * must be compiled with -ffp-contract=off.
  *
- * Scope: ocean-only (coupled_T = coupled_S = 0), idealized forcing (ite = its = 1,
- * iza = 2), no internal Levitus forcing, vmix = 0 (mixing Jacobian not restated yet:
- * SURVEY.md §8f row 1).
+ * Scope: ocean-only or coupled to an external atmosphere (coupled_T / coupled_S, no sea
+ * ice: msi = gsi = mc = 0), idealized forcing (ite = its = 1, iza = 2), no internal
+ * Levitus forcing; vertical mixing per the default vmix parameters.
  */
 #include "thcm_oracle.h"
 #include <math.h>
@@ -33,6 +33,10 @@ enum { AL_T = 1, RAYL, EK_V, EK_H, ROSB, MIXP, RESC, SPL1, HMTP, SUNP, PE_H, PE_
        LAMB, SALT, WIND, TEMP, BIOT, COMB, ARCL, NLES, IFRICB, CONT, ENER, ALPC, CMPR,
        FPER, SPER, MKAP, SPL2 };
 
+/* m_atm constants (atm.F90:5-19) */
+static const double rhoa_atm = 1.25, ch_atm = 0.94 * 1.3e-03, cpa_atm = 1000., uw_atm = 8.5;
+static const double sun0_atm = 1360., c0_atm = 0.43, lv_atm = 2.5e+06;
+
 /* usr.F90:131-160 fixed parameters */
 static const double pi_ = 3.14159265358979323846;
 static const double omegadim = 7.292e-05, r0dim = 6.37e+06, udim = 0.1e+00, gdim = 9.8e+00;
@@ -51,6 +55,10 @@ struct orc {
     double par[31];
     double QTnd, QSnd;
     double *taux, *tauy, *tatm, *emip, *spert;
+    /* coupled atmosphere (m_atm: atmos_coef usrc.F90:1183-1223, set_atmos_parameters
+     * 237-293; inserted fields inserts.F90) */
+    double *qatm, *albe, *patm, *suno;
+    double Ooa, Os, lvsc, nus, eta_a, qdim_a, dqso, eo0, albe0, albed;
     double* Frc;                       /* forcing.F90 (before boundaries zeroing) */
     int rowintcon;                     /* 0-based, -1 if SRES != 0 */
     int vmix_temp, vmix_salt, vmix_fix; /* m_mix flags (mix_imp.f vmix_init/control)   */
@@ -213,12 +221,24 @@ static void forcing(orc_t* o)
         }
     double etabi = par[COMB] * par[TEMP] * ((double)(1 - TRES) + TRES * par[BIOT]);
     double temcor = 0.0;
+    if (!o->c.coupled_t) {
+        for (int j = 1; j <= m; j++)
+            for (int i = 1; i <= n; i++) o->tatm[(j - 1) * n + i - 1] = temfun(o, Y(j));
+        if (TRES == 0) temcor = qint(o, o->tatm);
+    }
     for (int j = 1; j <= m; j++)
-        for (int i = 1; i <= n; i++) o->tatm[(j - 1) * n + i - 1] = temfun(o, Y(j));
-    if (TRES == 0) temcor = qint(o, o->tatm);
-    for (int j = 1; j <= m; j++)
-        for (int i = 1; i <= n; i++)
-            o->Frc[frow(o, i, j, l, TT)] = etabi * (o->tatm[(j - 1) * n + i - 1] - temcor);
+        for (int i = 1; i <= n; i++) {
+            const int q = (j - 1) * n + i - 1;
+            if (o->c.coupled_t) {
+                /* forcing.F90:75-94: QToa = QSW - QSH - QLH; no sea ice (msi = 0) */
+                double QToa = par[COMB] * par[SUNP] * o->suno[j] * (1 - o->albe0 - o->albed * o->albe[q]) +
+                              o->Ooa * o->tatm[q] + o->lvsc * o->eta_a * o->qdim_a * o->qatm[q] -
+                              o->lvsc * o->eo0;
+                o->Frc[frow(o, i, j, l, TT)] = QToa * (double)(1 - LM(o, i, j, l));
+            } else {
+                o->Frc[frow(o, i, j, l, TT)] = etabi * (o->tatm[q] - temcor);
+            }
+        }
     double gamma = par[COMB] * par[SALT] * ((double)(1 - SRES) + SRES * par[BIOT]);
     double salcor = 0.0, adapted_salcor = 0.0, spertcor = 0.0;
     for (int j = 1; j <= m; j++)
@@ -231,9 +251,16 @@ static void forcing(orc_t* o)
         free(zero);
         spertcor = qint(o, o->spert);
     }
+    const double pQSnd = par[COMB] * par[SALT] * o->QSnd;
     for (int j = 1; j <= m; j++)
         for (int i = 1; i <= n; i++) {
             int q = (j - 1) * n + i - 1;
+            if (o->c.coupled_s) {
+                /* forcing.F90:162-182: E - P, patm dimensional; no sea ice (msi = gsi = 0) */
+                double QSoa = pQSnd * (o->eo0 - o->eta_a * o->qdim_a * o->qatm[q] - o->patm[q]);
+                o->Frc[frow(o, i, j, l, SS)] = QSoa * (double)(1 - LM(o, i, j, l));
+                continue;
+            }
             o->Frc[frow(o, i, j, l, SS)] =
                 gamma * (1 - par[HMTP]) * (o->emip[q] - salcor) +
                 gamma * par[HMTP] * (0.0 - adapted_salcor) +
@@ -475,7 +502,7 @@ static void gradp(const orc_t* o, int type, int j, int k, atom_t a)
 /* Local block An(27,6,6) of one cell: Aloc[kk][ii][jj], 1-based like the Fortran. */
 typedef double aloc_t[NP + 1][NUN + 1][NUN + 1];
 
-/* usrc.F90:588-772 lin, restricted to one cell (coupled_T = coupled_S = 0) */
+/* usrc.F90:588-772 lin, restricted to one cell (coupled terms without sea ice, mc = 0) */
 static void lin_cell(const orc_t* o, int i, int j, int k, aloc_t A)
 {
     const double* par = o->par;
@@ -531,9 +558,22 @@ static void lin_cell(const orc_t* o, int i, int j, int k, aloc_t A)
     tderiv(o, 3, i, j, k, txx);
     tderiv(o, 4, i, j, k, tyy);
     tderiv(o, 5, i, j, k, tzz);
+    /* usrc.F90:724-766: the latent-heat dependence dedt = lvsc eta qdim (deltat/qdim) dqso
+     * of T on T (coupled_T) and nus (deltat/qdim) dqso of S on T (coupled_S), deltat = 1 */
+    const double deltat = 1.0;
+    const double dedt_t = o->lvsc * o->eta_a * o->qdim_a * (deltat / o->qdim_a) * o->dqso;
+    const double dedt_s = o->nus * (deltat / o->qdim_a) * o->dqso;
     for (int s = 1; s <= NP; s++) {
-        A[s][TT][TT] = -ph * (txx[s] + tyy[s]) - pv * tzz[s] + TRES * bi * tc[s];
-        A[s][SS][SS] = -ph * (txx[s] + tyy[s]) - pv * tzz[s] + SRES * bi * sc[s];
+        if (o->c.coupled_t)
+            A[s][TT][TT] = -ph * (txx[s] + tyy[s]) - pv * tzz[s] + o->Ooa * tc[s] + dedt_t * sc[s];
+        else
+            A[s][TT][TT] = -ph * (txx[s] + tyy[s]) - pv * tzz[s] + TRES * bi * tc[s];
+        if (o->c.coupled_s) {
+            A[s][SS][SS] = -ph * (txx[s] + tyy[s]) - pv * tzz[s];
+            A[s][SS][TT] = -dedt_s * sc[s];
+        } else {
+            A[s][SS][SS] = -ph * (txx[s] + tyy[s]) - pv * tzz[s] + SRES * bi * sc[s];
+        }
     }
 }
 
@@ -1259,7 +1299,7 @@ static void fillcolB_cell(const orc_t* o, int i, int j, int k, double* coB)
 orc_t* orc_create(const orc_cfg* cfg, const int* landm, const double* spert)
 {
     if (cfg->ite != 1 || cfg->its != 1 || cfg->iza != 2 || cfg->vmix < 0 || cfg->vmix > 2) {
-        fprintf(stderr, "orc_create: only idealized ocean-only forcing, vmix 0..2 supported\n");
+        fprintf(stderr, "orc_create: only idealized forcing, vmix 0..2 supported\n");
         return NULL;
     }
     orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
@@ -1303,12 +1343,26 @@ orc_t* orc_create(const orc_cfg* cfg, const int* landm, const double* spert)
     o->tatm = (double*)calloc((size_t)n * m, sizeof(double));
     o->emip = (double*)calloc((size_t)n * m, sizeof(double));
     o->spert = (double*)calloc((size_t)n * m, sizeof(double));
+    o->qatm = (double*)calloc((size_t)n * m, sizeof(double));
+    o->albe = (double*)calloc((size_t)n * m, sizeof(double));
+    o->patm = (double*)calloc((size_t)n * m, sizeof(double));
+    o->suno = (double*)calloc((size_t)m + 2, sizeof(double));
     if (spert) memcpy(o->spert, spert, sizeof(double) * n * m);
     o->Frc = (double*)calloc(o->ndim, sizeof(double));
     grid(o);
     double dzne = o->dz * DFZT(l);
     o->QTnd = r0dim / (udim * cp0 * rhodim * cfg->hdim * dzne);
     o->QSnd = s0 * r0dim / (deltas * udim * cfg->hdim * dzne);
+    /* atmos_coef (usrc.F90:1183-1223) */
+    {
+        const double muoa = rhoa_atm * ch_atm * cpa_atm * uw_atm;
+        o->Os = sun0_atm * c0_atm / 4 * o->QTnd;
+        o->Ooa = muoa * o->QTnd;
+        for (int j = 1; j <= m; j++) {
+            const double sy = sin(Y(j));
+            o->suno[j] = o->Os * (1 - .482 * (3 * (sy * sy) - 1.) / 2.);
+        }
+    }
     stpnt(o);
     forcing(o);
     /* integral condition row (THCM.C:661-711) */
@@ -1403,7 +1457,8 @@ void orc_destroy(orc_t* o)
     if (!o) return;
     free(o->x); free(o->y); free(o->z); free(o->xu); free(o->yv); free(o->zw); free(o->ze);
     free(o->zwe); free(o->dfzT); free(o->dfzW); free(o->landm); free(o->taux); free(o->tauy);
-    free(o->tatm); free(o->emip); free(o->spert); free(o->Frc); free(o->gptr); free(o->gcol);
+    free(o->tatm); free(o->emip); free(o->spert);
+    free(o->qatm); free(o->albe); free(o->patm); free(o->suno); free(o->Frc); free(o->gptr); free(o->gcol);
     free(o);
 }
 
@@ -1607,4 +1662,39 @@ void orc_csr_spmv(int nrows, const int64_t* rowptr, const int* col, const double
         for (int64_t p = rowptr[r]; p < rowptr[r + 1]; p++) s += val[p] * x[col[p]];
         y[r] = s;
     }
+}
+
+/* Ocean::synchronize(atmos): inserts.F90 setters and set_atmos_parameters (usrc.F90:237-293,
+ * pars = AtmosLocal::CommPars: tdim, qdim, nuq, eta, dqso, dqsi, dqdt, Eo0, Ei0, Cs, t0o, t0i,
+ * a0, da, tauf, tauc, comb, albf), then forcing */
+void orc_set_atmos(orc_t* o, const double* t, const double* q, const double* a, const double* p,
+                   const double* pars)
+{
+    const size_t nm = (size_t)o->n * o->m;
+    memcpy(o->tatm, t, sizeof(double) * nm);
+    memcpy(o->qatm, q, sizeof(double) * nm);
+    memcpy(o->albe, a, sizeof(double) * nm);
+    if (p) memcpy(o->patm, p, sizeof(double) * nm);
+    else memset(o->patm, 0, sizeof(double) * nm);
+    o->qdim_a = pars[1];
+    o->eta_a = pars[3];
+    o->dqso = pars[4];
+    o->eo0 = pars[7];
+    o->albe0 = pars[12];
+    o->albed = pars[13];
+    o->nus = o->par[COMB] * o->par[SALT] * o->eta_a * o->qdim_a * o->QSnd;
+    o->lvsc = o->par[COMB] * o->par[TEMP] * rhodim * lv_atm * o->QTnd;
+    forcing(o);
+}
+
+/* getdeps (usrc.F90:201-219) */
+void orc_get_deps(const orc_t* o, double* out)
+{
+    out[0] = o->Ooa;
+    out[1] = o->Os;
+    out[2] = o->nus;
+    out[3] = o->eta_a;
+    out[4] = o->lvsc;
+    out[5] = o->qdim_a;
+    out[6] = o->par[COMB] * o->par[SALT] * o->QSnd;
 }

@@ -29,6 +29,7 @@ typedef struct {
     int int_sign;                      /* "Salinity Integral Sign" (THCM.C:235)     */
     int nic, mic;                      /* integral row coordinates (-1 = default)   */
     int rho_mixing;                    /* "Rho mixing" (mix_imp.f vmix_fun)         */
+    int coupled_t, coupled_s;          /* "Coupled Temperature/Salinity" (THCM.C:232) */
 } orc_cfg;
 
 typedef struct orc orc_t;
@@ -36,6 +37,13 @@ typedef struct orc orc_t;
 /* landm: (n+2)(m+2)(l+2) ints in THCM layout (i fastest), as passed to init_
  * (usrc.F90:29); spert: n*m (get_spert, global.F90:590-611).  */
 orc_t* orc_create(const orc_cfg* cfg, const int* landm, const double* spert);
+/* Ocean::synchronize(atmos) (Ocean.C:1443-1472): atmosphere T, q, albedo, P on the n*m
+ * surface (i fastest) -> THCM::setAtmosphereT/Q/A/P (inserts.F90) and the 18 CommPars ->
+ * set_atmos_parameters (usrc.F90:237-293), then forcing */
+void orc_set_atmos(orc_t* o, const double* t, const double* q, const double* a, const double* p,
+                   const double* pars18);
+/* getdeps (usrc.F90:201-219): Ooa, Os, nus, eta, lvsc, qdim, pQSnd */
+void orc_get_deps(const orc_t* o, double* out7);
 void orc_destroy(orc_t* o);
 void orc_set_par(orc_t* o, int idx, double v);
 double orc_get_par(const orc_t* o, int idx);

@@ -158,3 +158,20 @@ def test_ocean_block_matches_fortran_fd(oracle_lib, name):
         else:
             col = at.row(i, j, {"t": ao.TT, "q": ao.QQ, "a": ao.AA}[fld])
         np.testing.assert_allclose(dF, Cb[:, col], rtol=1e-6, atol=1e-9 * np.abs(Cb).max())
+
+
+@pytest.mark.parametrize("name", ["coupled_natl8", "coupled_natl8s"])
+@pytest.mark.parametrize("kind", ["zero", "synthetic"])
+def test_oracle_coupled_ocean_bitexact(oracle_lib, name, kind):
+    """The oracle's C restatement in coupled mode (usrc.F90:724-766 lin, forcing.F90:75-94 /
+    162-182, set_atmos_parameters) against the reference Fortran: J and F bitwise -- the
+    checker behind the coupled CPU baseline."""
+    c = cf.preset(name)
+    g = golden(name)
+    o = oracle_lib.Oracle(c.ref_dict(), landm_of(name), c.par_list())
+    o.set_atmos(g["atm_t"], g["atm_q"], g["atm_a"], g["atm_pars"], p=g["atm_p"])
+    x = g[f"{kind}_x"]
+    val, _ = o.jacobian(x)
+    ref = fortran_placed(oracle_lib, o.rowptr, o.col, g, kind)
+    np.testing.assert_array_equal(val, ref)
+    np.testing.assert_array_equal(bits(o.rhs(x)), bits(-g[f"{kind}_B"]))
