@@ -468,6 +468,18 @@ extern "C" int iemic_layout(const iemic_ctx* c, int64_t* out)
     return 0;
 }
 
+/* communication counters since the last call (halo batches, messages and bytes sent,
+ * all-reduces), reset by the call */
+extern "C" int iemic_comm_stats(iemic_ctx* c, int64_t* out4)
+{
+    if (!c || !out4) return IEMIC_EINVAL;
+    for (int q = 0; q < 4; q++) {
+        out4[q] = c->stat[q];
+        c->stat[q] = 0;
+    }
+    return 0;
+}
+
 /* Maximal-graph rows owned by this context (THCM.C:2288-2521) */
 extern "C" int64_t iemic_graph_nnz(const iemic_ctx* c)
 {

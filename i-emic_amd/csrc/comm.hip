@@ -127,6 +127,7 @@ void comm_destroy(iemic_ctx* c)
 int allreduce_sum(iemic_ctx* c, double* dev, int count)
 {
     if (c->nranks <= 1 || count <= 0) return 0;
+    c->stat[3]++;
     if (c->group) return local_allreduce(c, dev, count);
     if (c->tp.send) return host_allreduce(c, dev, count);
     NCCL_OK(ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)c->comm,
@@ -295,6 +296,12 @@ static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
 int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops)
 {
     if (c->nranks <= 1 || ops.empty()) return 0;
+    c->stat[0]++;
+    for (const Msg& op : ops)
+        if (op.send) {
+            c->stat[1]++;
+            c->stat[2] += (int64_t)(sizeof(double) * seg_count(op.s));
+        }
     if (c->group) return run_local(c, ops);
     if (c->tp.send) return run_host(c, ops);
     return run_rccl(c, ops);

