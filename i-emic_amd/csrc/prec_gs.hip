@@ -586,7 +586,9 @@ __global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__
 
 /* ---- apply ------------------------------------------------------------------------ */
 
-/* z = r on identity rows; rr = r - A(:, known) r(known) on the others (slot bitmask) */
+/* z = r on identity rows and 0 on the others (the apply's starting iterate: no separate
+ * memset; halo cells are only read after an exchange, and one rank reads none);
+ * rr = r - A(:, known) r(known) on the others (slot bitmask) */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const uint64_t* __restrict__ kmask, const double* __restrict__ r,
                         double* __restrict__ z, double* __restrict__ rr, Lay L)
@@ -598,7 +600,7 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     for (int R = 0; R < NUN; R++) {
         const int64_t row = NUN * cell + R;
         acc[R] = r[row];
-        if (known[row]) z[row] = acc[R];
+        z[row] = known[row] ? acc[R] : 0.0;
     }
     uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
     if (b[0] | b[1]) {
@@ -2839,7 +2841,6 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     };
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
-    HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
                        r, z, gs.rr.p, L);
     if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;

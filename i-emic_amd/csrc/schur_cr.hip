@@ -400,27 +400,32 @@ __global__ void k_cr_transpose(const double* __restrict__ X, double* __restrict_
 }
 
 /* dense tail, apply: x = Tinv b (row-major, M <= CR_TAIL_MAX), one wave per row, b staged
- * in LDS, four independent accumulators per lane, a fixed shuffle tree (deterministic) */
-constexpr int CR_TAIL_MAX = 2048;
+ * in LDS; every load of the row is issued before the first multiply (up to 32 per lane,
+ * eight independent accumulators), then a fixed shuffle tree (deterministic) */
+constexpr int CR_TAIL_MAX = 1024;          /* cr_init: tail_max */
 __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv, const double* __restrict__ b,
                                                  double* __restrict__ x, int M)
 {
     __shared__ double vb[CR_TAIL_MAX];
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const double* A = Tinv + (size_t)(r < M ? r : 0) * M;
+    constexpr int NL = CR_TAIL_MAX / 64;
+    double a[NL];
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int c = lane + 64 * u;
+        a[u] = c < M ? A[c] : 0.0;
+    }
     for (int c = threadIdx.x; c < M; c += 256) vb[c] = b[c];
     __syncthreads();
-    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= M) return;
-    const double* A = Tinv + (size_t)r * M;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    int c = lane;
-    for (; c + 192 < M; c += 256) {
-        a0 += A[c] * vb[c];
-        a1 += A[c + 64] * vb[c + 64];
-        a2 += A[c + 128] * vb[c + 128];
-        a3 += A[c + 192] * vb[c + 192];
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int c = lane + 64 * u;
+        if (c < M) acc[u & 7] += a[u] * vb[c];
     }
-    for (; c < M; c += 64) a0 += A[c] * vb[c];
-    double v = (a0 + a1) + (a2 + a3);
+    double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) x[r] = v;
@@ -883,7 +888,7 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
     /* dense tail: the first level of at most 1024 unknowns (2048: no gain) and its
      * descendants become one explicit inverse (built at set-up by solving the tail for the
      * identity), so the apply spends one GEMV launch instead of 2 (nlev - lt) + 1 */
-    constexpr int tail_max = 1024;
+    constexpr int tail_max = CR_TAIL_MAX;
     cr.lt = cr.nlev;
     cr.tM = 0;
     for (int l = 0; l < cr.nlev; l++)

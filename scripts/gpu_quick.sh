@@ -20,3 +20,6 @@ if [ -n "$PROF" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
       python -u bench.py --steps 1 --warmup 1 --no-cpu ${BENCH_ARGS} > gpurun_out/prof.log 2>&1 && echo "prof ok"
 fi
+if [ -n "$MB" ]; then
+  timeout -k 10 120 $MB > gpurun_out/mb.log 2>&1 && echo "mb ok" || { echo "mb FAILED"; exit 1; }
+fi
