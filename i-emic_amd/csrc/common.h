@@ -136,7 +136,10 @@ struct BlockGS {
                                      /* columns, -1 otherwise                           */
     DevBuf<int> ocol;                /* (j*n+i) -> this band's Schur rhs entry, -2 - entry */
                                      /* for a pinned column (written 0), -1 for none     */
-    DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8), halo-filled */
+    DevBuf<double> gslot;            /* per cell: U/V rows' P couplings (8) and the W row's */
+                                     /* P couplings (2), halo-filled                     */
+    DevBuf<double> rcol;             /* per owned water column: the Schur right-hand side */
+                                     /* as a linear form in rr (18 x l coefficients)     */
     DevBuf<uint8_t> known;           /* per row: identity row (z = r)                   */
     DevBuf<int> col_of_ij;           /* (j*n+i) -> Schur index i*m+j, or -1 (no water)   */
     DevBuf<int> ij_of_col;           /* Schur index -> j*n+i                            */

@@ -24,23 +24,6 @@
 namespace iemic {
 
 /* ---- SpMV ------------------------------------------------------------------------ */
-/* row R of one cell: slot-major coefficients (coalesced over adjacent cells) times the
- * implicit-column gathers; nc: the neighbour cells (nb_cells) */
-template <int R>
-__device__ __forceinline__ double row_dot_rb(const double* __restrict__ val, const double* __restrict__ x,
-                                             int64_t lc, int64_t nloc, const int (*nc)[9])
-{
-    constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
-    double acc = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const Slot sl = SLOTS[B + s];
-        const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc += val[(int64_t)(B + s) * nloc + lc] * x[NUN * (int64_t)cidx + sl.var];
-    }
-    return acc;
-}
-
 /* ---- k_spmv7: LDS-staged x, slot-balanced waves ----------------------------------------
  * One workgroup (4 waves) per tile of up to 64 cells along i of one (j, k) grid row.  The
  * x values of the tile's neighbourhood -- the six (dj, dk) grid rows the slot table reaches
@@ -147,35 +130,56 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
 /* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
  * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
  * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
- * full rows of the SpMV are used: one wavefront per (64 cells, dynamics equation). */
+ * full rows of the SpMV are used.  One workgroup per 64 cells; the 64 slots of the four rows
+ * are split evenly over the waves (U | U+V | V+W | W+P, 16 each: a wave per equation would
+ * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
+ * rows' partials meet in LDS. */
+template <int S0, int S1>
+__device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
+                                            int64_t lc, int64_t nloc, const int (*nc)[9], double* acc)
+{
+#pragma unroll
+    for (int s = S0; s < S1; s++) {
+        const Slot sl = SLOTS[s];
+        const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
+        acc[sp7_row(s) - sp7_row(S0)] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+    }
+}
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
                                                   const uint8_t* __restrict__ known,
                                                   double* __restrict__ d, int64_t nloc, int nblk)
 {
+    __shared__ double red[4][2][64];
     const int per = (nblk + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     if (tile >= nblk) return;
-    const int64_t lc = (int64_t)tile * 64 + (threadIdx.x & 63);
-    if (lc >= nloc) return;
-    const int R = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
-    int nc[3][9];
-    nb_cells(X, il, j, k, nc);
-    const int64_t row = NUN * ((int64_t)HALO * X.l * X.nx + lc) + R;
-    if (known[row]) {
-        d[row] = 0.0;
-        return;
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t lc0 = (int64_t)tile * 64, lc = lc0 + c;
+    const bool act = lc < nloc;
+    double acc[2] = {0.0, 0.0};
+    if (act) {
+        const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
+        int nc[3][9];
+        nb_cells(X, il, j, k, nc);
+        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, acc);
+        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, acc);
+        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, acc);
+        else dyn_partial<48, 64>(val, z, lc, nloc, nc, acc);
     }
-    double acc;
-    switch (R) {
-    case UU: acc = row_dot_rb<UU>(val, z, lc, nloc, nc); break;
-    case VV: acc = row_dot_rb<VV>(val, z, lc, nloc, nc); break;
-    case WW: acc = row_dot_rb<WW>(val, z, lc, nloc, nc); break;
-    default: acc = row_dot_rb<PP>(val, z, lc, nloc, nc); break;
-    }
-    d[row] = r[row] - acc;
+    red[g][0][c] = acc[0];
+    red[g][1][c] = acc[1];
+    __syncthreads();
+    /* rows of the waves: g0 {U} g1 {U,V} g2 {V,W} g3 {W,P}; thread = (cell, row) */
+    const int cc = threadIdx.x >> 2, R = threadIdx.x & 3;
+    if (lc0 + cc >= nloc) return;
+    const double sum = R == 0 ? red[0][0][cc] + red[1][0][cc]
+                     : R == 1 ? red[1][1][cc] + red[2][0][cc]
+                     : R == 2 ? red[2][1][cc] + red[3][0][cc]
+                              : red[3][1][cc];
+    const int64_t row = NUN * ((int64_t)HALO * X.l * X.nx + lc0 + cc) + R;
+    d[row] = known[row] ? 0.0 : r[row] - sum;
 }
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d)
@@ -300,21 +304,27 @@ __device__ __forceinline__ void block_sum_n(double* v, double* sm)
 }
 
 /* DCGS2 dot pass: rows 2i, 2i+1 = Q_i.u, Q_i.w (i < nvec); rows 2nvec..2nvec+2 = u.u, u.w,
- * w.w.  Block y < ceil(nvec/8) handles eight basis vectors so that u and w are read once
- * per eight; the last y handles the three self products.  partial[row*gridDim.x + blk]. */
+ * w.w.  Block (bx, by), by < ceil(nvec / DG), handles DG basis vectors against u and w over
+ * chunk bx; by == nq the three self products.  The group index varies fastest in the block
+ * order, so the groups of one chunk run together and u, w come from L2 after the first;
+ * every lane reads two consecutive elements (16-byte loads; N even, 16-byte aligned).
+ * partial[row * nbx + bx].  (scripts/orth_probe.hip: DG = 4 in this order 5.5 TB/s at 89
+ * vectors against 4.5 for DG = 8 with the group index slowest.) */
+constexpr int DCGS_DG = 4;
 __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, int64_t ldv, int nvec,
                                                   const double* __restrict__ u,
                                                   const double* __restrict__ w, int64_t N,
-                                                  double* __restrict__ partial)
+                                                  double* __restrict__ partial, int nbx)
 {
-    /* blockIdx.y < nq: a group of DG basis vectors against u and w (u, w re-read once per
-     * group, so larger groups cut their traffic); blockIdx.y == nq: u.u, u.w, w.w */
-    constexpr int DG = 8;
-    __shared__ double sm[8 * 2 * DG];
+    constexpr int DG = DCGS_DG;
+    __shared__ double sm[4 * 2 * DG];
     const int nq = (nvec + DG - 1) / DG;
-    const int by = blockIdx.y;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int by = blockIdx.x % (nq + 1), bx = blockIdx.x / (nq + 1);
+    const int64_t N2 = N / 2;
+    const int64_t stride = (int64_t)nbx * blockDim.x;
+    const int64_t e0 = (int64_t)bx * blockDim.x + threadIdx.x;
+    const double2* u2 = reinterpret_cast<const double2*>(u);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
     if (by < nq) {
         const int i0 = DG * by;
         const int nv = min(DG, nvec - i0);
@@ -322,42 +332,31 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
 #pragma unroll
         for (int t = 0; t < 2 * DG; t++) acc[t] = 0.0;
         const double* q0 = V + (int64_t)i0 * ldv;
-        if (nv == DG) {
-            for (int64_t e = e0; e < N; e += stride) {
-                const double ue = u[e], we = w[e];
+        for (int64_t e = e0; e < N2; e += stride) {
+            const double2 ue = u2[e], we = w2[e];
 #pragma unroll
-                for (int t = 0; t < DG; t++) {
-                    const double qe = q0[(int64_t)t * ldv + e];
-                    acc[2 * t] += qe * ue;
-                    acc[2 * t + 1] += qe * we;
-                }
-            }
-        } else {
-            for (int64_t e = e0; e < N; e += stride) {
-                const double ue = u[e], we = w[e];
-                for (int t = 0; t < nv; t++) {
-                    const double qe = q0[(int64_t)t * ldv + e];
-                    acc[2 * t] += qe * ue;
-                    acc[2 * t + 1] += qe * we;
+            for (int t = 0; t < DG; t++) {
+                if (t < nv) {
+                    const double2 qe = reinterpret_cast<const double2*>(q0 + (int64_t)t * ldv)[e];
+                    acc[2 * t] += qe.x * ue.x + qe.y * ue.y;
+                    acc[2 * t + 1] += qe.x * we.x + qe.y * we.y;
                 }
             }
         }
         block_sum_n<2 * DG>(acc, sm);
         if (threadIdx.x == 0)
-            for (int t = 0; t < 2 * nv; t++)
-                partial[(int64_t)(2 * i0 + t) * gridDim.x + blockIdx.x] = acc[t];
+            for (int t = 0; t < 2 * nv; t++) partial[(int64_t)(2 * i0 + t) * nbx + bx] = acc[t];
     } else {
         double acc[3] = {0, 0, 0};
-        for (int64_t e = e0; e < N; e += stride) {
-            const double ue = u[e], we = w[e];
-            acc[0] += ue * ue;
-            acc[1] += ue * we;
-            acc[2] += we * we;
+        for (int64_t e = e0; e < N2; e += stride) {
+            const double2 ue = u2[e], we = w2[e];
+            acc[0] += ue.x * ue.x + ue.y * ue.y;
+            acc[1] += ue.x * we.x + ue.y * we.y;
+            acc[2] += we.x * we.x + we.y * we.y;
         }
         block_sum_n<3>(acc, sm);
         if (threadIdx.x == 0)
-            for (int t = 0; t < 3; t++)
-                partial[(int64_t)(2 * nvec + t) * gridDim.x + blockIdx.x] = acc[t];
+            for (int t = 0; t < 3; t++) partial[(int64_t)(2 * nvec + t) * nbx + bx] = acc[t];
     }
 }
 
@@ -372,28 +371,42 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
                                                      double* __restrict__ u, double* __restrict__ w,
                                                      int64_t N)
 {
+    /* two consecutive elements per lane (16-byte loads; N even), four basis vectors per step */
+    constexpr int UN = 4;
     __shared__ double cs[2 * 1024];
     for (int i = threadIdx.x; i < 2 * nvec; i += blockDim.x) cs[i] = coef[i];
     __syncthreads();
     const double* a = cs;
     const double* cc = cs + nvec;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N;
+    const int64_t N2 = N / 2;
+    double2* u2 = reinterpret_cast<double2*>(u);
+    double2* w2 = reinterpret_cast<double2*>(w);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N2;
          e += (int64_t)gridDim.x * blockDim.x) {
-        double su = 0.0, sw = 0.0;
+        double sux = 0.0, suy = 0.0, swx = 0.0, swy = 0.0;
         int i = 0;
-        for (; i + 2 <= nvec; i += 2) {
-            const double q0 = V[(int64_t)i * ldv + e], q1 = V[(int64_t)(i + 1) * ldv + e];
-            su += a[i] * q0 + a[i + 1] * q1;
-            sw += cc[i] * q0 + cc[i + 1] * q1;
+        for (; i + UN <= nvec; i += UN) {
+            double2 q[UN];
+#pragma unroll
+            for (int k = 0; k < UN; k++) q[k] = reinterpret_cast<const double2*>(V + (int64_t)(i + k) * ldv)[e];
+#pragma unroll
+            for (int k = 0; k < UN; k++) {
+                sux += a[i + k] * q[k].x;
+                suy += a[i + k] * q[k].y;
+                swx += cc[i + k] * q[k].x;
+                swy += cc[i + k] * q[k].y;
+            }
         }
         for (; i < nvec; i++) {
-            const double q0 = V[(int64_t)i * ldv + e];
-            su += a[i] * q0;
-            sw += cc[i] * q0;
+            const double2 q = reinterpret_cast<const double2*>(V + (int64_t)i * ldv)[e];
+            sux += a[i] * q.x;
+            suy += a[i] * q.y;
+            swx += cc[i] * q.x;
+            swy += cc[i] * q.y;
         }
-        const double ue = u[e];
-        u[e] = (ue - su) * inv_beta;
-        w[e] = (w[e] - sw - gamma * ue) * inv_beta;
+        const double2 ue = u2[e], we = w2[e];
+        u2[e] = make_double2((ue.x - sux) * inv_beta, (ue.y - suy) * inv_beta);
+        w2[e] = make_double2((we.x - swx - gamma * ue.x) * inv_beta, (we.y - swy - gamma * ue.y) * inv_beta);
     }
 }
 
@@ -727,8 +740,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
-                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS, (nv + 7) / 8 + 1), dim3(256), 0,
-                                   c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p);
+                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS * ((nv + DCGS_DG - 1) / DCGS_DG + 1)), dim3(256),
+                                   0, c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p, RED_BLOCKS);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
                 if ((rc = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc;
@@ -791,7 +804,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 htent[nv] = hjj / bt;
                 zs[jj] = bt;
                 if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
-                hipLaunchKernelGGL(k_dcgs_update, dim3(G), dim3(256), 0, c->stream, V + o, NE, nv,
+                hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, V + o, NE, nv,
                                    c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u + o, wv + o, NL);
             }
             j = ncolf;

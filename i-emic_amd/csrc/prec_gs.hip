@@ -44,6 +44,7 @@ constexpr int S_PU = 54, S_PV = 58;                 /* P row: U/V (0,0),(-1,0),(
 constexpr int S_PW0 = 62, S_PWM = 63;               /* P row: W(k), W(k-1)              */
 constexpr int S_TT0 = 64, S_TS0 = 81;               /* T row: T self, S self            */
 constexpr int S_SS0 = 84, S_ST0 = 101;              /* S row: S self, T self            */
+constexpr int GSL = 10;                             /* gslot doubles per cell           */
 
 /* subdomain layout seen by the kernels (stencil.h ext layout, Decomp2D): n, m global;
  * owned columns [ib0, ib0 + nx), rows from jb0; per-cell arrays are indexed by ext cell,
@@ -215,8 +216,8 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
             const double yu = du * Di[0] + dv * Di[2];
             const double yv = du * Di[1] + dv * Di[3];
             const int g4 = e + 2 * f;                      /* (0,0),(1,0),(0,1),(1,1) */
-            const double gu = ua ? gslot[8 * qc + g4] : 0.0;
-            const double gv = va ? gslot[8 * qc + 4 + g4] : 0.0;
+            const double gu = ua ? gslot[GSL * qc + g4] : 0.0;
+            const double gv = va ? gslot[GSL * qc + 4 + g4] : 0.0;
             acc += yu * gu + yv * gv;
         }
         s += pw[pc] * acc;
@@ -224,14 +225,17 @@ __global__ void k_schur_build(const double* __restrict__ val, const uint8_t* __r
     row[o] = s;
 }
 
-/* per owned cell: the U and V rows' couplings to the 4 P corners (slots 20..23, 42..45) */
+/* per owned cell: the U and V rows' couplings to the 4 P corners (slots 20..23, 42..45)
+ * and the W row's to P(k), P(k+1) (slots 47, 48) */
 __global__ void k_gslot_pack(const double* __restrict__ val, Lay L, double* __restrict__ gslot)
 {
     OWNED_CELL;
     for (int g = 0; g < 4; g++) {
-        gslot[8 * cell + g] = val[(int64_t)(S_UP + g) * ncell + lc];
-        gslot[8 * cell + 4 + g] = val[(int64_t)(S_VP + g) * ncell + lc];
+        gslot[GSL * cell + g] = val[(int64_t)(S_UP + g) * ncell + lc];
+        gslot[GSL * cell + 4 + g] = val[(int64_t)(S_VP + g) * ncell + lc];
     }
+    gslot[GSL * cell + 8] = val[(int64_t)S_WP0 * ncell + lc];
+    gslot[GSL * cell + 9] = val[(int64_t)S_WP1 * ncell + lc];
 }
 
 /* identity-row flags <-> doubles (for the halo exchange of the flags) */
@@ -713,81 +717,49 @@ __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restr
 __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                          const double* __restrict__ z, int i, int j, int k,
                                          int64_t pl, const Lay& L);
-/* Column recurrences as parallel scans: P lanes (P = power of two >= l) per water column,
- * lane = level k.  Each level is an affine map x_k = A_k + B_k x_{k+-1}; a Hillis-Steele
- * scan over the lanes composes them, so the l-step dependency chain becomes log2(P)
- * shuffle steps and every load is issued at once. */
-template <int P>
-__global__ void __launch_bounds__(256) k_gs_ptil_scan(const double* __restrict__ val,
-                                                      const uint8_t* __restrict__ known,
-                                                      const int* __restrict__ col_of_ij,
-                                                      const double* __restrict__ rr,
-                                                      double* __restrict__ z, Lay L)
+/* Column kernels, transposed: one workgroup of 1024 threads per tile of TI = 1024 / LP
+ * consecutive columns of one latitude row (LP = power of two >= l), thread = (column, level)
+ * with the column fastest, so every per-cell load of a wave runs along i (the slot-major
+ * Jacobian rows contiguously, the interleaved vectors at one cell stride); the column
+ * recurrences meet in LDS, where each thread composes the affine maps of the levels it
+ * depends on (at most l steps of LDS reads). */
+__device__ __forceinline__ void col_tile(const Lay& L, int LP, int& il, int& jl, int& k, bool& on)
 {
-    (void)col_of_ij;
-    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-    const int k = threadIdx.x % P;
-    if (t_ >= (int)(L.nloc / L.l)) return;                  /* whole column groups exit */
-    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
-    const int ij = j * L.n + i;
-    const int64_t ncell = L.nloc;
-    double A = 0.0, B = 0.0;
-    bool pa = false;
-    int64_t cell = 0;
-    if (k < L.l) {
-        /* every load of the level at once (no gating on the flags: one memory round) */
-        cell = ecell(L, i, j, k);
-        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
-        const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
-        const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
-        const double rw = rr[NUN * cell + WW];
-        pa = !kp;
-        if (pa && k < L.l - 1 && !kw && g0 != 0.0) {
-            A = rw / g0;
-            B = -g1 / g0;
-        }
-    }
-    /* suffix composition from the top: p_k = A_k + B_k p_{k+1}, p_l = 0 */
-#pragma unroll
-    for (int d = 1; d < P; d <<= 1) {
-        const double A2 = __shfl_down(A, d, P), B2 = __shfl_down(B, d, P);
-        if (k + d < P) {
-            A = A + B * A2;
-            B = B * B2;
-        }
-    }
-    if (pa) z[NUN * cell + PP] = A;
+    const int TI = 1024 / LP;
+    const int tpr = (L.nx + TI - 1) / TI;
+    jl = blockIdx.x / tpr;
+    il = (blockIdx.x % tpr) * TI + (int)threadIdx.x % TI;
+    k = (int)threadIdx.x / TI;
+    on = k < L.l && il < L.nx;
 }
 
-template <int P>
-__global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ val,
-                                                    const uint8_t* __restrict__ known,
-                                                    const int* __restrict__ col_of_ij,
-                                                    const double* __restrict__ pbar,
-                                                    const double* __restrict__ crhs,
-                                                    double* __restrict__ z, Lay L,
-                                                    const double* __restrict__ rr,
-                                                    double* __restrict__ zo, double omega)
+/* 4b/5. p = ptil + pbar and the continuity rows bottom-up, w_k = A_k + B_k w_k-1 (the
+ * transposed column layout of k_gs_ptil_rcol); zo += omega (p, w) in the correction passes */
+template <int LP>
+__global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val,
+                                                  const uint8_t* __restrict__ known,
+                                                  const double* __restrict__ pbar,
+                                                  double* __restrict__ z, Lay L,
+                                                  const double* __restrict__ rr,
+                                                  double* __restrict__ zo, double omega)
 {
-    (void)col_of_ij;
-    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-    const int k = threadIdx.x % P;
-    if (t_ >= (int)(L.nloc / L.l)) return;
-    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
-    const int ij = j * L.n + i;
+    constexpr int TI = 1024 / LP;
+    __shared__ double sA[LP][TI], sB[LP][TI];
+    int il, jl, k;
+    bool on;
+    col_tile(L, LP, il, jl, k, on);
+    const int ii = (int)threadIdx.x % TI;
+    const int i = L.ib0 + il, j = L.jb0 + jl;
     const int64_t ncell = L.nloc;
     double A = 0.0, B = 0.0, pb = 0.0, zp = 0.0;
     bool pa = false, wa = false;
     int64_t cell = 0;
-    if (k < L.l) {
-        /* pbar by Schur index i*m + j (0 on columns without water); every load at once */
+    if (on) {
         cell = ecell(L, i, j, k);
         const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
         const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
         const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
-        /* continuity right-hand side rr_p - Duv uv, evaluated in place */
-        const double rhs = crhs ? crhs[cell]
-                                : rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
+        const double rhs = rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
         pb = pbar[(int64_t)i * L.m + j];
         zp = z[NUN * cell + PP];
         pa = !kp;
@@ -797,24 +769,20 @@ __global__ void __launch_bounds__(256) k_gs_pw_scan(const double* __restrict__ v
             B = -b / a;
         }
     }
-    /* prefix composition from the bottom: w_k = A_k + B_k w_{k-1}, w_{-1} = 0 */
-#pragma unroll
-    for (int d = 1; d < P; d <<= 1) {
-        const double A2 = __shfl_up(A, d, P), B2 = __shfl_up(B, d, P);
-        if (k >= d) {
-            A = A + B * A2;
-            B = B * B2;
-        }
+    if (k < LP) {
+        sA[k][ii] = A;
+        sB[k][ii] = B;
     }
-    if (k < L.l) {
-        const double pn = zp + pb, wn = pa ? A : 0.0;
-        if (pa) z[NUN * cell + PP] = pn;
-        if (wa) z[NUN * cell + WW] = wn;
-        /* defect-correction passes: z_out += omega z on the final W/P rows (k_dyn_add fused) */
-        if (zo) {
-            if (pa) zo[NUN * cell + PP] += omega * pn;
-            if (wa) zo[NUN * cell + WW] += omega * wn;
-        }
+    __syncthreads();
+    if (!on) return;
+    double w = 0.0;
+    for (int kk = 0; kk <= k; kk++) w = sA[kk][ii] + sB[kk][ii] * w;
+    const double pn = zp + pb, wn = pa ? w : 0.0;
+    if (pa) z[NUN * cell + PP] = pn;
+    if (wa) z[NUN * cell + WW] = wn;
+    if (zo) {
+        if (pa) zo[NUN * cell + PP] += omega * pn;
+        if (wa) zo[NUN * cell + WW] += omega * wn;
     }
 }
 
@@ -915,40 +883,179 @@ __global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ 
     rhs[c] = pinned[c] ? 0.0 : s;
 }
 
-/* 3a'. the Schur right-hand side of a water column in one pass: P lanes per column
- * (lane = level k) evaluate w_k (Duv uv - rr_p), a shuffle reduction sums them, and the
- * entry goes straight to this band's slab of the right-hand side (no per-cell buffer, no
- * gather) */
-template <int P>
-__global__ void __launch_bounds__(256) k_gs_pcol_scan(const double* __restrict__ val,
-                                                      const uint8_t* __restrict__ known,
-                                                      const double* __restrict__ pw,
-                                                      const double* __restrict__ rr,
-                                                      const double* __restrict__ z,
-                                                      const int* __restrict__ ocol,
-                                                      double* __restrict__ colv_own, Lay L)
+/* ---- the Schur right-hand side as a linear form in rr ----------------------------------
+ * Steps 1-3a (ptil, uv*, the depth-weighted continuity defect) are linear in rr, so the
+ * Schur right-hand side of water column (i, j) is a fixed combination of rr over its
+ * neighbourhood: W rows of the 3 x 3 columns around it (through ptil, which the U/V points
+ * of its four corners read), U/V rows of those corners, its own P rows.  The coefficients
+ * are formed at set-up (k_rcol_uvp, k_rcol_w), so the apply evaluates ptil and the
+ * right-hand side in one column kernel (k_gs_ptil_rcol) and the U/V points only once, after
+ * the Schur solve (k_gs_uvp): two launches fewer per dynamics pass.
+ * Layout: rcol[(e * l + k) * ncolb + t], t = band column (j - jb0) * nx + (i - ib0);
+ * e < 9: rr_W at column (i + e % 3 - 1, j + e / 3 - 1), level k; e = 9 + q4 / 13 + q4: rr_U
+ * / rr_V at corner q4 = (i - (q4 & 1), j - (q4 >> 1)); e = 17: rr_P at (i, j, k). */
+constexpr int RC_NE = 18;
+
+/* U/V and P coefficients, thread per (band column, level): with w_k the depth weight,
+ * a the P row's couplings to its corners and D the corner's 2x2 U/V inverse, the column's
+ * entry sum_k w_k (Duv uv* - rr_p) has d/d rr_U(q) = [ua] (cu d0 + cv d2), d/d rr_V(q) =
+ * [va] (cu d1 + cv d3), cu = w_k a_U [in, ua], cv = w_k a_V [in, va]; d/d rr_P = -w_k. */
+__global__ void k_rcol_uvp(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                           const double* __restrict__ uvinv, const double* __restrict__ pw,
+                           double* __restrict__ rcol, Lay L)
 {
-    const int t_ = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-    const int k = threadIdx.x % P;
-    if (t_ >= (int)(L.nloc / L.l)) return;
-    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;
-    const int ij = j * L.n + i;
-    /* ocol: this band's entry of the column (pinned: -2 - entry, written 0; -1: none),
-     * loaded with the rest (no gating round) */
-    const int q = ocol[ij];
-    double v = 0.0;
-    if (k < L.l) {
-        const int64_t cell = ecell(L, i, j, k);
-        const uint8_t kp = known[NUN * cell + PP];
-        const double w = pw[cell], rp = rr[NUN * cell + PP];
-        const double d = duv_uv(val, known, z, i, j, k, cell - L.own0, L);
-        v = kp ? 0.0 : w * (d - rp);
+    LAY_ALIASES;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ncolb = (int)(L.nloc / l);
+    if (g >= (int64_t)ncolb * l) return;
+    const int t = (int)(g / l), k = (int)(g % l);
+    const int i = L.ib0 + t % L.nx, j = L.jb0 + t / L.nx;
+    const int64_t cell = ecell(L, i, j, k), pl = cell - L.own0, ncell = L.nloc;
+    const bool pa = !known[NUN * cell + PP];
+    const double w = pa ? pw[cell] : 0.0;
+    /* coefficient e of level k: R[e * l * ncolb] */
+    double* R = rcol + (int64_t)k * ncolb + t;
+    const int64_t es = (int64_t)l * ncolb;
+    for (int q4 = 0; q4 < 4; q4++) {
+        int qi = i - (q4 & 1), qj = j - ((q4 >> 1) & 1);
+        double cu_r = 0.0, cv_r = 0.0;
+        if (pa && hnb(qi, qj, n, m, periodic)) {
+            const int64_t qc = ecell(L, qi, qj, k);
+            const bool ua = !known[NUN * qc + UU], va = !known[NUN * qc + VV];
+            const double cu = ua ? w * val[(int64_t)(S_PU + q4) * ncell + pl] : 0.0;
+            const double cv = va ? w * val[(int64_t)(S_PV + q4) * ncell + pl] : 0.0;
+            const double* D = uvinv + 4 * qc;
+            cu_r = ua ? cu * D[0] + cv * D[2] : 0.0;
+            cv_r = va ? cu * D[1] + cv * D[3] : 0.0;
+        }
+        R[(9 + q4) * es] = cu_r;
+        R[(13 + q4) * es] = cv_r;
     }
+    R[17 * es] = pa ? -w : 0.0;
+}
+
+/* W coefficients, thread per (band column, neighbour column c'): with D_k the entry's
+ * derivative in ptil(c', k) (through every corner U/V point of the column that reads
+ * P(c', k)), and ptil(c', k) = A_k + B_k ptil(c', k+1), A_k = rr_W / g0, B_k = -g1 / g0 on
+ * the active hydrostatic rows (0, 0 elsewhere), the coefficient of rr_W(c', k') is
+ * S_k' / g0_k' with S_k' = S_k'-1 B_k'-1 + D_k'.  Reads the U/V coefficients of k_rcol_uvp. */
+__global__ void k_rcol_w(const uint8_t* __restrict__ known, const double* __restrict__ gslot,
+                         double* __restrict__ rcol, Lay L)
+{
+    LAY_ALIASES;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ncolb = (int)(L.nloc / l);
+    if (g >= (int64_t)ncolb * 9) return;
+    const int t = (int)(g / 9), e = (int)(g % 9);
+    const int i = L.ib0 + t % L.nx, j = L.jb0 + t / L.nx;
+    const int di = e % 3 - 1, dj = e / 3 - 1;
+    /* coefficient e of level k: R[(e * l + k) * ncolb] */
+    double* R = rcol + t;
+    const int64_t ks = ncolb;
+    int gi = i + di, gj = j + dj;
+    if (!hnb(gi, gj, n, m, periodic)) {
+        for (int k = 0; k < l; k++) R[((int64_t)e * l + k) * ks] = 0.0;
+        return;
+    }
+    double S = 0.0, Bprev = 0.0;
+    for (int k = 0; k < l; k++) {
+        const int64_t gc = ecell(L, gi, gj, k);
+        const bool pa = !known[NUN * gc + PP], wa = !known[NUN * gc + WW];
+        double D = 0.0;
+        if (pa) {
+            for (int q4 = 0; q4 < 4; q4++) {
+                const int a = -(q4 & 1), b = -((q4 >> 1) & 1);
+                const int ex = di - a, fy = dj - b;          /* c' as a P corner of q */
+                if (ex < 0 || ex > 1 || fy < 0 || fy > 1) continue;
+                int qi = i + a, qj = j + b;
+                if (!hnb(qi, qj, n, m, periodic)) continue;
+                const int64_t qc = ecell(L, qi, qj, k);
+                const int g4 = ex + 2 * fy;
+                D -= R[((int64_t)(9 + q4) * l + k) * ks] * gslot[GSL * qc + g4] +
+                     R[((int64_t)(13 + q4) * l + k) * ks] * gslot[GSL * qc + 4 + g4];
+            }
+        }
+        const double g0 = gslot[GSL * gc + 8], g1 = gslot[GSL * gc + 9];
+        const bool act = pa && k < l - 1 && wa && g0 != 0.0;
+        S = S * Bprev + D;
+        R[((int64_t)e * l + k) * ks] = act ? S / g0 : 0.0;
+        Bprev = act ? -g1 / g0 : 0.0;
+    }
+}
+
+/* 1 + 3a. ptil (top-down: p_k = A_k + B_k p_k+1) and the column's Schur right-hand side
+ * sum_e rcol_e rr_e (summed over the levels in a fixed order), written as k_gs_pcol wrote it */
+template <int LP>
+__global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict__ val,
+                                                       const uint8_t* __restrict__ known,
+                                                       const double* __restrict__ rcol,
+                                                       const double* __restrict__ rr,
+                                                       double* __restrict__ z,
+                                                       const int* __restrict__ ocol,
+                                                       double* __restrict__ colv_own, Lay L)
+{
+    LAY_ALIASES;
+    constexpr int TI = 1024 / LP;
+    __shared__ double sA[LP][TI], sB[LP][TI], sv[LP][TI];
+    int il, jl, k;
+    bool on;
+    col_tile(L, LP, il, jl, k, on);
+    const int ii = (int)threadIdx.x % TI;
+    const int i = L.ib0 + il, j = L.jb0 + jl;
+    const int64_t ncell = L.nloc;
+    const int ncolb = (int)(L.nloc / l);
+    const int t = jl * L.nx + il;
+    double A = 0.0, B = 0.0, v = 0.0;
+    bool pa = false;
+    int64_t cell = 0;
+    if (on) {
+        int64_t nc9[9];
 #pragma unroll
-    for (int o = P / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, P);
-    if (k == 0 && q != -1) {
-        if (q >= 0) colv_own[q] = v;
-        else colv_own[-2 - q] = 0.0;
+        for (int e = 0; e < 9; e++) {
+            int i2 = i + e % 3 - 1, j2 = j + e / 3 - 1;
+            if (!hnb(i2, j2, n, m, periodic)) { i2 = i; j2 = j; }
+            nc9[e] = ecell(L, i2, j2, k);
+        }
+        cell = nc9[4];
+        const double* R = rcol + (int64_t)k * ncolb + t;
+        const int64_t es = (int64_t)l * ncolb;
+        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
+        const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
+        const double rw = rr[NUN * cell + WW];
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+        for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[NUN * nc9[e] + WW];
+        /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++) {
+            const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
+            a1 += R[(9 + q4) * es] * rr[NUN * qc + UU];
+            a2 += R[(13 + q4) * es] * rr[NUN * qc + VV];
+        }
+        v = (a0 + (a1 + a2)) + R[17 * es] * rr[NUN * cell + PP];
+        pa = !kp;
+        if (pa && k < l - 1 && !kw && g0 != 0.0) {
+            A = rw / g0;
+            B = -g1 / g0;
+        }
+    }
+    if (k < LP) {
+        sA[k][ii] = A;
+        sB[k][ii] = B;
+        sv[k][ii] = v;
+    }
+    __syncthreads();
+    if (!on) return;
+    double p = 0.0;
+    for (int kk = l - 1; kk >= k; kk--) p = sA[kk][ii] + sB[kk][ii] * p;
+    if (pa) z[NUN * cell + PP] = p;
+    if (k == 0) {
+        const int q = ocol[j * n + i];
+        double s = 0.0;
+        for (int kk = 0; kk < l; kk++) s += sv[kk][ii];
+        if (q >= 0) colv_own[q] = s;
+        else if (q != -1) colv_own[-2 - q] = 0.0;
     }
 }
 
@@ -1094,6 +1201,48 @@ __global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __rest
     if (ua) z[NUN * cell + UU] = nu;
     if (va) z[NUN * cell + VV] = nv;
     /* defect-correction passes: z_out += omega z on the final U/V rows (k_dyn_add fused) */
+    if (zo) {
+        if (ua) zo[NUN * cell + UU] += omega * nu;
+        if (va) zo[NUN * cell + VV] += omega * nv;
+    }
+}
+
+/* 2 + 4. uv = D^-1 (rr_uv - Guv (ptil + Mz1^T pbar)) in one pass once pbar is known (the
+ * Schur right-hand side came from rcol, so uv* is never formed); zo += omega uv as in
+ * k_gs_uvfix */
+__global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restrict__ known,
+                         const double* __restrict__ uvinv, const double* __restrict__ rr,
+                         const double* __restrict__ pbar, double* __restrict__ z, Lay L,
+                         double* __restrict__ zo, double omega)
+{
+    OWNED_CELL;
+    const int n = L.n, m = L.m, periodic = L.periodic;
+    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
+    double gu = 0.0, gv = 0.0;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; g4++) {
+        int pi = i + (g4 & 1), pj = j + ((g4 >> 1) & 1);
+        const bool in = hnb(pi, pj, n, m, periodic);
+        if (!in) { pi = i; pj = j; }
+        const int64_t pc = ecell(L, pi, pj, k);
+        const uint8_t kp = known[NUN * pc + PP];
+        const double p = z[NUN * pc + PP] + pbar[(int64_t)pi * m + pj];
+        const double au = val[(int64_t)(S_UP + g4) * ncell + lc];
+        const double av = val[(int64_t)(S_VP + g4) * ncell + lc];
+        const bool use = in && !kp;
+        gu += use ? au * p : 0.0;
+        gv += use ? av * p : 0.0;
+    }
+    const double* D = uvinv + 4 * cell;
+    const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
+    const double r0 = rr[NUN * cell + UU], r1 = rr[NUN * cell + VV];
+    const bool ua = !ku, va = !kv;
+    if (!ua && !va) return;
+    const double ru = ua ? r0 - gu : 0.0;
+    const double rv = va ? r1 - gv : 0.0;
+    const double nu = d0 * ru + d1 * rv, nv = d2 * ru + d3 * rv;
+    if (ua) z[NUN * cell + UU] = nu;
+    if (va) z[NUN * cell + VV] = nv;
     if (zo) {
         if (ua) zo[NUN * cell + UU] += omega * nu;
         if (va) zo[NUN * cell + VV] += omega * nv;
@@ -2688,8 +2837,8 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         if (flags != gs.flags_h)
             if ((rc = build_structure(c, flags))) return rc;
     }
-    if (gs.gslot.n < (size_t)8 * next) {
-        if (gs.gslot.alloc((size_t)8 * next)) return IEMIC_ENOMEM;
+    if (gs.gslot.n < (size_t)GSL * next) {
+        if (gs.gslot.alloc((size_t)GSL * next)) return IEMIC_ENOMEM;
         HIP_OK(hipMemsetAsync(gs.gslot.p, 0, sizeof(double) * gs.gslot.n, c->stream));
     }
     hipLaunchKernelGGL(k_cell_factors, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
@@ -2698,7 +2847,17 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     hipLaunchKernelGGL(k_gslot_pack, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L, gs.gslot.p);
     if (c->nranks > 1) {
         if ((rc = halo_exchange_w(c, gs.uvinv.p, 4, 1))) return rc;
-        if ((rc = halo_exchange_w(c, gs.gslot.p, 8, 1))) return rc;
+        if ((rc = halo_exchange_w(c, gs.gslot.p, GSL, 1))) return rc;
+    }
+    if (c->l <= 64) {
+        /* the Schur right-hand side as a linear form in rr (k_gs_ptil_rcol) */
+        const int64_t ncolb = c->nloc / c->l;
+        if (gs.rcol.n < (size_t)(ncolb * RC_NE * c->l) && gs.rcol.alloc((size_t)(ncolb * RC_NE * c->l)))
+            return IEMIC_ENOMEM;
+        hipLaunchKernelGGL(k_rcol_uvp, dim3(blocks_for(ncolb * c->l)), dim3(256), 0, c->stream, c->d_val.p,
+                           gs.known.p, gs.uvinv.p, gs.pw.p, gs.rcol.p, L);
+        hipLaunchKernelGGL(k_rcol_w, dim3(blocks_for(ncolb * 9)), dim3(256), 0, c->stream, gs.known.p,
+                           gs.gslot.p, gs.rcol.p, L);
     }
     hipLaunchKernelGGL(k_knownmask, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, gs.known.p,
                        gs.kmask.p, L, c->jb1);
@@ -2750,40 +2909,55 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     int rc = 0;
     const int64_t ncolb = c->nloc / c->l;                        /* water columns of the band */
     const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : (c->l <= 64 ? 64 : 0));
-    const unsigned gsc = (unsigned)((ncolb * std::max(Pl, 1) + 255) / 256);
-    if (Pl == 0)
-        hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                           rr, z, L);
-    else if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_ptil_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, rr, z, L);
-    else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_ptil_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, rr, z, L);
-    else
-        hipLaunchKernelGGL(k_gs_ptil_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, rr, z, L);
+    /* transposed column kernels: 1024 / Pl columns of one row per workgroup */
+    const unsigned gct = Pl ? (unsigned)(((c->nx + 1024 / Pl - 1) / (1024 / Pl)) * (ncolb / c->nx)) : 0u;
+    if (Pl != 0) {
+        /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
+         * after the Schur solve, then p and w */
+        if (band && (rc = halo_exchange(c, const_cast<double*>(rr), 1))) return rc;   /* rr around the band */
+        if (Pl == 16)
+            hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+        else if (Pl == 32)
+            hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+        else
+            hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* ptil above the band */
+        const double* sb = gs.colv_own.p;
+        if (band) {
+            HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
+                                  hipMemcpyDeviceToDevice, s));
+            if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
+            sb = gs.colv.p;
+        }
+        if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
+        hipLaunchKernelGGL(k_gs_uvp, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
+                           rr, gs.colv2.p, z, L, zo, omega);
+        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* uv below the band */
+        if (Pl == 16)
+            hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.colv2.p, z, L, rr, zo, omega);
+        else if (Pl == 32)
+            hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.colv2.p, z, L, rr, zo, omega);
+        else
+            hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), dim3(1024), 0, s, c->d_val.p, gs.known.p,
+                               gs.colv2.p, z, L, rr, zo, omega);
+        return 0;
+    }
+    /* more than 64 levels: the cell / column kernels of the original pass */
+    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       rr, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
     hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
                        rr, z, L);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
-    if (Pl == 0) {
-        hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                           rr, z, gs.tcell.p, L, 0);
-        hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                           gs.pinned.p, gs.colv_own.p, L);
-    } else if (Pl == 16) {
-        hipLaunchKernelGGL(k_gs_pcol_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-    } else if (Pl == 32) {
-        hipLaunchKernelGGL(k_gs_pcol_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-    } else {
-        hipLaunchKernelGGL(k_gs_pcol_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.pw.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-    }
-    /* pbar = S^-1 b: the bands' entries of b summed, then the cyclic-reduction solve
-     * (redundant on every rank: O(n m^2) bytes) */
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       rr, z, gs.tcell.p, L, 0);
+    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
+                       gs.pinned.p, gs.colv_own.p, L);
     const double* sb = gs.colv_own.p;
     if (band) {
         /* colv_own keeps 0 outside this band's columns; the sum goes to colv */
@@ -2793,27 +2967,14 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
         sb = gs.colv.p;
     }
     if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
-    double* zf = Pl == 0 ? nullptr : zo;      /* fused only with the column-scan kernels */
     hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.col_of_ij.p, gs.colv2.p, z, L, zf, omega);
+                       gs.col_of_ij.p, gs.colv2.p, z, L, nullptr, 0.0);
     if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
-    if (Pl == 0) {
-        hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                           rr, z, gs.tcell.p, L, 1);
-    }
-    if (Pl == 0)
-        hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                           gs.colv2.p, gs.tcell.p, z, L);
-    else if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_pw_scan<16>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
-    else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_pw_scan<32>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
-    else
-        hipLaunchKernelGGL(k_gs_pw_scan<64>, dim3(gsc), dim3(256), 0, s, c->d_val.p, gs.known.p,
-                           gs.col_of_ij.p, gs.colv2.p, (const double*)nullptr, z, L, rr, zf, omega);
-    if (zo && !zf)
+    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
+                       rr, z, gs.tcell.p, L, 1);
+    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
+                       gs.colv2.p, gs.tcell.p, z, L);
+    if (zo)
         hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, z, zo, L, omega);
     return 0;
 }
