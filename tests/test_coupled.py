@@ -11,6 +11,7 @@
 * The coupled operator and solve on the device against the oracle.
 """
 import json
+import math
 import os
 
 import numpy as np
@@ -175,3 +176,71 @@ def test_oracle_coupled_ocean_bitexact(oracle_lib, name, kind):
     ref = fortran_placed(oracle_lib, o.rowptr, o.col, g, kind)
     np.testing.assert_array_equal(val, ref)
     np.testing.assert_array_equal(bits(o.rhs(x)), bits(-g[f"{kind}_B"]))
+
+
+def test_atmos_coefficients_hand_derived():
+    """The atmosphere restatement's coefficients against numbers written out here straight
+    from the reference's formulas (AtmosLocal::setup, AtmosLocal.C:174-245; discretize
+    1141-1234; computeJacobian 585-700), independently of oracle/atmos_oracle.py's code:
+    the setup() scalars with run/coupled's parameter values, and the T / q rows of one
+    interior ocean cell and one interior land cell (no boundaries() change there)."""
+    p = dict(ao.COUPLED_RUN_PARAMS)
+    p["Combined Forcing"] = 0.7
+    P = ao.AtmosParams(p, Ooa=5.4, Os=120.0)
+    # setup(): rhoa 1.25, ch 0.94*1.3e-3, cpa 1000, uw 8.5, A 216, B 1.5, t0a 15, hdima 8400,
+    # D0 3.4e6, r0 6.37e6, udim 0.1, sun0 1360, c0 0.43, rhoo 1024, ce 1.3e-3, hdimq 1800,
+    # kappa 3.1e6, q0 8e-3, qdim 1e-3, t0o 15, t0i -5, lv 2.5e6
+    muoa = 1.25 * (0.94 * 1.3e-3) * 1000.0 * 8.5
+    eta = (1.25 / 1024.0) * 1.3e-3 * 8.5
+    qso = 3.8e-3 * math.exp(17.67 * 15.0 / (15.0 + 243.5))
+    qsi = 3.8e-3 * math.exp(21.87 * -5.0 / (-5.0 + 265.5))
+    hand = {
+        "muoa": muoa,
+        "amua": (216.0 + 1.5 * 15.0) / muoa,
+        "bmua": 1.5 / muoa,
+        "Ai": 1.25 * 8400.0 * 1000.0 * 0.1 / (6.37e6 * muoa),
+        "Ad": 1.25 * 8400.0 * 1000.0 * 3.4e6 / (muoa * 6.37e6 * 6.37e6),
+        "As": 1360.0 * (1 - 0.43) / (4 * muoa),
+        "eta": eta,
+        "nuq": 0.7 * 1.0 * (eta / 1800.0) * (1024.0 / 1.25) * (6.37e6 / 0.1),
+        "Phv": 3.1e6 / (0.1 * 6.37e6),
+        "Eo0": eta * (qso - 8e-3),
+        "Cs": (eta * (qsi - 8e-3) - eta * (qso - 8e-3)) / eta / 1e-3,
+        "dqso": 5e-4,
+        "dqsi": 3.8e-3 * 21.87 * 265.5 / (-5.0 + 265.5) ** 2 * math.exp(21.87 * -5.0 / (-5.0 + 265.5)),
+        "lvscale": 1024.0 * 2.5e6 / muoa,
+        "tauf": 10.0 * 3600.0 * 24.0 * 0.1 / 6.37e6,
+    }
+    for k, v in hand.items():
+        assert abs(getattr(P, k) - v) <= 1e-14 * abs(v), (k, getattr(P, k), v)
+
+    n, m = 8, 6
+    surf = np.zeros((m, n), int)
+    surf[2, 5] = 1                                       # one land cell
+    at = ao.AtmosOracle(n, m, 0, 359.99, -85.5, 85.5, True, surf, Ooa=5.4, Os=120.0, params=p)
+    x = np.zeros(at.dim)
+    x[2:3 * n * m:3] = 0.3
+    J = at.jacobian(x).toarray()
+    deg = math.pi / 180.0
+    dx, dy = 359.99 * deg / n, 171.0 * deg / m
+    j = 3                                                # 1-based interior latitude, row index 2
+    yc = -85.5 * deg + (j - 0.5) * dy
+    yvm, yvp = -85.5 * deg + (j - 1) * dy, -85.5 * deg + j * dy
+    dat = lambda y: 0.9 + 1.5 * math.exp(-12 * y * y / math.pi)   # noqa: E731 (datc / datv)
+    cx = 1.0 / (math.cos(yc) * dx) ** 2
+    q4 = math.cos(yvm) / math.cos(yc) / dy ** 2
+    q6 = math.cos(yvp) / math.cos(yc) / dy ** 2
+    t4, t6 = dat(yvm) * q4, dat(yvp) * q6
+    for i, land in ((2, False), (5, True)):              # 0-based longitude of the cell
+        rT, rq = at.row(i, j - 1, ao.TT), at.row(i, j - 1, ao.QQ)
+        tc = 0.0 if land else 1.0                        # discretize(1): no land points
+        # Al(TT,TT) = tdif Ad (txx + tyy) - tc - bmua tc2, centre and east neighbour
+        Tc = hand["Ad"] * (-2 * dat(yc) * cx - (t4 + t6)) - tc - hand["bmua"] * 1.0
+        assert abs(J[rT, rT] - Tc) <= 1e-13 * abs(Tc), (i, J[rT, rT], Tc)
+        rTe = at.row((i + 1) % n, j - 1, ao.TT)
+        assert abs(J[rT, rTe] - hand["Ad"] * dat(yc) * cx) <= 1e-13 * hand["Ad"] * dat(yc) * cx
+        # Al(QQ,QQ) = Phv (qxx + qyy) - nuq qc
+        Qc = hand["Phv"] * (-2 * cx - (q4 + q6)) - hand["nuq"] * tc
+        assert abs(J[rq, rq] - Qc) <= 1e-13 * abs(Qc), (i, J[rq, rq], Qc)
+        rqn = at.row(i, j, ao.QQ)
+        assert abs(J[rq, rqn] - hand["Phv"] * q6) <= 1e-13 * hand["Phv"] * q6
