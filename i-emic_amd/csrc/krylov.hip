@@ -134,15 +134,20 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
  * are split evenly over the waves (U | U+V | V+W | W+P, 16 each: a wave per equation would
  * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
  * rows' partials meet in LDS. */
+/* on[q]: row sp7_row(S0) + q of the cell is active; an identity row's coefficients are
+ * neither loaded nor used (about half the cells are land at 2 degrees) */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
-                                            int64_t lc, int64_t nloc, const int (*nc)[9], double* acc)
+                                            int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
+                                            double* acc)
 {
 #pragma unroll
     for (int s = S0; s < S1; s++) {
         const Slot sl = SLOTS[s];
+        const int q = sp7_row(s) - sp7_row(S0);
+        if (!on[q]) continue;
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc[sp7_row(s) - sp7_row(S0)] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+        acc[q] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
     }
 }
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
@@ -163,10 +168,13 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
         const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
         int nc[3][9];
         nb_cells(X, il, j, k, nc);
-        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, acc);
-        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, acc);
-        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, acc);
-        else dyn_partial<48, 64>(val, z, lc, nloc, nc, acc);
+        /* the wave's two rows: g0 {U, -} g1 {U, V} g2 {V, W} g3 {W, P} */
+        const int64_t row0 = NUN * ((int64_t)HALO * X.l * X.nx + lc) + (g == 0 ? 0 : g - 1);
+        const bool on[2] = {!known[row0], g > 0 && !known[row0 + 1]};
+        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, on, acc);
+        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, on, acc);
+        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, on, acc);
+        else dyn_partial<48, 64>(val, z, lc, nloc, nc, on, acc);
     }
     red[g][0][c] = acc[0];
     red[g][1][c] = acc[1];

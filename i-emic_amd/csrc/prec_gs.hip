@@ -757,14 +757,17 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
     if (on) {
         cell = ecell(L, i, j, k);
         const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        pa = !kp;
+        wa = !kw;
+    }
+    if (pa) {
+        /* an inactive P row (land) reads nothing: its (A, B) = (0, 0) */
         const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
         const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
         const double rhs = rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
         pb = pbar[(int64_t)i * L.m + j];
         zp = z[NUN * cell + PP];
-        pa = !kp;
-        wa = !kw;
-        if (pa && wa && a != 0.0) {
+        if (wa && a != 0.0) {
             A = rhs / a;
             B = -b / a;
         }
@@ -1020,25 +1023,30 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
         const double* R = rcol + (int64_t)k * ncolb + t;
         const int64_t es = (int64_t)l * ncolb;
         const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
-        const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
-        const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
-        const double rw = rr[NUN * cell + WW];
+        pa = !kp;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[NUN * nc9[e] + WW];
-        /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
+        if (pa) {
+            /* the corner and own-P coefficients vanish on an inactive P row (land): not read */
 #pragma unroll
-        for (int q4 = 0; q4 < 4; q4++) {
-            const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
-            a1 += R[(9 + q4) * es] * rr[NUN * qc + UU];
-            a2 += R[(13 + q4) * es] * rr[NUN * qc + VV];
+            for (int q4 = 0; q4 < 4; q4++) {
+                /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
+                const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
+                a1 += R[(9 + q4) * es] * rr[NUN * qc + UU];
+                a2 += R[(13 + q4) * es] * rr[NUN * qc + VV];
+            }
+            a2 += R[17 * es] * rr[NUN * cell + PP];
+            if (k < l - 1 && !kw) {
+                const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
+                const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
+                if (g0 != 0.0) {
+                    A = rr[NUN * cell + WW] / g0;
+                    B = -g1 / g0;
+                }
+            }
         }
-        v = (a0 + (a1 + a2)) + R[17 * es] * rr[NUN * cell + PP];
-        pa = !kp;
-        if (pa && k < l - 1 && !kw && g0 != 0.0) {
-            A = rw / g0;
-            B = -g1 / g0;
-        }
+        v = a0 + (a1 + a2);
     }
     if (k < LP) {
         sA[k][ii] = A;
@@ -1218,6 +1226,8 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
     OWNED_CELL;
     const int n = L.n, m = L.m, periodic = L.periodic;
     const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
+    const bool ua = !ku, va = !kv;
+    if (!ua && !va) return;                 /* land: none of the point's operands is read */
     double gu = 0.0, gv = 0.0;
 #pragma unroll
     for (int g4 = 0; g4 < 4; g4++) {
@@ -1236,8 +1246,6 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
     const double* D = uvinv + 4 * cell;
     const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
     const double r0 = rr[NUN * cell + UU], r1 = rr[NUN * cell + VV];
-    const bool ua = !ku, va = !kv;
-    if (!ua && !va) return;
     const double ru = ua ? r0 - gu : 0.0;
     const double rv = va ? r1 - gv : 0.0;
     const double nu = d0 * ru + d1 * rv, nv = d2 * ru + d3 * rv;
