@@ -723,14 +723,28 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
  * Jacobian rows contiguously, the interleaved vectors at one cell stride); the column
  * recurrences meet in LDS, where each thread composes the affine maps of the levels it
  * depends on (at most l steps of LDS reads). */
-__device__ __forceinline__ void col_tile(const Lay& L, int LP, int& il, int& jl, int& k, bool& on)
+/* logical workgroup of block b for nwg workgroups launched as xcd_grid(nwg) blocks: the
+ * XCDs (blocks dealt round robin, b % 8) get contiguous runs of workgroups, so tiles of
+ * neighbouring latitude rows, which read each other's rows, share an L2; -1: idle block */
+__device__ __forceinline__ int xcd_block(int nwg)
+{
+    const int per = (nwg + 7) >> 3;
+    const int w = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    return w < nwg ? w : -1;
+}
+static inline unsigned xcd_grid(int64_t nwg) { return 8u * (unsigned)((nwg + 7) / 8); }
+
+__device__ __forceinline__ bool col_tile(const Lay& L, int LP, int& il, int& jl, int& k, bool& on)
 {
     const int TI = 1024 / LP;
     const int tpr = (L.nx + TI - 1) / TI;
-    jl = blockIdx.x / tpr;
-    il = (blockIdx.x % tpr) * TI + (int)threadIdx.x % TI;
+    const int w = xcd_block(tpr * (int)(L.nloc / ((int64_t)L.l * L.nx)));
+    if (w < 0) return false;
+    jl = w / tpr;
+    il = (w % tpr) * TI + (int)threadIdx.x % TI;
     k = (int)threadIdx.x / TI;
     on = k < L.l && il < L.nx;
+    return true;
 }
 
 /* 4b/5. p = ptil + pbar and the continuity rows bottom-up, w_k = A_k + B_k w_k-1 (the
@@ -747,7 +761,7 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
     __shared__ double sA[LP][TI], sB[LP][TI];
     int il, jl, k;
     bool on;
-    col_tile(L, LP, il, jl, k, on);
+    if (!col_tile(L, LP, il, jl, k, on)) return;    /* whole idle workgroups */
     const int ii = (int)threadIdx.x % TI;
     const int i = L.ib0 + il, j = L.jb0 + jl;
     const int64_t ncell = L.nloc;
@@ -1002,7 +1016,7 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
     __shared__ double sA[LP][TI], sB[LP][TI], sv[LP][TI];
     int il, jl, k;
     bool on;
-    col_tile(L, LP, il, jl, k, on);
+    if (!col_tile(L, LP, il, jl, k, on)) return;    /* whole idle workgroups */
     const int ii = (int)threadIdx.x % TI;
     const int i = L.ib0 + il, j = L.jb0 + jl;
     const int64_t ncell = L.nloc;
@@ -2918,7 +2932,7 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const int64_t ncolb = c->nloc / c->l;                        /* water columns of the band */
     const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : (c->l <= 64 ? 64 : 0));
     /* transposed column kernels: 1024 / Pl columns of one row per workgroup */
-    const unsigned gct = Pl ? (unsigned)(((c->nx + 1024 / Pl - 1) / (1024 / Pl)) * (ncolb / c->nx)) : 0u;
+    const unsigned gct = Pl ? xcd_grid(((c->nx + 1024 / Pl - 1) / (1024 / Pl)) * (ncolb / c->nx)) : 0u;
     if (Pl != 0) {
         /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
          * after the Schur solve, then p and w */

@@ -436,14 +436,21 @@ __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv
  * 4 up).  The term vectors are staged in LDS while the matrix rows are loaded into
  * registers; per row the column groups' partial sums meet in LDS in a fixed order. */
 template <int CPT>
-__global__ void __launch_bounds__(256) k_cr_multi(const CrOut* __restrict__ outs, int m, int nch,
+__global__ void __launch_bounds__(256) k_cr_multi(const CrOut* __restrict__ outs, int nout, int m, int nch,
                                                   const double* __restrict__ b, double* __restrict__ x,
                                                   double* __restrict__ bv, double* __restrict__ xv)
 {
     __shared__ double vs[CR_MT][CR_MAXM];
     __shared__ double red[256];
-    const CrOut& o = outs[blockIdx.x / nch];
-    const int r0 = (blockIdx.x % nch) * CR_RC;
+    /* the nch row chunks of one output block share the cache lines of its column-major
+     * blocks (an m = 76 column is 608 B: three of four chunk edges split a line), so they
+     * are dealt to one XCD (workgroups are dealt to the XCDs round robin): block b runs on
+     * XCD b % 8; output = (slot / nch) * 8 + b % 8, chunk = slot % nch, slot = b / 8 */
+    const int slot = (int)(blockIdx.x >> 3);
+    const int oi = (slot / nch) * 8 + (int)(blockIdx.x & 7);
+    if (oi >= nout) return;
+    const CrOut& o = outs[oi];
+    const int r0 = (slot % nch) * CR_RC;
     const int t = threadIdx.x, g = t / CR_RC, r = r0 + t % CR_RC;
     const int nt = o.nt;
     const double* base[4] = {b, x, bv, xv};
@@ -1004,14 +1011,14 @@ static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double
 {
     const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC;
     const int need = (m + CR_G - 1) / CR_G;
-    const dim3 g((unsigned)(st.nout * nch));
+    const dim3 g((unsigned)(8 * nch * ((st.nout + 7) / 8)));
     double* bv = const_cast<double*>(cr.bv.p);
     double* xv = const_cast<double*>(cr.xv.p);
-    if (need <= 3) hipLaunchKernelGGL(k_cr_multi<3>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
-    else if (need <= 5) hipLaunchKernelGGL(k_cr_multi<5>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
-    else if (need <= 8) hipLaunchKernelGGL(k_cr_multi<8>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
-    else if (need <= 10) hipLaunchKernelGGL(k_cr_multi<10>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
-    else hipLaunchKernelGGL(k_cr_multi<12>, g, dim3(256), 0, s, st.d.p, m, nch, b, x, bv, xv);
+    if (need <= 3) hipLaunchKernelGGL(k_cr_multi<3>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
+    else if (need <= 5) hipLaunchKernelGGL(k_cr_multi<5>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
+    else if (need <= 8) hipLaunchKernelGGL(k_cr_multi<8>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
+    else if (need <= 10) hipLaunchKernelGGL(k_cr_multi<10>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
+    else hipLaunchKernelGGL(k_cr_multi<12>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
 }
 
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)
