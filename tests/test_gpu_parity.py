@@ -206,7 +206,7 @@ def test_block_gs_apply_global2(oracle_lib, Ocean, mixing):
 @pytest.mark.parametrize("mr", [False, True])
 def test_dyn_defect_correction(oracle_lib, Ocean, name, dyn, mr):
     """Block GS with defect-correction passes on the dynamics block: converges FGMRES in
-    fewer steps; with a fixed step (damping 0.95) it is a linear operator
+    fewer steps; with a fixed step (the default damping) it is a linear operator
     (apply(a r1 + r2) = a apply(r1) + apply(r2)), with minimal-residual steps a
     deterministic nonlinear one (FGMRES is flexible)."""
     its = {}
