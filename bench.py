@@ -80,7 +80,7 @@ def parse():
     p.add_argument("--idr-s", type=int, default=4)
     p.add_argument("--dyn-iters", type=int, default=4,
                    help="defect-correction passes on the dynamics block of the block GS")
-    p.add_argument("--dyn-omega", type=float, default=1.0, help="step of the correction passes")
+    p.add_argument("--dyn-omega", type=float, default=0.95, help="step of the correction passes")
     p.add_argument("--dyn-mr", action="store_true", help="minimal-residual step per pass")
     p.add_argument("--ts-mg", type=int, default=1,
                    help="T/S aggregation-multigrid V-cycles (0: --ts-sweeps plain sweeps)")

@@ -63,7 +63,7 @@ class Ocean:
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
         sp = {"FGMRES iterations": 500, "FGMRES tolerance": 1e-8, "FGMRES restarts": 0,
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
-              "Dyn iterations": 4, "Dyn damping": 1.0, "Dyn minimal residual": False, "TS multigrid cycles": 1,
+              "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
               "Solver": "FGMRES", "IDR s": 4, "IDR angle": 0.7, "IDR replace residuals": False,
               "Multigrid sweeps": 1, "TS after dyn pass": 0}
         if solver_params:
