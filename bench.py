@@ -10,13 +10,18 @@ the timed region): by default the near-solution branch state bench_data/<config>
 with --state synthetic SURVEY §8d's splitmix64 state (seed 20261015; a Newton step from it
 diverges).  The state is named in config["state"].
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): the same 2-degree problem is split
-into N latitude bands (``--npx 1``, the default; ``--npx 0`` the reference's Decomp2D rule,
-TRIOS_Domain.C:88-109, 8 GPUs: 4 x 2, 48 x 38 columns each -- x cuts through the zonal flow
-double the FGMRES steps), one per GPU: halo exchanges and Krylov reductions
-over RCCL; the preconditioner's Schur problem and coarsest T/S level are
-global, the rest couples across subdomain edges through halos -- strong
-scaling; the step time is the max over ranks.
+Multi-GPU (``--gpus N``): one process per GPU.  Run as ``python bench.py --gpus N`` the
+script starts its N ranks itself (a ``torch.distributed.run`` child process, before anything
+touches the GPU); under an external ``torch.distributed.run`` it is one rank and checks that
+WORLD_SIZE equals N.  The same 2-degree problem is split into N latitude bands (``--npx 1``,
+the default; ``--npx 0`` the reference's Decomp2D rule, TRIOS_Domain.C:88-109, 8 GPUs: 4 x 2,
+48 x 38 columns each -- x cuts through the zonal flow cost FGMRES steps): halo
+exchanges and Krylov reductions over RCCL (``--transport rccl``), or through the library's
+host transport over gloo (``--transport host``: several ranks may share one GPU, to check
+the decomposition on a one-GPU box); the preconditioner's Schur problem and coarsest T/S level
+are global, the rest couples across subdomain edges through halos -- strong
+scaling; the step time is the max over ranks.  The line reports the ranks the communicator
+itself saw (``ranks_seen``: ncclCommCount under RCCL) and the communication per FGMRES step.
 
 Prints ONE JSON line (rank 0) with the metric, the SpMV roofline of the same run (HIP
 events on the library's stream) and the CPU baseline (the oracle port, rank 0, N=1).
@@ -51,7 +56,11 @@ def stencil_ell_bytes(ncell: int, nslot: int, n: int) -> int:
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks, one per GPU (started here unless WORLD_SIZE is set)")
+    p.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                   help="rccl: RCCL over xGMI, one GPU per rank; host: the library's host transport "
+                        "over gloo (ranks may share a GPU)")
     p.add_argument("--npx", type=int, default=1,
                    help="x parts of the process grid (1: latitude bands, the default: x cuts through the "
                         "zonal flow double the FGMRES steps, DESIGN.md §7; 0: the reference's Decomp2D rule)")
@@ -376,22 +385,63 @@ def bench_coupled(args):
     print(json.dumps(out), flush=True)
 
 
+def launch(args) -> int:
+    """--gpus N > 1 outside torch.distributed.run: start the N ranks as a torch.distributed.run
+    child (nothing in this process touches the GPU: device_count() does not initialise it) and
+    return its exit code."""
+    import socket
+    import subprocess
+    if args.transport == "rccl":
+        import torch
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs for RCCL (one per rank), "
+                  f"{ndev} visible (--transport host runs several ranks on one GPU)", file=sys.stderr)
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(launch(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world} ranks were started", file=sys.stderr)
+        sys.exit(2)
+    if world > 1 and (args.config == "coupled4" or args.mode == "continuation"):
+        print("bench.py: the coupled (C4) and continuation (C5) lines run on one GPU", file=sys.stderr)
+        sys.exit(2)
     if args.config == "coupled4":
         return bench_coupled(args)
     if args.mode == "continuation":
         return bench_continuation(args)
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    host = args.transport == "host"
     dist = None
+    ndev = torch.cuda.device_count()
+    if world > 1 and not host and ndev < world:
+        print(f"bench.py: rank {rank}: {world} RCCL ranks need {world} GPUs, {ndev} visible", file=sys.stderr)
+        sys.exit(2)
+    device = local % max(1, ndev) if host else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        if host:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    dev = torch.device("cuda", device)
     torch.cuda.set_device(dev)
 
     from iemic import _lib
@@ -406,15 +456,23 @@ def main():
           "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps,
           "Solver": args.solver, "IDR s": args.idr_s, "TS after dyn pass": args.ts_at}
-    comm_id = None
-    if world > 1:
+    comm_id, tp = None, None
+    if world > 1 and host:
+        from iemic.transport import GlooTransport
+        tp = GlooTransport()
+    elif world > 1:
         idt = torch.zeros(128, dtype=torch.uint8, device=dev)
         if rank == 0:
             idt.copy_(torch.frombuffer(bytearray(Ocean.unique_id()), dtype=torch.uint8))
         dist.broadcast(idt, 0)
         comm_id = bytes(idt.cpu().numpy().tobytes())
-    oc = Ocean(cfg, device=local, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id,
-               npx=args.npx)
+    oc = Ocean(cfg, device=device, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id,
+               npx=args.npx, transport=tp)
+    ranks_seen, transport = oc.comm_size()
+    if ranks_seen != world:
+        print(f"bench.py: rank {rank}: the communicator reports {ranks_seen} ranks, WORLD_SIZE {world}",
+              file=sys.stderr)
+        sys.exit(2)
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
     state = args.state if (args.state == "synthetic" or os.path.exists(fix)) else "synthetic"
@@ -445,6 +503,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    oc.comm_stats()                      # reset the counters: the timed steps only
     infos = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -454,10 +513,18 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ms = dt / args.steps * 1e3
+    comm = oc.comm_stats()
+    its_total = sum(i.solve.iters for i in infos)
     if dist:
-        tt = torch.tensor([ms], device=dev, dtype=torch.float64)
+        tdev = "cpu" if host else dev
+        tt = torch.tensor([ms], device=tdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms = float(tt.item())
+        rs = torch.tensor([ranks_seen, -ranks_seen], device=tdev, dtype=torch.float64)
+        dist.all_reduce(rs, op=dist.ReduceOp.MAX)
+        if int(rs[0]) != world or int(-rs[1]) != world:
+            print(f"bench.py: ranks disagree on the communicator size ({rs.tolist()})", file=sys.stderr)
+            sys.exit(2)
 
     # SpMV roofline: the k_spmv launches of the timed Newton steps themselves (HIP events
     # on the library stream around every SpMV inside FGMRES; at N > 1 the span includes
@@ -518,6 +585,7 @@ def main():
                              else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
                    "parallelism": (f"decomp2d {lay['npx']}x{lay['npy']}" if world > 1 else "single"),
+                   "transport": transport if world > 1 else "none",
                    "subdomain_rank0": {"cols": [lay["ib0"], lay["ib1"]], "rows": [lay["jb0"], lay["jb1"]]}},
         "newton": {"iters": s.iters, "converged": s.converged,
                    "explicit_rel_res": s.explicit_rel_res, "norm_f0": last.norm_f0,
@@ -526,6 +594,11 @@ def main():
                    "t_solve_ms": last.t_solve_ms, "t_solve_prec_ms": s.t_prec_ms,
                    "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms,
                    "dgks_reorth": s.reorth, "sequence": seq},
+        "ranks_seen": ranks_seen,
+        "process_grid": [lay["npx"], lay["npy"]],
+        "comm": {"per_fgmres_step": {k: round(v / max(1, its_total), 2) for k, v in comm.items()},
+                 "per_newton_step": {k: round(v / args.steps, 1) for k, v in comm.items()},
+                 "rank": rank},
         "spmv_gbps": round(achieved, 1),
         "roofline": {"kernel": "k_spmv (per GPU, rank 0; in-solve launches)", "bound": "hbm",
                      "achieved": round(achieved, 1),

@@ -480,6 +480,13 @@ extern "C" int iemic_comm_stats(iemic_ctx* c, int64_t* out4)
     return 0;
 }
 
+/* the ranks the communicator reports (RCCL: ncclCommCount) and the transport kind */
+extern "C" int iemic_comm_size(const iemic_ctx* c, int* size, int* kind)
+{
+    if (!c || !size || !kind) return IEMIC_EINVAL;
+    return comm_size(c, size, kind);
+}
+
 /* Maximal-graph rows owned by this context (THCM.C:2288-2521) */
 extern "C" int64_t iemic_graph_nnz(const iemic_ctx* c)
 {
@@ -561,6 +568,18 @@ int host_sum(iemic_ctx* c, std::vector<double>& v)
     return rc;
 }
 }  // namespace
+
+/* Epetra_Comm::SumAll over the context's ranks (host buffer, in place) */
+extern "C" int iemic_allreduce_sum(iemic_ctx* c, double* buf, int64_t count)
+{
+    CTX_CHECK(c);
+    if (count < 0 || (count > 0 && !buf) || count > INT32_MAX) return IEMIC_EINVAL;
+    if (c->nranks <= 1 || count == 0) return 0;
+    std::vector<double> v(buf, buf + count);
+    int rc = host_sum(c, v);
+    if (!rc) std::copy(v.begin(), v.end(), buf);
+    return rc;
+}
 
 /* Ocean::getPsiM (Ocean.C:872-886): the meridional overturning streamfunction of the
  * state, OceanGrid::recomputePsiM (OceanGrid.C:270-346: v of usol integrated over x, times

@@ -124,6 +124,29 @@ void comm_destroy(iemic_ctx* c)
     c->comm = nullptr;
 }
 
+/* the ranks the transport itself reports (RCCL: ncclCommCount) and its kind: 0 none (one
+ * rank), 1 RCCL, 2 in-process group, 3 host transport (the caller's, which reports none:
+ * its nranks) */
+int comm_size(const iemic_ctx* c, int* size, int* kind)
+{
+    if (c->nranks <= 1) {
+        *size = 1;
+        *kind = 0;
+    } else if (c->group) {
+        *size = ((LocalGroup*)c->group)->P;
+        *kind = 2;
+    } else if (c->tp.send) {
+        *size = c->nranks;
+        *kind = 3;
+    } else {
+        int n = 0;
+        NCCL_OK(ncclCommCount((ncclComm_t)c->comm, &n));
+        *size = n;
+        *kind = 1;
+    }
+    return 0;
+}
+
 int allreduce_sum(iemic_ctx* c, double* dev, int count)
 {
     if (c->nranks <= 1 || count <= 0) return 0;
@@ -154,21 +177,65 @@ static int seg_copy(iemic_ctx* c, const Seg& g, double* buf, bool to_buf, hipMem
 }
 static bool seg_contig(const Seg& g) { return g.nblk == 1 || g.len == g.stride; }
 
+/* device buffers of a batch: contiguous messages straight from / into the vector, strided
+ * ones in the device staging buffer, the sends packed there (stream-ordered).  Shared by
+ * RCCL and the in-process group, so the packing offsets of the RCCL path run on one GPU. */
+static int stage_sends(iemic_ctx* c, const std::vector<Msg>& ops, std::vector<double*>& buf)
+{
+    size_t tot = 0;
+    for (const Msg& op : ops)
+        if (!seg_contig(op.s)) tot += seg_count(op.s);
+    if (c->d_stage.n < tot && c->d_stage.alloc(tot)) {
+        set_error("halo exchange: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    buf.assign(ops.size(), nullptr);
+    size_t o = 0;
+    int rc;
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
+        if (seg_contig(op.s)) {
+            buf[q] = op.s.base + op.s.off;
+            continue;
+        }
+        buf[q] = c->d_stage.p + o;
+        o += seg_count(op.s);
+        if (op.send && (rc = seg_copy(c, op.s, buf[q], true, hipMemcpyDeviceToDevice))) return rc;
+    }
+    return 0;
+}
+
+/* the strided receives of a batch, from the staging buffer into the vector */
+static int unstage_recvs(iemic_ctx* c, const std::vector<Msg>& ops, const std::vector<double*>& buf)
+{
+    int rc;
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
+        if (!op.send && !seg_contig(op.s) && (rc = seg_copy(c, op.s, buf[q], false, hipMemcpyDeviceToDevice)))
+            return rc;
+    }
+    return 0;
+}
+
 static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
 {
     LocalGroup* g = (LocalGroup*)c->group;
+    std::vector<double*> buf;
+    int rc = stage_sends(c, ops, buf);
+    if (rc) return rc;
     std::map<int, int> ksend, krecv;
-    for (const Msg& op : ops) {
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
         if (!op.send) continue;
         std::vector<double> h(seg_count(op.s));
-        int rc = seg_copy(c, op.s, h.data(), true, hipMemcpyDeviceToHost);
-        if (rc) return rc;
+        HIP_OK(hipMemcpyAsync(h.data(), buf[q], sizeof(double) * h.size(), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
         std::lock_guard<std::mutex> lk(g->mu);
         g->box[std::make_tuple(c->rank, op.peer, ksend[op.peer]++)] = std::move(h);
     }
     g->barrier();
-    for (const Msg& op : ops) {
+    for (size_t q = 0; q < ops.size(); q++) {
+        const Msg& op = ops[q];
         if (op.send) continue;
         std::vector<double> h;
         {
@@ -181,10 +248,11 @@ static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
             h = std::move(it->second);
             g->box.erase(it);
         }
-        int rc = seg_copy(c, op.s, h.data(), false, hipMemcpyHostToDevice);
-        if (rc) return rc;
+        HIP_OK(hipMemcpyAsync(buf[q], h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
     }
+    if ((rc = unstage_recvs(c, ops, buf))) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));
     g->barrier();
     return 0;
 }
@@ -232,30 +300,13 @@ static int run_host(iemic_ctx* c, const std::vector<Msg>& ops)
     return 0;
 }
 
-/* RCCL: contiguous messages straight from / into the vector, strided ones through the
- * device staging buffer (packed before the group, unpacked after it, stream-ordered) */
+/* RCCL: one group of sends and receives on the stream between the packing and the
+ * unpacking of the strided messages */
 static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
 {
-    size_t tot = 0;
-    for (const Msg& op : ops)
-        if (!seg_contig(op.s)) tot += seg_count(op.s);
-    if (c->d_stage.n < tot && c->d_stage.alloc(tot)) {
-        set_error("halo exchange: out of device memory");
-        return IEMIC_ENOMEM;
-    }
-    std::vector<double*> buf(ops.size());
-    size_t o = 0;
-    int rc;
-    for (size_t q = 0; q < ops.size(); q++) {
-        const Msg& op = ops[q];
-        if (seg_contig(op.s)) {
-            buf[q] = op.s.base + op.s.off;
-            continue;
-        }
-        buf[q] = c->d_stage.p + o;
-        o += seg_count(op.s);
-        if (op.send && (rc = seg_copy(c, op.s, buf[q], true, hipMemcpyDeviceToDevice))) return rc;
-    }
+    std::vector<double*> buf;
+    int rc = stage_sends(c, ops, buf);
+    if (rc) return rc;
     ncclComm_t comm = (ncclComm_t)c->comm;
     ncclResult_t first = ncclSuccess;
     std::string what;
@@ -285,12 +336,7 @@ static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
         set_error(what + ": " + ncclGetErrorString(first));
         return IEMIC_EDEVICE;
     }
-    for (size_t q = 0; q < ops.size(); q++) {
-        const Msg& op = ops[q];
-        if (!op.send && !seg_contig(op.s) && (rc = seg_copy(c, op.s, buf[q], false, hipMemcpyDeviceToDevice)))
-            return rc;
-    }
-    return 0;
+    return unstage_recvs(c, ops, buf);
 }
 
 int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops)

@@ -308,6 +308,7 @@ struct Msg {
     Seg s;
 };
 int allreduce_sum(iemic_ctx* c, double* dev, int count);
+int comm_size(const iemic_ctx* c, int* size, int* kind);
 /* depth latitude rows and x columns of the ext layout (width doubles per cell) */
 int halo_exchange(iemic_ctx* c, double* ext_vec, int depth);
 int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int depth);

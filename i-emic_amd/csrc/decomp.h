@@ -57,6 +57,7 @@ struct Sub {
 inline const char* sub_init(Sub& d, int n, int m, int l, int periodic, int rank, int nranks, int npx)
 {
     if (nranks < 1 || rank < 0 || rank >= nranks) return "bad rank / nranks";
+    if (npx < 0 || npx > nranks) return "npx must be 0 (Decomp2D rule) or a divisor of nranks";
     int npy = 1;
     if (npx <= 0) decomp2d(n, m, nranks, npx, npy);
     if (npx < 1 || nranks % npx) return "npx must divide nranks";

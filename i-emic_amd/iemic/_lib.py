@@ -114,6 +114,8 @@ def lib():
         "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
         "iemic_layout": (C.c_int, [vp, P64]),
         "iemic_comm_stats": (C.c_int, [vp, P64]),
+        "iemic_comm_size": (C.c_int, [vp, PI, PI]),
+        "iemic_allreduce_sum": (C.c_int, [vp, PD, C.c_int64]),
         "iemic_local_group_new": (vp, [C.c_int]),
         "iemic_local_group_free": (None, [vp]),
         "iemic_create_local": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int]),
@@ -193,6 +195,7 @@ def lib():
 
 
 EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout", "iemic_comm_stats",
+            "iemic_comm_size", "iemic_allreduce_sum",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_create_local_2d", "iemic_create_transport", "iemic_decomp2d",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",

@@ -36,7 +36,8 @@ class Ocean:
         the RCCL unique id of rank 0 (Ocean.unique_id()), shared by the caller; transport:
         a host transport instead of RCCL (iemic.transport.GlooTransport); local_group: the
         in-process test facility.  npx: x parts (0: the reference's Decomp2D factorisation,
-        1: latitude bands; default 0, and 1 for a local group)."""
+        1: latitude bands, the default on every transport: x cuts through the zonal flow cost
+        FGMRES steps)."""
         self.cfg = cfg
         L = landmask(cfg) if landm is None else landm
         L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
@@ -48,10 +49,10 @@ class Ocean:
                                              local_group, rank, nranks, 1 if npx is None else npx)
         elif transport is not None:
             rc = lib().iemic_create_transport(C.byref(h), C.byref(self._grid), ptr(L, C.c_int), rank,
-                                              nranks, 0 if npx is None else npx, C.byref(transport.c))
+                                              nranks, 1 if npx is None else npx, C.byref(transport.c))
         elif nranks > 1:
             d = _lib.Dist(rank, nranks)
-            d.npx = 0 if npx is None else npx
+            d.npx = 1 if npx is None else npx
             C.memmove(d.id, comm_id, 128)
             rc = lib().iemic_create_dist(C.byref(h), C.byref(self._grid), ptr(L, C.c_int),
                                          C.byref(d))
@@ -330,18 +331,45 @@ class Ocean:
         """Ocean::getColumnIntegral (Ocean.C:1851-1895): for every S column of the last
         Jacobian the integral-condition-weighted column sum sum_r coeff_r J[r, c] (the
         intcond row's own coefficient dropped when SRES = 0 and use_sres), 0 elsewhere.
-        Host side, from the exported CSR, as the reference's Epetra computation."""
+        Host side, from the exported CSR, as the reference's Epetra computation; on several
+        ranks each sums its owned rows and the sums are added over the ranks (collective)."""
         rowptr, col, val = self.exportCSR()
         coef = self.getIntCondCoeff()
         ri = self.rowintcon
         if use_sres and ri >= 0:
             coef[ri] = 0.0
-        rows = np.repeat(np.arange(self.N), np.diff(rowptr))
+        rows = self.owned_rows()
+        nown = len(rows)
+        grow = np.repeat(rows, np.diff(rowptr[:nown + 1]))
         sums = np.zeros(self.N)
-        np.add.at(sums, col, coef[rows] * val)
+        np.add.at(sums, col[:len(grow)], coef[grow] * val[:len(grow)])
+        if self.layout()["nranks"] > 1:
+            check(lib().iemic_allreduce_sum(self._h, ptr(sums), self.N), "iemic_allreduce_sum")
         sel = np.zeros(self.N)
         sel[5::6] = 1.0
         return sums * sel
+
+    def owned_rows(self) -> np.ndarray:
+        """Global (reference-order) rows of this rank, in the order exportCSR lists them:
+        levels, then latitudes, then longitudes of the subdomain, six unknowns per cell."""
+        lay, c = self.layout(), self.cfg
+        k = np.arange(c.l)[:, None, None, None]
+        j = np.arange(lay["jb0"], lay["jb1"])[None, :, None, None]
+        i = np.arange(lay["ib0"], lay["ib1"])[None, None, :, None]
+        v = np.arange(6)[None, None, None, :]
+        return (6 * ((k * c.m + j) * c.n + i) + v).reshape(-1)
+
+    def comm_size(self):
+        """(ranks the communicator reports -- ncclCommCount under RCCL --, transport name)."""
+        n, kind = C.c_int(), C.c_int()
+        check(lib().iemic_comm_size(self._h, C.byref(n), C.byref(kind)), "iemic_comm_size")
+        return n.value, {0: "none", 1: "rccl", 2: "local", 3: "host"}[kind.value]
+
+    def comm_stats(self) -> dict:
+        """Communication counters since the previous call (then reset)."""
+        out = np.zeros(4, dtype=np.int64)
+        check(lib().iemic_comm_stats(self._h, ptr(out, C.c_int64)), "iemic_comm_stats")
+        return dict(batches=int(out[0]), messages=int(out[1]), bytes=int(out[2]), allreduces=int(out[3]))
 
     # ---- fused device-resident Newton step -------------------------------------------
     def newtonStep(self, allow_unconverged: bool = False) -> _lib.NewtonInfo:

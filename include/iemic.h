@@ -260,6 +260,13 @@ int     iemic_layout(const iemic_ctx* ctx, int64_t* out);
  * (one per phase of a halo exchange), out[1] messages sent, out[2] bytes sent, out[3]
  * all-reduces */
 int     iemic_comm_stats(iemic_ctx* ctx, int64_t* out4);
+/* the ranks the communicator itself reports (RCCL: ncclCommCount; one rank: 1) and the
+ * transport: 0 none, 1 RCCL, 2 in-process group, 3 host transport (reports its nranks).
+ * The reference queries Epetra_Comm::NumProc (e.g. THCM.C:404, 1717). */
+int     iemic_comm_size(const iemic_ctx* ctx, int* size, int* transport);
+/* Epetra_Comm::SumAll (e.g. Ocean::getColumnIntegral's column sums, Ocean.C:1851-1895):
+ * buf (host, count doubles) summed over the context's ranks in place; collective */
+int     iemic_allreduce_sum(iemic_ctx* ctx, double* buf, int64_t count);
 
 /* ---- state ------------------------------------------------------------------------ */
 int iemic_set_state(iemic_ctx* ctx, const double* x);     /* host -> device state     */

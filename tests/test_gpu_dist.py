@@ -204,7 +204,7 @@ def test_subdomains_spmv_and_solve(oracle_lib, name, nranks, npx, prec):
     assert lin <= 1e-8, lin
 
 
-def _rccl_worker(rank, nranks, port, q):
+def _rccl_worker(rank, nranks, npx, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "i-emic_amd"), os.path.join(root, "tests")]
@@ -217,8 +217,9 @@ def _rccl_worker(rank, nranks, port, q):
         dist.broadcast_object_list(ids, 0)
         c = cf.preset("gateway16", mixing=0)
         L0 = golden_landm("gateway16")
-        oc = Ocean(c, landm=L0, device=rank, rank=rank, nranks=nranks, comm_id=ids[0],
+        oc = Ocean(c, landm=L0, device=rank, rank=rank, nranks=nranks, comm_id=ids[0], npx=npx,
                    solver_params={"FGMRES tolerance": 1e-10})
+        assert oc.comm_size() == (nranks, "rccl"), oc.comm_size()
         L = oc.landmask().reshape(c.l + 2, c.m + 2, c.n + 2)
         x = cf.synthetic_state(c, L, amp_ts=1e-3)
         v = cf.synthetic_vector(c, seed=5)
@@ -236,15 +237,17 @@ def _rccl_worker(rank, nranks, port, q):
         dist.destroy_process_group()
 
 
-def test_rccl_ranks(oracle_lib):
-    """Two ranks, one GPU each, over RCCL: J (through J v), the halo exchanges and the
-    Krylov all-reduces of a solve; the gathered owned rows match the oracle."""
+@pytest.mark.parametrize("npx", [1, 2])
+def test_rccl_ranks(oracle_lib, npx):
+    """Two ranks, one GPU each, over RCCL (latitude bands, and an x split whose strided
+    messages go through the device staging buffer): J (through J v), the halo exchanges and
+    the Krylov all-reduces of a solve; the gathered owned rows match the oracle."""
     import torch
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, 29811, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, npx, 29811 + npx, q)) for r in range(2)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
@@ -291,11 +294,14 @@ def _transport_worker(rank, nranks, npx, name, port, q):
         oc.computeJacobian()
         rowptr, col, val = oc.exportCSR()
         y = oc.applyMatrix(v)
+        colint = oc.getColumnIntegral()
         info = oc.newtonStep()
         x1 = oc.getState().copy()
         lay = oc.layout()
         q.put((rank, {"lay": lay, "y": y, "x": x, "v": v, "x1": x1, "csr": (rowptr, col, val),
-                      "converged": info.solve.converged, "f0": info.norm_f0, "f1": info.norm_f1}))
+                      "converged": info.solve.converged, "f0": info.norm_f0, "f1": info.norm_f1,
+                      "colint": colint, "coeff": oc.getIntCondCoeff(), "ri": oc.rowintcon,
+                      "comm": oc.comm_size()}))
         oc.close()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -338,6 +344,20 @@ def test_transport_processes(oracle_lib, name, nranks, npx):
         x1[rows] = r["x1"][rows]
         assert r["converged"] == 1
     assert np.max(np.abs(y - yref)) <= 1e-13 * np.abs(ov).max() * np.abs(v).max()
+    # Ocean::getColumnIntegral over the ranks (Epetra SumAll): the whole matrix's S-column sums
+    coef = np.zeros(c.nrows)
+    for r in out.values():
+        rows = np.array(owned_rows(c, r["lay"]))
+        coef[rows] = r["coeff"][rows]
+        assert r["comm"] == (nranks, "host")
+    ri = out[0]["ri"]
+    if ri >= 0:
+        coef[ri] = 0.0
+    ref = np.zeros(c.nrows)
+    np.add.at(ref, o.col, coef[np.repeat(np.arange(c.nrows), np.diff(o.rowptr))] * ov)
+    ref[np.arange(c.nrows) % 6 != 5] = 0.0
+    for r in out.values():
+        np.testing.assert_allclose(r["colint"], ref, rtol=0, atol=1e-12 * np.abs(ref).max())
     F0 = o.rhs(x)
     f0 = np.linalg.norm(F0)
     assert abs(out[0]["f0"] - f0) <= 1e-12 * f0
