@@ -41,7 +41,23 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PMC_TAG = "r02"         # profiles/<tag>_spmv_pmc.json: PMC HBM bytes per k_spmv launch
+PMC_TAG = "r04"         # bench_data/pmc_<tag>.json: per-kernel PMC bytes and trace times of a step
+
+
+def pmc_table(config: str):
+    """The measured per-kernel table of one benchmark step (tools/pmc_table.py), if it was
+    measured on the device sources this tree builds (its src_digest) and this config."""
+    path = os.path.join(ROOT, "bench_data", f"pmc_{PMC_TAG}.json")
+    if not os.path.exists(path):
+        return None, f"no table {os.path.relpath(path, ROOT)}"
+    with open(path) as f:
+        t = json.load(f)
+    from iemic._lib import src_digest
+    if t.get("src_digest") != src_digest():
+        return None, f"{os.path.relpath(path, ROOT)} was measured on other kernel sources"
+    if t.get("config") != config:
+        return None, f"{os.path.relpath(path, ROOT)} holds config {t.get('config')}"
+    return t, None
 
 
 def spmv_bytes(nnz: int, n: int) -> int:
@@ -102,6 +118,8 @@ def parse():
     p.add_argument("--cold-reps", type=int, default=0,
                    help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-samples", type=int, default=3,
+                   help="timed CPU Newton steps (the line reports their median and spread)")
     p.add_argument("--mode", default="newton", choices=["newton", "continuation"],
                    help="continuation: config C5, one pseudo-arclength continuation step of the "
                         "1-degree ocean (run/ocean settings) from bench_data/<config>_cf05.npz")
@@ -116,33 +134,42 @@ def cpu_baseline(cfg, L, x, args):
     workload with the same algorithm: F and J assembly, the block Gauss-Seidel set-up (4
     damped defect-correction passes on the dynamics block, one T/S aggregation-multigrid
     V-cycle with z-line smoothing: oracle/prec_oracle.c, the GPU apply's CPU twin; Schur by
-    band LU), FGMRES(krylov) with restarts to the same tolerance (CGS2), x += dx, new F."""
+    band LU), FGMRES(krylov) with restarts to the same tolerance (CGS2), x += dx, new F.
+    args.cpu_samples timed steps; the value is their median."""
     from oracle import oracle as orc
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
-    T0 = time.perf_counter()
-    t = time.perf_counter()
-    F = o.rhs(x)
-    t_rhs = time.perf_counter() - t
-    t = time.perf_counter()
-    val, _ = o.jacobian(x)
-    t_jac = time.perf_counter() - t
-    t = time.perf_counter()
-    P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
-                    ts_mg=args.ts_mg, ts_at=args.ts_at)
-    t_prec = time.perf_counter() - t
-    t = time.perf_counter()
-    dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=args.tol, m=args.krylov,
-                               maxit=args.krylov * (args.restarts + 1))
-    t_solve = time.perf_counter() - t
-    F1 = o.rhs(x + dx)
-    total = time.perf_counter() - T0
+    samples = []
+    for _ in range(max(1, args.cpu_samples)):
+        T0 = time.perf_counter()
+        t = time.perf_counter()
+        F = o.rhs(x)
+        t_rhs = time.perf_counter() - t
+        t = time.perf_counter()
+        val, _ = o.jacobian(x)
+        t_jac = time.perf_counter() - t
+        t = time.perf_counter()
+        P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
+                        ts_mg=args.ts_mg, ts_at=args.ts_at)
+        t_prec = time.perf_counter() - t
+        t = time.perf_counter()
+        dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=args.tol, m=args.krylov,
+                                   maxit=args.krylov * (args.restarts + 1))
+        t_solve = time.perf_counter() - t
+        F1 = o.rhs(x + dx)
+        samples.append(time.perf_counter() - T0)
+        del P
+    ms = sorted(v * 1e3 for v in samples)
+    med = float(np.median(ms))
     return {
-        "value": round(total * 1e3, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
-        "sample": (f"timed, one full Newton step on the oracle C port (OpenMP {cores} threads), same "
-                   f"state and algorithm: F {t_rhs*1e3:.0f} ms, J {t_jac*1e3:.0f} ms, block GS set-up "
-                   f"{t_prec*1e3:.0f} ms (dyn x{args.dyn_iters}, T/S multigrid x{args.ts_mg}), FGMRES"
-                   f"({args.krylov}) {its} iterations to {rel:.1e} in {t_solve:.1f} s"),
+        "value": round(med, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
+        "samples_ms": [round(v, 1) for v in ms], "spread_ms": round(ms[-1] - ms[0], 1),
+        "sample": (f"median of {len(ms)} timed full Newton steps (SURVEY §8d asks for 10 after 2 "
+                   f"warm-ups; {len(ms)} keep the line within minutes) on the oracle C port "
+                   f"(OpenMP {cores} threads), same state and algorithm; last: F {t_rhs*1e3:.0f} ms, "
+                   f"J {t_jac*1e3:.0f} ms, block GS set-up {t_prec*1e3:.0f} ms (dyn x{args.dyn_iters}, "
+                   f"T/S multigrid x{args.ts_mg}), FGMRES({args.krylov}) {its} iterations to {rel:.1e} "
+                   f"in {t_solve:.1f} s"),
         "iters": its, "norm_f0": float(np.linalg.norm(F)), "norm_f1": float(np.linalg.norm(F1)),
     }
 
@@ -549,13 +576,23 @@ def main():
             extra["cold_us"] = round(oc.time_spmv_cold(fl.data_ptr(), fl.numel(),
                                                        args.cold_reps) * 1e3, 2)
             del fl
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"{PMC_TAG}_spmv_pmc.json")
-    if os.path.exists(pmc) and world == 1:
-        with open(pmc) as f:
-            pm = json.load(f)
-        if pm.get("config") == args.config:
-            traffic = pm.get("hbm_bytes_per_launch")
+    # measured per-kernel PMC bytes and trace times of this step (bench_data/pmc_<tag>.json)
+    traffic, step_rf, dom_rf = None, None, None
+    tab, why = pmc_table(args.config) if world == 1 else (None, "one GPU only")
+    if tab:
+        ks = {r["kernel"]: r for r in tab["kernels"]}
+        if "k_spmv7" in ks:
+            traffic = ks["k_spmv7"]["hbm_bytes_per_launch"]
+        sb = tab["step_hbm_bytes"]
+        step_rf = {"hbm_bytes": sb, "ms": round(ms, 3), "achieved": round(sb / (ms * 1e-3) / 1e9, 1),
+                   "frac": round(sb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "source": f"bench_data/pmc_{PMC_TAG}.json (PMC counter bytes of one step) / live ms_per_step"}
+        d = ks[tab["dominant"]]
+        dg = d["hbm_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
+        dom_rf = {"kernel": d["kernel"], "share": round(d["total_ms"] / tab["step_kernel_ms"], 4),
+                  "hbm_bytes_per_launch": d["hbm_bytes_per_launch"], "avg_us": d["avg_us"],
+                  "achieved": round(dg, 1), "frac": round(dg / HBM_PEAK_GBS, 4),
+                  "source": f"bench_data/pmc_{PMC_TAG}.json (PMC bytes / rocprofv3 kernel-trace average)"}
 
     # the Newton residual sequence from the benchmark state (untimed)
     seq = []
@@ -606,7 +643,8 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes": bsp, "stencil_ell_bytes": ell,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
-                     "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp, **extra},
+                     "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp,
+                     "step": step_rf, "dominant": dom_rf, **({"table": why} if why else {}), **extra},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -93,9 +93,38 @@ struct CrComp {
     const double* B[4];
     double s[4];
 };
-struct CrStep {                      /* one apply launch: its output descriptors         */
-    DevBuf<CrOut> d;
-    int nout = 0;
+/* Packed apply step.  The matrix terms of every (output block, row chunk of rc rows) --
+ * one workgroup -- are copied at set-up, scaled, into one contiguous run of the step's
+ * buffer P: term-major, then column, then the chunk's rc rows, so a wave reads 512
+ * contiguous bytes per load and no two workgroups share a cache line.  The workgroups are
+ * sorted by their number of matrix terms into at most CR_NCLS classes, whose bounds travel
+ * as kernel arguments: a workgroup finds its run in P without a memory load and issues its
+ * matrix loads at once; only the vector references (CrWg) come from memory. */
+constexpr int CR_NCLS = 8;
+struct CrCls {
+    int ncls;
+    int w0[CR_NCLS + 1];             /* first workgroup of each class (w0[ncls] = nwg)     */
+    int nA[CR_NCLS];                 /* matrix terms per workgroup of the class            */
+    int64_t p0[CR_NCLS];             /* first double of the class in P                     */
+};
+struct CrWg {                        /* vectors of one workgroup                           */
+    int yref, r0;                    /* output (base << 28 | offset), first row            */
+    int nv, hasid;                   /* vector terms; the last is the identity (scale 1)   */
+    int vref[CR_MT];                 /* (base << 28 | offset)                              */
+};
+struct CrPack {                      /* set-up copy: P[dst + c rc + rr] = s A[r0 + rr, c]  */
+    const double* A;
+    double s;
+    int64_t dst;
+    int r0;
+};
+struct CrStep {                      /* one apply launch                                  */
+    int nwg = 0, rc = 16;            /* workgroups, rows per chunk                        */
+    CrCls cls{};
+    DevBuf<CrWg> wg;
+    DevBuf<double> P;
+    DevBuf<CrPack> jobs;
+    int njobs = 0;
 };
 struct SchurCR {
     int n = 0, m = 0, periodic = 0, nlev = 0;

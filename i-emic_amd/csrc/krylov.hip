@@ -135,7 +135,8 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
  * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
  * rows' partials meet in LDS. */
 /* on[q]: row sp7_row(S0) + q of the cell is active; an identity row's coefficients are
- * neither loaded nor used (about half the cells are land at 2 degrees) */
+ * neither loaded nor used (about half the cells are land at 2 degrees).  The coefficients are
+ * streamed with non-temporal loads, so the z rows the neighbouring tiles gather stay in L2. */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
                                             int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
@@ -147,7 +148,7 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
         const int q = sp7_row(s) - sp7_row(S0);
         if (!on[q]) continue;
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc[q] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+        acc[q] += __builtin_nontemporal_load(val + (int64_t)s * nloc + lc) * z[NUN * (int64_t)cidx + sl.var];
     }
 }
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
@@ -314,11 +315,13 @@ __device__ __forceinline__ void block_sum_n(double* v, double* sm)
 /* DCGS2 dot pass: rows 2i, 2i+1 = Q_i.u, Q_i.w (i < nvec); rows 2nvec..2nvec+2 = u.u, u.w,
  * w.w.  Block (bx, by), by < ceil(nvec / DG), handles DG basis vectors against u and w over
  * chunk bx; by == nq the three self products.  The group index varies fastest in the block
- * order, so the groups of one chunk run together and u, w come from L2 after the first;
+ * order, so the groups of one chunk run together on one XCD and u, w come from its L2
+ * after the first;
  * every lane reads two consecutive elements (16-byte loads; N even, 16-byte aligned).
  * partial[row * nbx + bx].  (scripts/orth_probe.hip: DG = 4 in this order 5.5 TB/s at 89
  * vectors against 4.5 for DG = 8 with the group index slowest.) */
 constexpr int DCGS_DG = 4;
+static_assert(RED_BLOCKS % 8 == 0, "k_dcgs_dot deals chunks to the 8 XCDs");
 __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, int64_t ldv, int nvec,
                                                   const double* __restrict__ u,
                                                   const double* __restrict__ w, int64_t N,
@@ -327,7 +330,11 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
     constexpr int DG = DCGS_DG;
     __shared__ double sm[4 * 2 * DG];
     const int nq = (nvec + DG - 1) / DG;
-    const int by = blockIdx.x % (nq + 1), bx = blockIdx.x / (nq + 1);
+    /* XCD-aware order (workgroups are dealt to the 8 XCDs round robin): the nq + 1 groups of
+     * chunk bx run on XCD bx % 8, launched together, so u and w of the chunk are read from
+     * HBM once and from that XCD's L2 by the other groups (nbx % 8 == 0) */
+    const int G = nq + 1, sb = blockIdx.x / (8 * G), rem = blockIdx.x % (8 * G);
+    const int by = rem / 8, bx = sb * 8 + rem % 8;
     const int64_t N2 = N / 2;
     const int64_t stride = (int64_t)nbx * blockDim.x;
     const int64_t e0 = (int64_t)bx * blockDim.x + threadIdx.x;
@@ -598,6 +605,14 @@ static int nonfinite()
     return IEMIC_ERANGE;
 }
 
+int prec_safeguard(iemic_ctx* c);
+
+/* a restart cycle of at least STAG_MIN steps that cut the true residual by less than
+ * 1 / STAG_RATIO counts as stagnation (a converging cycle at the 2-degree bench state cuts it
+ * by ~1e-3, one at the 1-degree continuation tolerance by ~30) */
+constexpr double STAG_RATIO = 0.25;
+constexpr int STAG_MIN = 20;
+
 int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info)
 {
     /* vectors are ext-layout (stride NE); kernels touch the owned rows [o, o + NL) */
@@ -636,9 +651,16 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     }
     /* r = b (x0 = 0) */
     HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
-    double beta = bnorm, res = 1.0;
+    double beta = bnorm, res = 1.0, res_c0 = 1.0;
     int it = 0;
+    /* the safeguard's switch lasts for this solve only */
+    struct Restore {
+        iemic_ctx* c;
+        int mr;
+        ~Restore() { c->gs.dyn_mr = mr; }
+    } restore{c, c->gs.dyn_mr};
     for (int cycle = 0; cycle <= opt->max_restarts; cycle++) {
+        const int it_c0 = it;
         hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r + o, 1.0 / beta, V + o, NL);
         std::fill(g.begin(), g.end(), 0.0);
         g[0] = beta;
@@ -839,6 +861,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         beta = sqrt0(dot(c, r, r, 0));
         res = beta / bnorm;
         if (res <= opt->tol) break;
+        /* stagnation: switch the preconditioner to its safe variant (FGMRES is flexible) */
+        if (opt->prec == 2 && it - it_c0 >= STAG_MIN && res > STAG_RATIO * res_c0 && prec_safeguard(c))
+            inf.safeguard++;
+        res_c0 = res;
     }
     /* explicit residual (Ocean.C:1140-1150) */
     rc = spmv(c, x, w, c->stream);

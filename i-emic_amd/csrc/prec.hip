@@ -126,6 +126,18 @@ int prec_compute(iemic_ctx* c, const iemic_krylov* opt)
     return 0;
 }
 
+/* stagnation safeguard of the solvers: the block GS's damped correction passes diverge on
+ * states where the fixed step is too long (eigenvalues of the pass near 1 - 2 omega); the
+ * minimal-residual step length cannot.  Returns 1 when it switched, 0 when there is nothing
+ * to switch (another preconditioner, one pass, or already minimal-residual). */
+int prec_safeguard(iemic_ctx* c)
+{
+    BlockGS& gs = c->gs;
+    if (!gs.ready || gs.kind != 2 || gs.dyn_iters < 2 || gs.dyn_mr) return 0;
+    gs.dyn_mr = 1;
+    return 1;
+}
+
 int prec_apply(iemic_ctx* c, const double* r, double* z)
 {
     if (!c->gs.ready) {

@@ -431,66 +431,80 @@ __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv
     if (lane == 0) x[r] = v;
 }
 
-/* Apply step: one (output block, row chunk of CR_RC rows) per workgroup,
- * y = sum_t s_t A_t v_t over up to CR_MT terms (the composite of two levels: 7 terms down,
- * 4 up).  The term vectors are staged in LDS while the matrix rows are loaded into
- * registers; per row the column groups' partial sums meet in LDS in a fixed order. */
-template <int CPT>
-__global__ void __launch_bounds__(256) k_cr_multi(const CrOut* __restrict__ outs, int nout, int m, int nch,
-                                                  const double* __restrict__ b, double* __restrict__ x,
-                                                  double* __restrict__ bv, double* __restrict__ xv)
+/* Apply step (packed, CrStep): workgroup w computes rows [r0, r0 + RC) of one output block,
+ * y = sum_t A_t v_t (+ v_id), its nA scaled matrix terms read from its own run of P
+ * (term, column, row; thread = (row, column group) with the row fastest).  The class
+ * bounds are kernel arguments, so the matrix loads are issued before the vector references
+ * arrive; the vectors are staged in LDS meanwhile.  Per row the column groups' partial sums
+ * meet by a fixed shuffle tree inside each wave and in LDS across the four waves
+ * (deterministic). */
+template <int RC, int CPT>
+__global__ void __launch_bounds__(256) k_cr_pk(const double* __restrict__ P, const CrCls cls,
+                                               const CrWg* __restrict__ wgs, int m, const double* __restrict__ b,
+                                               double* __restrict__ x, double* __restrict__ bv,
+                                               double* __restrict__ xv)
 {
-    __shared__ double vs[CR_MT][CR_MAXM];
-    __shared__ double red[256];
-    /* the nch row chunks of one output block share the cache lines of its column-major
-     * blocks (an m = 76 column is 608 B: three of four chunk edges split a line), so they
-     * are dealt to one XCD (workgroups are dealt to the XCDs round robin): block b runs on
-     * XCD b % 8; output = (slot / nch) * 8 + b % 8, chunk = slot % nch, slot = b / 8 */
-    const int slot = (int)(blockIdx.x >> 3);
-    const int oi = (slot / nch) * 8 + (int)(blockIdx.x & 7);
-    if (oi >= nout) return;
-    const CrOut& o = outs[oi];
-    const int r0 = (slot % nch) * CR_RC;
-    const int t = threadIdx.x, g = t / CR_RC, r = r0 + t % CR_RC;
-    const int nt = o.nt;
-    const double* base[4] = {b, x, bv, xv};
+    constexpr int G = 256 / RC;
+    __shared__ double vs[CR_MT + 1][192];          /* m <= 192 (cr_init) */
+    __shared__ double red[4][RC];
+    const int w = blockIdx.x;
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < CR_NCLS; q++)
+        if (q < cls.ncls && w >= cls.w0[q]) k = q;
+    const int nA = cls.nA[k];
+    const double* __restrict__ Pw = P + cls.p0[k] + (int64_t)(w - cls.w0[k]) * nA * m * RC;
+    const int t = threadIdx.x, g = t / RC, rr = t % RC;
     double a[CR_MT][CPT];
 #pragma unroll
     for (int q = 0; q < CR_MT; q++)
 #pragma unroll
         for (int u = 0; u < CPT; u++) {
-            const int c = g + CR_G * u;
-            a[q][u] = (q < nt && o.A[q] && r < m && c < m) ? o.A[q][r + (size_t)c * m] : 0.0;
+            const int c = g + G * u;
+            a[q][u] = (q < nA && c < m) ? __builtin_nontemporal_load(Pw + ((int64_t)q * m + c) * RC + rr) : 0.0;
         }
-    for (int e = t; e < nt * m; e += 256) {
-        const int q = e / m, c = e - q * m;
-        vs[q][c] = base[o.vb[q]][o.vo[q] + c];
+    const CrWg& d = wgs[w];
+    const int nv = d.nv;
+    const double* base[4] = {b, x, bv, xv};
+    for (int q = 0; q < nv; q++) {
+        const int ref = d.vref[q];
+        const double* src = base[ref >> 28] + (ref & 0x0fffffff);
+        for (int c = t; c < m; c += 256) vs[q][c] = src[c];
     }
     __syncthreads();
-    double acc = 0.0;
+    const int r = d.r0 + rr;
+    double acc = (d.hasid && g == 0 && r < m) ? vs[nv - 1][r] : 0.0;
 #pragma unroll
     for (int q = 0; q < CR_MT; q++) {
-        if (q >= nt) break;
+        if (q >= nA) break;
         double p = 0.0;
-        if (o.A[q]) {
 #pragma unroll
-            for (int u = 0; u < CPT; u++) {
-                const int c = g + CR_G * u;
-                if (c < m) p += a[q][u] * vs[q][c];
-            }
-        } else if (g == 0 && r < m) {
-            p = vs[q][r];
+        for (int u = 0; u < CPT; u++) {
+            const int c = g + G * u;
+            if (c < m) p += a[q][u] * vs[q][c];
         }
-        acc += o.s[q] * p;
+        acc += p;
     }
-    red[t] = acc;
-    __syncthreads();
-    if (t < CR_RC && r < m) {
-        double sum = 0.0;
+    /* lanes of one row within a wave are RC apart */
 #pragma unroll
-        for (int q = 0; q < CR_G; q++) sum += red[q * CR_RC + t];
+    for (int o = 32; o >= RC; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    const int lane = t & 63, wave = t >> 6;
+    if (lane < RC) red[wave][lane] = acc;
+    __syncthreads();
+    if (t < RC && r < m) {
+        const double sum = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
         double* const ys[4] = {nullptr, x, bv, xv};
-        ys[o.yb][o.yo + r] = sum;
+        ys[d.yref >> 28][(d.yref & 0x0fffffff) + r] = sum;
+    }
+}
+
+/* set-up copy of the matrix terms into the packed layout, one job per workgroup */
+__global__ void __launch_bounds__(256) k_cr_pack(const CrPack* __restrict__ jobs, double* __restrict__ P, int m, int rc)
+{
+    const CrPack j = jobs[blockIdx.x];
+    for (int e = threadIdx.x; e < m * rc; e += 256) {
+        const int c = e / rc, rr = e - c * rc, r = j.r0 + rr;
+        P[j.dst + e] = r < m ? j.s * j.A[r + (size_t)c * m] : 0.0;
     }
 }
 
@@ -696,6 +710,78 @@ static std::vector<OutSpec> step_outputs(const SchurCR& cr, int l0, int nl, bool
     return out;
 }
 
+/* the packed form of one apply step (CrStep): rows per chunk so that the step has >= 448
+ * workgroups where it can (the small steps of the deep levels would leave CUs idle), the
+ * workgroups sorted by matrix-term count into classes, the set-up copy jobs */
+static int cr_pack_step(iemic_ctx* c, const SchurCR& cr, const std::vector<CrOut>& outs, CrStep& st)
+{
+    const int m = cr.m;
+    int rcw = 16;
+    while (rcw > 4 && (int64_t)outs.size() * ((m + rcw - 1) / rcw) < 448) rcw /= 2;
+    const int nch = (m + rcw - 1) / rcw;
+    struct W { int nA, o, ch; };
+    std::vector<W> ws;
+    for (int o = 0; o < (int)outs.size(); o++) {
+        int nA = 0, nid = 0;
+        for (int t = 0; t < outs[o].nt; t++) {
+            if (outs[o].A[t]) nA++;
+            else if (outs[o].s[t] != 1.0 || ++nid > 1) {
+                set_error("Schur cyclic reduction: unexpected identity term in an apply step");
+                return IEMIC_EINVAL;
+            }
+        }
+        for (int ch = 0; ch < nch; ch++) ws.push_back({nA, o, ch});
+    }
+    std::stable_sort(ws.begin(), ws.end(), [](const W& a, const W& b) { return a.nA > b.nA; });
+    CrCls cls{};
+    std::vector<CrWg> wg(ws.size());
+    std::vector<CrPack> jobs;
+    int64_t pos = 0;
+    auto ref = [](int base, int64_t off) { return (base << 28) | (int)off; };
+    for (size_t w = 0; w < ws.size(); w++) {
+        const W& q = ws[w];
+        if (w == 0 || q.nA != ws[w - 1].nA) {
+            if (cls.ncls == CR_NCLS) {
+                set_error("Schur cyclic reduction: too many term classes in an apply step");
+                return IEMIC_EINVAL;
+            }
+            cls.w0[cls.ncls] = (int)w;
+            cls.nA[cls.ncls] = q.nA;
+            cls.p0[cls.ncls] = pos;
+            cls.ncls++;
+        }
+        const CrOut& o = outs[q.o];
+        CrWg& d = wg[w];
+        d.yref = ref(o.yb, o.yo);
+        d.r0 = q.ch * rcw;
+        int v = 0, id = -1;
+        for (int t = 0; t < o.nt; t++) {
+            if (!o.A[t]) {
+                id = t;
+                continue;
+            }
+            d.vref[v++] = ref(o.vb[t], o.vo[t]);
+            jobs.push_back({o.A[t], o.s[t], pos, d.r0});
+            pos += (int64_t)m * rcw;
+        }
+        d.hasid = id >= 0;
+        if (id >= 0) d.vref[v++] = ref(o.vb[id], o.vo[id]);
+        d.nv = v;
+    }
+    cls.w0[cls.ncls] = (int)ws.size();
+    st.nwg = (int)ws.size();
+    st.rc = rcw;
+    st.cls = cls;
+    st.njobs = (int)jobs.size();
+    if (st.wg.alloc(wg.size()) || st.P.alloc(std::max<int64_t>(pos, 1)) || st.jobs.alloc(std::max<size_t>(jobs.size(), 1))) {
+        set_error("Schur cyclic reduction: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    int rc = h2d(c, st.wg.p, wg.data(), sizeof(CrWg) * wg.size());
+    if (!rc && !jobs.empty()) rc = h2d(c, st.jobs.p, jobs.data(), sizeof(CrPack) * jobs.size());
+    return rc;
+}
+
 /* apply steps (descriptors) and the composite operators they need; two levels per step
  * where the composed step stays within CR_MT terms */
 static int cr_build_steps(iemic_ctx* c, SchurCR& cr)
@@ -777,13 +863,8 @@ static int cr_build_steps(iemic_ctx* c, SchurCR& cr)
             }
             /* down steps top-first in plan order; up steps applied bottom-first (reverse) */
             CrStep& st = dir == 0 ? cr.down[ip] : cr.up[plan.size() - 1 - ip];
-            st.nout = (int)outs.size();
             int rc;
-            if (st.d.alloc(outs.size())) {
-                set_error("Schur cyclic reduction: out of device memory");
-                return IEMIC_ENOMEM;
-            }
-            if ((rc = h2d(c, st.d.p, outs.data(), sizeof(CrOut) * outs.size()))) return rc;
+            if ((rc = cr_pack_step(c, cr, outs, st))) return rc;
         }
     }
     if (cr.ncomp) {
@@ -977,6 +1058,11 @@ int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
         return rc;
     if (cr.ncomp)                          /* the composite operators of the apply steps */
         hipLaunchKernelGGL(k_cr_comp, dim3(T * T, cr.ncomp), dim3(256), 0, s, cr.cdesc.p, m);
+    for (const auto* v : {&cr.down, &cr.up})   /* the apply steps' packed operators */
+        for (const CrStep& st : *v)
+            if (st.njobs)
+                hipLaunchKernelGGL(k_cr_pack, dim3(st.njobs), dim3(256), 0, s, (const CrPack*)st.jobs.p, st.P.p, m,
+                                   st.rc);
     if (cr.tM) {                           /* the tail's inverse, column r = tail solve of e_r */
         const int M = cr.tM;
         auto tb = [&](int l) { return cr.tb.p + cr.tb_off[l - cr.lt]; };
@@ -1009,16 +1095,23 @@ int cr_check(iemic_ctx* c, SchurCR& cr)
  * dense GEMV */
 static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double* x, hipStream_t s)
 {
-    const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC;
-    const int need = (m + CR_G - 1) / CR_G;
-    const dim3 g((unsigned)(8 * nch * ((st.nout + 7) / 8)));
+    const int m = cr.m;
     double* bv = const_cast<double*>(cr.bv.p);
     double* xv = const_cast<double*>(cr.xv.p);
-    if (need <= 3) hipLaunchKernelGGL(k_cr_multi<3>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
-    else if (need <= 5) hipLaunchKernelGGL(k_cr_multi<5>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
-    else if (need <= 8) hipLaunchKernelGGL(k_cr_multi<8>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
-    else if (need <= 10) hipLaunchKernelGGL(k_cr_multi<10>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
-    else hipLaunchKernelGGL(k_cr_multi<12>, g, dim3(256), 0, s, st.d.p, st.nout, m, nch, b, x, bv, xv);
+    const dim3 g((unsigned)st.nwg), blk(256);
+#define CR_PK(RC, CPT) hipLaunchKernelGGL((k_cr_pk<RC, CPT>), g, blk, 0, s, (const double*)st.P.p, st.cls, \
+                                          (const CrWg*)st.wg.p, m, b, x, bv, xv)
+    if (st.rc == 16) {
+        if (m <= 80) CR_PK(16, 5);
+        else CR_PK(16, 12);
+    } else if (st.rc == 8) {
+        if (m <= 96) CR_PK(8, 3);
+        else CR_PK(8, 6);
+    } else {
+        if (m <= 128) CR_PK(4, 2);
+        else CR_PK(4, 3);
+    }
+#undef CR_PK
 }
 
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)

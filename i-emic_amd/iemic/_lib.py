@@ -63,7 +63,7 @@ class SolveInfo(C.Structure):
                 ("implicit_rel_res", C.c_double), ("explicit_rel_res", C.c_double),
                 ("t_prec_ms", C.c_double), ("t_spmv_ms", C.c_double),
                 ("t_orth_ms", C.c_double), ("t_total_ms", C.c_double), ("reorth", C.c_int),
-                ("n_spmv", C.c_int)]
+                ("n_spmv", C.c_int), ("safeguard", C.c_int)]
 
 
 class AtmosParams(C.Structure):
@@ -218,6 +218,22 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_atmos_pdist", "iemic_coupled_create", "iemic_coupled_destroy",
             "iemic_coupled_synchronize", "iemic_coupled_rhs", "iemic_coupled_jacobian",
             "iemic_coupled_spmv", "iemic_coupled_solve")
+
+
+def src_digest() -> str:
+    """SHA-256 over the device library's sources (csrc/ and include/iemic.h, sorted by path):
+    the key under which measured per-kernel tables (bench_data/pmc_*.json) apply."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*")))
+    files.append(os.path.join(os.path.dirname(PKG_DIR), "include", "iemic.h"))
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
 
 
 class IemicError(RuntimeError):

@@ -104,6 +104,10 @@ typedef struct {
     double t_prec_ms, t_spmv_ms, t_orth_ms, t_total_ms;
     int reorth;                  /* DGKS second passes taken                         */
     int n_spmv;                  /* SpMV launches inside the Arnoldi loop (t_spmv_ms) */
+    int safeguard;               /* stagnation safeguards taken: a restart cycle that cut */
+                                 /* the true residual less than 4x switched the block GS  */
+                                 /* correction passes to minimal-residual steps for the  */
+                                 /* rest of the solve (Continuation.H:724-741's role)     */
 } iemic_solve_info;
 
 /* Domain decomposition over several GPUs (one process and one context per GPU, RCCL over

@@ -1,23 +1,23 @@
 #!/bin/bash
-# PMC passes (one counter group per run, kernel-trace only, no other trace domains):
-# calibration streams of known size, then the cold-cache SpMV probe.  Each pass has its
-# own hard time limit; the first failure ends the call.
+# PMC passes for bench_data/pmc_<tag>.json (tools/pmc_table.py): one counter group per run,
+# kernel-trace only, no other trace domains.  Calibration streams of known size, then the
+# in-solve counters of every kernel of one benchmark Newton step (FETCH_SIZE and WRITE_SIZE
+# in separate runs) and a kernel-trace pass of the same command for the launch times.
+# Each pass has its own hard time limit; the first failure ends the call.
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-CFG=${CFG:-global2}
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 60 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/calib_$ctr -o run \
       -- ./scripts/_build/pmc_calib > gpurun_out/pmc/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/spmv_$ctr -o run \
-      -- python3 -u scripts/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_$ctr.log 2>&1 || { echo "spmv $ctr failed"; exit 1; }
 done
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/spmv_trace -o run \
-    -- python3 -u scripts/spmv_probe.py $CFG 5 > gpurun_out/pmc/spmv_trace.log 2>&1 || { echo "trace failed"; exit 1; }
-echo "pmc ok"
-# in-solve counters of every kernel of one benchmark Newton step (warm caches, as timed)
+echo "calib ok"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/bench_$ctr -o run \
       -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 > gpurun_out/pmc/bench_$ctr.log 2>&1 || { echo "bench $ctr failed"; exit 1; }
 done
 echo "bench pmc ok"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/bench_trace -o run \
+    -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 > gpurun_out/pmc/bench_trace.log 2>&1 \
+    || { echo "bench trace failed"; exit 1; }
+echo "bench trace ok"

@@ -398,3 +398,34 @@ def test_idr_newton_step_global2(oracle_lib, Ocean):
     lin = np.linalg.norm(F0 + o.spmv(ov, oc.getState() - x)) / np.linalg.norm(F0)
     assert info.solve.converged == 1 and lin <= 2e-8, (info.solve.iters, lin)
     print(f"IDR(4) global2 Newton step: {info.solve.iters} iterations, {info.t_total_ms:.0f} ms")
+
+
+@pytest.mark.parametrize("name,omega", [("global4", 1.1), ("global2", 1.1), ("global2", 0.95)])
+def test_stagnation_safeguard(oracle_lib, Ocean, name, omega):
+    """Defect-correction passes with a step too long for the state (omega = 1.1: the passes'
+    error propagation has eigenvalues near 1 - 2 omega; at the 2-degree branch state FGMRES
+    used to stall at 2e-4 after 1890 steps): a restart cycle that cuts the true residual less
+    than 4x switches the passes to minimal-residual steps, and the Newton step converges.  At
+    the default omega nothing switches (the default path is unchanged)."""
+    import os
+    from conftest import ROOT
+    c, oc, o, L = make(Ocean, oracle_lib, name, mixing=1,
+                       solver_params={"FGMRES tolerance": 1e-8, "FGMRES iterations": 90,
+                                      "FGMRES restarts": 20, "Dyn damping": omega})
+    if name == "global2":
+        with np.load(os.path.join(ROOT, "bench_data", "global2_cf05.npz"), allow_pickle=False) as d:
+            x = d["x"].astype(np.float64)
+    else:
+        x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    info = oc.newtonStep()
+    F0 = o.rhs(x)
+    ov, _ = o.jacobian(x)
+    lin = np.linalg.norm(F0 + o.spmv(ov, oc.getState() - x)) / np.linalg.norm(F0)
+    print(f"{name} omega {omega}: {info.solve.iters} FGMRES steps, safeguard {info.solve.safeguard}, "
+          f"lin {lin:.2e}")
+    assert info.solve.converged == 1 and lin <= 2e-8, (info.solve.iters, lin)
+    if omega < 1.0:
+        assert info.solve.safeguard == 0
+    if name == "global2" and omega > 1.0:
+        assert info.solve.safeguard == 1
