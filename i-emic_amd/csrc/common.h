@@ -145,8 +145,11 @@ struct SchurCR {
     DevBuf<CrGemm> gd;
     DevBuf<int> info;
 };
-int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic);
+/* tail_max: the dense tail starts at the first level of at most tail_max unknowns (0: the
+ * apply's default, 1024; n m: the whole problem, whose inverse cr.tinv is then built) */
+int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic, int tail_max = 0);
 int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij);
+int cr_factor_blocks(iemic_ctx* c, SchurCR& cr);
 int cr_check(iemic_ctx* c, SchurCR& cr);
 int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s);
 int cr_inverse_dev(hipStream_t s, int m, const double* src, double* dst, int* info);
@@ -195,6 +198,8 @@ struct BlockGS {
     static constexpr int MG_MAX = 12;
     int ts_mg = 1, mg_sweeps = 1, mg_nlev = 0;
     int mg_n[MG_MAX] = {}, mg_m[MG_MAX] = {};
+    int mg_par[MG_MAX] = {};         /* colour parity of the level's cell (0, 0): global   */
+                                     /* column + row offset of the subdomain's aggregates  */
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
     DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_fac[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
     DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
@@ -204,6 +209,13 @@ struct BlockGS {
     DevBuf<double> mg_gX, mg_gband, mg_gvec, mg_gtmp, mg_glpan;
     DevBuf<int> mg_gpiv, mg_ginfo, mg_gcols;
     DevBuf<double> mg_cdense;        /* coarsest dense operator (device assembly)        */
+    /* one rank: the coarsest level is the first of <= MG_CR_CELLS cells whose columns of
+     * one longitude fit a cyclic-reduction block (2 mb l <= 192); its inverse (mg_cinv, in
+     * the level's unknown order) comes from a whole-problem cyclic reduction over
+     * longitudes (schur_cr.hip, the explicit "tail" inverse) */
+    static constexpr int MG_CR_CELLS = 1024;
+    int mg_crd = 0;
+    SchurCR mg_cr;
     DevBuf<int> mg_cinfo;            /* its Gauss-Jordan pivot flag                      */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */

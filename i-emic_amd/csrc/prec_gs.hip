@@ -1103,6 +1103,37 @@ __global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ X, int 
     if (lane == 0) y[row] = s;
 }
 
+/* y = X b for a dense row-major N x N inverse (N <= 64 NL), one wave per row: every load
+ * of the row is issued before the first multiply, b staged in LDS, eight independent
+ * accumulators and a fixed shuffle tree (deterministic) */
+template <int NL>
+__global__ void __launch_bounds__(256) k_gemv_w(const double* __restrict__ X, int N, const double* __restrict__ b,
+                                                double* __restrict__ y)
+{
+    __shared__ double vb[64 * NL];
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const double* A = X + (size_t)(r < N ? r : 0) * N;
+    double a[NL];
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int c = lane + 64 * u;
+        a[u] = c < N ? __builtin_nontemporal_load(A + c) : 0.0;
+    }
+    for (int c = threadIdx.x; c < N; c += 256) vb[c] = b[c];
+    __syncthreads();
+    if (r >= N) return;
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int c = lane + 64 * u;
+        if (c < N) acc[u & 7] += a[u] * vb[c];
+    }
+    double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) y[r] = v;
+}
+
 /* dynamics defect: d = rr - A_DD z on the active U/V/W/P rows (couplings to active
  * U/V/W/P columns only: the block the dynamics solve approximates), 0 elsewhere */
 __global__ void k_dyn_resid(const double* __restrict__ val, const uint8_t* __restrict__ known,
@@ -1956,7 +1987,8 @@ __global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double
                     if (v == 0.0) continue;
                     int ii = i, jj = jl, kk = k;
                     if (!mg_nb(F, q < 6 ? q : q - 2, ii, jj, kk)) continue;
-                    if (q < 6 && (ii >> 1) == I && (jj >> 1) == J && kk == k)
+                    if (q < 6 && ii >= 0 && ii < F.n && jj >= 0 && jj < F.mb && (ii >> 1) == I && (jj >> 1) == J &&
+                        kk == k)
                         d[3 * R] += v;                    /* same variable, same aggregate */
                     else
                         o[8 * R + q] += v;
@@ -2183,15 +2215,19 @@ static TsLev mg_view(iemic_ctx* c, int q)
     V.n = gs.mg_n[q];
     V.mb = gs.mg_m[q];
     /* subdomains: the level-0 smoother and residual see the neighbours' edge rows and
-     * columns (halo rows / columns in the layout, exchanged before every relaxation),
-     * colours by the global i + j parity so that all subdomains relax the same colour in
-     * the same launch; coarse levels subdomain-local; the x wrap only with one x part */
+     * columns (halo rows / columns in the layout, exchanged before every relaxation); with
+     * an x split the intermediate levels see the neighbours' edge columns too (a cut across
+     * the zonal flow would otherwise make them block Jacobi), the coarsest is
+     * the global problem; colours by the global i + j parity of the level's aggregates, so
+     * that all subdomains relax the same colour in the same launch and a cell's neighbours
+     * across a cut have the other colour; the x wrap only with one x part */
+    const int qc = gs.mg_nlev - 1;
     V.periodic = c->cfg.periodic && c->npx == 1;
     V.hj = (q == 0 && c->npy > 1) ? 1 : 0;
-    V.hi = (q == 0 && c->npx > 1) ? 1 : 0;
+    V.hi = (q < qc && c->npx > 1) ? 1 : 0;
     V.vis = V.hj;
     V.visi = V.hi;
-    V.jpar = q == 0 ? ((c->jb0 + c->ib0) & 1) : 0;
+    V.jpar = gs.mg_par[q];
     V.cstr = (int64_t)(V.mb + 2 * V.hj) * (V.n + 2 * V.hi) * V.l;
     V.off = gs.mg_off[q].p;
     V.diag = gs.mg_diag[q].p;
@@ -2488,11 +2524,79 @@ __global__ void k_mg_coarse_dense(const double* __restrict__ off, const double* 
     if (!any) Ar[rowq] = 1.0;
 }
 
+/* the coarsest level's operator as cyclic-reduction blocks over longitudes (one rank, no
+ * halo): block i holds the unknowns (jl l + k) 2 + var of longitude i; D_i couples them
+ * within the longitude (2x2 cell block, -+j, -+k, the T/S cross couplings along k), L_i / R_i
+ * to longitude i -+ 1 (wrapping when periodic).  Inactive unknowns become identity rows.
+ * One thread per (cell, var) row: no write races. */
+__global__ void k_mg_cr_expand(TsLev V, int mc, int periodic, double* __restrict__ D, double* __restrict__ Lb,
+                               double* __restrict__ Rb)
+{
+    const int64_t ncl = (int64_t)V.n * V.mb * V.l;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 2 * ncl) return;
+    const int R = (int)(q / ncl);
+    const int64_t t = q % ncl;
+    const int k = (int)(t % V.l), i = (int)((t / V.l) % V.n), jl = (int)(t / ((int64_t)V.l * V.n));
+    const int64_t cs = V.cstr, c = mg_cell(V, i, jl, k);
+    const size_t mm = (size_t)mc * mc;
+    auto idx = [&](int j2, int k2, int var) { return (j2 * V.l + k2) * 2 + var; };
+    const int r = idx(jl, k, R);
+    double* Di = D + (size_t)i * mm;
+    if (V.diag[(int64_t)(3 * R) * cs + c] == 0.0) {
+        Di[r + (size_t)r * mc] = 1.0;
+        return;
+    }
+    Di[r + (size_t)r * mc] += V.diag[(int64_t)(3 * R) * cs + c];
+    Di[r + (size_t)idx(jl, k, 1 - R) * mc] += V.diag[(int64_t)(1 + R) * cs + c];
+    for (int qq = 0; qq < 8; qq++) {
+        const double v = V.off[(int64_t)(8 * R + qq) * cs + c];
+        if (v == 0.0) continue;
+        const int dir = qq < 6 ? qq : qq - 2, var = qq < 6 ? R : 1 - R;
+        int jj = jl, kk = k;
+        double* B = Di;
+        switch (dir) {
+        case 0:
+            if (i == 0 && !periodic) continue;
+            B = Lb + (size_t)i * mm;
+            break;
+        case 1:
+            if (i == V.n - 1 && !periodic) continue;
+            B = Rb + (size_t)i * mm;
+            break;
+        case 2: jj--; break;
+        case 3: jj++; break;
+        case 4: kk--; break;
+        default: kk++; break;
+        }
+        if (jj < 0 || jj >= V.mb || kk < 0 || kk >= V.l) continue;
+        B[r + (size_t)idx(jj, kk, var) * mc] += v;
+    }
+}
+
+/* the whole-problem inverse of the cyclic reduction (row-major, longitude-block order) in
+ * the level's unknown order var ncl + cell, row-major -- what the coarse GEMV applies */
+__global__ void k_mg_cr_perm(const double* __restrict__ T, TsLev V, int N, double* __restrict__ X)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)N * N) return;
+    const int64_t ncl = N / 2;
+    const int rq = (int)(e / N), cq = (int)(e % N);
+    auto cr_of = [&](int u) {
+        const int var = (int)(u / ncl);
+        const int64_t t = u % ncl;
+        const int k = (int)(t % V.l), i = (int)((t / V.l) % V.n), jl = (int)(t / ((int64_t)V.l * V.n));
+        return (int64_t)i * (2 * V.mb * V.l) + (jl * V.l + k) * 2 + var;
+    };
+    X[e] = T[cr_of(rq) * N + cr_of(cq)];
+}
+
 /* levels, Galerkin operators, z-line factors and the coarsest inverse (once per Jacobian) */
 static int mg_setup(iemic_ctx* c)
 {
     BlockGS& gs = c->gs;
     const int l = c->l;
+    int rc;
     if (l > 64) {                /* the z-line smoother runs one lane per level */
         gs.ts_mg = 0;
         return 0;
@@ -2505,7 +2609,16 @@ static int mg_setup(iemic_ctx* c)
         int n = c->nx, m = c->jb1 - c->jb0;
         gs.mg_n[0] = n;
         gs.mg_m[0] = m;
-        while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)N * M * l > 128) && (N > 1 || M > 1)) {
+        gs.mg_crd = 0;
+        /* one rank: stop at the first level of <= MG_CR_CELLS cells that the whole-problem
+         * cyclic reduction takes (blocks of one longitude, 2 m l <= 192 unknowns, >= 2
+         * longitudes): an exact coarse solve, one GEMV per V-cycle instead of the last
+         * levels' ~9 latency-bound launches */
+        auto cr_ok = [&](int nn, int mm) {
+            return c->nranks == 1 && (int64_t)nn * mm * l <= BlockGS::MG_CR_CELLS && 2 * mm * l <= 192 && nn >= 2;
+        };
+        while (q + 1 < BlockGS::MG_MAX && (q == 0 || (int64_t)N * M * l > 128) && (N > 1 || M > 1) &&
+               !(q > 0 && cr_ok(n, m))) {
             N = (N + 1) / 2;
             M = (M + 1) / 2;
             n = (n + 1) / 2;
@@ -2518,9 +2631,30 @@ static int mg_setup(iemic_ctx* c)
             gs.ts_mg = 0;            /* a single water column per band: plain sweeps */
             return 0;
         }
+        gs.mg_crd = cr_ok(n, m) && (int64_t)n * m * l > 128 ? 1 : 0;
+        if (gs.mg_crd && (rc = cr_init(c, gs.mg_cr, n, 2 * m * l, c->cfg.periodic, 2 * n * m * l))) return rc;
         if ((int64_t)n * m * l > 1024) {
             set_error("block GS: T/S multigrid coarsest level too large");
             return IEMIC_EINVAL;
+        }
+        gs.mg_nlev = q + 1;
+        /* global offsets of this subdomain's aggregates on every level: the x parts to the
+         * west / the y parts to the south, each coarsened like this one (decomp.h part_of) */
+        for (int lv = 0; lv <= q; lv++) {
+            auto coarse = [&](int v) {
+                for (int t = 0; t < lv; t++) v = (v + 1) / 2;
+                return v;
+            };
+            int io = 0, jo = 0, off, cnt;
+            for (int px = 0; px < c->px; px++) {
+                part_of(c->n, c->npx, px, off, cnt);
+                io += coarse(cnt);
+            }
+            for (int py = 0; py < c->py; py++) {
+                part_of(c->m, c->npy, py, off, cnt);
+                jo += coarse(cnt);
+            }
+            gs.mg_par[lv] = (io + jo) & 1;
         }
         for (int lv = 0; lv <= q; lv++) {
             const size_t cs = (size_t)mg_view(c, lv).cstr;
@@ -2530,7 +2664,6 @@ static int mg_setup(iemic_ctx* c)
             for (DevBuf<double>* bptr : {&gs.mg_off[lv], &gs.mg_diag[lv], &gs.mg_fac[lv], &gs.mg_b[lv], &gs.mg_z[lv]})
                 HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         }
-        gs.mg_nlev = q + 1;
         const size_t NC = (size_t)2 * n * m * l;
         if (gs.mg_cinv.alloc(NC * NC)) return IEMIC_ENOMEM;
     }
@@ -2543,7 +2676,11 @@ static int mg_setup(iemic_ctx* c)
     for (int q = 1; q < gs.mg_nlev; q++) {
         TsLev F = mg_view(c, q - 1);
         const TsLev C = mg_view(c, q);
-        F.vis = F.visi = 0;          /* aggregates and coarse operators stay local      */
+        /* the coarse operator keeps the couplings across a cut where the coarse level has a
+         * halo there (x splits, intermediate levels); the coarsest stays local (its global
+         * problem adds the cross couplings itself, mg_global_setup) */
+        F.vis = C.hj;
+        F.visi = C.hi;
         hipLaunchKernelGGL(k_mg_galerkin, dim3(blocks_for((int64_t)C.n * C.mb * C.l)), dim3(256), 0, s, F, C,
                            gs.mg_off[q].p, gs.mg_diag[q].p);
     }
@@ -2558,7 +2695,27 @@ static int mg_setup(iemic_ctx* c)
     const int qc = gs.mg_nlev - 1;
     const int64_t ncl = (int64_t)gs.mg_n[qc] * gs.mg_m[qc] * l;
     const int N = (int)(2 * ncl);
-    int rc;
+    if (gs.mg_crd) {
+        /* cyclic reduction over the level's longitudes: blocks of one longitude, unknown
+         * (jl l + k) 2 + var; the whole problem is its tail, whose explicit inverse is
+         * permuted into the level's (var, cell) order for the coarse GEMV */
+        SchurCR& cr = gs.mg_cr;
+        const int mc = cr.m;
+        const size_t mm = (size_t)mc * mc;
+        HIP_OK(hipMemsetAsync(cr.dlr.p, 0, sizeof(double) * 3 * (size_t)cr.n * mm, s));
+        const TsLev C = mg_view(c, qc);
+        hipLaunchKernelGGL(k_mg_cr_expand, dim3(blocks_for(2 * ncl)), dim3(256), 0, s, C, mc, cr.periodic,
+                           cr.dlr.p, cr.dlr.p + (size_t)cr.n * mm, cr.dlr.p + 2 * (size_t)cr.n * mm);
+        if ((rc = cr_factor_blocks(c, cr))) return rc;
+        if ((rc = cr_check(c, cr))) {
+            set_error("block GS: singular coarsest T/S operator");
+            return rc;
+        }
+        hipLaunchKernelGGL(k_mg_cr_perm, dim3(blocks_for((int64_t)N * N)), dim3(256), 0, s,
+                           (const double*)cr.tinv.p, C, N, gs.mg_cinv.p);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     if (N <= 192 && c->nranks <= 1) {
         DevBuf<double>& A = gs.mg_cdense;
         if (A.n < (size_t)N * N && A.alloc((size_t)N * N)) return IEMIC_ENOMEM;
@@ -2682,8 +2839,15 @@ static int mg_coarsest(iemic_ctx* c, int q)
                            gs.mg_n[q], c->l, gs.mg_gGX, gs.mg_gI0, gs.mg_gJ0, gs.mg_z[q].p);
         return 0;
     }
-    hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
-                       gs.mg_b[q].p, gs.mg_z[q].p);
+    if (N <= 1024)
+        hipLaunchKernelGGL(k_gemv_w<16>, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, (const double*)gs.mg_cinv.p,
+                           N, (const double*)gs.mg_b[q].p, gs.mg_z[q].p);
+    else if (N <= 2048)
+        hipLaunchKernelGGL(k_gemv_w<32>, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, (const double*)gs.mg_cinv.p,
+                           N, (const double*)gs.mg_b[q].p, gs.mg_z[q].p);
+    else
+        hipLaunchKernelGGL(k_gemv, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, gs.mg_cinv.p, N, N,
+                           gs.mg_b[q].p, gs.mg_z[q].p);
     return 0;
 }
 

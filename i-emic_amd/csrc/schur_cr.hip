@@ -70,145 +70,123 @@ __global__ void k_cr_expand(const double* __restrict__ S9, const int* __restrict
     }
 }
 
-/* Gauss-Jordan inverse with row pivoting of src block (s0 + blockIdx.x * sstep) into dst
- * block blockIdx.x, the matrix held in registers: 1024 threads as a 32 x 32 grid, thread
- * (tr, tc) owns rows tr + 32 a and columns tc + 32 b (a, b < RPT; m <= 32 RPT); per
- * elimination step the pivot column and row go through LDS.  A zero pivot sets *info. */
-template <int RPT>
-__global__ void __launch_bounds__(1024) k_cr_inv(const double* __restrict__ src, int s0, int sstep,
-                                                 double* __restrict__ dst, int m, int* __restrict__ info)
+/* Gauss-Jordan inverse with partial pivoting of src block (s0 + blockIdx.x * sstep) into
+ * dst block blockIdx.x (m x m column-major, m <= TR RA, m <= 32 RB), in place in registers:
+ * 32 TR threads as a TR x 32 grid, thread (tr, tc) holds rows tr + TR x and columns
+ * tc + 32 y.  Rows are never swapped: step k takes the unused row p with the largest
+ * |a(p, k)|, scales it, eliminates column k from every other row, and column k -- dead in
+ * the eliminated matrix -- keeps column p of the inverse's row-permuted form (the in-place
+ * trick), so the result is written out through the two permutations (row p_k of the
+ * storage is row k of the inverse, storage column k is its column p_k).  The step loop is
+ * unrolled over blocks of TR steps, so the register column of k is a compile-time index;
+ * the pivot row's register row is selected under a branch on its row lane.  Two barriers
+ * per step (the LDS vectors are double-buffered by step parity).  A zero pivot sets *info. */
+template <int TR, int RA, int RB>
+__global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ src, int s0, int sstep,
+                                                     double* __restrict__ dst, int m, int* __restrict__ info)
 {
     const size_t mm = (size_t)m * m;
     const double* A = src + (size_t)(s0 + blockIdx.x * sstep) * mm;
     double* X = dst + (size_t)blockIdx.x * mm;
-    const int t = threadIdx.x, tr = t & 31, tc = t >> 5;
-    __shared__ double pcol[32 * RPT], prow[32 * RPT], rk[32 * RPT], rp[32 * RPT];
-    __shared__ int perm[32 * RPT];
-    __shared__ int s_p;
-    double a[RPT][RPT];
+    const int t = threadIdx.x, tr = t % TR, tc = t / TR;
+    __shared__ double pcol[2][TR * RA], prow[2][32 * RB];
+    __shared__ int s_p[2];
+    __shared__ int piv_row[TR * RA], step_of[TR * RA];
+    double a[RA][RB];
 #pragma unroll
-    for (int x = 0; x < RPT; x++)
+    for (int x = 0; x < RA; x++)
 #pragma unroll
-        for (int y = 0; y < RPT; y++) {
-            const int i = tr + 32 * x, j = tc + 32 * y;
+        for (int y = 0; y < RB; y++) {
+            const int i = tr + TR * x, j = tc + 32 * y;
             a[x][y] = (i < m && j < m) ? A[i + (size_t)j * m] : 0.0;
         }
-    for (int k = 0; k < m; k++) {
-        const int kc = k & 31, kb = k >> 5;
-        /* pivot column k -> LDS */
-        if (tc == kc) {
+    unsigned used = 0;                                 /* bit x: row tr + TR x was a pivot */
 #pragma unroll
-            for (int x = 0; x < RPT; x++) {
-                double v = 0.0;
+    for (int kbr = 0; kbr < RA; kbr++) {
+        const int yk = kbr * TR / 32;                   /* register column of k (compile time) */
+        for (int kk = 0; kk < TR; kk++) {
+            const int k = kbr * TR + kk;
+            if (k >= m) break;
+            const int sel = k & 1, kc = k & 31;
+            /* 1. pivot search in column k (TR lanes of one wave), column k -> LDS */
+            if (tc == kc) {
+                double best = -1.0;
+                int bi = m;
 #pragma unroll
-                for (int y = 0; y < RPT; y++) v = y == kb ? a[x][y] : v;
-                pcol[tr + 32 * x] = v;
-            }
-        }
-        __syncthreads();
-        if (t < 64) {
-            double best = -1.0;
-            int bi = k;
-            for (int i = k + t; i < m; i += 64) {
-                const double v = fabs(pcol[i]);
-                if (v > best) { best = v; bi = i; }
-            }
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ob = __shfl_xor(best, off, 64);
-                const int oi = __shfl_xor(bi, off, 64);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            if (t == 0) {
-                if (!(best > 0.0)) *info = 1;
-                s_p = bi;
-                perm[k] = bi;
-            }
-        }
-        __syncthreads();
-        const int p = s_p;
-        const int pr = p & 31, pa = p >> 5, kr = k & 31, ka = k >> 5;
-        /* rows k and p -> LDS */
-        if (tr == kr || tr == pr) {
-#pragma unroll
-            for (int y = 0; y < RPT; y++) {
-                double vk = 0.0, vp = 0.0;
-#pragma unroll
-                for (int x = 0; x < RPT; x++) {
-                    vk = x == ka ? a[x][y] : vk;
-                    vp = x == pa ? a[x][y] : vp;
+                for (int x = 0; x < RA; x++) {
+                    const int i = tr + TR * x;
+                    const double v = a[x][yk];
+                    if (i < m) pcol[sel][i] = v;
+                    const double av = (i < m && !((used >> x) & 1u)) ? fabs(v) : -1.0;
+                    if (av > best) { best = av; bi = i; }
                 }
-                if (tr == kr) rk[tc + 32 * y] = vk;
-                if (tr == pr) rp[tc + 32 * y] = vp;
+#pragma unroll
+                for (int o = 1; o < TR; o <<= 1) {
+                    const double ob = __shfl_xor(best, o, 64);
+                    const int oi = __shfl_xor(bi, o, 64);
+                    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+                }
+                if (tr == 0) {
+                    if (!(best > 0.0)) *info = 1;
+                    s_p[sel] = bi;
+                    piv_row[k] = bi;
+                    step_of[bi < m ? bi : 0] = k;
+                }
             }
-        }
-        __syncthreads();
-        /* swap, scale the pivot row: row k = row p / a(p,k), entry (k,k) = 1 / a(p,k) */
-        const double piv = rp[k];
-        const double inv = piv != 0.0 ? 1.0 / piv : 0.0;
-        if (tr == pr && p != k) {
+            __syncthreads();
+            const int p = __builtin_amdgcn_readfirstlane(s_p[sel]);
+            const int pr = p % TR, pa = p / TR;
+            /* 2. row p -> LDS */
+            if (tr == pr) {
+                used |= 1u << pa;
 #pragma unroll
-            for (int y = 0; y < RPT; y++)
+                for (int x = 0; x < RA; x++)
+                    if (x == pa)
 #pragma unroll
-                for (int x = 0; x < RPT; x++)
-                    if (x == pa) a[x][y] = rk[tc + 32 * y];
-        }
-        if (tr == kr) {
+                        for (int y = 0; y < RB; y++) {
+                            const int j = tc + 32 * y;
+                            if (j < m) prow[sel][j] = a[x][y];
+                        }
+            }
+            __syncthreads();
+            /* 3. scale row p, eliminate column k from the other rows; column k keeps the
+             * inverse's column (1 / piv in row p, -a(i, k) / piv elsewhere) */
+            const double piv = prow[sel][k];
+            const double inv = piv != 0.0 ? 1.0 / piv : 0.0;
+            double pr_s[RB];
 #pragma unroll
-            for (int y = 0; y < RPT; y++) {
+            for (int y = 0; y < RB; y++) {
                 const int j = tc + 32 * y;
-                const double v = j == k ? inv : rp[j] * inv;
-#pragma unroll
-                for (int x = 0; x < RPT; x++)
-                    if (x == ka) a[x][y] = v;
-                prow[j] = v;
+                pr_s[y] = j < m ? prow[sel][j] * inv : 0.0;
             }
-        }
-        /* the pivot column after the swap (row p now holds the old row k) */
-        if (tc == kc) {
+            const bool colk = tc == kc;
 #pragma unroll
-            for (int x = 0; x < RPT; x++) {
-                const int i = tr + 32 * x;
-                if (i == p && p != k) pcol[i] = rk[k];
+            for (int x = 0; x < RA; x++) {
+                const int i = tr + TR * x;
+                const double f = i < m ? pcol[sel][i] : 0.0;
+#pragma unroll
+                for (int y = 0; y < RB; y++) {
+                    if (y == yk && colk) a[x][y] = -f * inv;
+                    else a[x][y] -= f * pr_s[y];
+                }
             }
-        }
-        __syncthreads();
-        /* eliminate column k from every other row */
+            if (tr == pr) {
 #pragma unroll
-        for (int x = 0; x < RPT; x++) {
-            const int i = tr + 32 * x;
-            if (i == k) continue;
-            const double f = pcol[i];
+                for (int x = 0; x < RA; x++)
+                    if (x == pa)
 #pragma unroll
-            for (int y = 0; y < RPT; y++) {
-                const int j = tc + 32 * y;
-                const double old = j == k ? 0.0 : a[x][y];
-                a[x][y] = old - f * prow[j];
+                        for (int y = 0; y < RB; y++) a[x][y] = (y == yk && colk) ? inv : pr_s[y];
             }
-        }
-        __syncthreads();
-    }
-    /* undo the row interchanges as column interchanges, in reverse order: column j of the
-     * result is column q(j) of the eliminated matrix, q = the composed permutation */
-    __shared__ int colmap[32 * RPT];
-    if (t == 0) {
-        for (int j = 0; j < m; j++) colmap[j] = j;
-        for (int k = m - 1; k >= 0; k--) {
-            const int p = perm[k];
-            if (p != k) { const int x = colmap[k]; colmap[k] = colmap[p]; colmap[p] = x; }
         }
     }
     __syncthreads();
-    /* column j of the eliminated matrix is column dest[j] of the inverse */
-    double* T = X;
-    __shared__ int dest[32 * RPT];
-    if (t < m) dest[colmap[t]] = t;
-    __syncthreads();
+    /* storage (i, k) = inverse (step_of[i], piv_row[k]) */
 #pragma unroll
-    for (int x = 0; x < RPT; x++)
+    for (int x = 0; x < RA; x++)
 #pragma unroll
-        for (int y = 0; y < RPT; y++) {
-            const int i = tr + 32 * x, j = tc + 32 * y;
-            if (i < m && j < m) T[i + (size_t)dest[j] * m] = a[x][y];
+        for (int y = 0; y < RB; y++) {
+            const int i = tr + TR * x, j = tc + 32 * y;
+            if (i < m && j < m) X[step_of[i] + (size_t)piv_row[j] * m] = a[x][y];
         }
 }
 
@@ -875,7 +853,7 @@ static int cr_build_steps(iemic_ctx* c, SchurCR& cr)
 }
 
 /* level sizes, storage offsets and the GEMM descriptors (host, once per grid) */
-int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
+int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic, int tail_max)
 {
     if (m > 192) {
         set_error("Schur cyclic reduction: more than 192 latitudes");
@@ -976,7 +954,7 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic)
     /* dense tail: the first level of at most 1024 unknowns (2048: no gain) and its
      * descendants become one explicit inverse (built at set-up by solving the tail for the
      * identity), so the apply spends one GEMV launch instead of 2 (nlev - lt) + 1 */
-    constexpr int tail_max = CR_TAIL_MAX;
+    if (tail_max <= 0) tail_max = CR_TAIL_MAX;
     cr.lt = cr.nlev;
     cr.tM = 0;
     for (int l = 0; l < cr.nlev; l++)
@@ -1004,16 +982,15 @@ static int cr_inverse(hipStream_t s, int m, int count, const double* src, int s0
                       int* info)
 {
     if (count <= 0) return 0;
-    const int rpt = (m + 31) / 32;
-#define CR_INV(R) hipLaunchKernelGGL(k_cr_inv<R>, dim3(count), dim3(1024), 0, s, src, s0, sstep, dst, m, info)
-    switch (rpt) {
-    case 1: CR_INV(1); break;
-    case 2: CR_INV(2); break;
-    case 3: CR_INV(3); break;
-    case 4: CR_INV(4); break;
-    case 5: CR_INV(5); break;
-    case 6: CR_INV(6); break;
-    default:
+#define CR_INV(TR, RA, RB)                                                                           \
+    hipLaunchKernelGGL((k_cr_inv<TR, RA, RB>), dim3(count), dim3(32 * TR), 0, s, src, s0, sstep, dst, m, info)
+    if (m <= 32) CR_INV(16, 2, 1);
+    else if (m <= 64) CR_INV(16, 4, 2);
+    else if (m <= 96) CR_INV(16, 6, 3);
+    else if (m <= 128) CR_INV(32, 4, 4);
+    else if (m <= 160) CR_INV(32, 5, 5);
+    else if (m <= 192) CR_INV(32, 6, 6);
+    else {
         set_error("Schur cyclic reduction: more than 192 latitudes");
         return IEMIC_EINVAL;
     }
@@ -1033,15 +1010,24 @@ int cr_inverse_dev(hipStream_t s, int m, const double* src, double* dst, int* in
 int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij)
 {
     hipStream_t s = c->stream;
+    const int m = cr.m;
+    const size_t mm = (size_t)m * m;
+    HIP_OK(hipMemsetAsync(cr.dlr.p, 0, sizeof(double) * 3 * (size_t)cr.n * mm, s));
+    const int nm = cr.n * m;
+    hipLaunchKernelGGL(k_cr_expand, dim3((nm + 255) / 256), dim3(256), 0, s, S9, col_of_ij, cr.n, m,
+                       cr.periodic, cr.dlr.p, cr.dlr.p + (size_t)cr.n * mm, cr.dlr.p + 2 * (size_t)cr.n * mm);
+    return cr_factor_blocks(c, cr);
+}
+
+/* set-up from level-0 blocks already in cr.dlr (D, L, R: 3 n column-major m x m blocks) */
+int cr_factor_blocks(iemic_ctx* c, SchurCR& cr)
+{
+    hipStream_t s = c->stream;
     int rc;
     const int m = cr.m;
     const size_t mm = (size_t)m * m;
     const int T = (m + 31) / 32;
     HIP_OK(hipMemsetAsync(cr.info.p, 0, sizeof(int), s));
-    HIP_OK(hipMemsetAsync(cr.dlr.p, 0, sizeof(double) * 3 * (size_t)cr.n * mm, s));
-    const int nm = cr.n * m;
-    hipLaunchKernelGGL(k_cr_expand, dim3((nm + 255) / 256), dim3(256), 0, s, S9, col_of_ij, cr.n, m,
-                       cr.periodic, cr.dlr.p, cr.dlr.p + (size_t)cr.n * mm, cr.dlr.p + 2 * (size_t)cr.n * mm);
     for (int l = 0; l < cr.nlev; l++) {
         const int Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
         if (cr.g_cnt[3 * l])

@@ -535,6 +535,7 @@ static void dense_inverse(double* A, int N, double* X)
         const double d = A[(size_t)k * N + k];
         const double qd = d != 0.0 ? 1.0 / d : 0.0;
         for (int j = 0; j < N; j++) { A[(size_t)k * N + j] *= qd; X[(size_t)k * N + j] *= qd; }
+#pragma omp parallel for schedule(static) if (N > 256)
         for (int i = 0; i < N; i++) {
             if (i == k) continue;
             const double f = A[(size_t)i * N + k];
@@ -555,7 +556,12 @@ static void* mg_build(gs_t* g)
     M->periodic = g->periodic;
     int nn = n, mm = m, q = 0;
     M->n[0] = n; M->m[0] = m;
-    while (q + 1 < MG_MAXL && (q == 0 || (int64_t)nn * mm * l > 128) && (nn > 1 || mm > 1)) {
+    /* the GPU's one-rank rule (prec_gs.hip mg_setup): stop at the first level of <= 1024
+     * cells whose longitudes fit a cyclic-reduction block (2 mm l <= 192, >= 2 longitudes),
+     * solved exactly (the GPU by whole-problem cyclic reduction, here Gauss-Jordan) */
+#define MG_CR_OK(a, b) ((int64_t)(a) * (b) * l <= 1024 && 2 * (b) * l <= 192 && (a) >= 2)
+    while (q + 1 < MG_MAXL && (q == 0 || (int64_t)nn * mm * l > 128) && (nn > 1 || mm > 1) &&
+           !(q > 0 && MG_CR_OK(nn, mm))) {
         nn = (nn + 1) / 2; mm = (mm + 1) / 2; q++;
         M->n[q] = nn; M->m[q] = mm;
     }
