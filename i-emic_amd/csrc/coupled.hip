@@ -75,6 +75,7 @@ struct iemic_coupled {
     int64_t NL = 0, NA = 0, NC = 0;      /* ocean owned rows, atmosphere rows, packed total  */
     DevBuf<double> xo, yo, ro, zo;       /* ocean ext-layout scratch                         */
     DevBuf<double> V, Z, w, r, tmpa, part, hb;
+    DevBuf<double> tsurf;            /* n*m surface T of a packed vector (several ranks)  */
     int mk = 0;
     int synced = 0;
     double pars[18] = {};                /* CommPars of the last synchronisation            */
@@ -456,6 +457,7 @@ __global__ void k_atm_prec_b(AtmGeo G, const double* __restrict__ zt, const doub
 /* ---- coupling (applied matrix-free) -------------------------------------------------- */
 struct CplPar {
     int n, m, l;
+    int ib0, jb0, nx, mb;  /* the ocean subdomain's owned columns / rows (Decomp2D)  */
     int64_t own0;          /* first owned ext cell of the ocean                    */
     double dTFQ;           /* nuq tdim/qdim dqso (1 - M)  (Atmosphere.C:547)        */
     double pfac;           /* (1/A)(tdim/qdim) dqso        (Atmosphere.C:596-597)   */
@@ -465,14 +467,25 @@ struct CplPar {
     int64_t sint_row;      /* packed row of the ocean's integral condition, or -1   */
 };
 
-/* SST of the ocean state: T at (i, j, l-1) (Ocean::interfaceT -> Atmosphere::synchronize) */
+/* SST of the ocean state: T at (i, j, l-1) (Ocean::interfaceT -> Atmosphere::synchronize),
+ * the subdomain's owned surface cells into the n*m surface (the other entries untouched:
+ * on several ranks zeroed before and summed after) */
 __global__ void k_sst(CplPar K, const double* __restrict__ xo_ext, double* __restrict__ sst)
 {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= K.n * K.m) return;
-    const int i = q % K.n, j = q / K.n;
-    const int64_t cell = ((int64_t)(j + HALO) * K.l + (K.l - 1)) * K.n + i;
-    sst[q] = xo_ext[NUN * cell + TT];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= K.nx * K.mb) return;
+    const int il = e % K.nx, jl = e / K.nx;
+    const int64_t cell = ((int64_t)(jl + HALO) * K.l + (K.l - 1)) * K.nx + il;
+    sst[(int64_t)(K.jb0 + jl) * K.n + K.ib0 + il] = xo_ext[NUN * cell + TT];
+}
+/* surface T of a packed ocean vector (owned rows) into the n*m surface, owned cells */
+__global__ void k_surf_t(CplPar K, const double* __restrict__ xo_packed, double* __restrict__ out)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= K.nx * K.mb) return;
+    const int il = e % K.nx, jl = e / K.nx;
+    const int64_t lc = ((int64_t)jl * K.l + (K.l - 1)) * K.nx + il;
+    out[(int64_t)(K.jb0 + jl) * K.n + K.ib0 + il] = xo_packed[NUN * lc + TT];
 }
 /* Atmosphere::interfaceT/Q/A/P (449-493, getP 1160-1225): the surface fields the ocean
  * needs; P dimensional, Pdist (Eo0 + eta qdim P) over water */
@@ -492,11 +505,12 @@ __global__ void k_cpl_oa(CplPar K, const int* __restrict__ surf, const double* _
                          const double* __restrict__ pdist, int rowP, const double* __restrict__ xa,
                          double* __restrict__ yo_packed)
 {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= K.n * K.m) return;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= K.nx * K.mb) return;
+    const int il = e % K.nx, jl = e / K.nx, j = K.jb0 + jl;
+    const int q = j * K.n + K.ib0 + il;
     if (surf[q]) return;
-    const int i = q % K.n, j = q / K.n;
-    const int64_t lc = ((int64_t)j * K.l + (K.l - 1)) * K.n + i;   /* owned-local cell */
+    const int64_t lc = ((int64_t)jl * K.l + (K.l - 1)) * K.nx + il;   /* owned-local cell */
     const double S = suno[j + 1];
     const double dTFT = K.Ooa * (1.0 - 0.0);
     const double dAFT = K.aft * S * (1.0 - 0.0);
@@ -517,29 +531,35 @@ __global__ void k_cpl_oa(CplPar K, const int* __restrict__ surf, const double* _
         yo_packed[NUN * lc + SS] += z;
     }
 }
+/* surface T of cell q: from the gathered n*m surface (several ranks) or straight from the
+ * packed ocean vector (one rank) */
+__device__ __forceinline__ double surf_t(const CplPar& K, const double* __restrict__ tsurf,
+                                         const double* __restrict__ xo_packed, int q)
+{
+    if (tsurf) return tsurf[q];
+    const int i = q % K.n, j = q / K.n;
+    return xo_packed[NUN * (((int64_t)j * K.l + (K.l - 1)) * K.n + i) + TT];
+}
 /* y_a += C_ao x_o on the T and q rows (Atmosphere::getBlock(ocean)) */
-__global__ void k_cpl_ao(CplPar K, AtmGeo G, const double* __restrict__ xo_packed, double* __restrict__ ya)
+__global__ void k_cpl_ao(CplPar K, AtmGeo G, const double* __restrict__ tsurf, const double* __restrict__ xo_packed,
+                         double* __restrict__ ya)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= K.n * K.m) return;
     if (G.surf[q]) return;
-    const int i = q % K.n, j = q / K.n;
-    const int64_t lc = ((int64_t)j * K.l + (K.l - 1)) * K.n + i;
-    const double t = xo_packed[NUN * lc + TT];
+    const double t = surf_t(K, tsurf, xo_packed, q);
     if (ANUN * q + AT != G.rowint) ya[ANUN * q + AT] += (1.0 - 0.0) * t;
     if (ANUN * q + AQ != G.rowint) ya[ANUN * q + AQ] += K.dTFQ * t;
 }
 /* partials of sum_q intc_q T_o(q) (the precipitation row's SST dependence) */
 __global__ void __launch_bounds__(256) k_cpl_pdot(CplPar K, const double* __restrict__ pint,
+                                                  const double* __restrict__ tsurf,
                                                   const double* __restrict__ xo_packed, double* __restrict__ part)
 {
     __shared__ double sm[256];
     double s = 0.0;
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < K.n * K.m; q += gridDim.x * blockDim.x) {
-        const int i = q % K.n, j = q / K.n;
-        const int64_t lc = ((int64_t)j * K.l + (K.l - 1)) * K.n + i;
-        s += pint[q] * xo_packed[NUN * lc + TT];
-    }
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < K.n * K.m; q += gridDim.x * blockDim.x)
+        s += pint[q] * surf_t(K, tsurf, xo_packed, q);
     sm[threadIdx.x] = s;
     __syncthreads();
     for (int k = 128; k > 0; k >>= 1) {
@@ -662,10 +682,6 @@ unsigned blocks_for(int64_t N) { return (unsigned)std::max<int64_t>(1, std::min<
 
 int coupled_check(iemic_ctx* c)
 {
-    if (c->nranks != 1) {
-        set_error("coupled model: one process only (the coupled grid is 4 degrees)");
-        return IEMIC_EINVAL;
-    }
     if (!c->cfg.coupled_t && !c->cfg.coupled_s) {
         set_error("coupled model: the ocean context needs coupled_t = 1 (or coupled_s = 1)");
         return IEMIC_EINVAL;
@@ -1084,6 +1100,7 @@ CplPar cpl_par(const iemic_coupled* cm)
     const host::Setup& su = oc->su;
     CplPar K{};
     K.n = oc->n; K.m = oc->m; K.l = oc->l;
+    K.ib0 = oc->ib0; K.jb0 = oc->jb0; K.nx = oc->nx; K.mb = oc->jb1 - oc->jb0;
     K.own0 = oc->own0;
     const AtmPar& P = a->P;
     K.dTFQ = P.nuq * P.tdim / P.qdim * P.dqso * (1.0 - 0.0);
@@ -1117,9 +1134,32 @@ int cpl_sync(iemic_coupled* cm)
     oc->su.set_atmos(pars);
     int rc = compute_forcing(oc);
     if (rc) return rc;
+    /* the atmosphere (replicated on every rank) sees the whole surface: each rank writes its
+     * owned cells, the sum over the ranks fills the rest */
+    if (oc->nranks > 1) HIP_OK(hipMemsetAsync(a->d_sst.p, 0, sizeof(double) * nm, s));
     hipLaunchKernelGGL(k_sst, dim3((nm + 255) / 256), dim3(256), 0, s, cpl_par(cm), (const double*)oc->d_x.p,
                        a->d_sst.p);
     HIP_OK(hipGetLastError());
+    if (oc->nranks > 1 && (rc = allreduce_sum(oc, a->d_sst.p, nm))) return rc;
+    return 0;
+}
+
+/* the surface T of a packed ocean vector for the atmosphere rows: null on one rank (the
+ * coupling kernels read the vector), else the n*m surface summed over the ranks */
+int cpl_surf(iemic_coupled* cm, const double* xo_packed, const double** tsurf)
+{
+    iemic_ctx* oc = cm->oc;
+    *tsurf = nullptr;
+    if (oc->nranks <= 1) return 0;
+    const int nm = oc->n * oc->m;
+    hipStream_t s = oc->stream;
+    double* t = cm->tsurf.p;
+    HIP_OK(hipMemsetAsync(t, 0, sizeof(double) * nm, s));
+    hipLaunchKernelGGL(k_surf_t, dim3((nm + 255) / 256), dim3(256), 0, s, cpl_par(cm), xo_packed, t);
+    HIP_OK(hipGetLastError());
+    int rc = allreduce_sum(oc, t, nm);
+    if (rc) return rc;
+    *tsurf = t;
     return 0;
 }
 
@@ -1140,8 +1180,10 @@ int cpl_apply(iemic_coupled* cm, const double* x, double* y)
     hipLaunchKernelGGL(k_cpl_oa, dim3((nm + 255) / 256), dim3(256), 0, s, K, (const int*)a->d_surf.p,
                        (const double*)(oc->d_tab.p + 9 * (oc->m + 2) + 2 * (oc->l + 2)), (const double*)a->d_pdist.p,
                        a->rowP, x + NL, y);
-    hipLaunchKernelGGL(k_cpl_ao, dim3((nm + 255) / 256), dim3(256), 0, s, K, atm_geo(a), x, y + NL);
-    hipLaunchKernelGGL(k_cpl_pdot, dim3(AR_BLOCKS), dim3(256), 0, s, K, (const double*)a->d_pint.p, x,
+    const double* ts = nullptr;
+    if ((rc = cpl_surf(cm, x, &ts))) return rc;
+    hipLaunchKernelGGL(k_cpl_ao, dim3((nm + 255) / 256), dim3(256), 0, s, K, atm_geo(a), ts, x, y + NL);
+    hipLaunchKernelGGL(k_cpl_pdot, dim3(AR_BLOCKS), dim3(256), 0, s, K, (const double*)a->d_pint.p, ts, x,
                        a->d_red.p + 3 * AR_BLOCKS);
     hipLaunchKernelGGL(k_cpl_pfin, dim3(1), dim3(64), 0, s, K, atm_geo(a), (const double*)a->d_red.p + 3 * AR_BLOCKS,
                        y + NL, 1.0);
@@ -1170,9 +1212,11 @@ int cpl_prec(iemic_coupled* cm, const double* r, double* z, int use_prec)
     double* b = cm->tmpa.p;
     HIP_OK(hipMemsetAsync(b, 0, sizeof(double) * NA, s));
     const CplPar K = cpl_par(cm);
-    hipLaunchKernelGGL(k_cpl_ao, dim3((nm + 255) / 256), dim3(256), 0, s, K, atm_geo(a), (const double*)z, b);
-    hipLaunchKernelGGL(k_cpl_pdot, dim3(AR_BLOCKS), dim3(256), 0, s, K, (const double*)a->d_pint.p, (const double*)z,
-                       a->d_red.p + 3 * AR_BLOCKS);
+    const double* ts = nullptr;
+    if ((rc = cpl_surf(cm, z, &ts))) return rc;
+    hipLaunchKernelGGL(k_cpl_ao, dim3((nm + 255) / 256), dim3(256), 0, s, K, atm_geo(a), ts, (const double*)z, b);
+    hipLaunchKernelGGL(k_cpl_pdot, dim3(AR_BLOCKS), dim3(256), 0, s, K, (const double*)a->d_pint.p, ts,
+                       (const double*)z, a->d_red.p + 3 * AR_BLOCKS);
     hipLaunchKernelGGL(k_cpl_pfin, dim3(1), dim3(64), 0, s, K, atm_geo(a), (const double*)a->d_red.p + 3 * AR_BLOCKS,
                        b, 1.0);
     hipLaunchKernelGGL(k_axpby_c, dim3(blocks_for(NA)), dim3(256), 0, s, 1.0, r + NL, -1.0, (const double*)b, b, NA);
@@ -1201,6 +1245,7 @@ extern "C" int iemic_coupled_create(iemic_coupled** out, iemic_ctx* oc, iemic_at
     rc |= cm->ro.alloc(NE);
     rc |= cm->zo.alloc(NE);
     rc |= cm->tmpa.alloc(cm->NA);
+    rc |= cm->tsurf.alloc((size_t)oc->n * oc->m);
     rc |= cm->w.alloc(cm->NC);
     rc |= cm->r.alloc(cm->NC);
     rc |= cm->part.alloc((size_t)KB * (MAX_KRYLOV + 2));
@@ -1292,11 +1337,18 @@ extern "C" int iemic_coupled_spmv(iemic_coupled* cm, const double* x, double* y)
 }
 
 namespace {
+/* dots of packed vectors: the ocean's owned rows on every rank, the (replicated) atmosphere
+ * on rank 0 only, summed over the ranks -- the same values on every rank */
 double cdot_host(iemic_coupled* cm, const double* V, int64_t ld, int nv, const double* w, double* out)
 {
     hipStream_t s = cm->oc->stream;
-    hipLaunchKernelGGL(k_cdots, dim3(KB, nv + 1), dim3(256), 0, s, V, ld, nv, w, cm->NC, cm->part.p);
+    const int64_t N = cm->oc->rank == 0 ? cm->NC : cm->NL;
+    hipLaunchKernelGGL(k_cdots, dim3(KB, nv + 1), dim3(256), 0, s, V, ld, nv, w, N, cm->part.p);
     hipLaunchKernelGGL(k_cfinal, dim3(nv + 1), dim3(256), 0, s, (const double*)cm->part.p, nv + 1, cm->hb.p);
+    if (cm->oc->nranks > 1 && allreduce_sum(cm->oc, cm->hb.p, nv + 1)) {
+        for (int i = 0; i <= nv; i++) out[i] = std::nan("");
+        return out[nv];
+    }
     (void)hipMemcpyAsync(cm->h_red, cm->hb.p, sizeof(double) * (nv + 1), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     for (int i = 0; i <= nv; i++) out[i] = cm->h_red[i];

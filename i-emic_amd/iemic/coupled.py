@@ -336,9 +336,22 @@ class CoupledModel:
             raise _lib.IemicError(
                 f"coupled Newton step: {method} did not converge ({self.last_solve.iters} steps, "
                 f"relative residual {self.last_solve.explicit_rel_res:.3e}); the update was applied")
-        return dict(norm_f0=float(np.linalg.norm(F0)), norm_f1=float(np.linalg.norm(F1)),
+        return dict(norm_f0=self._norm(F0), norm_f1=self._norm(F1),
                     iters=int(self.last_solve.iters), converged=bool(self.last_solve.converged),
                     explicit_rel_res=float(self.last_solve.explicit_rel_res))
+
+    def _norm(self, v: np.ndarray) -> float:
+        """2-norm of a coupled vector [ocean (global, owned rows filled) | atmosphere]: on
+        several ranks the ocean's owned rows summed over the ranks, the (replicated)
+        atmosphere once."""
+        oc = self.ocean
+        if oc.layout()["nranks"] == 1:
+            return float(np.linalg.norm(v))
+        rows = oc.owned_rows()
+        s = np.array([float(np.dot(v[rows], v[rows]))])
+        check(lib().iemic_allreduce_sum(oc._h, ptr(s), 1), "iemic_allreduce_sum")
+        va = v[oc.N:]
+        return float(np.sqrt(s[0] + np.dot(va, va)))
 
     def solve(self, b: np.ndarray) -> np.ndarray:
         sp = self.solver_params

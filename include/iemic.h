@@ -217,7 +217,11 @@ typedef struct {
 int  iemic_atmos_default_params(iemic_atmos_params* p);
 /* the atmosphere on the ocean context's grid, device and stream; its surface mask is the
  * ocean's top layer (AtmosLocal::setSurfaceMask 1722-1756), Ooa/Os from getdeps.  The
- * ocean context must have coupled_t = 1 and one rank. */
+ * ocean context must have coupled_t = 1 (or coupled_s = 1).  On several ranks (Decomp2D
+ * subdomains, CoupledModel.C:274-343) the atmosphere is replicated on every rank: its
+ * host vectors are whole, the SST and the coupling rows' surface T are summed over the
+ * ranks, and the coupled solver's dots count it once; ocean vectors are global
+ * reference-ordered vectors of which each rank reads / writes its owned rows. */
 int  iemic_atmos_create(iemic_atmos** a, iemic_ctx* ocean, const iemic_atmos_params* p);
 void iemic_atmos_destroy(iemic_atmos* a);                       /* refcounted like the ocean */
 int  iemic_atmos_dim(const iemic_atmos* a);                    /* 3 n m + 1               */

@@ -278,3 +278,89 @@ def test_gpu_atmosphere_state_file(coupled4, tmp_path):
     np.testing.assert_array_equal(atm.getState(), g["xa"])
     assert atm.getPar("Humidity Forcing") == 0.75
     atm.setPar("Humidity Forcing", 1.0)
+
+
+@pytest.mark.parametrize("nranks,npx", [(2, 1), (4, 2)])
+def test_gpu_coupled_subdomains(oracle_lib, nranks, npx):
+    """The coupled model over Decomp2D subdomains (CoupledModel.C:274-343 distributes it on
+    the ocean's maps): in-process ranks on one GPU, the atmosphere replicated on every rank
+    (the SST and the coupling rows' surface T summed over the ranks, the packed dots counting
+    the atmosphere once).  The ocean Jacobian rows are bit-identical to one rank's, J v
+    matches to 1e-13 of |J||v|, and a coupled Newton step solves the assembled one-rank
+    system to 1e-8 with the same initial residual."""
+    import threading
+    from iemic import _lib
+    from iemic.coupled import Atmosphere, CoupledModel
+    from iemic.ocean import Ocean
+    name = "coupled4"
+    c = cf.preset(name)
+    g = golden(name)
+    L = landm_of(name)
+    t, q, a, pars = atm_args(g)
+    x = cf.synthetic_state(c, cf.landmask(c), amp_ts=1e-3)
+    xa = g["xa"]
+    sp_ = {"FGMRES iterations": 150, "FGMRES restarts": 6}
+    prm = {**ao.COUPLED_RUN_PARAMS, "Combined Forcing": c.start_params["Combined Forcing"]}
+
+    def model(**kw):
+        oc = Ocean(c, landm=L, analyze_jacobian=False, **kw)
+        oc.setAtmosphere(t, q, a, g["atm_p"], pars)
+        atm = Atmosphere(oc, prm)
+        return oc, atm, CoupledModel(oc, atm, sp_)
+
+    oc1, atm1, cm1 = model()
+    oc1.setState(x)
+    atm1.setState(xa)
+    cm1.computeJacobian()
+    rp1, col1, val1 = oc1.exportCSR()
+    v = np.random.default_rng(7).standard_normal(cm1.N)
+    y1 = cm1.applyMatrix(v)
+    A = assembled(cm1, c, g, L, oc1)
+    group = _lib.lib().iemic_local_group_new(nranks)
+    out = [None] * nranks
+
+    def work(r):
+        try:
+            oc, atm, cm = model(local_group=group, rank=r, nranks=nranks, npx=npx)
+            oc.setState(x)
+            atm.setState(xa)
+            cm.computeJacobian()
+            csr = oc.exportCSR()
+            y = cm.applyMatrix(v)
+            rec = cm.newtonStep()
+            out[r] = dict(rows=oc.owned_rows(), csr=csr, y=y, rec=rec, x1=oc.getState(),
+                          xa1=atm.getState(), lay=oc.layout())
+            cm.close(); atm.close(); oc.close()
+        except Exception as e:  # noqa: BLE001
+            out[r] = repr(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    for h in th:
+        h.start()
+    for h in th:
+        h.join()
+    _lib.lib().iemic_local_group_free(group)
+    assert all(isinstance(o, dict) for o in out), out
+    x1 = np.zeros(cm1.N)
+    scale = abs(A) @ np.abs(v)
+    for o in out:
+        rows = o["rows"]
+        rp, col, val = o["csr"]
+        for k, qr in enumerate(rows):
+            np.testing.assert_array_equal(col[rp[k]:rp[k + 1]], col1[rp1[qr]:rp1[qr + 1]])
+            np.testing.assert_array_equal(bits(val[rp[k]:rp[k + 1]]), bits(val1[rp1[qr]:rp1[qr + 1]]))
+        sel = np.concatenate([rows, np.arange(c.nrows, cm1.N)])
+        assert np.max(np.abs(o["y"][sel] - y1[sel]) / np.maximum(scale[sel], 1e-300)) <= 1e-13
+        x1[rows] = o["x1"][rows]
+        np.testing.assert_array_equal(o["xa1"], out[0]["xa1"])     # the replicas agree
+        assert o["rec"]["converged"]
+        assert o["rec"]["norm_f0"] == out[0]["rec"]["norm_f0"]
+    x1[c.nrows:] = out[0]["xa1"]
+    oc1.setState(x)
+    atm1.setState(xa)
+    F = cm1.computeRHS()
+    f0 = np.linalg.norm(F)
+    assert abs(out[0]["rec"]["norm_f0"] - f0) <= 1e-12 * f0
+    dx = x1 - np.concatenate([x, xa])
+    lin = np.linalg.norm(A @ dx + F) / f0
+    assert lin <= 1e-7, lin
