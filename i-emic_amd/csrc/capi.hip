@@ -884,6 +884,18 @@ extern "C" int iemic_time_prec(iemic_ctx* c, int nrep, double* ms_per_apply, dou
     return 0;
 }
 
+namespace iemic {
+int gs_time_parts(iemic_ctx* c, int nrep, double* us);
+}
+/* GPU microseconds of the block GS apply's parts (gs_time_parts): Schur solve, T/S block
+ * solve, one dynamics pass, one dynamics defect */
+extern "C" int iemic_time_prec_parts(iemic_ctx* c, int nrep, double* us4)
+{
+    CTX_CHECK(c);
+    if (!us4) return IEMIC_EINVAL;
+    return gs_time_parts(c, nrep, us4);
+}
+
 /* streaming read of a scratch buffer (evicts the Infinity Cache without leaving dirty
  * lines behind, which a memset would); the store never happens for finite data */
 __global__ void k_flush_read(const double2* __restrict__ a, int64_t n2, double* __restrict__ sink)

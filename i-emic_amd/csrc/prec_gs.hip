@@ -3170,6 +3170,50 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d);
 
+/* GPU time of the apply's parts (HIP events on the library stream, nrep back-to-back
+ * launches each, zero data): us[0] one Schur solve (cyclic reduction), us[1] one T/S block
+ * solve (right-hand side + V-cycle), us[2] one dynamics pass (column kernels + Schur solve),
+ * us[3] one dynamics defect.  Diagnostics for DESIGN.md's per-part table (one rank). */
+int gs_time_parts(iemic_ctx* c, int nrep, double* us)
+{
+    BlockGS& gs = c->gs;
+    if (!gs.ready || gs.kind != 2 || nrep < 1) {
+        set_error("gs_time_parts: the block GS preconditioner is not computed");
+        return IEMIC_ESTATE;
+    }
+    hipStream_t s = c->stream;
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    double* z = c->d_tmp2.p;
+    HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, s));
+    HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
+    HIP_OK(hipMemsetAsync(gs.rr.p, 0, sizeof(double) * c->nerows, s));
+    HIP_OK(hipMemsetAsync(gs.colv_own.p, 0, sizeof(double) * c->n * c->m, s));
+    int rc = 0;
+    for (int part = 0; part < 4 && !rc; part++) {
+        auto once = [&]() -> int {
+            switch (part) {
+            case 0: return cr_solve(c, gs.cr, gs.colv_own.p, gs.colv2.p, s);
+            case 1: return ts_solve(c, z, true);
+            case 2: return dyn_solve(c, gs.rr.p, z);
+            default: return spmv_dyn_defect(c, z, c->d_tmp1.p, gs.known.p, gs.dres.p ? gs.dres.p : c->d_tmp1.p);
+            }
+        };
+        if ((rc = once())) break;                  /* warm */
+        HIP_OK(hipEventRecord(e0, s));
+        for (int q = 0; q < nrep && !rc; q++) rc = once();
+        HIP_OK(hipEventRecord(e1, s));
+        HIP_OK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+        us[part] = 1e3 * ms / nrep;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
 int gs_apply(iemic_ctx* c, const double* r, double* z)
 {
     BlockGS& gs = c->gs;

@@ -147,6 +147,7 @@ def lib():
         "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
         "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
         "iemic_time_prec": (C.c_int, [vp, C.c_int, PD, PD]),
+        "iemic_time_prec_parts": (C.c_int, [vp, C.c_int, PD]),
         "iemic_time_spmv_cold": (C.c_int, [vp, C.c_int, vp, C.c_int64, PD]),
         "iemic_set_intcond_correction": (C.c_int, [vp, PD]),
         "iemic_get_intcond_correction": (C.c_int, [vp, PD]),
@@ -207,6 +208,7 @@ EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
             "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold", "iemic_time_prec",
+            "iemic_time_prec_parts",
             "iemic_ilu_create", "iemic_ilu_compute", "iemic_ilu_apply", "iemic_ilu_apply_dev",
             "iemic_ilu_stats", "iemic_ilu_destroy",
             "iemic_set_atmosphere", "iemic_get_deps", "iemic_get_suno",

@@ -421,6 +421,13 @@ class Ocean:
         check(lib().iemic_time_prec(self._h, int(nrep), C.byref(ms), C.byref(hms)), "iemic_time_prec")
         return ms.value, hms.value
 
+    def time_prec_parts(self, nrep: int = 50) -> dict:
+        """GPU microseconds of the block GS apply's parts (iemic_time_prec_parts)."""
+        self.buildPreconditioner()
+        us = np.zeros(4)
+        check(lib().iemic_time_prec_parts(self._h, int(nrep), ptr(us)), "iemic_time_prec_parts")
+        return dict(schur_solve_us=us[0], ts_solve_us=us[1], dyn_pass_us=us[2], dyn_defect_us=us[3])
+
     def time_spmv_cold(self, flush_ptr: int, flush_bytes: int, nrep: int = 10) -> float:
         """Mean SpMV kernel ms with the Infinity Cache flushed (device memset of a caller
         buffer) before each launch -- the in-solve, cold-cache rate."""

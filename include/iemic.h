@@ -321,6 +321,10 @@ int iemic_time_spmv(iemic_ctx* ctx, int nrep, double* ms_per_launch);
  * (iemic_prec_compute first) on the device, GPU ms per apply (events) and host ms per apply
  * spent enqueueing */
 int iemic_time_prec(iemic_ctx* ctx, int nrep, double* ms_per_apply, double* host_ms_per_apply);
+/* GPU microseconds per launch group of the block GS apply's parts, nrep each on zero data:
+ * us4 = one Schur solve, one T/S block solve (right-hand side + V-cycle), one dynamics pass
+ * (column kernels + Schur solve), one dynamics defect (diagnostics; block GS computed) */
+int iemic_time_prec_parts(iemic_ctx* ctx, int nrep, double* us4);
 /* Same, with the Infinity Cache flushed before every launch (a streaming read of
  * flush_bytes of flush_dev on the library stream, outside the timed span): the cold rate. */
 int iemic_time_spmv_cold(iemic_ctx* ctx, int nrep, void* flush_dev, int64_t flush_bytes,

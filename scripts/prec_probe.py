@@ -35,8 +35,9 @@ def main():
         oc.setState(x)
         oc.computeJacobian()
         ms, hms = oc.time_prec(50)
+        parts = {k: round(u, 2) for k, u in oc.time_prec_parts(50).items()}
         print(json.dumps({"config": name, "variant": v, "gpu_us": round(ms * 1e3, 1),
-                          "host_us": round(hms * 1e3, 1)}), flush=True)
+                          "host_us": round(hms * 1e3, 1), **parts}), flush=True)
         del oc
 
 
