@@ -54,4 +54,9 @@ def test_two_ranks_host_transport_match_one():
     assert two["comm"]["per_fgmres_step"]["batches"] > 0
     f0, f1 = one["newton"]["norm_f0"], one["newton"]["norm_f1"]
     assert abs(two["newton"]["norm_f0"] - f0) <= 1e-12 * f0
-    assert abs(two["newton"]["norm_f1"] - f1) <= 1e-8 * f0
+    # both solves reach the tolerance; the decompositions' preconditioners differ, so the
+    # updates agree to the solve tolerance, amplified by the (diverging, far from a
+    # solution) step's nonlinearity in ||F1||
+    assert one["newton"]["converged"] and two["newton"]["converged"]
+    assert two["newton"]["explicit_rel_res"] <= 2e-8
+    assert abs(two["newton"]["norm_f1"] - f1) <= 1e-6 * f1 + 1e-8 * f0
