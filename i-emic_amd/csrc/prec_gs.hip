@@ -1439,8 +1439,9 @@ __device__ __forceinline__ double bts_row(const double* __restrict__ val, const 
         const Slot sl = SLOTS[B + s];
         if (sl.var == TT || sl.var == SS) continue;
         /* identity-row columns (coupling already in rr) weigh 0: no branch, so the loads of
-         * all the row's slots issue together */
-        const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : val[(int64_t)(B + s) * nloc + lc];
+         * all the row's slots issue together; the coefficients stream (non-temporal), the
+         * gathered z stays in L2 */
+        const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : __builtin_nontemporal_load(val + (int64_t)(B + s) * nloc + lc);
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
         acc -= v * z[NUN * (int64_t)cidx + sl.var];
     }
