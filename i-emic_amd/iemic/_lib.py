@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libiemic_amd.so")
+# IEMIC_LIB names another build of the library under lib/ (kernel A/B measurements of
+# scripts/ab_probe.py run every variant on the same box); the default is the in-tree build
+LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("IEMIC_LIB", "libiemic_amd.so"))
 
 IEMIC_ENODEV = -19
 IEMIC_ENOCONV = 1           # iemic_newton_step: applied, but the solve missed its tolerance
@@ -188,6 +190,8 @@ def lib():
         "iemic_coupled_solve": (C.c_int, [vp, PD, PD, P(Krylov), P(SolveInfo)]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("IEMIC_LIB") and not hasattr(L, name):
+            continue                  # an older build under A/B measurement lacks newer entry points
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
