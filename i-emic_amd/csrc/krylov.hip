@@ -135,8 +135,8 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
  * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
  * rows' partials meet in LDS. */
 /* on[q]: row sp7_row(S0) + q of the cell is active; an identity row's coefficients are
- * neither loaded nor used (about half the cells are land at 2 degrees).  The coefficients are
- * streamed with non-temporal loads, so the z rows the neighbouring tiles gather stay in L2. */
+ * neither loaded nor used (about half the cells are land at 2 degrees).  (Non-temporal
+ * coefficient loads measured 35.6 against 26.1 us per defect, scripts/ab_probe.py.) */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
                                             int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
@@ -148,7 +148,7 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
         const int q = sp7_row(s) - sp7_row(S0);
         if (!on[q]) continue;
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc[q] += __builtin_nontemporal_load(val + (int64_t)s * nloc + lc) * z[NUN * (int64_t)cidx + sl.var];
+        acc[q] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
     }
 }
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,

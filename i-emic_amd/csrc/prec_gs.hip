@@ -722,9 +722,10 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
  * with the column fastest, so every per-cell load of a wave runs along i in 128-byte runs
  * (the slot-major Jacobian rows contiguously, the interleaved vectors at one cell stride);
  * the column recurrences meet in LDS, where each thread composes the affine maps of the
- * levels it depends on (at most l steps of LDS reads).  16-column tiles give the 2-degree
- * grid 928 workgroups of 256 threads (64-column tiles: 232 of 1024, fewer than the CUs). */
-constexpr int COL_TI = 16;
+ * levels it depends on (at most l steps of LDS reads).  64-column tiles (232 workgroups of
+ * 1024 threads at 2 degrees): 16-column tiles (928 of 256) measured 2 ms slower per Newton
+ * step (scripts/ab_probe.py). */
+constexpr int COL_TI = 64;
 /* logical workgroup of block b for nwg workgroups launched as xcd_grid(nwg) blocks: the
  * XCDs (blocks dealt round robin, b % 8) get contiguous runs of workgroups, so tiles of
  * neighbouring latitude rows, which read each other's rows, share an L2; -1: idle block */
@@ -1439,9 +1440,9 @@ __device__ __forceinline__ double bts_row(const double* __restrict__ val, const 
         const Slot sl = SLOTS[B + s];
         if (sl.var == TT || sl.var == SS) continue;
         /* identity-row columns (coupling already in rr) weigh 0: no branch, so the loads of
-         * all the row's slots issue together; the coefficients stream (non-temporal), the
-         * gathered z stays in L2 */
-        const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : __builtin_nontemporal_load(val + (int64_t)(B + s) * nloc + lc);
+         * all the row's slots issue together (default load policy: non-temporal loads made
+         * the T/S solve 6.5 us slower, scripts/ab_probe.py) */
+        const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : val[(int64_t)(B + s) * nloc + lc];
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
         acc -= v * z[NUN * (int64_t)cidx + sl.var];
     }
