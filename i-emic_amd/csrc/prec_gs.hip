@@ -2001,9 +2001,10 @@ __global__ void k_mg_galerkin(TsLev F, TsLev C, double* __restrict__ off, double
     const bool at = d[0] != 0.0, as = d[3] != 0.0;
     if (!at) { d[1] = d[2] = 0.0; for (int q = 0; q < 8; q++) o[q] = 0.0; }
     if (!as) { d[1] = d[2] = 0.0; for (int q = 8; q < 16; q++) o[q] = 0.0; }
-    const int64_t cs = C.cstr;
-    for (int e = 0; e < 16; e++) off[(int64_t)e * cs + t] = o[e];
-    for (int e = 0; e < 4; e++) diag[(int64_t)e * cs + t] = d[e];
+    /* the level's layout (a level with an x halo pads its rows) */
+    const int64_t cs = C.cstr, cc = mg_cell(C, I, J, k);
+    for (int e = 0; e < 16; e++) off[(int64_t)e * cs + cc] = o[e];
+    for (int e = 0; e < 4; e++) diag[(int64_t)e * cs + cc] = d[e];
 }
 
 /* z-line factors of every owned column (one thread each, serial block Thomas along k, the

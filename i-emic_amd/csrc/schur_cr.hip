@@ -287,15 +287,19 @@ __device__ __forceinline__ void crf_finish(const CrFrag& f, const double* v0, co
     }
 }
 
+/* Set-up (batched right-hand sides: the tail's inverse is built by solving for the
+ * identity): each workgroup keeps its row chunk of the level operators in registers and runs
+ * CR_RB right-hand sides (blockIdx.y groups), so the blocks are read once per CR_RB columns
+ * instead of once per column. */
+constexpr int CR_RB = 8;
+
 /* level down, one row chunk of one even block per workgroup (blockIdx.x = q * nch + chunk):
  * b'_q = b_e - XL_q b_{e-1} - XR_q b_{e+1} (odd neighbours only), e = 2q */
 __global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, double* __restrict__ bn,
                                                 const double* __restrict__ XL, const double* __restrict__ XR,
-                                                int N, int per, int m, int nch, int64_t sl, int64_t sn)
+                                                int N, int per, int m, int nch, int64_t sl, int64_t sn, int nrhs)
 {
     __shared__ double vl[CR_MAXM], vr[CR_MAXM], red[256];
-    bl += blockIdx.y * sl;                               /* batched right-hand sides (set-up) */
-    bn += blockIdx.y * sn;
     const int q = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, e = 2 * q;
     const bool lex = e > 0 || per, rex = e + 1 < N || per;
     const int lnb = e > 0 ? e - 1 : N - 1, rnb = (e + 1) % N;
@@ -303,12 +307,16 @@ __global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, d
     const size_t mm = (size_t)m * m;
     CrFrag f;
     crf_load(f, lo ? XL + q * mm : nullptr, ro ? XR + q * mm : nullptr, nullptr, m, r0);
-    for (int c = threadIdx.x; c < m; c += 256) {
-        vl[c] = lo ? bl[(size_t)lnb * m + c] : 0.0;
-        vr[c] = ro ? bl[(size_t)rnb * m + c] : 0.0;
+    const int r1 = min(nrhs, (int)(blockIdx.y + 1) * CR_RB);
+    for (int rh = blockIdx.y * CR_RB; rh < r1; rh++) {
+        const double* b = bl + rh * sl;
+        for (int c = threadIdx.x; c < m; c += 256) {
+            vl[c] = lo ? b[(size_t)lnb * m + c] : 0.0;
+            vr[c] = ro ? b[(size_t)rnb * m + c] : 0.0;
+        }
+        __syncthreads();
+        crf_finish(f, vl, vr, vl, -1.0, b + (size_t)e * m, bn + rh * sn + (size_t)q * m, m, r0, red);
     }
-    __syncthreads();
-    crf_finish(f, vl, vr, vl, -1.0, bl + (size_t)e * m, bn + (size_t)q * m, m, r0, red);
 }
 
 /* level up, one row chunk of one odd block per workgroup (blockIdx.x = p * nch + chunk):
@@ -317,44 +325,48 @@ __global__ void __launch_bounds__(256) k_cr_fwd(const double* __restrict__ bl, d
 __global__ void __launch_bounds__(256) k_cr_bwd(const double* __restrict__ bl, const double* __restrict__ xn,
                                                 double* __restrict__ xl, const double* __restrict__ Dinv,
                                                 const double* __restrict__ YL, const double* __restrict__ YR,
-                                                int N, int per, int m, int nch, int64_t sl, int64_t sn)
+                                                int N, int per, int m, int nch, int64_t sl, int64_t sn, int nrhs)
 {
     __shared__ double vb[CR_MAXM], vl[CR_MAXM], vr[CR_MAXM], red[256];
-    bl += blockIdx.y * sl;
-    xl += blockIdx.y * sl;
-    xn += blockIdx.y * sn;
     const int p = blockIdx.x / nch, r0 = (blockIdx.x % nch) * CR_RC, b = 2 * p + 1;
     const bool rex = b + 1 < N || per;
     const int rn = (b + 1) % N;
     const size_t mm = (size_t)m * m;
     CrFrag f;
     crf_load(f, Dinv + p * mm, YL + p * mm, rex ? YR + p * mm : nullptr, m, r0);
-    for (int c = threadIdx.x; c < m; c += 256) {
-        vb[c] = bl[(size_t)b * m + c];
-        vl[c] = -xn[(size_t)p * m + c];
-        vr[c] = rex ? -xn[(size_t)(rn / 2) * m + c] : 0.0;
+    const int r1 = min(nrhs, (int)(blockIdx.y + 1) * CR_RB);
+    for (int rh = blockIdx.y * CR_RB; rh < r1; rh++) {
+        const double* bq = bl + rh * sl;
+        const double* xq = xn + rh * sn;
+        double* xo = xl + rh * sl;
+        for (int c = threadIdx.x; c < m; c += 256) {
+            vb[c] = bq[(size_t)b * m + c];
+            vl[c] = -xq[(size_t)p * m + c];
+            vr[c] = rex ? -xq[(size_t)(rn / 2) * m + c] : 0.0;
+        }
+        if (threadIdx.x < CR_RC && r0 + threadIdx.x < m) {
+            const int r = r0 + threadIdx.x;
+            xo[(size_t)(b - 1) * m + r] = xq[(size_t)p * m + r];
+            if (b == N - 2) xo[(size_t)(N - 1) * m + r] = xq[(size_t)((N - 1) / 2) * m + r];
+        }
+        __syncthreads();
+        crf_finish(f, vb, vl, vr, 1.0, nullptr, xo + (size_t)b * m, m, r0, red);
     }
-    if (threadIdx.x < CR_RC && r0 + threadIdx.x < m) {
-        const int r = r0 + threadIdx.x;
-        xl[(size_t)(b - 1) * m + r] = xn[(size_t)p * m + r];
-        if (b == N - 2) xl[(size_t)(N - 1) * m + r] = xn[(size_t)((N - 1) / 2) * m + r];
-    }
-    __syncthreads();
-    crf_finish(f, vb, vl, vr, 1.0, nullptr, xl + (size_t)b * m, m, r0, red);
 }
 
 /* the last level: x = Dfin b, one row chunk per workgroup */
 __global__ void __launch_bounds__(256) k_cr_final(const double* __restrict__ Dfin, const double* __restrict__ b,
-                                                  double* __restrict__ x, int m)
+                                                  double* __restrict__ x, int m, int nrhs)
 {
     __shared__ double vb[CR_MAXM], red[256];
-    b += (size_t)blockIdx.y * m;
-    x += (size_t)blockIdx.y * m;
     CrFrag f;
     crf_load(f, Dfin, nullptr, nullptr, m, blockIdx.x * CR_RC);
-    for (int c = threadIdx.x; c < m; c += 256) vb[c] = b[c];
-    __syncthreads();
-    crf_finish(f, vb, vb, vb, 1.0, nullptr, x, m, blockIdx.x * CR_RC, red);
+    const int r1 = min(nrhs, (int)(blockIdx.y + 1) * CR_RB);
+    for (int rh = blockIdx.y * CR_RB; rh < r1; rh++) {
+        for (int c = threadIdx.x; c < m; c += 256) vb[c] = b[(size_t)rh * m + c];
+        __syncthreads();
+        crf_finish(f, vb, vb, vb, 1.0, nullptr, x + (size_t)rh * m, m, blockIdx.x * CR_RC, red);
+    }
 }
 
 
@@ -551,17 +563,17 @@ static void cr_down(const SchurCR& cr, int l, const double* bl, double* bn, int 
     const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC, Nl = cr.N[l], ne = (Nl + 1) / 2;
     const size_t mm = (size_t)m * m;
     const double* ap = cr.ap.p + cr.ap_off[l];
-    hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch, nrhs), dim3(256), 0, s, bl, bn, ap, ap + (size_t)ne * mm, Nl,
-                       cr.per[l], m, nch, (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m);
+    hipLaunchKernelGGL(k_cr_fwd, dim3(ne * nch, (nrhs + CR_RB - 1) / CR_RB), dim3(256), 0, s, bl, bn, ap,
+                       ap + (size_t)ne * mm, Nl, cr.per[l], m, nch, (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m, nrhs);
 }
 static void cr_up(const SchurCR& cr, int l, const double* bl, const double* xn, double* xl, int nrhs, hipStream_t s)
 {
     const int m = cr.m, nch = (m + CR_RC - 1) / CR_RC, Nl = cr.N[l], ne = (Nl + 1) / 2, no = Nl / 2;
     const size_t mm = (size_t)m * m;
     const double* ap = cr.ap.p + cr.ap_off[l];
-    hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch, nrhs), dim3(256), 0, s, bl, xn, xl, ap + (size_t)2 * ne * mm,
-                       ap + (size_t)(2 * ne + no) * mm, ap + (size_t)(2 * ne + 2 * no) * mm, Nl, cr.per[l], m, nch,
-                       (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m);
+    hipLaunchKernelGGL(k_cr_bwd, dim3(no * nch, (nrhs + CR_RB - 1) / CR_RB), dim3(256), 0, s, bl, xn, xl,
+                       ap + (size_t)2 * ne * mm, ap + (size_t)(2 * ne + no) * mm, ap + (size_t)(2 * ne + 2 * no) * mm,
+                       Nl, cr.per[l], m, nch, (int64_t)Nl * m, (int64_t)cr.N[l + 1] * m, nrhs);
 }
 
 /* ---- apply steps: the level operations as block expressions, composed two levels at a
@@ -1056,8 +1068,8 @@ int cr_factor_blocks(iemic_ctx* c, SchurCR& cr)
         auto tx = [&](int l) { return cr.tx.p + cr.tb_off[l - cr.lt]; };
         hipLaunchKernelGGL(k_cr_eye, dim3((unsigned)(((int64_t)M * M + 255) / 256)), dim3(256), 0, s, tb(cr.lt), M);
         for (int l = cr.lt; l < cr.nlev; l++) cr_down(cr, l, tb(l), tb(l + 1), M, s);
-        hipLaunchKernelGGL(k_cr_final, dim3((m + CR_RC - 1) / CR_RC, M), dim3(256), 0, s,
-                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), (const double*)tb(cr.nlev), tx(cr.nlev), m);
+        hipLaunchKernelGGL(k_cr_final, dim3((m + CR_RC - 1) / CR_RC, (M + CR_RB - 1) / CR_RB), dim3(256), 0, s,
+                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), (const double*)tb(cr.nlev), tx(cr.nlev), m, M);
         for (int l = cr.nlev - 1; l >= cr.lt; l--) cr_up(cr, l, tb(l), tx(l + 1), tx(l), M, s);
         hipLaunchKernelGGL(k_cr_transpose, dim3((M + 31) / 32, (M + 31) / 32), dim3(256), 0, s,
                            (const double*)tx(cr.lt), cr.tinv.p, M);
@@ -1113,7 +1125,7 @@ int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStr
                            xvec(le), cr.tM);
     else
         hipLaunchKernelGGL(k_cr_final, dim3((cr.m + CR_RC - 1) / CR_RC), dim3(256), 0, s,
-                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), bvec(le), xvec(le), cr.m);
+                           (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), bvec(le), xvec(le), cr.m, 1);
     for (const CrStep& st : cr.up) cr_step(cr, st, b, x, s);
     HIP_OK(hipGetLastError());
     return 0;
