@@ -2212,6 +2212,8 @@ static bool ts_compact(const iemic_ctx* c) { return (c->n & 1) == 0 && (c->nx & 
 
 
 /* ---- T/S multigrid: host side ------------------------------------------------------ */
+/* intermediate levels (1 ..) that carry the x halo under x splits */
+constexpr int MG_XHALO_LEVELS = 99;
 static TsLev mg_view(iemic_ctx* c, int q)
 {
     BlockGS& gs = c->gs;
@@ -2229,7 +2231,7 @@ static TsLev mg_view(iemic_ctx* c, int q)
     const int qc = gs.mg_nlev - 1;
     V.periodic = c->cfg.periodic && c->npx == 1;
     V.hj = (q == 0 && c->npy > 1) ? 1 : 0;
-    V.hi = (q < qc && c->npx > 1) ? 1 : 0;
+    V.hi = (q < qc && q <= MG_XHALO_LEVELS && c->npx > 1) ? 1 : 0;
     V.vis = V.hj;
     V.visi = V.hi;
     V.jpar = gs.mg_par[q];
