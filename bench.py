@@ -594,6 +594,24 @@ def main():
                   "achieved": round(dg, 1), "frac": round(dg / HBM_PEAK_GBS, 4),
                   "source": f"bench_data/pmc_{PMC_TAG}.json (PMC bytes / rocprofv3 kernel-trace average)"}
 
+    # STREAM-copy rate of this box: device-to-device copy of 1 GiB, read +
+    # write bytes / time, median of 5 -- the achievable HBM rate beside the 8 TB/s spec
+    stream = None
+    if rank == 0:
+        a = torch.empty(1 << 27, dtype=torch.float64, device=dev)
+        b = torch.empty_like(a)
+        a.fill_(1.0)
+        ts = []
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            b.copy_(a)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        stream = round(2 * a.numel() * 8 / (float(np.median(ts[1:])) * 1e-3) / 1e9, 1)
+        del a, b
+
     # the Newton residual sequence from the benchmark state (untimed)
     seq = []
     if args.newton_seq > 0:
@@ -631,6 +649,7 @@ def main():
                    "t_solve_ms": last.t_solve_ms, "t_solve_prec_ms": s.t_prec_ms,
                    "t_solve_spmv_ms": s.t_spmv_ms, "t_solve_orth_ms": s.t_orth_ms,
                    "dgks_reorth": s.reorth, "sequence": seq},
+        "hbm_copy_gbps": stream,
         "ranks_seen": ranks_seen,
         "process_grid": [lay["npx"], lay["npy"]],
         "comm": {"per_fgmres_step": {k: round(v / max(1, its_total), 2) for k, v in comm.items()},
