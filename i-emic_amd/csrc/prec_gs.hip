@@ -717,15 +717,16 @@ __global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restr
 __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
                                          const double* __restrict__ z, int i, int j, int k,
                                          int64_t pl, const Lay& L);
-/* Column kernels, transposed: one workgroup of COL_TI LP threads per tile of COL_TI
+/* Column kernels, transposed: one workgroup of 1024 threads per tile of COL_TI = 1024 / LP
  * consecutive columns of one latitude row (LP = power of two >= l), thread = (column, level)
  * with the column fastest, so every per-cell load of a wave runs along i in 128-byte runs
  * (the slot-major Jacobian rows contiguously, the interleaved vectors at one cell stride);
  * the column recurrences meet in LDS, where each thread composes the affine maps of the
- * levels it depends on (at most l steps of LDS reads).  64-column tiles (232 workgroups of
- * 1024 threads at 2 degrees): 16-column tiles (928 of 256) measured 2 ms slower per Newton
- * step (scripts/ab_probe.py). */
-constexpr int COL_TI = 64;
+ * levels it depends on (at most l steps of LDS reads).  At 2 degrees (LP = 16) 64-column
+ * tiles, 232 workgroups: 16-column tiles (928 of 256 threads) measured 2 ms slower per
+ * Newton step (scripts/ab_probe.py). */
+template <int LP>
+constexpr int col_ti() { return 1024 / LP; }
 /* logical workgroup of block b for nwg workgroups launched as xcd_grid(nwg) blocks: the
  * XCDs (blocks dealt round robin, b % 8) get contiguous runs of workgroups, so tiles of
  * neighbouring latitude rows, which read each other's rows, share an L2; -1: idle block */
@@ -737,9 +738,10 @@ __device__ __forceinline__ int xcd_block(int nwg)
 }
 static inline unsigned xcd_grid(int64_t nwg) { return 8u * (unsigned)((nwg + 7) / 8); }
 
+template <int LP>
 __device__ __forceinline__ bool col_tile(const Lay& L, int& il, int& jl, int& k, bool& on)
 {
-    constexpr int TI = COL_TI;
+    constexpr int TI = col_ti<LP>();
     const int tpr = (L.nx + TI - 1) / TI;
     const int w = xcd_block(tpr * (int)(L.nloc / ((int64_t)L.l * L.nx)));
     if (w < 0) return false;
@@ -753,18 +755,18 @@ __device__ __forceinline__ bool col_tile(const Lay& L, int& il, int& jl, int& k,
 /* 4b/5. p = ptil + pbar and the continuity rows bottom-up, w_k = A_k + B_k w_k-1 (the
  * transposed column layout of k_gs_ptil_rcol); zo += omega (p, w) in the correction passes */
 template <int LP>
-__global__ void __launch_bounds__(COL_TI * LP) k_gs_pw_t(const double* __restrict__ val,
+__global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val,
                                                   const uint8_t* __restrict__ known,
                                                   const double* __restrict__ pbar,
                                                   double* __restrict__ z, Lay L,
                                                   const double* __restrict__ rr,
                                                   double* __restrict__ zo, double omega)
 {
-    constexpr int TI = COL_TI;
+    constexpr int TI = col_ti<LP>();
     __shared__ double sA[LP][TI], sB[LP][TI];
     int il, jl, k;
     bool on;
-    if (!col_tile(L, il, jl, k, on)) return;    /* whole idle workgroups */
+    if (!col_tile<LP>(L, il, jl, k, on)) return;    /* whole idle workgroups */
     const int ii = (int)threadIdx.x % TI;
     const int i = L.ib0 + il, j = L.jb0 + jl;
     const int64_t ncell = L.nloc;
@@ -1006,7 +1008,7 @@ __global__ void k_rcol_w(const uint8_t* __restrict__ known, const double* __rest
 /* 1 + 3a. ptil (top-down: p_k = A_k + B_k p_k+1) and the column's Schur right-hand side
  * sum_e rcol_e rr_e (summed over the levels in a fixed order), written as k_gs_pcol wrote it */
 template <int LP>
-__global__ void __launch_bounds__(COL_TI * LP) k_gs_ptil_rcol(const double* __restrict__ val,
+__global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict__ val,
                                                        const uint8_t* __restrict__ known,
                                                        const double* __restrict__ rcol,
                                                        const double* __restrict__ rr,
@@ -1015,11 +1017,11 @@ __global__ void __launch_bounds__(COL_TI * LP) k_gs_ptil_rcol(const double* __re
                                                        double* __restrict__ colv_own, Lay L)
 {
     LAY_ALIASES;
-    constexpr int TI = COL_TI;
+    constexpr int TI = col_ti<LP>();
     __shared__ double sA[LP][TI], sB[LP][TI], sv[LP][TI];
     int il, jl, k;
     bool on;
-    if (!col_tile(L, il, jl, k, on)) return;    /* whole idle workgroups */
+    if (!col_tile<LP>(L, il, jl, k, on)) return;    /* whole idle workgroups */
     const int ii = (int)threadIdx.x % TI;
     const int i = L.ib0 + il, j = L.jb0 + jl;
     const int64_t ncell = L.nloc;
@@ -3102,9 +3104,10 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     int rc = 0;
     const int64_t ncolb = c->nloc / c->l;                        /* water columns of the band */
     const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : (c->l <= 64 ? 64 : 0));
-    /* transposed column kernels: COL_TI columns of one row per workgroup of COL_TI Pl threads */
-    const unsigned gct = Pl ? xcd_grid(((c->nx + COL_TI - 1) / COL_TI) * (ncolb / c->nx)) : 0u;
-    const dim3 bct((unsigned)(COL_TI * Pl));
+    /* transposed column kernels: 1024 / Pl columns of one row per workgroup of 1024 threads */
+    const int cti = Pl ? 1024 / Pl : 1;
+    const unsigned gct = Pl ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx)) : 0u;
+    const dim3 bct(1024u);
     if (Pl != 0) {
         /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
          * after the Schur solve, then p and w */
