@@ -6,6 +6,7 @@
 # usage: scripts/ab_build.sh name=spec ...   (spec empty: the tree as it is)
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
+export ROOT
 for arg in "$@"; do
   name=${arg%%=*}; spec=${arg#*=}
   W=$(mktemp -d /tmp/ab_XXXX)
