@@ -229,7 +229,10 @@ struct Krylov {
 
 constexpr int RED_BLOCKS = 1024;     /* partial-sum blocks of the reductions            */
 constexpr int MAX_KRYLOV = 1000;     /* largest Krylov dimension                        */
-constexpr int RED_ROWS = 2 * MAX_KRYLOV + 4; /* reduction rows (DCGS2: 2 per basis vector + 3) */
+/* reduction rows (DCGS2: 2 per basis vector + 3 sums + beta, h_jj; the coefficient area
+ * d_hbuf[RED_ROWS..] holds 2 per basis vector and 1/beta, gamma at DCGS_SCAL) */
+constexpr int RED_ROWS = 2 * MAX_KRYLOV + 8;
+constexpr int DCGS_SCAL = 2 * MAX_KRYLOV + 2;
 
 }  // namespace iemic
 

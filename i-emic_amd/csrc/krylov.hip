@@ -375,14 +375,53 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
     }
 }
 
+/* DCGS2 coefficients on the device (no host round trip before the update pass): from the
+ * summed dot rows hb = [Q^T u, Q^T w interleaved | u.u, u.w, w.w], beta = sqrt(u.u - |a|^2),
+ * h_jj = (u.w - a.b) / beta, gamma = h_jj / beta; coef = [a | b - gamma a], coef[DCGS_SCAL..] =
+ * 1/beta, gamma; beta, h_jj appended to hb (rows 2nv+3, 2nv+4) for the host's Hessenberg
+ * column.  A breakdown (beta = 0) gives zero scales; the host stops on it. */
+__global__ void __launch_bounds__(256) k_dcgs_coef(double* __restrict__ hb, int nv, double* __restrict__ coef)
+{
+    __shared__ double sm[2 * 4];
+    __shared__ double tot[2];
+    double v[2] = {0.0, 0.0};
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+        const double a = hb[2 * i], b = hb[2 * i + 1];
+        v[0] += a * a;
+        v[1] += a * b;
+    }
+    block_sum_n<2>(v, sm);
+    if (threadIdx.x == 0) {
+        tot[0] = v[0];
+        tot[1] = v[1];
+    }
+    __syncthreads();
+    const double beta2 = hb[2 * nv] - tot[0];
+    const double bt = beta2 > 0.0 ? sqrt(beta2) : 0.0;
+    const bool ok = bt > 0.0 && bt <= 1.79e308;
+    const double hjj = ok ? (hb[2 * nv + 1] - tot[1]) / bt : 0.0;
+    const double gamma = ok ? hjj / bt : 0.0;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+        const double a = hb[2 * i], b = hb[2 * i + 1];
+        coef[i] = a;
+        coef[nv + i] = b - a * gamma;
+    }
+    if (threadIdx.x == 0) {
+        coef[DCGS_SCAL] = ok ? 1.0 / bt : 0.0;
+        coef[DCGS_SCAL + 1] = gamma;
+        hb[2 * nv + 3] = bt;
+        hb[2 * nv + 4] = hjj;
+    }
+}
+
 /* DCGS2 update pass, one read of Q:  q_j = (u - Q a) * inv_beta,
- * w = (w - Q c - gamma * u) * inv_beta  (coef = [a (nvec) | c (nvec)]); u is overwritten by
- * q_j.  Scaling the next candidate w by the same 1/beta (lagged normalisation) keeps every
- * candidate at the scale of a normalised Arnoldi vector, so its norm never compounds the
- * earlier subdiagonals (no overflow / false breakdown over long cycles). */
+ * w = (w - Q c - gamma * u) * inv_beta  (coef = [a (nvec) | c (nvec)], inv_beta and gamma at
+ * coef[DCGS_SCAL..]); u is overwritten by q_j.  Scaling the next candidate w by the same
+ * 1/beta (lagged normalisation) keeps every candidate at the scale of a normalised Arnoldi
+ * vector, so its norm never compounds the earlier subdiagonals (no overflow / false breakdown
+ * over long cycles). */
 __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ V, int64_t ldv,
                                                      int nvec, const double* __restrict__ coef,
-                                                     double inv_beta, double gamma,
                                                      double* __restrict__ u, double* __restrict__ w,
                                                      int64_t N)
 {
@@ -391,6 +430,7 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
     __shared__ double cs[2 * 1024];
     for (int i = threadIdx.x; i < 2 * nvec; i += blockDim.x) cs[i] = coef[i];
     __syncthreads();
+    const double inv_beta = coef[DCGS_SCAL], gamma = coef[DCGS_SCAL + 1];
     const double* a = cs;
     const double* cc = cs + nvec;
     const int64_t N2 = N / 2;
@@ -629,17 +669,21 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     const unsigned G = grid_for(NL);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
     std::vector<double> zs(m + 1, 1.0);   /* DCGS2: scale of the stored z_j (1 for DGKS) */
-    if (2 * m + 3 > RED_ROWS) {
+    if (2 * m + 5 > RED_ROWS) {
         set_error("fgmres: Krylov dimension too large");
         return IEMIC_EINVAL;
     }
     int inf_reorth = 0;
+    /* prec / SpMV timing events (two sets: the DCGS2 loop runs one iteration ahead) and the
+     * DCGS2 row-copy events */
     struct Events {
-        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        hipEvent_t e[8] = {};
         ~Events() { for (auto& x : e) if (x) (void)hipEventDestroy(x); }
     } evs;
     hipEvent_t* ev = evs.e;
-    for (int q = 0; q < 3; q++) HIP_OK(hipEventCreate(&ev[q]));
+    hipEvent_t* evr = evs.e + 6;
+    for (int q = 0; q < 6; q++) HIP_OK(hipEventCreate(&ev[q]));
+    for (int q = 6; q < 8; q++) HIP_OK(hipEventCreateWithFlags(&evs.e[q], hipEventDisableTiming));
 
     HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
     double bnorm = sqrt0(dot(c, b, b, 0));
@@ -740,33 +784,38 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
              * vector u_j is orthogonalised once when produced and re-orthogonalised one step
              * later in the same pass over the basis that orthogonalises the next candidate;
              * normalisation is folded in.  One read pass (k_dcgs_dot) + one update pass
-             * (k_dcgs_update) over the basis and one host synchronisation per iteration;
-             * the Hessenberg column j-1 is final (and the residual known) at iteration j. */
-            std::vector<double> htent(m + 1), col(m + 1), coef(2 * (size_t)m + 2);
+             * (k_dcgs_update) over the basis per iteration; the Hessenberg column j-1 is final
+             * (and the residual known) at iteration j.
+             * Pipelined: the update coefficients come from the device (k_dcgs_coef), so the
+             * host enqueues iteration jj+1 (update, preconditioner, SpMV, dot pass) before it
+             * waits for iteration jj's dot rows; the queue never drains on a host round trip.
+             * The one speculative iteration past convergence only touches columns the
+             * solution update does not read. */
+            std::vector<double> htent(m + 1), col(m + 1);
             int ncolf = 0;                 /* finalised columns */
             /* z_jj = M u_jj with u_jj of norm bt_jj: the Hessenberg column of z_jj / bt_jj is
              * the one assembled below, so the solution update divides y_jj by bt_jj */
             std::fill(zs.begin(), zs.end(), 1.0);
-            for (int jj = 0; jj <= m; jj++) {
+            /* iteration jj: [update of jj-1 enqueued before] prec, SpMV, dot pass, coefficients,
+             * rows -> pinned slot jj % 2, update */
+            auto enqueue = [&](int jj) -> int {
                 double* u = V + (int64_t)jj * NE;
                 double* wv = jj < m ? V + (int64_t)(jj + 1) * NE : nullptr;
-                float a1 = 0.f, a2 = 0.f;
+                hipEvent_t* e = ev + 3 * (jj & 1);
+                int rc2;
                 if (jj < m) {
                     double* zj = Z + (int64_t)jj * NE;
-                    HIP_OK(hipEventRecord(ev[0], c->stream));
+                    HIP_OK(hipEventRecord(e[0], c->stream));
                     if (opt->prec > 0) {
-                        rc = prec_apply(c, u, zj);
-                        if (rc) return rc;
+                        if ((rc2 = prec_apply(c, u, zj))) return rc2;
                     } else {
                         HIP_OK(hipMemcpyAsync(zj, u, sizeof(double) * NE, hipMemcpyDeviceToDevice,
                                               c->stream));
                     }
-                    HIP_OK(hipEventRecord(ev[1], c->stream));
-                    rc = spmv(c, zj, wv, c->stream);
-                    if (rc) return rc;
-                    HIP_OK(hipEventRecord(ev[2], c->stream));
+                    HIP_OK(hipEventRecord(e[1], c->stream));
+                    if ((rc2 = spmv(c, zj, wv, c->stream))) return rc2;
+                    HIP_OK(hipEventRecord(e[2], c->stream));
                 }
-
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
@@ -774,27 +823,38 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                                    0, c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p, RED_BLOCKS);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
-                if ((rc = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc;
-                HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (2 * nv + 3),
-                                      hipMemcpyDeviceToHost, c->stream));
-                HIP_OK(hipStreamSynchronize(c->stream));
+                if ((rc2 = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc2;
+                hipLaunchKernelGGL(k_dcgs_coef, dim3(1), dim3(256), 0, c->stream, c->d_hbuf.p, nv,
+                                   c->d_hbuf.p + RED_ROWS);
+                HIP_OK(hipMemcpyAsync(c->h_red + (size_t)RED_ROWS * (jj & 1), c->d_hbuf.p,
+                                      sizeof(double) * (2 * nv + 5), hipMemcpyDeviceToHost, c->stream));
+                HIP_OK(hipEventRecord(evr[jj & 1], c->stream));
+                if (jj < m)
+                    hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, V + o, NE, nv,
+                                       c->d_hbuf.p + RED_ROWS, u + o, wv + o, NL);
+                return 0;
+            };
+            if ((rc = enqueue(0))) return rc;
+            for (int jj = 0; jj <= m; jj++) {
+                if (jj < m && (rc = enqueue(jj + 1))) return rc;
+                HIP_OK(hipEventSynchronize(evr[jj & 1]));
                 if (jj < m) {
-                    (void)hipEventElapsedTime(&a1, ev[0], ev[1]);
-                    (void)hipEventElapsedTime(&a2, ev[1], ev[2]);
+                    float a1 = 0.f, a2 = 0.f;
+                    hipEvent_t* e = ev + 3 * (jj & 1);
+                    (void)hipEventElapsedTime(&a1, e[0], e[1]);
+                    (void)hipEventElapsedTime(&a2, e[1], e[2]);
                     inf.t_prec_ms += a1;
                     inf.t_spmv_ms += a2;
                     inf.n_spmv++;
                 }
-                const double* hr = c->h_red;
-                double aa = 0.0, ab = 0.0;
-                for (int i = 0; i < nv; i++) {
-                    aa += hr[2 * i] * hr[2 * i];
-                    ab += hr[2 * i] * hr[2 * i + 1];
-                }
+                const int nv = jj;
+                const double* hr = c->h_red + (size_t)RED_ROWS * (jj & 1);
                 const double uu = hr[2 * nv], uw = hr[2 * nv + 1];
-                if (!std::isfinite(uu) || !std::isfinite(uw)) return nonfinite();
-                const double beta2 = uu - aa;
-                const double bt = beta2 > 0.0 ? std::sqrt(beta2) : 0.0;
+                if (!std::isfinite(uu) || !std::isfinite(uw)) {
+                    (void)hipStreamSynchronize(c->stream);
+                    return nonfinite();
+                }
+                const double bt = hr[2 * nv + 3], hjj = hr[2 * nv + 4];
                 bool stop = false;
                 if (jj >= 1) {
                     /* finalise column jj-1: tentative + reorthogonalisation coefficients */
@@ -820,23 +880,15 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     it++;
                     stop = res <= opt->tol || !(bt > 0.0);
                 }
-                if (stop || jj == m || !(bt > 0.0)) {
-                    break;
-                }
-                /* update pass: q_jj = (u - Q a)/bt,  w -= Q c + gamma u */
-                const double hjj = (uw - ab) / bt;
-                const double gamma = hjj / bt;
-                for (int i = 0; i < nv; i++) {
-                    coef[i] = hr[2 * i];
-                    coef[nv + i] = hr[2 * i + 1] - hr[2 * i] * gamma;
-                    htent[i] = hr[2 * i + 1] / bt;
-                }
+                if (stop || jj == m || !(bt > 0.0)) break;
+                /* the update pass (already enqueued): q_jj = (u - Q a)/bt,  w -= Q c + gamma u */
+                for (int i = 0; i < nv; i++) htent[i] = hr[2 * i + 1] / bt;
                 htent[nv] = hjj / bt;
                 zs[jj] = bt;
-                if (nv > 0 && (rc = upload_coeffs(c, coef.data(), 2 * nv))) return rc;
-                hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, V + o, NE, nv,
-                                   c->d_hbuf.p + RED_ROWS, 1.0 / bt, gamma, u + o, wv + o, NL);
             }
+            /* the speculative iteration and its copy into the pinned slots finish before the
+             * slots are reused as the staging area of the solution update */
+            HIP_OK(hipStreamSynchronize(c->stream));
             j = ncolf;
         }
         /* y = H \ g ; x += Z y */
