@@ -375,6 +375,94 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
     }
 }
 
+/* DCGS2 dot pass, one read of everything: a workgroup holds its chunk of u and w in
+ * registers (DOT1_E 16-byte elements per lane) and streams every basis vector past them once;
+ * each vector's two sums are reduced across the wave and accumulated per wave in LDS
+ * (4 x (2 nvec + 3) doubles, dynamic).  Chunks are dealt to the nbx <= RED_BLOCKS workgroups
+ * round robin.  partial[row * nbx + bx] as k_dcgs_dot. */
+constexpr int DOT1_E = 4;
+__device__ __forceinline__ double wave_sum(double v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__global__ void __launch_bounds__(256) k_dcgs_dot1(const double* __restrict__ V, int64_t ldv, int nvec,
+                                                   const double* __restrict__ u,
+                                                   const double* __restrict__ w, int64_t N,
+                                                   double* __restrict__ partial, int nbx)
+{
+    constexpr int E = DOT1_E;
+    extern __shared__ double acc_s[];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int R = 2 * nvec + 3;
+    double* my = acc_s + wid * R;
+    for (int t = lane; t < R; t += 64) my[t] = 0.0;
+    __syncthreads();
+    const int64_t N2 = N / 2, CH = 256 * E;
+    const int64_t nch = (N2 + CH - 1) / CH;
+    const double2* u2 = reinterpret_cast<const double2*>(u);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double suu = 0.0, suw = 0.0, sww = 0.0;
+    for (int64_t ch = blockIdx.x; ch < nch; ch += nbx) {
+        const int64_t e0 = ch * CH + threadIdx.x;
+        double2 ue[E], we[E];
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+            const int64_t e = e0 + (int64_t)k * 256;
+            ue[k] = e < N2 ? u2[e] : make_double2(0.0, 0.0);
+            we[k] = e < N2 ? w2[e] : make_double2(0.0, 0.0);
+            suu += ue[k].x * ue[k].x + ue[k].y * ue[k].y;
+            suw += ue[k].x * we[k].x + ue[k].y * we[k].y;
+            sww += we[k].x * we[k].x + we[k].y * we[k].y;
+        }
+        /* out-of-range lanes read element 0 of the vector (their u, w are zero) */
+        int64_t ex[E];
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+            const int64_t e = e0 + (int64_t)k * 256;
+            ex[k] = e < N2 ? e : 0;
+        }
+        double2 qn[E];
+        if (nvec > 0) {
+#pragma unroll
+            for (int k = 0; k < E; k++) qn[k] = reinterpret_cast<const double2*>(V)[ex[k]];
+        }
+        for (int i = 0; i < nvec; i++) {
+            double2 q[E];
+#pragma unroll
+            for (int k = 0; k < E; k++) q[k] = qn[k];
+            if (i + 1 < nvec) {
+                const double2* qv = reinterpret_cast<const double2*>(V + (int64_t)(i + 1) * ldv);
+#pragma unroll
+                for (int k = 0; k < E; k++) qn[k] = qv[ex[k]];
+            }
+            double a = 0.0, b = 0.0;
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+                a += q[k].x * ue[k].x + q[k].y * ue[k].y;
+                b += q[k].x * we[k].x + q[k].y * we[k].y;
+            }
+            a = wave_sum(a);
+            b = wave_sum(b);
+            if (lane == 0) {
+                my[2 * i] += a;
+                my[2 * i + 1] += b;
+            }
+        }
+    }
+    suu = wave_sum(suu);
+    suw = wave_sum(suw);
+    sww = wave_sum(sww);
+    if (lane == 0) {
+        my[2 * nvec] += suu;
+        my[2 * nvec + 1] += suw;
+        my[2 * nvec + 2] += sww;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < R; t += blockDim.x)
+        partial[(int64_t)t * nbx + blockIdx.x] = acc_s[t] + acc_s[R + t] + acc_s[2 * R + t] + acc_s[3 * R + t];
+}
+
 /* DCGS2 coefficients on the device (no host round trip before the update pass): from the
  * summed dot rows hb = [Q^T u, Q^T w interleaved | u.u, u.w, w.w], beta = sqrt(u.u - |a|^2),
  * h_jj = (u.w - a.b) / beta, gamma = h_jj / beta; coef = [a | b - gamma a], coef[DCGS_SCAL..] =
@@ -793,6 +881,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
              * solution update does not read. */
             std::vector<double> htent(m + 1), col(m + 1);
             int ncolf = 0;                 /* finalised columns */
+            const int nbx1 = (int)std::min<int64_t>(RED_BLOCKS, (NL / 2 + 256 * DOT1_E - 1) / (256 * DOT1_E));
             /* z_jj = M u_jj with u_jj of norm bt_jj: the Hessenberg column of z_jj / bt_jj is
              * the one assembled below, so the solution update divides y_jj by bt_jj */
             std::fill(zs.begin(), zs.end(), 1.0);
@@ -819,10 +908,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
-                hipLaunchKernelGGL(k_dcgs_dot, dim3(RED_BLOCKS * ((nv + DCGS_DG - 1) / DCGS_DG + 1)), dim3(256),
-                                   0, c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p, RED_BLOCKS);
+                hipLaunchKernelGGL(k_dcgs_dot1, dim3(nbx1), dim3(256), sizeof(double) * 4 * (2 * nv + 3),
+                                   c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p, nbx1);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
-                                   RED_BLOCKS, 2 * nv + 3, c->d_hbuf.p);
+                                   nbx1, 2 * nv + 3, c->d_hbuf.p);
                 if ((rc2 = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc2;
                 hipLaunchKernelGGL(k_dcgs_coef, dim3(1), dim3(256), 0, c->stream, c->d_hbuf.p, nv,
                                    c->d_hbuf.p + RED_ROWS);
