@@ -78,8 +78,8 @@ def parse():
                    help="rccl: RCCL over xGMI, one GPU per rank; host: the library's host transport "
                         "over gloo (ranks may share a GPU)")
     p.add_argument("--npx", type=int, default=1,
-                   help="x parts of the process grid (1: latitude bands, the default: x cuts through the "
-                        "zonal flow double the FGMRES steps, DESIGN.md §7; 0: the reference's Decomp2D rule)")
+                   help="x parts of the process grid (1: latitude bands, the default: the fewest exchange "
+                        "batches per FGMRES step, DESIGN.md §7; 0: the reference's Decomp2D rule)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="global2")
