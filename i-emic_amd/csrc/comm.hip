@@ -373,6 +373,18 @@ int halo_exchange_w(iemic_ctx* c, double* v, int width, int depth)
     return run_msgs(c, y);
 }
 
+/* halo of a component-planar vector: nplanes planes of ps doubles (one per unknown, each
+ * in the ext cell order), exchanged as one x and one y batch */
+int halo_exchange_planar(iemic_ctx* c, double* v, int nplanes, int64_t ps, int depth)
+{
+    if (c->nranks <= 1) return 0;
+    std::vector<Msg> x, y;
+    for (int q = 0; q < nplanes; q++) halo_plan_ext(c, v + (int64_t)q * ps, 1, depth, x, y);
+    int rc = run_msgs(c, x);
+    if (rc) return rc;
+    return run_msgs(c, y);
+}
+
 /* state-vector halo (NUN doubles per cell) */
 int halo_exchange(iemic_ctx* c, double* v, int depth) { return halo_exchange_w(c, v, NUN, depth); }
 

@@ -217,6 +217,11 @@ struct BlockGS {
     int mg_crd = 0;
     SchurCR mg_cr;
     DevBuf<int> mg_cinfo;            /* its Gauss-Jordan pivot flag                      */
+    /* the dynamics passes work on component-planar copies (plane q = unknown q of every ext
+     * cell, plane stride next): known flags, iterate and right-hand side; dres, zc, dq and
+     * dzero are planar too.  The AoS rr is kept for the T/S sweeps (ts_mg = 0) */
+    DevBuf<uint8_t> knP;
+    DevBuf<double> zP, rrP;
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */
 };
@@ -357,6 +362,7 @@ int comm_size(const iemic_ctx* c, int* size, int* kind);
 int halo_exchange(iemic_ctx* c, double* ext_vec, int depth);
 int halo_exchange_w(iemic_ctx* c, double* ext_cells, int width, int depth);
 /* the two phases of an exchange of arrays of the ext layout (appended to x / y) */
+int halo_exchange_planar(iemic_ctx* c, double* v, int nplanes, int64_t ps, int depth);
 void halo_plan_ext(const iemic_ctx* c, double* v, int width, int depth, std::vector<Msg>& x,
                    std::vector<Msg>& y);
 int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops);

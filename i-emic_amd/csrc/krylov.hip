@@ -133,14 +133,15 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
  * full rows of the SpMV are used.  One workgroup per 64 cells; the 64 slots of the four rows
  * are split evenly over the waves (U | U+V | V+W | W+P, 16 each: a wave per equation would
  * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
- * rows' partials meet in LDS. */
+ * rows' partials meet in LDS.  z, the flags and d are component-planar (plane stride ps:
+ * the gathers of one unknown are unit-stride along i), r is the AoS right-hand side. */
 /* on[q]: row sp7_row(S0) + q of the cell is active; an identity row's coefficients are
  * neither loaded nor used (about half the cells are land at 2 degrees).  (Non-temporal
  * coefficient loads measured 35.6 against 26.1 us per defect, scripts/ab_probe.py.) */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
                                             int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
-                                            double* acc)
+                                            int64_t ps, double* acc)
 {
 #pragma unroll
     for (int s = S0; s < S1; s++) {
@@ -148,14 +149,14 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
         const int q = sp7_row(s) - sp7_row(S0);
         if (!on[q]) continue;
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc[q] += val[(int64_t)s * nloc + lc] * z[NUN * (int64_t)cidx + sl.var];
+        acc[q] += val[(int64_t)s * nloc + lc] * z[(int64_t)cidx + ps * sl.var];
     }
 }
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
-                                                  const uint8_t* __restrict__ known,
-                                                  double* __restrict__ d, int64_t nloc, int nblk)
+                                                  const uint8_t* __restrict__ knP,
+                                                  double* __restrict__ d, int64_t nloc, int nblk, int64_t ps)
 {
     __shared__ double red[4][2][64];
     const int per = (nblk + 7) >> 3;
@@ -164,39 +165,42 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int64_t lc0 = (int64_t)tile * 64, lc = lc0 + c;
     const bool act = lc < nloc;
+    const int64_t e0 = (int64_t)HALO * X.l * X.nx;     /* ext cell of owned cell 0 */
     double acc[2] = {0.0, 0.0};
     if (act) {
         const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
         int nc[3][9];
         nb_cells(X, il, j, k, nc);
         /* the wave's two rows: g0 {U, -} g1 {U, V} g2 {V, W} g3 {W, P} */
-        const int64_t row0 = NUN * ((int64_t)HALO * X.l * X.nx + lc) + (g == 0 ? 0 : g - 1);
-        const bool on[2] = {!known[row0], g > 0 && !known[row0 + 1]};
-        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, on, acc);
-        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, on, acc);
-        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, on, acc);
-        else dyn_partial<48, 64>(val, z, lc, nloc, nc, on, acc);
+        const int64_t cell = e0 + lc;
+        const int v0 = g == 0 ? 0 : g - 1;
+        const bool on[2] = {!knP[cell + ps * v0], g > 0 && !knP[cell + ps * (v0 + 1)]};
+        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, on, ps, acc);
+        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, on, ps, acc);
+        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, on, ps, acc);
+        else dyn_partial<48, 64>(val, z, lc, nloc, nc, on, ps, acc);
     }
     red[g][0][c] = acc[0];
     red[g][1][c] = acc[1];
     __syncthreads();
-    /* rows of the waves: g0 {U} g1 {U,V} g2 {V,W} g3 {W,P}; thread = (cell, row) */
-    const int cc = threadIdx.x >> 2, R = threadIdx.x & 3;
+    /* rows of the waves: g0 {U} g1 {U,V} g2 {V,W} g3 {W,P}; thread = (row, cell), the
+     * cell fastest (planar stores) */
+    const int R = threadIdx.x >> 6, cc = threadIdx.x & 63;
     if (lc0 + cc >= nloc) return;
     const double sum = R == 0 ? red[0][0][cc] + red[1][0][cc]
                      : R == 1 ? red[1][1][cc] + red[2][0][cc]
                      : R == 2 ? red[2][1][cc] + red[3][0][cc]
                               : red[3][1][cc];
-    const int64_t row = NUN * ((int64_t)HALO * X.l * X.nx + lc0 + cc) + R;
-    d[row] = known[row] ? 0.0 : r[row] - sum;
+    const int64_t cell = e0 + lc0 + cc, e = cell + ps * R;
+    d[e] = knP[e] ? 0.0 : r[NUN * cell + R] - sum;
 }
 
-int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d)
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d)
 {
     const int nblk = (int)((c->nloc + 63) / 64);
     const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
-    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, known, d,
-                       c->nloc, nblk);
+    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, knP, d,
+                       c->nloc, nblk, (int64_t)c->next);
     return 0;
 }
 

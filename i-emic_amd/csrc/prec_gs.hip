@@ -52,7 +52,10 @@ constexpr int GSL = 10;                             /* gslot doubles per cell   
 struct Lay {
     int n, m, l, periodic, jb0, ib0, nx, hx;
     int64_t nloc, own0, xb;
+    int64_t ps;                      /* plane stride of the planar dynamics vectors (next) */
 };
+/* unknown v of ext cell e in a component-planar vector */
+#define PL(e, v) ((e) + (int64_t)(v) * L.ps)
 /* ext cell of global (i, j, k) (i in the grid after hnb's wrap; the x halo when split) */
 __device__ __forceinline__ int64_t ecell(const Lay& L, int i, int j, int k)
 {
@@ -592,19 +595,25 @@ __global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__
 
 /* z = r on identity rows and 0 on the others (the apply's starting iterate: no separate
  * memset; halo cells are only read after an exchange, and one rank reads none);
- * rr = r - A(:, known) r(known) on the others (slot bitmask) */
+ * rr = r - A(:, known) r(known) on the others (slot bitmask).  z goes to the output (AoS)
+ * and to the planar iterate zP, rr to the planar rrP and (rr != null, the T/S sweeps) AoS */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const uint64_t* __restrict__ kmask, const double* __restrict__ r,
-                        double* __restrict__ z, double* __restrict__ rr, Lay L)
+                        double* __restrict__ z, double* __restrict__ rr, double* __restrict__ zP,
+                        double* __restrict__ rrP, Lay L)
 {
     LAY_ALIASES;
     OWNED_CELL;
     double acc[NUN];
+    bool kn[NUN];
 #pragma unroll
     for (int R = 0; R < NUN; R++) {
         const int64_t row = NUN * cell + R;
         acc[R] = r[row];
-        z[row] = known[row] ? acc[R] : 0.0;
+        kn[R] = known[row] != 0;
+        const double zv = kn[R] ? acc[R] : 0.0;
+        z[row] = zv;
+        zP[PL(cell, R)] = zv;
     }
     uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
     if (b[0] | b[1]) {
@@ -623,9 +632,19 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     }
 #pragma unroll
     for (int R = 0; R < NUN; R++) {
-        const int64_t row = NUN * cell + R;
-        rr[row] = known[row] ? 0.0 : acc[R];
+        const double v = kn[R] ? 0.0 : acc[R];
+        if (rr) rr[NUN * cell + R] = v;
+        rrP[PL(cell, R)] = v;
     }
+}
+
+/* the identity-row flags in the planar layout */
+__global__ void k_known_planar(const uint8_t* __restrict__ known, uint8_t* __restrict__ knP, int64_t next)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= next) return;
+#pragma unroll
+    for (int R = 0; R < NUN; R++) knP[e + R * next] = known[NUN * e + R];
 }
 
 /* per cell: bitmask of the slots (104 bits) through which an active row couples to an
@@ -683,44 +702,15 @@ __global__ void k_ts_compact(const double* __restrict__ val, const uint8_t* __re
     }
 }
 
-/* 1. hydrostatic rows top-down: ptil (stored in z at the P rows) */
-/* column kernels: one thread per (i, j) of the band, i fastest (lanes read adjacent cells) */
-#define BAND_COLUMN                                                                      \
-    const int t_ = blockIdx.x * blockDim.x + threadIdx.x;                                \
-    if (t_ >= (int)(L.nloc / L.l)) return;                                               \
-    const int i = L.ib0 + t_ % L.nx, j = L.jb0 + t_ / L.nx;                              \
-    const int ij = j * L.n + i;                                                          \
-    const int64_t ncell = L.nloc
-
-__global__ void k_gs_ptil(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                          const int* __restrict__ col_of_ij, const double* __restrict__ rr,
-                          double* __restrict__ z, Lay L)
-{
-    LAY_ALIASES;
-    BAND_COLUMN;
-    if (col_of_ij[ij] < 0) return;
-    double pabove = 0.0;
-    for (int k = l - 1; k >= 0; k--) {
-        const int64_t cell = ecell(L, i, j, k);
-        const bool pa = !known[NUN * cell + PP];
-        double p = 0.0;
-        if (pa && k < l - 1 && !known[NUN * cell + WW]) {
-            const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
-            const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
-            if (g0 != 0.0) p = (rr[NUN * cell + WW] - g1 * pabove) / g0;
-        }
-        if (pa) z[NUN * cell + PP] = p;
-        pabove = pa ? p : 0.0;
-    }
-}
-
-__device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
+__device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                                          const double* __restrict__ z, int i, int j, int k,
                                          int64_t pl, const Lay& L);
 /* Column kernels, transposed: one workgroup of 1024 threads per tile of COL_TI = 1024 / LP
  * consecutive columns of one latitude row (LP = power of two >= l), thread = (column, level)
  * with the column fastest, so every per-cell load of a wave runs along i in 128-byte runs
- * (the slot-major Jacobian rows contiguously, the interleaved vectors at one cell stride);
+ * (the slot-major Jacobian rows and the planar dynamics vectors contiguously: with the
+ * interleaved AoS vectors at a 48-byte cell stride the U/V and p/w kernels took 12.3 and
+ * 12.6 against 7.2 and 6.9 us, scripts/ab/soa_probe.sh);
  * the column recurrences meet in LDS, where each thread composes the affine maps of the
  * levels it depends on (at most l steps of LDS reads).  At 2 degrees (LP = 16) 64-column
  * tiles, 232 workgroups: 16-column tiles (928 of 256 threads) measured 2 ms slower per
@@ -756,11 +746,12 @@ __device__ __forceinline__ bool col_tile(const Lay& L, int& il, int& jl, int& k,
  * transposed column layout of k_gs_ptil_rcol); zo += omega (p, w) in the correction passes */
 template <int LP>
 __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val,
-                                                  const uint8_t* __restrict__ known,
+                                                  const uint8_t* __restrict__ knP,
                                                   const double* __restrict__ pbar,
                                                   double* __restrict__ z, Lay L,
                                                   const double* __restrict__ rr,
-                                                  double* __restrict__ zo, double omega)
+                                                  double* __restrict__ zo, double omega,
+                                                  double* __restrict__ zaos)
 {
     constexpr int TI = col_ti<LP>();
     __shared__ double sA[LP][TI], sB[LP][TI];
@@ -775,7 +766,7 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
     int64_t cell = 0;
     if (on) {
         cell = ecell(L, i, j, k);
-        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        const uint8_t kp = knP[PL(cell, PP)], kw = knP[PL(cell, WW)];
         pa = !kp;
         wa = !kw;
     }
@@ -783,9 +774,9 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
         /* an inactive P row (land) reads nothing: its (A, B) = (0, 0) */
         const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
         const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
-        const double rhs = rr[NUN * cell + PP] - duv_uv(val, known, z, i, j, k, cell - L.own0, L);
+        const double rhs = rr[PL(cell, PP)] - duv_uv(val, knP, z, i, j, k, cell - L.own0, L);
         pb = pbar[(int64_t)i * L.m + j];
-        zp = z[NUN * cell + PP];
+        zp = z[PL(cell, PP)];
         if (wa && a != 0.0) {
             A = rhs / a;
             B = -b / a;
@@ -800,65 +791,23 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
     double w = 0.0;
     for (int kk = 0; kk <= k; kk++) w = sA[kk][ii] + sB[kk][ii] * w;
     const double pn = zp + pb, wn = pa ? w : 0.0;
-    if (pa) z[NUN * cell + PP] = pn;
-    if (wa) z[NUN * cell + WW] = wn;
+    if (pa) z[PL(cell, PP)] = pn;
+    if (wa) z[PL(cell, WW)] = wn;
+    double fp = pn, fw = wn;
     if (zo) {
-        if (pa) zo[NUN * cell + PP] += omega * pn;
-        if (wa) zo[NUN * cell + WW] += omega * wn;
+        if (pa) zo[PL(cell, PP)] = fp = zo[PL(cell, PP)] + omega * pn;
+        if (wa) zo[PL(cell, WW)] = fw = zo[PL(cell, WW)] + omega * wn;
     }
-}
-
-/* sum over the 4 P corners of a U/V point of G * p(P)  (U row slots 20..23 / V 42..45) */
-__device__ __forceinline__ void guv_p(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                                      const double* __restrict__ pv, int64_t pstride, int i, int j,
-                                      int k, int64_t lc, const Lay& L, double& gu, double& gv,
-                                      bool colmode)
-{
-    /* branch-free: a corner outside the domain reads the cell itself with weight 0; with
-     * colmode the values are the column values pbar indexed i*m + j (0 without water) */
-    const int n = L.n, m = L.m, periodic = L.periodic;
-    const int64_t ncell = L.nloc;
-    const int64_t cell = lc;
-    gu = gv = 0.0;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; g4++) {
-        int pi = i + (g4 & 1), pj = j + ((g4 >> 1) & 1);
-        const bool in = hnb(pi, pj, n, m, periodic);
-        if (!in) { pi = i; pj = j; }
-        const int64_t pc = ecell(L, pi, pj, k);
-        const uint8_t kp = known[NUN * pc + PP];
-        const double p = colmode ? pv[(int64_t)pi * m + pj] : pv[pstride * pc + PP];
-        const double au = val[(int64_t)(S_UP + g4) * ncell + cell];
-        const double av = val[(int64_t)(S_VP + g4) * ncell + cell];
-        const bool use = in && !kp;
-        gu += use ? au * p : 0.0;
-        gv += use ? av * p : 0.0;
+    /* the last pass: the final P/W rows into the preconditioner output (AoS) */
+    if (zaos) {
+        if (pa) zaos[NUN * cell + PP] = fp;
+        if (wa) zaos[NUN * cell + WW] = fw;
     }
-}
-
-/* 2. uv* = D^-1 (rr_uv - Guv ptil)  (stored in z at the U/V rows) */
-__global__ void k_gs_uvs(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                         const double* __restrict__ uvinv, const double* __restrict__ rr,
-                         double* __restrict__ z, Lay L)
-{
-    OWNED_CELL;
-    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
-    double gu, gv;
-    guv_p(val, known, z, NUN, i, j, k, lc, L, gu, gv, false);
-    const double* D = uvinv + 4 * cell;
-    const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
-    const double r0 = rr[NUN * cell + UU], r1 = rr[NUN * cell + VV];
-    const bool ua = !ku, va = !kv;
-    if (!ua && !va) return;
-    const double ru = ua ? r0 - gu : 0.0;
-    const double rv = va ? r1 - gv : 0.0;
-    if (ua) z[NUN * cell + UU] = d0 * ru + d1 * rv;
-    if (va) z[NUN * cell + VV] = d2 * ru + d3 * rv;
 }
 
 /* Duv uv at a P cell: sum over the 4 U/V corners (P row slots 54..61) */
 /* pl: owned index (Jacobian column) of the P cell */
-__device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ known,
+__device__ __forceinline__ double duv_uv(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                                          const double* __restrict__ z, int i, int j, int k,
                                          int64_t pl, const Lay& L)
 {
@@ -872,37 +821,13 @@ __device__ __forceinline__ double duv_uv(const double* __restrict__ val, const u
         const bool in = hnb(qi, qj, n, m, periodic);
         if (!in) { qi = i; qj = j; }
         const int64_t qc = ecell(L, qi, qj, k);
-        const uint8_t ku = known[NUN * qc + UU], kv = known[NUN * qc + VV];
+        const uint8_t ku = knP[PL(qc, UU)], kv = knP[PL(qc, VV)];
         const double au = val[(int64_t)(S_PU + q4) * ncell + pc], av = val[(int64_t)(S_PV + q4) * ncell + pc];
-        const double zu = z[NUN * qc + UU], zv = z[NUN * qc + VV];
+        const double zu = z[PL(qc, UU)], zv = z[PL(qc, VV)];
         acc += (in && !ku) ? au * zu : 0.0;
         acc += (in && !kv) ? av * zv : 0.0;
     }
     return acc;
-}
-
-/* 3a. Schur right-hand side: per P cell t = w_k (Duv uv - rr_p) (cell-parallel), then a
- * fixed-order sum over k per column (k_col_sum).  With w_k = 1 and mode 1 the same kernel
- * gives the continuity right-hand side rr_p - Duv uv used by the W sweep. */
-__global__ void k_gs_pcell(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                           const double* __restrict__ pw, const double* __restrict__ rr,
-                           const double* __restrict__ z, double* __restrict__ t, Lay L, int mode)
-{
-    OWNED_CELL;
-    if (known[NUN * cell + PP]) { t[cell] = 0.0; return; }
-    const double d = duv_uv(val, known, z, i, j, k, lc, L);
-    t[cell] = mode == 0 ? pw[cell] * (d - rr[NUN * cell + PP]) : rr[NUN * cell + PP] - d;
-}
-__global__ void k_col_sum(const double* __restrict__ t, const int* __restrict__ col_of_ij,
-                          const uint8_t* __restrict__ pinned, double* __restrict__ rhs, Lay L)
-{
-    BAND_COLUMN;
-    (void)ncell;
-    const int c = col_of_ij[ij];
-    if (c < 0) return;
-    double s = 0.0;
-    for (int k = 0; k < L.l; k++) s += t[ecell(L, i, j, k)];
-    rhs[c] = pinned[c] ? 0.0 : s;
 }
 
 /* ---- the Schur right-hand side as a linear form in rr ----------------------------------
@@ -1009,7 +934,7 @@ __global__ void k_rcol_w(const uint8_t* __restrict__ known, const double* __rest
  * sum_e rcol_e rr_e (summed over the levels in a fixed order), written as k_gs_pcol wrote it */
 template <int LP>
 __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict__ val,
-                                                       const uint8_t* __restrict__ known,
+                                                       const uint8_t* __restrict__ knP,
                                                        const double* __restrict__ rcol,
                                                        const double* __restrict__ rr,
                                                        double* __restrict__ z,
@@ -1041,26 +966,26 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
         cell = nc9[4];
         const double* R = rcol + (int64_t)k * ncolb + t;
         const int64_t es = (int64_t)l * ncolb;
-        const uint8_t kp = known[NUN * cell + PP], kw = known[NUN * cell + WW];
+        const uint8_t kp = knP[PL(cell, PP)], kw = knP[PL(cell, WW)];
         pa = !kp;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
-        for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[NUN * nc9[e] + WW];
+        for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[PL(nc9[e], WW)];
         if (pa) {
             /* the corner and own-P coefficients vanish on an inactive P row (land): not read */
 #pragma unroll
             for (int q4 = 0; q4 < 4; q4++) {
                 /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
                 const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
-                a1 += R[(9 + q4) * es] * rr[NUN * qc + UU];
-                a2 += R[(13 + q4) * es] * rr[NUN * qc + VV];
+                a1 += R[(9 + q4) * es] * rr[PL(qc, UU)];
+                a2 += R[(13 + q4) * es] * rr[PL(qc, VV)];
             }
-            a2 += R[17 * es] * rr[NUN * cell + PP];
+            a2 += R[17 * es] * rr[PL(cell, PP)];
             if (k < l - 1 && !kw) {
                 const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
                 const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
                 if (g0 != 0.0) {
-                    A = rr[NUN * cell + WW] / g0;
+                    A = rr[PL(cell, WW)] / g0;
                     B = -g1 / g0;
                 }
             }
@@ -1076,7 +1001,7 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
     if (!on) return;
     double p = 0.0;
     for (int kk = l - 1; kk >= k; kk--) p = sA[kk][ii] + sB[kk][ii] * p;
-    if (pa) z[NUN * cell + PP] = p;
+    if (pa) z[PL(cell, PP)] = p;
     if (k == 0) {
         const int q = ocol[j * n + i];
         double s = 0.0;
@@ -1139,60 +1064,22 @@ __global__ void __launch_bounds__(256) k_gemv_w(const double* __restrict__ X, in
     if (lane == 0) y[r] = v;
 }
 
-/* dynamics defect: d = rr - A_DD z on the active U/V/W/P rows (couplings to active
- * U/V/W/P columns only: the block the dynamics solve approximates), 0 elsewhere */
-__global__ void k_dyn_resid(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                            const double* __restrict__ rr, const double* __restrict__ z,
-                            double* __restrict__ d, Lay L)
-{
-    LAY_ALIASES;
-    OWNED_CELL;
-    for (int R = UU; R <= PP; R++) {
-        const int64_t row = NUN * cell + R;
-        if (known[row]) { d[row] = 0.0; continue; }
-        double acc = rr[row];
-        for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
-            const int var = SLOTS[s].var;
-            if (var > PP) continue;
-            const double v = val[(int64_t)s * ncell + lc];
-            if (v == 0.0) continue;
-            int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
-            const int kk = k + SLOTS[s].dk;
-            if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-            const int64_t col = NUN * ecell(L, ii, jj, kk) + var;
-            if (!known[col]) acc -= v * z[col];
-        }
-        d[row] = acc;
-    }
-    d[NUN * cell + TT] = 0.0;
-    d[NUN * cell + SS] = 0.0;
-}
-
-/* z += zc on the active U/V/W/P rows */
-__global__ void k_dyn_add(const uint8_t* __restrict__ known, const double* __restrict__ zc,
-                          double* __restrict__ z, Lay L, double omega)
-{
-    OWNED_CELL;
-#pragma unroll
-    for (int R = UU; R <= PP; R++) {
-        const int64_t row = NUN * cell + R;
-        if (!known[row]) z[row] += omega * zc[row];
-    }
-}
-
 /* Minimal-residual defect correction: with d the defect and q = -A_DD zc the change a
  * full correction zc would make to it, the step w = argmin ||d + w q|| = -(d.q)/(q.q).
  * Block partials in a fixed order (deterministic), summed by one thread. */
 constexpr int MR_NB = 256;
+/* over the owned cells of the planar U/V/W/P planes (fixed grid-stride order) */
 __global__ void __launch_bounds__(256) k_mr_dots(const double* __restrict__ d, const double* __restrict__ q,
-                                                 int64_t n, double* __restrict__ part)
+                                                 Lay L, double* __restrict__ part)
 {
     __shared__ double s0[256], s1[256];
     double a = 0.0, b = 0.0;
+    const int64_t n = 4 * L.nloc;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const double qv = q[t];
-        a += d[t] * qv;
+        const int64_t e = PL(L.own0 + t % L.nloc, t / L.nloc);
+        const double qv = q[e];
+        a += d[e] * qv;
         b += qv * qv;
     }
     s0[threadIdx.x] = a;
@@ -1221,61 +1108,36 @@ __global__ void k_mr_sum(double* __restrict__ part, int nb)
     part[2 * nb] = a;
     part[2 * nb + 1] = b;
 }
-/* z += w zc, and (upd) d += w q, on the active U/V/W/P rows */
-__global__ void k_mr_update(const uint8_t* __restrict__ known, const double* __restrict__ sums,
+/* z += w zc, and (upd) d += w q, on the active U/V/W/P rows (planar); zaos: the final
+ * values into the preconditioner output (AoS) */
+__global__ void k_mr_update(const uint8_t* __restrict__ knP, const double* __restrict__ sums,
                             const double* __restrict__ zc, const double* __restrict__ q,
-                            double* __restrict__ z, double* __restrict__ d, Lay L, int upd)
+                            double* __restrict__ z, double* __restrict__ d, Lay L, int upd,
+                            double* __restrict__ zaos)
 {
     OWNED_CELL;
     const double w = sums[1] > 0.0 ? -sums[0] / sums[1] : 0.0;
 #pragma unroll
     for (int R = UU; R <= PP; R++) {
-        const int64_t row = NUN * cell + R;
-        if (known[row]) continue;
-        z[row] += w * zc[row];
-        if (upd) d[row] += w * q[row];
-    }
-}
-
-/* 4. uv = uv* - D^-1 Guv Mz1^T pbar */
-__global__ void k_gs_uvfix(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                           const double* __restrict__ uvinv, const int* __restrict__ col_of_ij,
-                           const double* __restrict__ pbar, double* __restrict__ z, Lay L,
-                           double* __restrict__ zo, double omega)
-{
-    (void)col_of_ij;
-    OWNED_CELL;
-    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
-    double gu, gv;
-    guv_p(val, known, pbar, 0, i, j, k, lc, L, gu, gv, true);
-    const double* D = uvinv + 4 * cell;
-    const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
-    const double zu = z[NUN * cell + UU], zv = z[NUN * cell + VV];
-    const bool ua = !ku, va = !kv;
-    if (!ua && !va) return;
-    if (!ua) gu = 0.0;
-    if (!va) gv = 0.0;
-    const double nu = zu - (d0 * gu + d1 * gv), nv = zv - (d2 * gu + d3 * gv);
-    if (ua) z[NUN * cell + UU] = nu;
-    if (va) z[NUN * cell + VV] = nv;
-    /* defect-correction passes: z_out += omega z on the final U/V rows (k_dyn_add fused) */
-    if (zo) {
-        if (ua) zo[NUN * cell + UU] += omega * nu;
-        if (va) zo[NUN * cell + VV] += omega * nv;
+        const int64_t e = PL(cell, R);
+        if (knP[e]) continue;
+        const double zn = z[e] + w * zc[e];
+        z[e] = zn;
+        if (upd) d[e] += w * q[e];
+        if (zaos) zaos[NUN * cell + R] = zn;
     }
 }
 
 /* 2 + 4. uv = D^-1 (rr_uv - Guv (ptil + Mz1^T pbar)) in one pass once pbar is known (the
- * Schur right-hand side came from rcol, so uv* is never formed); zo += omega uv as in
- * k_gs_uvfix */
-__global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restrict__ known,
+ * Schur right-hand side came from rcol, so uv* is never formed); zo += omega uv */
+__global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                          const double* __restrict__ uvinv, const double* __restrict__ rr,
                          const double* __restrict__ pbar, double* __restrict__ z, Lay L,
-                         double* __restrict__ zo, double omega)
+                         double* __restrict__ zo, double omega, double* __restrict__ zaos)
 {
     OWNED_CELL;
     const int n = L.n, m = L.m, periodic = L.periodic;
-    const uint8_t ku = known[NUN * cell + UU], kv = known[NUN * cell + VV];
+    const uint8_t ku = knP[PL(cell, UU)], kv = knP[PL(cell, VV)];
     const bool ua = !ku, va = !kv;
     if (!ua && !va) return;                 /* land: none of the point's operands is read */
     double gu = 0.0, gv = 0.0;
@@ -1285,8 +1147,8 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
         const bool in = hnb(pi, pj, n, m, periodic);
         if (!in) { pi = i; pj = j; }
         const int64_t pc = ecell(L, pi, pj, k);
-        const uint8_t kp = known[NUN * pc + PP];
-        const double p = z[NUN * pc + PP] + pbar[(int64_t)pi * m + pj];
+        const uint8_t kp = knP[PL(pc, PP)];
+        const double p = z[PL(pc, PP)] + pbar[(int64_t)pi * m + pj];
         const double au = val[(int64_t)(S_UP + g4) * ncell + lc];
         const double av = val[(int64_t)(S_VP + g4) * ncell + lc];
         const bool use = in && !kp;
@@ -1295,44 +1157,21 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
     }
     const double* D = uvinv + 4 * cell;
     const double d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3];
-    const double r0 = rr[NUN * cell + UU], r1 = rr[NUN * cell + VV];
+    const double r0 = rr[PL(cell, UU)], r1 = rr[PL(cell, VV)];
     const double ru = ua ? r0 - gu : 0.0;
     const double rv = va ? r1 - gv : 0.0;
     const double nu = d0 * ru + d1 * rv, nv = d2 * ru + d3 * rv;
-    if (ua) z[NUN * cell + UU] = nu;
-    if (va) z[NUN * cell + VV] = nv;
+    if (ua) z[PL(cell, UU)] = nu;
+    if (va) z[PL(cell, VV)] = nv;
+    double fu = nu, fv = nv;
     if (zo) {
-        if (ua) zo[NUN * cell + UU] += omega * nu;
-        if (va) zo[NUN * cell + VV] += omega * nv;
+        if (ua) zo[PL(cell, UU)] = fu = zo[PL(cell, UU)] + omega * nu;
+        if (va) zo[PL(cell, VV)] = fv = zo[PL(cell, VV)] + omega * nv;
     }
-}
-
-/* 4b/5. p = ptil + pbar; continuity rows bottom-up for w (top P row excluded) */
-__global__ void k_gs_pw(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                        const int* __restrict__ col_of_ij, const double* __restrict__ pbar,
-                        const double* __restrict__ crhs, double* __restrict__ z, Lay L)
-{
-    LAY_ALIASES;
-    BAND_COLUMN;
-    const int c = col_of_ij[ij];
-    if (c < 0) return;
-    const double pb = pbar[c];
-    double wbelow = 0.0;
-    for (int k = 0; k < l; k++) {
-        const int64_t cell = ecell(L, i, j, k);
-        const bool pa = !known[NUN * cell + PP], wa = !known[NUN * cell + WW];
-        if (pa) z[NUN * cell + PP] += pb;
-        double w = 0.0;
-        if (pa && wa) {
-            const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
-            const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
-            const double rhs = crhs[cell];
-            if (a != 0.0) w = (rhs - b * wbelow) / a;
-            z[NUN * cell + WW] = w;
-        } else if (wa) {
-            z[NUN * cell + WW] = 0.0;
-        }
-        wbelow = wa ? w : 0.0;
+    /* the last pass: the final U/V rows into the preconditioner output (AoS) */
+    if (zaos) {
+        if (ua) zaos[NUN * cell + UU] = fu;
+        if (va) zaos[NUN * cell + VV] = fv;
     }
 }
 
@@ -1434,8 +1273,9 @@ __global__ void k_ts_pack(const double* __restrict__ tsoff, const double* __rest
 template <int R>
 __device__ __forceinline__ double bts_row(const double* __restrict__ val, const double* __restrict__ z,
                                           int64_t lc, int64_t nloc, const int (*nc)[9],
-                                          uint64_t kbits, double acc)
+                                          uint64_t kbits, double acc, int64_t zcell = NUN, int64_t zvar = 1)
 {
+    /* z(cell, var) = z[zcell cell + zvar var]: (NUN, 1) AoS, (1, plane stride) planar */
     constexpr int B = RowInfo<R>::B, NS = RowInfo<R>::NS;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -1446,7 +1286,7 @@ __device__ __forceinline__ double bts_row(const double* __restrict__ val, const 
          * the T/S solve 6.5 us slower, scripts/ab_probe.py) */
         const double v = ((kbits >> (B + s - 64)) & 1) ? 0.0 : val[(int64_t)(B + s) * nloc + lc];
         const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc -= v * z[NUN * (int64_t)cidx + sl.var];
+        acc -= v * z[zcell * (int64_t)cidx + zvar * sl.var];
     }
     return acc;
 }
@@ -1482,40 +1322,6 @@ __global__ void __launch_bounds__(128) k_gs_bts2(const double* __restrict__ val,
     bts[row] = acc;
     if (R == TT) zt[cell] = 0.0;
     else zs[cell] = 0.0;
-}
-
-/* T/S right-hand side into the colour layout; zt = zs = 0 */
-__global__ void k_gs_bts_c(const double* __restrict__ val, const uint8_t* __restrict__ known,
-                           const double* __restrict__ rr, const double* __restrict__ z,
-                           double* __restrict__ bc, double* __restrict__ zt, double* __restrict__ zs,
-                           Lay L, double* __restrict__ bts)
-{
-    LAY_ALIASES;
-    OWNED_CELL;
-    const int64_t half = ncell / 2;
-    const int c = (i + j + k) & 1;
-    for (int R = TT; R <= SS; R++) {
-        const int64_t row = NUN * cell + R;
-        double acc = 0.0;
-        if (!known[row]) {
-            acc = rr[row];
-            for (int s = ROW_BEGIN[R]; s < ROW_BEGIN[R + 1]; s++) {
-                const int var = SLOTS[s].var;
-                if (var == TT || var == SS) continue;
-                const double v = val[(int64_t)s * ncell + lc];
-                if (v == 0.0) continue;
-                int ii = i + SLOTS[s].di, jj = j + SLOTS[s].dj;
-                const int kk = k + SLOTS[s].dk;
-                if (kk < 0 || kk >= l || !hnb(ii, jj, n, m, periodic)) continue;
-                const int64_t col = NUN * ecell(L, ii, jj, kk) + var;
-                if (!known[col]) acc -= v * z[col];
-            }
-        }
-        bc[(int64_t)(c * 2 + (R - TT)) * half + (lc >> 1)] = acc;
-        bts[row] = acc;
-    }
-    zt[cell] = 0.0;
-    zs[cell] = 0.0;
 }
 
 __global__ void __launch_bounds__(256) k_gs_ts_half_c(const double* __restrict__ tsc,
@@ -1878,7 +1684,7 @@ __global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, i
  * to 0 (one launch instead of rhs + first colour). */
 constexpr int MG_TI = 16;
 template <int P>
-__global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val, const uint8_t* __restrict__ known,
+__global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                                                  const uint64_t* __restrict__ kmask,
                                                  const double* __restrict__ rr, const double* __restrict__ z,
                                                  Lay L, TsLev V)
@@ -1897,13 +1703,13 @@ __global__ void __launch_bounds__(256) k_mg_entry(const double* __restrict__ val
         if (i < nx) {
             const int64_t lc = ((int64_t)jl * l + k) * nx + i;
             const int64_t cell = L.own0 + lc;
-            const int64_t row = NUN * cell + R;
-            if (!known[row]) {
+            const int64_t row = PL(cell, R);
+            if (!knP[row]) {
                 int nc[3][9];
                 nb_cells(X, i, j, k, nc);
                 const uint64_t kb = kmask[2 * cell + 1];
-                acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, nc, kb, rr[row])
-                              : bts_row<SS>(val, z, lc, L.nloc, nc, kb, rr[row]);
+                acc = R == TT ? bts_row<TT>(val, z, lc, L.nloc, nc, kb, rr[row], 1, L.ps)
+                              : bts_row<SS>(val, z, lc, L.nloc, nc, kb, rr[row], 1, L.ps);
             }
         }
         sb[R - TT][k][ii] = acc;
@@ -2205,7 +2011,7 @@ static Lay lay_of(const iemic_ctx* c)
     Lay L;
     L.n = c->n; L.m = c->m; L.l = c->l; L.periodic = c->cfg.periodic; L.jb0 = c->jb0;
     L.ib0 = c->ib0; L.nx = c->nx; L.hx = c->hx; L.xb = c->xb;
-    L.nloc = c->nloc; L.own0 = c->own0;
+    L.nloc = c->nloc; L.own0 = c->own0; L.ps = c->next;
     return L;
 }
 /* colour-compacted T/S sweeps: the owned cells of one colour are every other cell of a
@@ -2902,13 +2708,14 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
     return 0;
 }
 
-/* the T/S block solve: right-hand side rr_TS - A_TS,D z_D from the dynamics iterate z, then
- * ts_mg V-cycles (or ts_sweeps symmetric red-black sweeps), result into z(T, S) -- for the
+/* the T/S block solve: right-hand side rr_TS - A_TS,D z_D from the dynamics iterate zd (the
+ * planar zP for the multigrid, the AoS output for the sweeps), then ts_mg V-cycles (or
+ * ts_sweeps symmetric red-black sweeps), result into z(T, S) of the output z -- for the
  * multigrid only when out (else later by k_mg_out).  side: the V-cycles (which read and
  * write only the multigrid's own buffers once the entry kernel has formed the right-hand
  * side) run on the side stream, forked after the entry kernel; gs_apply joins before
  * k_mg_out. */
-static int ts_solve(iemic_ctx* c, double* z, bool out, bool side = false)
+static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool side = false)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -2920,7 +2727,7 @@ static int ts_solve(iemic_ctx* c, double* z, bool out, bool side = false)
         const TsLev V0 = mg_view(c, 0);
         const int P = mg_lanes(c->l);
         const unsigned ge = (unsigned)(((c->nx + MG_TI - 1) / MG_TI) * V0.mb);
-        MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.known.p, gs.kmask.p, gs.rr.p, z, L, V0);
+        MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.knP.p, gs.kmask.p, gs.rrP.p, zd, L, V0);
         if (side) {
             HIP_OK(hipEventRecord(c->ev_fork, s));
             HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
@@ -2974,6 +2781,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.ready = 0;
     gs.ts_sweeps = opt ? std::max(0, opt->ts_sweeps) : 3;
     const int64_t NE = c->nerows, next = c->next;
+    if (c->l > 64) {
+        set_error("block GS: more than 64 levels per column (the column kernels hold a column in one workgroup)");
+        return IEMIC_EINVAL;
+    }
     const Lay L = lay_of(c);
     int rc = 0;
     if (gs.known.n < (size_t)NE) {
@@ -2994,12 +2805,15 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         rc |= gs.zs.alloc(next);
         rc |= gs.tcell.alloc(next);
         rc |= gs.tsdiag.alloc((size_t)4 * next);
+        rc |= gs.knP.alloc(NE);
+        rc |= gs.zP.alloc(NE);
+        rc |= gs.rrP.alloc(NE);
         if (rc) {
             set_error("block GS: out of device memory");
             return IEMIC_ENOMEM;
         }
         for (DevBuf<double>* bptr : {&gs.uvinv, &gs.tsinv, &gs.pw, &gs.rr, &gs.bts, &gs.tsoff, &gs.zt,
-                                     &gs.zs, &gs.tcell, &gs.tsdiag})
+                                     &gs.zs, &gs.tcell, &gs.tsdiag, &gs.zP, &gs.rrP})
             HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         HIP_OK(hipMemsetAsync(gs.kmask.p, 0, sizeof(uint64_t) * gs.kmask.n, c->stream));
         gs.flags_h.clear();
@@ -3016,6 +2830,8 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         if ((rc = halo_exchange_w(c, gs.rr.p, NUN, 1))) return rc;
         hipLaunchKernelGGL(k_d_to_u8, dim3(gN), dim3(256), 0, c->stream, gs.rr.p, gs.known.p, NE);
     }
+    hipLaunchKernelGGL(k_known_planar, dim3((unsigned)((next + 255) / 256)), dim3(256), 0, c->stream,
+                       gs.known.p, gs.knP.p, next);
     std::vector<uint8_t> kn(NE);
     if ((rc = d2h(c, kn.data(), gs.known.p, NE))) return rc;
     {
@@ -3090,93 +2906,64 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     return 0;
 }
 
-/* dynamics block: z(U/V/W/P) from the right-hand side rr (steps 1-5 of the header) */
-/* zo: when given, zo += omega z on the active U/V/W/P rows once z is final (the defect
- * correction's update, fused into the pass's last kernels where the column scans run) */
-static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0)
+/* dynamics block: z(U/V/W/P) from the right-hand side rr (steps 1-5 of the header), both
+ * component-planar (BlockGS::zP); zo: when given, zo += omega z on the active U/V/W/P rows
+ * once z is final (the defect correction's update, fused into the pass's last kernels where
+ * the column scans run); zaos: the pass's final values (zo's when given) also into the
+ * preconditioner output (AoS), on the last pass */
+static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0,
+                     double* zaos = nullptr)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
-    const unsigned gij = (unsigned)((c->nloc / c->l + 255) / 256);
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
     int rc = 0;
     const int64_t ncolb = c->nloc / c->l;                        /* water columns of the band */
-    const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : (c->l <= 64 ? 64 : 0));
+    const int Pl = c->l <= 16 ? 16 : (c->l <= 32 ? 32 : 64);     /* l <= 64 (gs_compute) */
     /* transposed column kernels: 1024 / Pl columns of one row per workgroup of 1024 threads */
-    const int cti = Pl ? 1024 / Pl : 1;
-    const unsigned gct = Pl ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx)) : 0u;
+    const int cti = 1024 / Pl;
+    const unsigned gct = xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx));
     const dim3 bct(1024u);
-    if (Pl != 0) {
-        /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
-         * after the Schur solve, then p and w */
-        if (band && (rc = halo_exchange(c, const_cast<double*>(rr), 1))) return rc;   /* rr around the band */
-        if (Pl == 16)
-            hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-        else if (Pl == 32)
-            hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-        else
-            hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* ptil above the band */
-        const double* sb = gs.colv_own.p;
-        if (band) {
-            HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
-                                  hipMemcpyDeviceToDevice, s));
-            if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
-            sb = gs.colv.p;
-        }
-        if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
-        hipLaunchKernelGGL(k_gs_uvp, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                           rr, gs.colv2.p, z, L, zo, omega);
-        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* uv below the band */
-        if (Pl == 16)
-            hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.colv2.p, z, L, rr, zo, omega);
-        else if (Pl == 32)
-            hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.colv2.p, z, L, rr, zo, omega);
-        else
-            hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.known.p,
-                               gs.colv2.p, z, L, rr, zo, omega);
-        return 0;
-    }
-    /* more than 64 levels: the cell / column kernels of the original pass */
-    hipLaunchKernelGGL(k_gs_ptil, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       rr, z, L);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* ptil above the band */
-    hipLaunchKernelGGL(k_gs_uvs, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       rr, z, L);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv* below the band  */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       rr, z, gs.tcell.p, L, 0);
-    hipLaunchKernelGGL(k_col_sum, dim3(gij), dim3(256), 0, s, gs.tcell.p, gs.col_of_ij.p,
-                       gs.pinned.p, gs.colv_own.p, L);
+    const int64_t ps = c->next;
+    /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
+     * after the Schur solve, then p and w */
+    if (band && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
+    if (Pl == 16)
+        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+    else if (Pl == 32)
+        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+    else
+        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+    if (band && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
     const double* sb = gs.colv_own.p;
     if (band) {
-        /* colv_own keeps 0 outside this band's columns; the sum goes to colv */
         HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
                               hipMemcpyDeviceToDevice, s));
         if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
         sb = gs.colv.p;
     }
     if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
-    hipLaunchKernelGGL(k_gs_uvfix, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.uvinv.p,
-                       gs.col_of_ij.p, gs.colv2.p, z, L, nullptr, 0.0);
-    if (band && (rc = halo_exchange(c, z, 1))) return rc;       /* uv below the band   */
-    hipLaunchKernelGGL(k_gs_pcell, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.pw.p,
-                       rr, z, gs.tcell.p, L, 1);
-    hipLaunchKernelGGL(k_gs_pw, dim3(gij), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.col_of_ij.p,
-                       gs.colv2.p, gs.tcell.p, z, L);
-    if (zo)
-        hipLaunchKernelGGL(k_dyn_add, dim3(gc), dim3(256), 0, s, gs.known.p, z, zo, L, omega);
+    hipLaunchKernelGGL(k_gs_uvp, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
+                       rr, gs.colv2.p, z, L, zo, omega, zaos);
+    if (band && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
+    if (Pl == 16)
+        hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.colv2.p, z, L, rr, zo, omega, zaos);
+    else if (Pl == 32)
+        hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.colv2.p, z, L, rr, zo, omega, zaos);
+    else
+        hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.colv2.p, z, L, rr, zo, omega, zaos);
     return 0;
 }
 
-int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* known, double* d);
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d);
 
 /* GPU time of the apply's parts (HIP events on the library stream, nrep back-to-back
  * launches each, zero data): us[0] one Schur solve (cyclic reduction), us[1] one T/S block
@@ -3197,15 +2984,17 @@ int gs_time_parts(iemic_ctx* c, int nrep, double* us)
     HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, s));
     HIP_OK(hipMemsetAsync(z, 0, sizeof(double) * c->nerows, s));
     HIP_OK(hipMemsetAsync(gs.rr.p, 0, sizeof(double) * c->nerows, s));
+    HIP_OK(hipMemsetAsync(gs.rrP.p, 0, sizeof(double) * c->nerows, s));
+    HIP_OK(hipMemsetAsync(gs.zP.p, 0, sizeof(double) * c->nerows, s));
     HIP_OK(hipMemsetAsync(gs.colv_own.p, 0, sizeof(double) * c->n * c->m, s));
     int rc = 0;
     for (int part = 0; part < 4 && !rc; part++) {
         auto once = [&]() -> int {
             switch (part) {
             case 0: return cr_solve(c, gs.cr, gs.colv_own.p, gs.colv2.p, s);
-            case 1: return ts_solve(c, z, true);
-            case 2: return dyn_solve(c, gs.rr.p, z);
-            default: return spmv_dyn_defect(c, z, c->d_tmp1.p, gs.known.p, gs.dres.p ? gs.dres.p : c->d_tmp1.p);
+            case 1: return ts_solve(c, gs.ts_mg > 0 ? gs.zP.p : z, z, true);
+            case 2: return dyn_solve(c, gs.rrP.p, gs.zP.p);
+            default: return spmv_dyn_defect(c, gs.zP.p, c->d_tmp1.p, gs.knP.p, gs.dres.p ? gs.dres.p : c->d_tmp1.p);
             }
         };
         if ((rc = once())) break;                  /* warm */
@@ -3229,6 +3018,8 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
     hipStream_t s = c->stream;
     const bool band = c->nranks > 1;
+    const int64_t ps = c->next;
+    double* zP = gs.zP.p;
     int rc = 0;
     /* the T/S block is solved with the right-hand side rr_TS - A_TS,D z_D of the dynamics
      * iterate after ts_at passes (default: after the last; the CPU twin: orc_gs_apply); the
@@ -3237,38 +3028,45 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     /* early T/S on one rank: its V-cycles run on the side stream beside the remaining
      * dynamics passes (both chains are latency-bound, so they overlap) */
     const bool par = ts_at < gs.dyn_iters && !band && gs.ts_mg > 0;
+    /* the dynamics passes iterate on the planar zP; the output z (AoS) gets their final
+     * values from the last pass (every pass for the T/S sweeps, which read z's AoS rows) */
+    const bool aos_all = gs.ts_mg <= 0;
+    auto zaos_of = [&](bool last) { return (last || aos_all) ? z : nullptr; };
     auto ts = [&]() -> int {
-        if (band && (ts_at < gs.dyn_iters || gs.dyn_iters > 1) && (rc = halo_exchange(c, z, 1))) return rc;
-        return ts_solve(c, z, ts_at == gs.dyn_iters, par);
+        if (band && (ts_at < gs.dyn_iters || gs.dyn_iters > 1)) {
+            rc = gs.ts_mg > 0 ? halo_exchange_planar(c, zP, NUN, ps, 1) : halo_exchange(c, z, 1);
+            if (rc) return rc;
+        }
+        return ts_solve(c, gs.ts_mg > 0 ? zP : z, z, ts_at == gs.dyn_iters, par);
     };
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
-                       r, z, gs.rr.p, L);
-    if ((rc = dyn_solve(c, gs.rr.p, z))) return rc;
+                       r, z, aos_all ? gs.rr.p : nullptr, zP, gs.rrP.p, L);
+    if ((rc = dyn_solve(c, gs.rrP.p, zP, nullptr, 0.0, zaos_of(gs.dyn_iters == 1)))) return rc;
     if (ts_at == 1 && gs.dyn_iters > 1 && (rc = ts())) return rc;
     /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
      * minimal-residual w (dyn_mr) or the fixed w = dyn_omega */
     if (gs.dyn_mr && gs.dyn_iters > 1) {
-        const int64_t o = NUN * c->own0, NL = c->nlrows;
-        if (band && (rc = halo_exchange(c, z, 1))) return rc;
-        if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
+        if (band && (rc = halo_exchange_planar(c, zP, NUN, ps, 1))) return rc;
+        if ((rc = spmv_dyn_defect(c, zP, r, gs.knP.p, gs.dres.p))) return rc;
         for (int it = 1; it < gs.dyn_iters; it++) {
+            const bool last = it + 1 == gs.dyn_iters;
             if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
-            if (band && (rc = halo_exchange(c, gs.zc.p, 1))) return rc;
-            if ((rc = spmv_dyn_defect(c, gs.zc.p, gs.dzero.p, gs.known.p, gs.dq.p))) return rc;
-            hipLaunchKernelGGL(k_mr_dots, dim3(MR_NB), dim3(256), 0, s, gs.dres.p + o, gs.dq.p + o, NL,
-                               gs.dmr.p);
+            if (band && (rc = halo_exchange_planar(c, gs.zc.p, NUN, ps, 1))) return rc;
+            if ((rc = spmv_dyn_defect(c, gs.zc.p, gs.dzero.p, gs.knP.p, gs.dq.p))) return rc;
+            hipLaunchKernelGGL(k_mr_dots, dim3(MR_NB), dim3(256), 0, s, gs.dres.p, gs.dq.p, L, gs.dmr.p);
             hipLaunchKernelGGL(k_mr_sum, dim3(1), dim3(64), 0, s, gs.dmr.p, MR_NB);
             if (band && (rc = allreduce_sum(c, gs.dmr.p + 2 * MR_NB, 2))) return rc;
-            hipLaunchKernelGGL(k_mr_update, dim3(gc), dim3(256), 0, s, gs.known.p, gs.dmr.p + 2 * MR_NB,
-                               gs.zc.p, gs.dq.p, z, gs.dres.p, L, it + 1 < gs.dyn_iters ? 1 : 0);
+            hipLaunchKernelGGL(k_mr_update, dim3(gc), dim3(256), 0, s, gs.knP.p, gs.dmr.p + 2 * MR_NB,
+                               gs.zc.p, gs.dq.p, zP, gs.dres.p, L, last ? 0 : 1, zaos_of(last));
         }
     }
     for (int it = 1; !gs.dyn_mr && it < gs.dyn_iters; it++) {
-        if (band && (rc = halo_exchange(c, z, 1))) return rc;   /* w, p of the neighbours */
-        if ((rc = spmv_dyn_defect(c, z, r, gs.known.p, gs.dres.p))) return rc;
-        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, z, gs.dyn_omega))) return rc;     /* z += w zc */
+        const bool last = it + 1 == gs.dyn_iters;
+        if (band && (rc = halo_exchange_planar(c, zP, NUN, ps, 1))) return rc;   /* w, p of the neighbours */
+        if ((rc = spmv_dyn_defect(c, zP, r, gs.knP.p, gs.dres.p))) return rc;
+        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last)))) return rc;   /* z += w zc */
         if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;
     }
     if (ts_at == gs.dyn_iters && (rc = ts())) return rc;

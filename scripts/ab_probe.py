@@ -2,7 +2,7 @@
 library (IEMIC_LIB, scripts/ab_build.sh): preconditioner apply, its parts, SpMV and a full
 Newton step, GPU-timed; run once per variant (the library is loaded once per process).
 
-usage: IEMIC_LIB=libiemic_amd_<v>.so python scripts/ab_probe.py <v> [newton steps]
+usage: IEMIC_LIB=libiemic_amd_<v>.so python scripts/ab_probe.py <v> [newton steps (0: none)]
 """
 import json
 import os
@@ -34,6 +34,9 @@ def main():
     if hasattr(_lib.lib(), "iemic_time_prec_parts"):
         out.update({k: round(v, 2) for k, v in oc.time_prec_parts(100).items()})
     out["spmv_us"] = round(oc.time_spmv(50) * 1e3, 2)
+    if nsteps == 0:                      # apply and SpMV timings only
+        print(json.dumps(out), flush=True)
+        return
     x0 = torch.from_numpy(x).cuda()
     L_ = _lib.lib()
     times, iters = [], []
