@@ -151,7 +151,7 @@ int cr_init(iemic_ctx* c, SchurCR& cr, int n, int m, int periodic, int tail_max 
 int cr_factor(iemic_ctx* c, SchurCR& cr, const double* S9, const int* col_of_ij);
 int cr_factor_blocks(iemic_ctx* c, SchurCR& cr);
 int cr_check(iemic_ctx* c, SchurCR& cr);
-int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s);
+int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s, double* xT = nullptr);
 int cr_inverse_dev(hipStream_t s, int m, const double* src, double* dst, int* info);
 
 /* Preconditioner state (prec.hip: block Jacobi, prec_gs.hip: block Gauss-Seidel). */
@@ -222,6 +222,7 @@ struct BlockGS {
      * dzero are planar too.  The AoS rr is kept for the T/S sweeps (ts_mg = 0) */
     DevBuf<uint8_t> knP;
     DevBuf<double> zP, rrP;
+    DevBuf<double> colvT;            /* the Schur solution transposed (j * n + i)          */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */
 };

@@ -775,7 +775,7 @@ __global__ void __launch_bounds__(1024) k_gs_pw_t(const double* __restrict__ val
         const double a = val[(int64_t)S_PW0 * ncell + (cell - L.own0)];
         const double b = val[(int64_t)S_PWM * ncell + (cell - L.own0)];
         const double rhs = rr[PL(cell, PP)] - duv_uv(val, knP, z, i, j, k, cell - L.own0, L);
-        pb = pbar[(int64_t)i * L.m + j];
+        pb = pbar[(int64_t)j * L.n + i];
         zp = z[PL(cell, PP)];
         if (wa && a != 0.0) {
             A = rhs / a;
@@ -1148,7 +1148,7 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
         if (!in) { pi = i; pj = j; }
         const int64_t pc = ecell(L, pi, pj, k);
         const uint8_t kp = knP[PL(pc, PP)];
-        const double p = z[PL(pc, PP)] + pbar[(int64_t)pi * m + pj];
+        const double p = z[PL(pc, PP)] + pbar[(int64_t)pj * n + pi];
         const double au = val[(int64_t)(S_UP + g4) * ncell + lc];
         const double av = val[(int64_t)(S_VP + g4) * ncell + lc];
         const bool use = in && !kp;
@@ -1983,6 +1983,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     rc |= gs.pinned.alloc(NC);
     rc |= gs.S9.alloc((size_t)9 * NC);
     rc |= gs.colv2.alloc(NC);
+    rc |= gs.colvT.alloc(NC);
     rc |= gs.colv_own.alloc(NC);
     rc |= gs.colv.alloc(NC);
     rc |= gs.own_pos.alloc(NC);
@@ -2947,19 +2948,19 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
         if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
         sb = gs.colv.p;
     }
-    if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s))) return rc;
+    if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s, gs.colvT.p))) return rc;
     hipLaunchKernelGGL(k_gs_uvp, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
-                       rr, gs.colv2.p, z, L, zo, omega, zaos);
+                       rr, gs.colvT.p, z, L, zo, omega, zaos);
     if (band && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
     if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.colv2.p, z, L, rr, zo, omega, zaos);
+                           gs.colvT.p, z, L, rr, zo, omega, zaos);
     else if (Pl == 32)
         hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.colv2.p, z, L, rr, zo, omega, zaos);
+                           gs.colvT.p, z, L, rr, zo, omega, zaos);
     else
         hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.colv2.p, z, L, rr, zo, omega, zaos);
+                           gs.colvT.p, z, L, rr, zo, omega, zaos);
     return 0;
 }
 

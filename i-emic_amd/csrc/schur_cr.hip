@@ -394,7 +394,7 @@ __global__ void k_cr_transpose(const double* __restrict__ X, double* __restrict_
  * eight independent accumulators), then a fixed shuffle tree (deterministic) */
 constexpr int CR_TAIL_MAX = 1024;          /* cr_init: tail_max */
 __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv, const double* __restrict__ b,
-                                                 double* __restrict__ x, int M)
+                                                 double* __restrict__ x, int M, double* __restrict__ xT, int nT, int m)
 {
     __shared__ double vb[CR_TAIL_MAX];
     const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -418,7 +418,10 @@ __global__ void __launch_bounds__(256) k_cr_tail(const double* __restrict__ Tinv
     double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) x[r] = v;
+    if (lane == 0) {
+        x[r] = v;
+        if (xT) xT[(int64_t)(r % m) * nT + r / m] = v;   /* a tail holding the whole problem */
+    }
 }
 
 /* Apply step (packed, CrStep): workgroup w computes rows [r0, r0 + RC) of one output block,
@@ -433,7 +436,7 @@ template <int RC, int CPT>
 __global__ void __launch_bounds__(256) k_cr_pk(const double* __restrict__ P, const CrCls cls,
                                                const CrWg* __restrict__ wgs, int m, const double* __restrict__ b,
                                                double* __restrict__ x, double* __restrict__ bv,
-                                               double* __restrict__ xv)
+                                               double* __restrict__ xv, double* __restrict__ xT, int nT)
 {
     constexpr int G = 256 / RC;
     __shared__ double vs[CR_MT + 1][192];          /* m <= 192 (cr_init) */
@@ -485,7 +488,11 @@ __global__ void __launch_bounds__(256) k_cr_pk(const double* __restrict__ P, con
     if (t < RC && r < m) {
         const double sum = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
         double* const ys[4] = {nullptr, x, bv, xv};
-        ys[d.yref >> 28][(d.yref & 0x0fffffff) + r] = sum;
+        const int yb = d.yref >> 28, yo = d.yref & 0x0fffffff;
+        ys[yb][yo + r] = sum;
+        /* the solution also transposed (row j of block i at j * n + i) for its consumers,
+         * whose lanes run along i */
+        if (xT && yb == 1) xT[(int64_t)r * nT + yo / m] = sum;
     }
 }
 
@@ -1092,14 +1099,16 @@ int cr_check(iemic_ctx* c, SchurCR& cr)
 /* x = S^-1 b (b, x: n*m, c = i*m + j): the levels above the tail in apply steps of one or
  * two levels each way (k_cr_multi), the tail (levels >= lt, tM = N[lt] m unknowns) one
  * dense GEMV */
-static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double* x, hipStream_t s)
+static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double* x, hipStream_t s,
+                    double* xT = nullptr)
 {
     const int m = cr.m;
     double* bv = const_cast<double*>(cr.bv.p);
     double* xv = const_cast<double*>(cr.xv.p);
     const dim3 g((unsigned)st.nwg), blk(256);
+    const int nT = cr.N[0];
 #define CR_PK(RC, CPT) hipLaunchKernelGGL((k_cr_pk<RC, CPT>), g, blk, 0, s, (const double*)st.P.p, st.cls, \
-                                          (const CrWg*)st.wg.p, m, b, x, bv, xv)
+                                          (const CrWg*)st.wg.p, m, b, x, bv, xv, xT, nT)
     if (st.rc == 16) {
         if (m <= 80) CR_PK(16, 5);
         else CR_PK(16, 12);
@@ -1113,7 +1122,7 @@ static void cr_step(const SchurCR& cr, const CrStep& st, const double* b, double
 #undef CR_PK
 }
 
-int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s)
+int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStream_t s, double* xT)
 {
     (void)c;
     auto bvec = [&](int l) { return l == 0 ? b : cr.bv.p + cr.v_off[l]; };
@@ -1122,11 +1131,13 @@ int cr_solve(iemic_ctx* c, const SchurCR& cr, const double* b, double* x, hipStr
     for (const CrStep& st : cr.down) cr_step(cr, st, b, x, s);
     if (cr.tM)
         hipLaunchKernelGGL(k_cr_tail, dim3((cr.tM + 3) / 4), dim3(256), 0, s, (const double*)cr.tinv.p, bvec(le),
-                           xvec(le), cr.tM);
+                           xvec(le), cr.tM, le == 0 ? xT : nullptr, cr.N[0], cr.m);
     else
         hipLaunchKernelGGL(k_cr_final, dim3((cr.m + CR_RC - 1) / CR_RC), dim3(256), 0, s,
                            (const double*)(cr.ap.p + cr.ap_off[cr.nlev]), bvec(le), xvec(le), cr.m, 1);
-    for (const CrStep& st : cr.up) cr_step(cr, st, b, x, s);
+    for (const CrStep& st : cr.up) cr_step(cr, st, b, x, s, xT);
+    if (xT && le == 0 && !cr.tM)           /* one block (n = 1): the transposed order is x's */
+        HIP_OK(hipMemcpyAsync(xT, x, sizeof(double) * cr.m, hipMemcpyDeviceToDevice, s));
     HIP_OK(hipGetLastError());
     return 0;
 }
