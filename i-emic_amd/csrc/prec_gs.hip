@@ -2058,6 +2058,15 @@ static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 /* lanes per z-line (one per level, a power of two >= l; the smoother needs l <= 64) */
 static int mg_lanes(int l) { return l <= 16 ? 16 : (l <= 32 ? 32 : 64); }
 
+/* the z-line and restriction launches in 64-thread workgroups (64 / P columns each): a
+ * coarse level's few columns spread over 4x the CUs of 256-thread groups (the T/S solve
+ * 112 -> 103 us per apply, scripts/ab/mg_wg64.sh) */
+#define MG_LAUNCH_P64(P, KERNEL, GRID, ...)                                                \
+    do {                                                                                   \
+        if ((P) == 16) hipLaunchKernelGGL(KERNEL<16>, dim3(GRID), dim3(64), 0, s, __VA_ARGS__); \
+        else if ((P) == 32) hipLaunchKernelGGL(KERNEL<32>, dim3(GRID), dim3(64), 0, s, __VA_ARGS__); \
+        else hipLaunchKernelGGL(KERNEL<64>, dim3(GRID), dim3(64), 0, s, __VA_ARGS__);     \
+    } while (0)
 #define MG_LAUNCH_P(P, KERNEL, GRID, ...)                                                  \
     do {                                                                                   \
         if ((P) == 16) hipLaunchKernelGGL(KERNEL<16>, dim3(GRID), dim3(256), 0, s, __VA_ARGS__); \
@@ -2627,11 +2636,11 @@ static int mg_zl(iemic_ctx* c, const TsLev& V, int colour, const TsLev* C, doubl
 {
     hipStream_t s = c->stream;
     const int P = mg_lanes(V.l);
-    const unsigned g = blocks_for(mg_columns_of(V, colour) * P);
+    const unsigned g = (unsigned)((mg_columns_of(V, colour) * P + 63) / 64);
     if (!g) return 0;
     const TsLev Cv = C ? *C : V;
     const int corr = C ? 1 : 0;
-    MG_LAUNCH_P(P, k_mg_zl, g, V, colour, Cv, corr, zout);
+    MG_LAUNCH_P64(P, k_mg_zl, g, V, colour, Cv, corr, zout);
     return 0;
 }
 
@@ -2689,7 +2698,7 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
         const int P = mg_lanes(V.l);
         const int shortcut = (first && nu == 1 && nc == 2) ? 1 : 0;
         const int relax = q + 1 < qc ? 1 : 0;
-        MG_LAUNCH_P(P, k_mg_rc, blocks_for((int64_t)C.n * C.mb * P), V, C, shortcut, relax);
+        MG_LAUNCH_P64(P, k_mg_rc, (unsigned)(((int64_t)C.n * C.mb * P + 63) / 64), V, C, shortcut, relax);
     }
     if (q + 1 == qc) {
         if ((rc = mg_coarsest(c, q + 1))) return rc;
