@@ -384,6 +384,16 @@ __global__ void __launch_bounds__(256) k_dcgs_dot(const double* __restrict__ V, 
  * each vector's two sums are reduced across the wave and accumulated per wave in LDS
  * (4 x (2 nvec + 3) doubles, dynamic).  Chunks are dealt to the nbx <= RED_BLOCKS workgroups
  * round robin.  partial[row * nbx + bx] as k_dcgs_dot. */
+/* 16-byte non-temporal load: the DCGS2 passes stream the basis (up to 1 GB at 2 degrees,
+ * past the Infinity Cache) once per pass, and keeping it out of the caches leaves them to
+ * u, w and the partial sums (dot pass 84.2 -> 73.7 us, update 84.0 -> 81.7 us,
+ * scripts/ab/dcgs_nt.sh) */
+__device__ __forceinline__ double2 ldnt2(const double2* p)
+{
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    return make_double2(v.x, v.y);
+}
 constexpr int DOT1_E = 4;
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -429,7 +439,7 @@ __global__ void __launch_bounds__(256) k_dcgs_dot1(const double* __restrict__ V,
         double2 qn[E];
         if (nvec > 0) {
 #pragma unroll
-            for (int k = 0; k < E; k++) qn[k] = reinterpret_cast<const double2*>(V)[ex[k]];
+            for (int k = 0; k < E; k++) qn[k] = ldnt2(reinterpret_cast<const double2*>(V) + ex[k]);
         }
         for (int i = 0; i < nvec; i++) {
             double2 q[E];
@@ -438,7 +448,7 @@ __global__ void __launch_bounds__(256) k_dcgs_dot1(const double* __restrict__ V,
             if (i + 1 < nvec) {
                 const double2* qv = reinterpret_cast<const double2*>(V + (int64_t)(i + 1) * ldv);
 #pragma unroll
-                for (int k = 0; k < E; k++) qn[k] = qv[ex[k]];
+                for (int k = 0; k < E; k++) qn[k] = ldnt2(qv + ex[k]);
             }
             double a = 0.0, b = 0.0;
 #pragma unroll
@@ -535,7 +545,7 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
         for (; i + UN <= nvec; i += UN) {
             double2 q[UN];
 #pragma unroll
-            for (int k = 0; k < UN; k++) q[k] = reinterpret_cast<const double2*>(V + (int64_t)(i + k) * ldv)[e];
+            for (int k = 0; k < UN; k++) q[k] = ldnt2(reinterpret_cast<const double2*>(V + (int64_t)(i + k) * ldv) + e);
 #pragma unroll
             for (int k = 0; k < UN; k++) {
                 sux += a[i + k] * q[k].x;
@@ -545,7 +555,7 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
             }
         }
         for (; i < nvec; i++) {
-            const double2 q = reinterpret_cast<const double2*>(V + (int64_t)i * ldv)[e];
+            const double2 q = ldnt2(reinterpret_cast<const double2*>(V + (int64_t)i * ldv) + e);
             sux += a[i] * q.x;
             suy += a[i] * q.y;
             swx += cc[i] * q.x;
