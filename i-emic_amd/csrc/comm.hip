@@ -374,12 +374,33 @@ int halo_exchange_w(iemic_ctx* c, double* v, int width, int depth)
 }
 
 /* halo of a component-planar vector: nplanes planes of ps doubles (one per unknown, each
- * in the ext cell order), exchanged as one x and one y batch */
+ * in the ext cell order), exchanged as one x and one y batch.  RCCL sends each plane's
+ * contiguous slab from the vector (one group); the host and in-process transports, whose
+ * cost is per message, send the planes' slabs of a message as one strided segment (nplanes
+ * blocks at stride ps) -- same plan on every rank, so the pairing rule holds */
 int halo_exchange_planar(iemic_ctx* c, double* v, int nplanes, int64_t ps, int depth)
 {
     if (c->nranks <= 1) return 0;
-    std::vector<Msg> x, y;
-    for (int q = 0; q < nplanes; q++) halo_plan_ext(c, v + (int64_t)q * ps, 1, depth, x, y);
+    std::vector<Msg> x0, y0, x, y;
+    halo_plan_ext(c, v, 1, depth, x0, y0);
+    const bool merge = c->group || c->tp.send;
+    for (auto* pr : {&x0, &y0}) {
+        std::vector<Msg>& out = pr == &x0 ? x : y;
+        for (const Msg& m : *pr) {
+            if (merge && m.s.nblk == 1) {
+                Msg mm = m;
+                mm.s.nblk = nplanes;
+                mm.s.stride = ps;
+                out.push_back(mm);
+            } else {
+                for (int q = 0; q < nplanes; q++) {
+                    Msg mq = m;
+                    mq.s.base = v + (int64_t)q * ps;
+                    out.push_back(mq);
+                }
+            }
+        }
+    }
     int rc = run_msgs(c, x);
     if (rc) return rc;
     return run_msgs(c, y);
