@@ -708,13 +708,14 @@ static std::vector<OutSpec> step_outputs(const SchurCR& cr, int l0, int nl, bool
     return out;
 }
 
-/* the packed form of one apply step (CrStep): rows per chunk so that the step has >= 448
- * workgroups where it can (the small steps of the deep levels would leave CUs idle), the
- * workgroups sorted by matrix-term count into classes, the set-up copy jobs */
+/* the packed form of one apply step (CrStep): 8 rows per chunk (16 measured 1.3 ms slower per
+ * Newton step at 2 degrees, scripts/ab/cr_rc8.sh), fewer where the step would have < 448
+ * workgroups (the small steps of the deep levels would leave CUs idle), the workgroups
+ * sorted by matrix-term count into classes, the set-up copy jobs */
 static int cr_pack_step(iemic_ctx* c, const SchurCR& cr, const std::vector<CrOut>& outs, CrStep& st)
 {
     const int m = cr.m;
-    int rcw = 16;
+    int rcw = 8;
     while (rcw > 4 && (int64_t)outs.size() * ((m + rcw - 1) / rcw) < 448) rcw /= 2;
     const int nch = (m + rcw - 1) / rcw;
     struct W { int nA, o, ch; };
