@@ -161,6 +161,7 @@ struct BlockGS {
     int ts_sweeps = 3;               /* symmetric red-black sweeps on the T/S block     */
     DevBuf<double> dinv;             /* block-Jacobi: 6x6 inverses, slot-major          */
     /* structure (rebuilt when the identity-row pattern changes) */
+    DevBuf<double> flags_d;          /* the same flags on the device (k_band_flags)       */
     std::vector<double> flags_h;     /* global (active column, U/V point) flags the      */
                                      /* structure was built for                         */
     int ncol = 0;                    /* active water columns                            */

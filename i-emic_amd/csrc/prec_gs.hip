@@ -638,6 +638,26 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     }
 }
 
+/* per owned water column (i, j): 1 in flags[j n + i] if a P row of it is active, 1 in
+ * flags[n m + j n + i] if a U or V row is (the host's Schur structure input; band_flags did
+ * this on a host copy of all the flags) */
+__global__ void k_band_flags(const uint8_t* __restrict__ known, Lay L, double* __restrict__ flags)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ncol = L.nloc / L.l;
+    if (t >= ncol) return;
+    const int il = (int)(t % L.nx), jl = (int)(t / L.nx);
+    bool p = false, uv = false;
+    for (int k = 0; k < L.l; k++) {
+        const int64_t cell = L.own0 + ((int64_t)jl * L.l + k) * L.nx + il;
+        p |= !known[NUN * cell + PP];
+        uv |= !known[NUN * cell + UU] || !known[NUN * cell + VV];
+    }
+    const int64_t q = (int64_t)(L.jb0 + jl) * L.n + L.ib0 + il;
+    if (p) flags[q] = 1.0;
+    if (uv) flags[(int64_t)L.n * L.m + q] = 1.0;
+}
+
 /* the identity-row flags in the planar layout */
 __global__ void k_known_planar(const uint8_t* __restrict__ known, uint8_t* __restrict__ knP, int64_t next)
 {
@@ -1858,19 +1878,6 @@ __global__ void k_mg_fac(TsLev V, double* __restrict__ fac)
 
 /* flags[j*n+i] = 1 for an active water column (any active P), flags[n*m + j*n+i] = 1
  * for an active U/V point, over the band's latitude rows */
-static void band_flags(const iemic_ctx* c, const std::vector<uint8_t>& kn, std::vector<double>& flags)
-{
-    const int n = c->n, m = c->m, l = c->l;
-    flags.assign((size_t)2 * n * m, 0.0);
-    for (int j = c->jb0; j < c->jb1; j++)
-        for (int i = c->ib0; i < c->ib1; i++)
-            for (int k = 0; k < l; k++) {
-                const int64_t cc = c->su.ext_cell(i, j, k);
-                if (!kn[NUN * cc + PP]) flags[(size_t)j * n + i] = 1.0;
-                if (!kn[NUN * cc + UU] || !kn[NUN * cc + VV]) flags[(size_t)n * m + j * n + i] = 1.0;
-            }
-}
-
 /* Schur structure of the whole grid from the global flags (identical on every rank) */
 int build_structure(iemic_ctx* c, const std::vector<double>& flags)
 {
@@ -2842,19 +2849,16 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     }
     hipLaunchKernelGGL(k_known_planar, dim3((unsigned)((next + 255) / 256)), dim3(256), 0, c->stream,
                        gs.known.p, gs.knP.p, next);
-    std::vector<uint8_t> kn(NE);
-    if ((rc = d2h(c, kn.data(), gs.known.p, NE))) return rc;
     {
         /* global column / U/V-point flags: the Schur structure is that of the whole grid */
-        std::vector<double> flags;
-        band_flags(c, kn, flags);
-        if (c->nranks > 1) {
-            DevBuf<double> fb;
-            if (fb.alloc(flags.size())) return IEMIC_ENOMEM;
-            if ((rc = h2d(c, fb.p, flags.data(), sizeof(double) * flags.size()))) return rc;
-            if ((rc = allreduce_sum(c, fb.p, (int)flags.size()))) return rc;
-            if ((rc = d2h(c, flags.data(), fb.p, sizeof(double) * flags.size()))) return rc;
-        }
+        const size_t nf = (size_t)2 * c->n * c->m;
+        if (gs.flags_d.n < nf && gs.flags_d.alloc(nf)) return IEMIC_ENOMEM;
+        HIP_OK(hipMemsetAsync(gs.flags_d.p, 0, sizeof(double) * nf, c->stream));
+        hipLaunchKernelGGL(k_band_flags, dim3((unsigned)((c->nloc / c->l + 255) / 256)), dim3(256), 0, c->stream,
+                           gs.known.p, L, gs.flags_d.p);
+        if ((rc = allreduce_sum(c, gs.flags_d.p, (int)nf))) return rc;
+        std::vector<double> flags(nf);
+        if ((rc = d2h(c, flags.data(), gs.flags_d.p, sizeof(double) * nf))) return rc;
         if (flags != gs.flags_h)
             if ((rc = build_structure(c, flags))) return rc;
     }
