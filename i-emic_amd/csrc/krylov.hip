@@ -1086,6 +1086,38 @@ __global__ void k_idr_random(double* __restrict__ P, int64_t ldp, int s, int64_t
     }
 }
 
+/* two independent combinations in one pass (y1 = a1 y1 + sum c_i X_i, y2 likewise) */
+__global__ void __launch_bounds__(256) k_lincomb2(LinComb L1, double* y1, LinComb L2, double* y2, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double a1 = L1.a == 0.0 ? 0.0 : L1.a * y1[q];
+        for (int i = 0; i < L1.nv; i++) a1 += L1.c[i] * L1.X[i][q];
+        double a2 = L2.a == 0.0 ? 0.0 : L2.a * y2[q];
+        for (int i = 0; i < L2.nv; i++) a2 += L2.c[i] * L2.X[i][q];
+        y1[q] = a1;
+        y2[q] = a2;
+    }
+}
+static LinComb make_lc(double a, const std::vector<double>& cs, const std::vector<const double*>& xs, int64_t o)
+{
+    LinComb L{};
+    L.a = a;
+    for (size_t q = 0; q < cs.size() && q < 16; q++) {
+        L.c[L.nv] = cs[q];
+        L.X[L.nv] = xs[q] + o;
+        L.nv++;
+    }
+    return L;
+}
+static void lincomb2(iemic_ctx* c, double a1, double* y1, const std::vector<double>& c1,
+                     const std::vector<const double*>& x1, double a2, double* y2, const std::vector<double>& c2,
+                     const std::vector<const double*>& x2, int64_t o, int64_t NL)
+{
+    hipLaunchKernelGGL(k_lincomb2, dim3(grid_for(NL)), dim3(256), 0, c->stream, make_lc(a1, c1, x1, o), y1 + o,
+                       make_lc(a2, c2, x2, o), y2 + o, NL);
+}
+
 static void lincomb(iemic_ctx* c, double a, double* y, std::initializer_list<std::pair<double, const double*>> terms,
                     int64_t o, int64_t NL)
 {
@@ -1210,8 +1242,8 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
         for (int k = 0; k < s; k++) {
             if (jj > 0) {
                 /* gamma from the lower-triangular M(k:s, k:s); v = r - G(:, k:s) gamma */
-                std::vector<double> cs;
-                std::vector<const double*> xs;
+                std::vector<double> cs{1.0};
+                std::vector<const double*> xs{r};
                 for (int i = k; i < s; i++) {
                     double gi = f[i];
                     for (int j = k; j < i; j++) gi -= M[i][j] * gamma[j];
@@ -1219,8 +1251,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
                     cs.push_back(-gamma[i]);
                     xs.push_back(Gi(i));
                 }
-                HIP_OK(hipMemcpyAsync(v, r, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
-                lincomb_v(c, 1.0, v, cs, xs, o, NL);
+                lincomb_v(c, 0.0, v, cs, xs, o, NL);                             /* v = r - G gamma */
                 if ((rc = prec(v, t))) return rc;
                 /* U(:,k) = om t + U(:, k:s) gamma */
                 cs.clear();
@@ -1260,8 +1291,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
                 std::vector<double> cs;
                 std::vector<const double*> xg, xu;
                 for (int i = 0; i < k; i++) { cs.push_back(-al[i]); xg.push_back(Gi(i)); xu.push_back(Ui(i)); }
-                lincomb_v(c, 1.0, Gi(k), cs, xg, o, NL);
-                lincomb_v(c, 1.0, Ui(k), cs, xu, o, NL);
+                lincomb2(c, 1.0, Gi(k), cs, xg, 1.0, Ui(k), cs, xu, o, NL);
             }
             if (!std::isfinite(M[k][k])) return nonfinite();
             if (M[k][k] == 0.0) {
@@ -1269,8 +1299,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
                 return IEMIC_ERANGE;
             }
             const double beta = f[k] / M[k][k];
-            lincomb(c, 1.0, r, {{-beta, Gi(k)}}, o, NL);                         /* r -= beta G */
-            lincomb(c, 1.0, x, {{beta, Ui(k)}}, o, NL);                          /* x += beta U */
+            lincomb2(c, 1.0, r, {-beta}, {Gi(k)}, 1.0, x, {beta}, {Ui(k)}, o, NL);   /* r -= beta G, x += beta U */
             if (opt->idr_replace) {
                 if ((rc = set_normr(dot(c, r, r, 0)))) return rc;
                 if (normr > tolb / mp) trueres = true;
@@ -1294,8 +1323,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
         const double rho = std::fabs(ts / (nt * normr));
         om = ts / (nt * nt);
         if (rho < angle) om = om * angle / rho;                                 /* calc_omega */
-        lincomb(c, 1.0, r, {{-om, t}}, o, NL);
-        lincomb(c, 1.0, x, {{om, v}}, o, NL);
+        lincomb2(c, 1.0, r, {-om}, {t}, 1.0, x, {om}, {v}, o, NL);
         if (opt->idr_replace) {
             if ((rc = set_normr(dot(c, r, r, 0)))) return rc;
             if (normr > tolb / mp) trueres = true;
