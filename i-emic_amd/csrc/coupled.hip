@@ -636,6 +636,18 @@ __global__ void __launch_bounds__(256) k_clincomb(LinC L, double* y, int64_t N)
         y[q] = acc;
     }
 }
+/* two independent combinations in one pass (the paired IDR updates) */
+__global__ void __launch_bounds__(256) k_clincomb2(LinC L1, double* y1, LinC L2, double* y2, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x) {
+        double a1 = L1.a == 0.0 ? 0.0 : L1.a * y1[q];
+        for (int i = 0; i < L1.nv; i++) a1 += L1.c[i] * L1.X[i][q];
+        double a2 = L2.a == 0.0 ? 0.0 : L2.a * y2[q];
+        for (int i = 0; i < L2.nv; i++) a2 += L2.c[i] * L2.X[i][q];
+        y1[q] = a1;
+        y2[q] = a2;
+    }
+}
 /* IDR shadow space: uniform in [-1, 1] from splitmix64 over the packed row index */
 __global__ void k_cidr_random(double* __restrict__ P, int64_t ld, int s, int64_t N)
 {
@@ -1357,7 +1369,7 @@ double cdot_host(iemic_coupled* cm, const double* V, int64_t ld, int nv, const d
 }  // namespace
 
 namespace {
-void clin(iemic_coupled* cm, double a, double* y, const std::vector<double>& cs, const std::vector<const double*>& xs)
+LinC make_linc(double a, const std::vector<double>& cs, const std::vector<const double*>& xs)
 {
     LinC L{};
     L.a = a;
@@ -1366,7 +1378,18 @@ void clin(iemic_coupled* cm, double a, double* y, const std::vector<double>& cs,
         L.X[L.nv] = xs[q];
         L.nv++;
     }
-    hipLaunchKernelGGL(k_clincomb, dim3(blocks_for(cm->NC)), dim3(256), 0, cm->oc->stream, L, y, cm->NC);
+    return L;
+}
+void clin(iemic_coupled* cm, double a, double* y, const std::vector<double>& cs, const std::vector<const double*>& xs)
+{
+    hipLaunchKernelGGL(k_clincomb, dim3(blocks_for(cm->NC)), dim3(256), 0, cm->oc->stream, make_linc(a, cs, xs), y,
+                       cm->NC);
+}
+void clin2(iemic_coupled* cm, double a1, double* y1, const std::vector<double>& c1, const std::vector<const double*>& x1,
+           double a2, double* y2, const std::vector<double>& c2, const std::vector<const double*>& x2)
+{
+    hipLaunchKernelGGL(k_clincomb2, dim3(blocks_for(cm->NC)), dim3(256), 0, cm->oc->stream, make_linc(a1, c1, x1), y1,
+                       make_linc(a2, c2, x2), y2, cm->NC);
 }
 
 /* IDR(s) on the packed coupled vector (IDRSolver.H:109-340: the same restatement as the
@@ -1426,8 +1449,8 @@ int coupled_idrs(iemic_coupled* cm, const double* b, double* x, const iemic_kryl
         cdot_host(cm, P, NC, s, r, f.data());                         /* f = P' r */
         for (int k = 0; k < s; k++) {
             if (jj > 0) {
-                std::vector<double> cs;
-                std::vector<const double*> xs;
+                std::vector<double> cs{1.0};
+                std::vector<const double*> xs{r};
                 for (int i = k; i < s; i++) {
                     double gi = f[i];
                     for (int j = k; j < i; j++) gi -= M[i][j] * gamma[j];
@@ -1435,8 +1458,7 @@ int coupled_idrs(iemic_coupled* cm, const double* b, double* x, const iemic_kryl
                     cs.push_back(-gamma[i]);
                     xs.push_back(Gi(i));
                 }
-                HIP_OK(hipMemcpyAsync(v, r, sizeof(double) * NC, hipMemcpyDeviceToDevice, st));
-                clin(cm, 1.0, v, cs, xs);
+                clin(cm, 0.0, v, cs, xs);                                    /* v = r - G gamma */
                 if ((rc = prec(v, t))) return rc;
                 cs.assign(1, om);
                 xs.assign(1, t);
@@ -1462,16 +1484,14 @@ int coupled_idrs(iemic_coupled* cm, const double* b, double* x, const iemic_kryl
                 std::vector<double> cs;
                 std::vector<const double*> xg, xu;
                 for (int i = 0; i < k; i++) { cs.push_back(-al[i]); xg.push_back(Gi(i)); xu.push_back(Ui(i)); }
-                clin(cm, 1.0, Gi(k), cs, xg);
-                clin(cm, 1.0, Ui(k), cs, xu);
+                clin2(cm, 1.0, Gi(k), cs, xg, 1.0, Ui(k), cs, xu);
             }
             if (!std::isfinite(M[k][k]) || M[k][k] == 0.0) {
                 set_error("coupled IDR(s): breakdown");
                 return IEMIC_ERANGE;
             }
             const double beta = f[k] / M[k][k];
-            clin(cm, 1.0, r, {-beta}, {Gi(k)});
-            clin(cm, 1.0, x, {beta}, {Ui(k)});
+            clin2(cm, 1.0, r, {-beta}, {Gi(k)}, 1.0, x, {beta}, {Ui(k)});
             normr = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, r, tmp.data())));
             if (!std::isfinite(normr)) {
                 set_error("coupled IDR(s): non-finite residual");
@@ -1498,8 +1518,7 @@ int coupled_idrs(iemic_coupled* cm, const double* b, double* x, const iemic_kryl
         const double rho = std::fabs(ts / (nt * normr));
         om = ts / (nt * nt);
         if (rho < angle) om = om * angle / rho;
-        clin(cm, 1.0, r, {-om}, {t});
-        clin(cm, 1.0, x, {om}, {v});
+        clin2(cm, 1.0, r, {-om}, {t}, 1.0, x, {om}, {v});
         normr = std::sqrt(std::max(0.0, cdot_host(cm, nullptr, 0, 0, r, tmp.data())));
         if (opt->idr_replace && normr > tolb / mp) trueres = true;
         if (trueres && normr < normb) {
