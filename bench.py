@@ -118,8 +118,13 @@ def parse():
     p.add_argument("--cold-reps", type=int, default=0,
                    help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-samples", type=int, default=3,
+    p.add_argument("--save-x1", default=None,
+                   help="write the state after the last timed Newton step (gathered from all ranks) "
+                        "and the starting state to this .npz (rank 0), for parity checks")
+    p.add_argument("--cpu-samples", type=int, default=5,
                    help="timed CPU Newton steps (the line reports their median and spread)")
+    p.add_argument("--cpu-warmup", type=int, default=2,
+                   help="untimed CPU Newton steps before the timed ones (SURVEY §8d: 2)")
     p.add_argument("--mode", default="newton", choices=["newton", "continuation"],
                    help="continuation: config C5, one pseudo-arclength continuation step of the "
                         "1-degree ocean (run/ocean settings) from bench_data/<config>_cf05.npz")
@@ -135,12 +140,14 @@ def cpu_baseline(cfg, L, x, args):
     damped defect-correction passes on the dynamics block, one T/S aggregation-multigrid
     V-cycle with z-line smoothing: oracle/prec_oracle.c, the GPU apply's CPU twin; Schur by
     band LU), FGMRES(krylov) with restarts to the same tolerance (CGS2), x += dx, new F.
-    args.cpu_samples timed steps; the value is their median."""
+    args.cpu_warmup untimed steps, then args.cpu_samples timed steps; the value is their
+    median (10 after 2 warm-ups; 5 keep the default line within minutes)."""
     from oracle import oracle as orc
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
     samples = []
-    for _ in range(max(1, args.cpu_samples)):
+    nwarm = max(0, args.cpu_warmup)
+    for it in range(nwarm + max(1, args.cpu_samples)):
         T0 = time.perf_counter()
         t = time.perf_counter()
         F = o.rhs(x)
@@ -157,15 +164,18 @@ def cpu_baseline(cfg, L, x, args):
                                    maxit=args.krylov * (args.restarts + 1))
         t_solve = time.perf_counter() - t
         F1 = o.rhs(x + dx)
-        samples.append(time.perf_counter() - T0)
+        if it >= nwarm:
+            samples.append(time.perf_counter() - T0)
         del P
     ms = sorted(v * 1e3 for v in samples)
     med = float(np.median(ms))
     return {
         "value": round(med, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
         "samples_ms": [round(v, 1) for v in ms], "spread_ms": round(ms[-1] - ms[0], 1),
-        "sample": (f"median of {len(ms)} timed full Newton steps (SURVEY §8d asks for 10 after 2 "
-                   f"warm-ups; {len(ms)} keep the line within minutes) on the oracle C port "
+        "warmup": nwarm,
+        "sample": (f"median of {len(ms)} timed full Newton steps after {nwarm} untimed warm-up steps "
+                   f"(SURVEY §8d asks for 10 after 2 warm-ups; {len(ms)} keep the line within minutes) "
+                   f"on the oracle C port "
                    f"(OpenMP {cores} threads), same state and algorithm; last: F {t_rhs*1e3:.0f} ms, "
                    f"J {t_jac*1e3:.0f} ms, block GS set-up {t_prec*1e3:.0f} ms (dyn x{args.dyn_iters}, "
                    f"T/S multigrid x{args.ts_mg}), FGMRES({args.krylov}) {its} iterations to {rel:.1e} "
@@ -553,6 +563,16 @@ def main():
             print(f"bench.py: ranks disagree on the communicator size ({rs.tolist()})", file=sys.stderr)
             sys.exit(2)
 
+    if args.save_x1:
+        # the updated state of the last timed step: each rank's owned rows, summed over ranks
+        x1 = oc.getState()
+        if dist:
+            t1 = torch.from_numpy(x1).to("cpu" if host else dev)
+            dist.all_reduce(t1)
+            x1 = t1.cpu().numpy()
+        if rank == 0:
+            np.savez(args.save_x1, x0=x0h, x1=x1)
+
     # SpMV roofline: the k_spmv launches of the timed Newton steps themselves (HIP events
     # on the library stream around every SpMV inside FGMRES; at N > 1 the span includes
     # the halo exchange), so the rocprofv3 average of the same command agrees.
@@ -593,6 +613,8 @@ def main():
                   "hbm_bytes_per_launch": d["hbm_bytes_per_launch"], "avg_us": d["avg_us"],
                   "achieved": round(dg, 1), "frac": round(dg / HBM_PEAK_GBS, 4),
                   "source": f"bench_data/pmc_{PMC_TAG}.json (PMC bytes / rocprofv3 kernel-trace average)"}
+
+    real_gbps = (traffic if traffic else ell) / (spmv_ms * 1e-3) / 1e9
 
     # STREAM-copy rate of this box: device-to-device copy of 1 GiB, read +
     # write bytes / time, median of 5 -- the achievable HBM rate beside the 8 TB/s spec
@@ -656,10 +678,15 @@ def main():
                  "per_newton_step": {k: round(v / args.steps, 1) for k, v in comm.items()},
                  "rank": rank},
         "spmv_gbps": round(achieved, 1),
+        # frac on the bytes the kernel really moves: the PMC counter bytes per launch when the
+        # table matches these sources, else the stencil-ELL minimum (values + x + y); the
+        # CSR-equivalent figure of SURVEY §8d (12 nnz + 20 N) is kept apart as frac_csr
         "roofline": {"kernel": "k_spmv (per GPU, rank 0; in-solve launches)", "bound": "hbm",
-                     "achieved": round(achieved, 1),
+                     "achieved": round(real_gbps, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac": round(real_gbps / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_basis": "traffic (PMC)" if traffic else "stencil_ell_bytes",
+                     "achieved_csr": round(achieved, 1), "frac_csr": round(achieved / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes": bsp, "stencil_ell_bytes": ell,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
                      "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp,

@@ -27,6 +27,8 @@ using namespace iemic;
 
 extern "C" const char* iemic_last_error(void) { return g_err.c_str(); }
 
+extern "C" int iemic_abi_version(void) { return IEMIC_ABI_VERSION; }
+
 extern "C" int iemic_device_count(void)
 {
     int n = 0;
@@ -262,6 +264,11 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
         delete c;
         return rc;
     }
+    if (sub.nranks > 1 && (rc = comm_verify_plans(c))) {
+        comm_destroy(c);
+        delete c;
+        return rc;
+    }
     const int64_t NE = c->nerows;
     rc |= c->d_landm.alloc(nl);
     rc |= c->d_ftab.alloc((size_t)3 * (m + 2) + (size_t)n * m);
@@ -477,6 +484,13 @@ extern "C" int iemic_comm_stats(iemic_ctx* c, int64_t* out4)
         out4[q] = c->stat[q];
         c->stat[q] = 0;
     }
+    return 0;
+}
+
+extern "C" int iemic_set_comm_timeout(iemic_ctx* c, double seconds)
+{
+    if (!c || !(seconds > 0.0)) return IEMIC_EINVAL;
+    c->comm_timeout_s = seconds;
     return 0;
 }
 

@@ -13,10 +13,12 @@
  */
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -49,7 +51,9 @@ struct LocalGroup {
     /* point-to-point mailbox: (src, dst, k) -> the k-th message src sent to dst in a batch */
     std::map<std::tuple<int, int, int>, std::vector<double>> box;
     explicit LocalGroup(int p) : P(p), slot(p), vec(p, nullptr), ctxs(p, nullptr) {}
-    void barrier()
+    /* false when the other ranks did not all arrive within timeout_s (the caller withdraws
+     * and reports; the group is unusable afterwards, as a communicator after an abort) */
+    bool barrier(double timeout_s)
     {
         std::unique_lock<std::mutex> lk(mu);
         const int gen = generation;
@@ -57,11 +61,23 @@ struct LocalGroup {
             arrived = 0;
             generation++;
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != gen; });
+            return true;
         }
+        if (cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return generation != gen; }))
+            return true;
+        arrived--;
+        return false;
     }
 };
+
+static int group_barrier(iemic_ctx* c, LocalGroup* g, const char* what)
+{
+    if (g->barrier(c->comm_timeout_s)) return 0;
+    set_error(std::string("rank group: ") + what + " on rank " + std::to_string(c->rank) +
+              ": the other ranks did not arrive within " + std::to_string(c->comm_timeout_s) +
+              " s (a rank skipped the collective or its exchange plan differs)");
+    return IEMIC_EDEVICE;
+}
 
 static int host_allreduce(iemic_ctx* c, double* dev, int count)
 {
@@ -82,11 +98,18 @@ static int local_allreduce(iemic_ctx* c, double* dev, int count)
     mine.resize(count);
     int rc = d2h(c, mine.data(), dev, sizeof(double) * count);
     if (rc) return rc;
-    g->barrier();
+    if ((rc = group_barrier(c, g, "all-reduce"))) return rc;
     std::vector<double> sum(count, 0.0);
-    for (int r = 0; r < g->P; r++)
+    for (int r = 0; r < g->P; r++) {
+        if (g->slot[r].size() != (size_t)count) {
+            set_error("rank group: all-reduce of " + std::to_string(count) + " doubles on rank " +
+                      std::to_string(c->rank) + ", " + std::to_string(g->slot[r].size()) + " on rank " +
+                      std::to_string(r));
+            return IEMIC_EINVAL;
+        }
         for (int q = 0; q < count; q++) sum[q] += g->slot[r][q];
-    g->barrier();
+    }
+    if ((rc = group_barrier(c, g, "all-reduce"))) return rc;
     return h2d(c, dev, sum.data(), sizeof(double) * count);
 }
 
@@ -147,14 +170,62 @@ int comm_size(const iemic_ctx* c, int* size, int* kind)
     return 0;
 }
 
+/* Bounded wait for the RCCL work enqueued on the stream (fail-fast for the first
+ * all-reduce and the first halo batch of a context, where a plan mismatch or a missing peer
+ * would otherwise hang the process until an outside time limit): polls the stream and the
+ * communicator's asynchronous error; on an error or after comm_timeout_s the communicator is
+ * aborted (its kernels see the abort flag and return) and the call fails naming `what`. */
+static int rccl_wait(iemic_ctx* c, const std::string& what)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    for (int it = 0;; it++) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) {
+            set_error(what + ": " + hipGetErrorString(q));
+            return IEMIC_EDEVICE;
+        }
+        ncclResult_t ae = ncclSuccess;
+        const bool failed = ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+                            ae != ncclInProgress;
+        const double dt = std::chrono::duration<double>(clk::now() - t0).count();
+        if (failed || dt > c->comm_timeout_s) {
+            (void)ncclCommAbort(comm);
+            c->comm = nullptr;
+            set_error(what + " on rank " + std::to_string(c->rank) + ": " +
+                      (failed ? std::string("RCCL error ") + ncclGetErrorString(ae)
+                              : "not complete after " + std::to_string(c->comm_timeout_s) +
+                                    " s (a peer never posted the matching call)") +
+                      "; communicator aborted");
+            return IEMIC_EDEVICE;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(it < 1000 ? 20 : 1000));
+    }
+}
+
+static int rccl_live(iemic_ctx* c)
+{
+    if (c->comm) return 0;
+    set_error("RCCL communicator was aborted by an earlier failure");
+    return IEMIC_EDEVICE;
+}
+
 int allreduce_sum(iemic_ctx* c, double* dev, int count)
 {
     if (c->nranks <= 1 || count <= 0) return 0;
     c->stat[3]++;
     if (c->group) return local_allreduce(c, dev, count);
     if (c->tp.send) return host_allreduce(c, dev, count);
+    int rc = rccl_live(c);
+    if (rc) return rc;
     NCCL_OK(ncclAllReduce(dev, dev, (size_t)count, ncclDouble, ncclSum, (ncclComm_t)c->comm,
                           c->stream));
+    if (!(c->comm_checked & 1)) {
+        c->comm_checked |= 1;
+        return rccl_wait(c, "first all-reduce (" + std::to_string(count) + " doubles)");
+    }
     return 0;
 }
 
@@ -233,7 +304,7 @@ static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
         std::lock_guard<std::mutex> lk(g->mu);
         g->box[std::make_tuple(c->rank, op.peer, ksend[op.peer]++)] = std::move(h);
     }
-    g->barrier();
+    if ((rc = group_barrier(c, g, "halo batch"))) return rc;
     for (size_t q = 0; q < ops.size(); q++) {
         const Msg& op = ops[q];
         if (op.send) continue;
@@ -253,8 +324,7 @@ static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
     }
     if ((rc = unstage_recvs(c, ops, buf))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
-    g->barrier();
-    return 0;
+    return group_barrier(c, g, "halo batch");
 }
 
 /* the caller's host transport: all sends (staged), all receives, wait, unpack */
@@ -305,8 +375,9 @@ static int run_host(iemic_ctx* c, const std::vector<Msg>& ops)
 static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
 {
     std::vector<double*> buf;
-    int rc = stage_sends(c, ops, buf);
+    int rc = rccl_live(c);
     if (rc) return rc;
+    if ((rc = stage_sends(c, ops, buf))) return rc;
     ncclComm_t comm = (ncclComm_t)c->comm;
     ncclResult_t first = ncclSuccess;
     std::string what;
@@ -335,6 +406,14 @@ static int run_rccl(iemic_ctx* c, const std::vector<Msg>& ops)
     if (first != ncclSuccess) {
         set_error(what + ": " + ncclGetErrorString(first));
         return IEMIC_EDEVICE;
+    }
+    if (!(c->comm_checked & 2)) {
+        c->comm_checked |= 2;
+        std::string peers;
+        for (const Msg& op : ops)
+            peers += std::string(peers.empty() ? "" : ", ") + (op.send ? "send to " : "recv from ") +
+                     std::to_string(op.peer) + " (" + std::to_string(seg_count(op.s)) + ")";
+        if ((rc = rccl_wait(c, "first halo batch [" + peers + "]"))) return rc;
     }
     return unstage_recvs(c, ops, buf);
 }
@@ -404,6 +483,50 @@ int halo_exchange_planar(iemic_ctx* c, double* v, int nplanes, int64_t ps, int d
     int rc = run_msgs(c, x);
     if (rc) return rc;
     return run_msgs(c, y);
+}
+
+int comm_verify_plans(iemic_ctx* c)
+{
+    if (c->nranks <= 1) return 0;
+    const int P = c->nranks;
+    const int spec[3][2] = {{NUN, HALO}, {NUN, 1}, {1, 1}};   /* (width, depth) of the plans */
+    /* per plan, per ordered pair (a -> b): message count and sum of (k + 1) * length over
+     * the k-th message; the sender adds, the receiver subtracts: all zero when they pair */
+    std::vector<double> t((size_t)3 * 2 * P * P, 0.0);
+    for (int q = 0; q < 3; q++) {
+        std::vector<MsgD> px, py;
+        plan_ext(c->sub, spec[q][0], spec[q][1], px, py);
+        for (const auto* ph : {&px, &py}) {
+            std::map<int, int> ks, kr;
+            for (const MsgD& mg : *ph) {
+                const int a = mg.send ? c->rank : mg.peer, b = mg.send ? mg.peer : c->rank;
+                const int k = mg.send ? ks[b]++ : kr[a]++;
+                const double sg = mg.send ? 1.0 : -1.0;
+                double* e = t.data() + ((size_t)q * 2 * P + a) * P + b;
+                e[0] += sg;
+                e[(size_t)P * P] += sg * (k + 1) * (double)(mg.s.nblk * mg.s.len);
+            }
+        }
+    }
+    DevBuf<double> d;
+    if (d.alloc(t.size())) return IEMIC_ENOMEM;
+    int rc = h2d(c, d.p, t.data(), sizeof(double) * t.size());
+    if (!rc) rc = allreduce_sum(c, d.p, (int)t.size());
+    if (!rc) rc = d2h(c, t.data(), d.p, sizeof(double) * t.size());
+    if (rc) return rc;
+    for (int q = 0; q < 3; q++)
+        for (int a = 0; a < P; a++)
+            for (int b = 0; b < P; b++) {
+                const double* e = t.data() + ((size_t)q * 2 * P + a) * P + b;
+                if (e[0] != 0.0 || e[(size_t)P * P] != 0.0) {
+                    set_error("halo plans do not pair: rank " + std::to_string(a) + " -> rank " +
+                              std::to_string(b) + " (plan width " + std::to_string(spec[q][0]) + ", depth " +
+                              std::to_string(spec[q][1]) + "): sends minus receives " +
+                              std::to_string((int)e[0]) + " messages");
+                    return IEMIC_EINVAL;
+                }
+            }
+    return 0;
 }
 
 /* state-vector halo (NUN doubles per cell) */

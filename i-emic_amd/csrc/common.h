@@ -271,6 +271,11 @@ struct iemic_ctx {
     iemic::DevBuf<double> d_stage;   /* packed strided messages (RCCL)                    */
     std::vector<double> h_stage;     /* host-staged messages (group / host transport)     */
     int64_t stat[4] = {0, 0, 0, 0};  /* exchange batches, messages, bytes sent, all-reduces */
+    /* fail-fast (comm.hip): the first all-reduce and the first halo batch of a context are
+     * waited for with this bound (RCCL: stream + async-error polling, then ncclCommAbort;
+     * in-process group: timed barriers, always); bits of comm_checked: 1 all-reduce, 2 halo */
+    double comm_timeout_s = 60.0;
+    int comm_checked = 0;
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
     iemic::DevBuf<int> d_landm;
@@ -369,6 +374,10 @@ void halo_plan_ext(const iemic_ctx* c, double* v, int width, int depth, std::vec
                    std::vector<Msg>& y);
 int run_msgs(iemic_ctx* c, const std::vector<Msg>& ops);
 int comm_init(iemic_ctx* c, const unsigned char* id, int rank, int nranks);
+/* collective check at creation that every rank's exchange plans pair up (the k-th message
+ * a sends to b has the size of the k-th b receives from a): a mismatch is an error naming
+ * the pair, before any exchange could hang */
+int comm_verify_plans(iemic_ctx* c);
 /* drop one reference to the context (iemic_destroy, a dependent's destroy); the last one
  * frees it */
 void ctx_release(iemic_ctx* c);

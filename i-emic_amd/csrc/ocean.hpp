@@ -70,6 +70,10 @@ class Ocean {
     /* grid: the THCM ParameterList subset; landm: (n+2)(m+2)(l+2) global mask */
     Ocean(const iemic_grid& grid, const std::vector<int>& landm)
     {
+        if (iemic_abi_version() != IEMIC_ABI_VERSION)
+            throw std::runtime_error("libiemic_amd was built from another iemic.h (ABI version " +
+                                     std::to_string(iemic_abi_version()) + ", header " +
+                                     std::to_string(IEMIC_ABI_VERSION) + ")");
         check(iemic_create(&ctx_, &grid, landm.data()), "iemic_create");
         N_ = (size_t)iemic_nrows(ctx_);
         state_ = std::make_shared<Vector>(N_);

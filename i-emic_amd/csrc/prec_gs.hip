@@ -2990,6 +2990,10 @@ int gs_time_parts(iemic_ctx* c, int nrep, double* us)
         set_error("gs_time_parts: the block GS preconditioner is not computed");
         return IEMIC_ESTATE;
     }
+    if (c->nranks > 1) {   /* parts 2 and 3 exchange halos: not callable on one rank alone */
+        set_error("gs_time_parts: one-rank diagnostic, the context has " + std::to_string(c->nranks) + " ranks");
+        return IEMIC_EINVAL;
+    }
     hipStream_t s = c->stream;
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));

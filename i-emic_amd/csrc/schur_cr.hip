@@ -117,7 +117,9 @@ __global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ s
                     const int i = tr + TR * x;
                     const double v = a[x][yk];
                     if (i < m) pcol[sel][i] = v;
-                    const double av = (i < m && !((used >> x) & 1u)) ? fabs(v) : -1.0;
+                    /* a NaN candidate counts as 0, so some unused row is always taken and
+                     * step_of / piv_row stay a permutation (the zero pivot sets *info) */
+                    const double av = (i < m && !((used >> x) & 1u)) ? (v == v ? fabs(v) : 0.0) : -1.0;
                     if (av > best) { best = av; bi = i; }
                 }
 #pragma unroll

@@ -16,6 +16,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("IEMIC_LIB", "libiemic_amd.so"))
 
 IEMIC_ENODEV = -19
+ABI_VERSION = 5             # IEMIC_ABI_VERSION of include/iemic.h this binding mirrors
 IEMIC_ENOCONV = 1           # iemic_newton_step: applied, but the solve missed its tolerance
 
 
@@ -109,8 +110,16 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"device library not built: {LIB_PATH} (run make -C i-emic_amd)")
     L = C.CDLL(LIB_PATH)
+    if not os.environ.get("IEMIC_LIB"):
+        # the structs below mirror one header version: a stale library must not be driven
+        L.iemic_abi_version.restype = C.c_int
+        got = L.iemic_abi_version() if hasattr(L, "iemic_abi_version") else None
+        if got != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH}: ABI version {got}, this binding expects {ABI_VERSION} "
+                               "(rebuild with make -C i-emic_amd)")
     vp = C.c_void_p
     sig = {
+        "iemic_abi_version": (C.c_int, []),
         "iemic_create": (C.c_int, [P(vp), P(Grid), PI]),
         "iemic_create_dist": (C.c_int, [P(vp), P(Grid), PI, P(Dist)]),
         "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
@@ -118,6 +127,7 @@ def lib():
         "iemic_comm_stats": (C.c_int, [vp, P64]),
         "iemic_comm_size": (C.c_int, [vp, PI, PI]),
         "iemic_allreduce_sum": (C.c_int, [vp, PD, C.c_int64]),
+        "iemic_set_comm_timeout": (C.c_int, [vp, C.c_double]),
         "iemic_local_group_new": (vp, [C.c_int]),
         "iemic_local_group_free": (None, [vp]),
         "iemic_create_local": (C.c_int, [P(vp), P(Grid), PI, vp, C.c_int, C.c_int]),
@@ -199,8 +209,8 @@ def lib():
     return L
 
 
-EXPORTED = ("iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout", "iemic_comm_stats",
-            "iemic_comm_size", "iemic_allreduce_sum",
+EXPORTED = ("iemic_abi_version", "iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout", "iemic_comm_stats",
+            "iemic_comm_size", "iemic_allreduce_sum", "iemic_set_comm_timeout",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_create_local_2d", "iemic_create_transport", "iemic_decomp2d",
             "iemic_destroy", "iemic_device_count", "iemic_last_error",

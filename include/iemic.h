@@ -43,6 +43,13 @@ extern "C" {
 #define IEMIC_ENOCONV (1)     /* warning: the step was applied but its linear solve did not
                                  reach the tolerance (iemic_newton_step)                   */
 
+/* Version of this header's structs and entry points.  Bumped whenever a struct changes
+ * size or meaning (5: iemic_solve_info gained `safeguard` in round 4, the device vector
+ * algebra of round 5); a caller built against another header must refuse to run:
+ *   if (iemic_abi_version() != IEMIC_ABI_VERSION) abort(); */
+#define IEMIC_ABI_VERSION 5
+int iemic_abi_version(void);
+
 typedef struct iemic_ctx iemic_ctx;
 
 /* THCM ParameterList subset used by the hot path (THCM.C:189-265; defaults 2748-2813). */
@@ -272,6 +279,12 @@ int     iemic_comm_stats(iemic_ctx* ctx, int64_t* out4);
  * transport: 0 none, 1 RCCL, 2 in-process group, 3 host transport (reports its nranks).
  * The reference queries Epetra_Comm::NumProc (e.g. THCM.C:404, 1717). */
 int     iemic_comm_size(const iemic_ctx* ctx, int* size, int* transport);
+/* Fail-fast bound (seconds, default 60) for this context's first all-reduce and first halo
+ * batch over RCCL (stream and ncclCommGetAsyncError polled; on an error or timeout the
+ * communicator is aborted and the call returns IEMIC_EDEVICE naming the batch and peers) and
+ * for every barrier of the in-process group.  Exchange plans are checked to pair up across
+ * the ranks when a context is created (a mismatch fails iemic_create_* with IEMIC_EINVAL). */
+int     iemic_set_comm_timeout(iemic_ctx* ctx, double seconds);
 /* Epetra_Comm::SumAll (e.g. Ocean::getColumnIntegral's column sums, Ocean.C:1851-1895):
  * buf (host, count doubles) summed over the context's ranks in place; collective */
 int     iemic_allreduce_sum(iemic_ctx* ctx, double* buf, int64_t count);

@@ -363,3 +363,39 @@ def test_transport_processes(oracle_lib, name, nranks, npx):
     assert abs(out[0]["f0"] - f0) <= 1e-12 * f0
     lin = np.linalg.norm(F0 + o.spmv(ov, x1 - x)) / f0
     assert lin <= 1e-8, lin
+
+
+def test_unmatched_exchange_fails_fast(oracle_lib):
+    """Fail-fast path (comm.hip group_barrier / rccl_wait): a halo exchange whose peer never
+    posts the matching call returns IEMIC_EDEVICE within the context's bound instead of
+    hanging.  Both ranks are created (creation is collective and checks that the exchange
+    plans pair up); then only rank 0 runs an SpMV, whose halo batch waits for rank 1."""
+    import time
+    from iemic import _lib
+    from iemic.ocean import Ocean
+    c = cf.preset("natl8", mixing=0)
+    L0 = golden_landm("natl8")
+    group = _lib.lib().iemic_local_group_new(2)
+    ocs = [None, None]
+
+    def mk(r):
+        ocs[r] = Ocean(c, landm=L0, local_group=group, rank=r, nranks=2, npx=1)
+
+    th = [threading.Thread(target=mk, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert all(o is not None for o in ocs)
+    oc = ocs[0]
+    _lib.check(_lib.lib().iemic_set_comm_timeout(oc._h, 2.0), "set_comm_timeout")
+    x = np.zeros(c.nrows)
+    oc.setState(x)
+    t0 = time.perf_counter()
+    with pytest.raises(_lib.IemicError, match="did not arrive"):
+        oc.applyMatrix(x)
+    dt = time.perf_counter() - t0
+    assert dt < 10.0, dt
+    for o in ocs:
+        o.close()
+    _lib.lib().iemic_local_group_free(group)

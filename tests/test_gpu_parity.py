@@ -429,3 +429,44 @@ def test_stagnation_safeguard(oracle_lib, Ocean, name, omega):
         assert info.solve.safeguard == 0
     if name == "global2" and omega > 1.0:
         assert info.solve.safeguard == 1
+
+
+@pytest.mark.timeout(300)
+def test_global2_bench_state_parity(oracle_lib, Ocean):
+    """The benchmarked input itself (bench.py's default line): the 2-degree branch state
+    bench_data/global2_cf05.npz with Mixing = 1 (convective adjustment active).  J values and
+    F bit-exact against the oracle, and the Newton step the bench times: its solve reaches
+    ||F + J dx|| <= 1e-8 ||F|| with the oracle's J, its new residual is the oracle's F at the
+    new state, and ||F1|| agrees with the CPU port's Newton step (same algorithm, oracle/
+    prec_oracle.c) to 1e-10 relative -- north_star's bar at the exact benchmarked input."""
+    import os
+    from conftest import ROOT
+    sp = {"FGMRES tolerance": 1e-8, "FGMRES iterations": 90, "FGMRES restarts": 20}
+    c, oc, o, L = make(Ocean, oracle_lib, "global2", mixing=1, solver_params=sp)
+    with np.load(os.path.join(ROOT, "bench_data", "global2_cf05.npz"), allow_pickle=False) as d:
+        x = d["x"].astype(np.float64)
+    # bench.py steps at the preset's Combined Forcing 0.5 from this state (continued to 0.50002)
+    oc.setState(x)
+    oc.computeJacobian()
+    _, col, val = oc.exportCSR()
+    ov, _ = o.jacobian(x)
+    np.testing.assert_array_equal(col, o.col)
+    del col
+    np.testing.assert_array_equal(bits(val), bits(ov))
+    del val
+    F0 = o.rhs(x)
+    np.testing.assert_array_equal(bits(oc.computeRHS()), bits(F0))
+    info = oc.newtonStep()
+    assert info.solve.converged == 1 and info.solve.explicit_rel_res <= 1e-8
+    x1 = oc.getState()
+    lin = np.linalg.norm(F0 + o.spmv(ov, x1 - x)) / np.linalg.norm(F0)
+    assert lin <= 1e-8, lin
+    F1 = o.rhs(x1)
+    assert abs(info.norm_f1 - np.linalg.norm(F1)) <= 1e-13 * np.linalg.norm(F1)
+    # the CPU port's Newton step from the same state (bench.py's cpu_baseline algorithm)
+    P = oracle_lib.BlockGS(o, ov, 12, dyn_iters=4, dyn_omega=0.95, ts_mg=1)
+    dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F0), tol=1e-8, m=90, maxit=90 * 21)
+    f1_cpu = np.linalg.norm(o.rhs(x + dx))
+    print(f"bench state: GPU {info.solve.iters} FGMRES steps |F1| {info.norm_f1:.16e}; "
+          f"CPU port {its} steps |F1| {f1_cpu:.16e}")
+    assert abs(info.norm_f1 - f1_cpu) <= 1e-10 * f1_cpu, (info.norm_f1, f1_cpu)
