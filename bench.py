@@ -129,6 +129,8 @@ def parse():
                    help="continuation: config C5, one pseudo-arclength continuation step of the "
                         "1-degree ocean (run/ocean settings) from bench_data/<config>_cf05.npz")
     p.add_argument("--ds", type=float, default=0.1, help="continuation step size (--mode continuation)")
+    p.add_argument("--cont-tol", type=float, default=1e-4,
+                   help="FGMRES tolerance of the continuation's solves (run/ocean solver_params.xml: 1e-4)")
     p.add_argument("--cpu-iters", type=int, default=8,
                    help="FGMRES iterations of the bounded CPU sample (--mode continuation)")
     return p.parse_args()
@@ -193,7 +195,105 @@ RUN_OCEAN_CONT = {                  # run/ocean/continuation_params.xml
     "post processing": "never"}
 
 
-def bench_continuation(args):
+class Ranks:
+    """This process's rank of the run (one per GPU, or several per GPU with --transport
+    host): torch.distributed set up, the device chosen, the RCCL id broadcast; builds the
+    rank's Ocean subdomain and takes max-over-ranks timings."""
+
+    def __init__(self, args):
+        import torch
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.host = args.transport == "host"
+        self.args = args
+        self.dist = None
+        ndev = torch.cuda.device_count()
+        if self.world > 1 and not self.host and ndev < self.world:
+            print(f"bench.py: rank {self.rank}: {self.world} RCCL ranks need {self.world} GPUs, {ndev} visible",
+                  file=sys.stderr)
+            sys.exit(2)
+        self.device = local % max(1, ndev) if self.host else local
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(self.device)
+            if self.host:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
+            self.dist = dist
+        self.dev = torch.device("cuda", self.device)
+        torch.cuda.set_device(self.dev)
+        self.tdev = "cpu" if self.host else self.dev
+        self.comm_id, self.tp = None, None
+        if self.world > 1 and self.host:
+            from iemic.transport import GlooTransport
+            self.tp = GlooTransport()
+        elif self.world > 1:
+            from iemic.ocean import Ocean
+            idt = torch.zeros(128, dtype=torch.uint8, device=self.dev)
+            if self.rank == 0:
+                idt.copy_(torch.frombuffer(bytearray(Ocean.unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, 0)
+            self.comm_id = bytes(idt.cpu().numpy().tobytes())
+
+    def ocean(self, cfg, **kw):
+        """this rank's Ocean (the Decomp2D subdomain of --npx); exits 2 unless the communicator
+        reports WORLD_SIZE ranks"""
+        from iemic.ocean import Ocean
+        oc = Ocean(cfg, device=self.device, rank=self.rank, nranks=self.world, comm_id=self.comm_id,
+                   npx=self.args.npx, transport=self.tp, **kw)
+        self.ranks_seen, self.transport = oc.comm_size()
+        if self.ranks_seen != self.world:
+            print(f"bench.py: rank {self.rank}: the communicator reports {self.ranks_seen} ranks, "
+                  f"WORLD_SIZE {self.world}", file=sys.stderr)
+            sys.exit(2)
+        return oc
+
+    def barrier(self):
+        self.torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if not self.dist:
+            return v
+        t = self.torch.tensor([v], device=self.tdev, dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def check_agree(self):
+        """all ranks saw the same communicator size"""
+        if not self.dist:
+            return
+        rs = self.torch.tensor([self.ranks_seen, -self.ranks_seen], device=self.tdev, dtype=self.torch.float64)
+        self.dist.all_reduce(rs, op=self.dist.ReduceOp.MAX)
+        if int(rs[0]) != self.world or int(-rs[1]) != self.world:
+            print(f"bench.py: ranks disagree on the communicator size ({rs.tolist()})", file=sys.stderr)
+            sys.exit(2)
+
+    def gather_ref(self, x):
+        """a global reference-ordered host vector of which each rank filled its own rows"""
+        if not self.dist:
+            return x
+        t = self.torch.from_numpy(np.ascontiguousarray(x)).to(self.tdev)
+        self.dist.all_reduce(t)
+        return t.cpu().numpy()
+
+    def fields(self, oc) -> dict:
+        lay = oc.layout()
+        return {"n_gpus": self.world, "ranks_seen": self.ranks_seen,
+                "process_grid": [lay["npx"], lay["npy"]],
+                "parallelism": (f"decomp2d {lay['npx']}x{lay['npy']}" if self.world > 1 else "single"),
+                "transport": self.transport if self.world > 1 else "none"}
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def bench_continuation(args, R: Ranks):
     """Config C5: one pseudo-arclength continuation step (Continuation.H:230-298: Euler
     predictor, Newton corrector on the bordered system with two solves per Jacobian,
     587-813) of the 1-degree global ocean (384x152x32, 11.2 M unknowns) with the
@@ -202,80 +302,90 @@ def bench_continuation(args):
     bench_data/<config>_cf05.npz (the model continued on the GPU from rest to Combined
     Forcing 0.5, scripts/branch_state.py, fp32-rounded).  The tangent (an Euler tangent: one
     solve with dF/dpar) is formed once, untimed; every timed step restarts from that state,
-    tangent and step size ds.  One GPU."""
-    import torch
+    tangent and step size ds.  The continuation's vectors live in HBM (iemic.ocean.DeviceOps):
+    on N ranks each holds its subdomain's rows and every dot / norm is summed over the ranks
+    (the reference's Utils::dot on the Epetra solve map) -- strong scaling, max over ranks."""
     from iemic import config as cf
     from iemic.continuation import Continuation
-    from iemic.ocean import Ocean
     cfg = cf.preset(args.config, mixing=args.mixing)
     fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
     with np.load(fix, allow_pickle=False) as d:
         x0 = d["x"].astype(np.float64)
         par0 = float(d["par"])
-    sp = {"FGMRES tolerance": 1e-4, "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
+    sp = {"FGMRES tolerance": args.cont_tol, "FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "Dyn iterations": args.dyn_iters, "Dyn damping": args.dyn_omega, "TS multigrid cycles": args.ts_mg}
-    oc = Ocean(cfg, solver_params=sp)
+    oc = R.ocean(cfg, solver_params=sp)
     solves = []
-    orig_solve = oc.solve
-
-    def solve(b):
-        x = orig_solve(b)
-        solves.append(oc.last_solve)
-        return x
-    oc.solve = solve
+    oc.solve_hook = solves.append
     oc.setState(x0)
     oc.setPar("Combined Forcing", par0)
     cont = Continuation(oc, {**RUN_OCEAN_CONT, "initial step size": args.ds})
+    ops = cont.ops
     cont.initialize()
     cont.createInitialTangent()
-    saved = (cont.state.copy(), cont.par, cont.stateDot.copy(), cont.parDot)
+    saved = (cont.state, cont.par, cont.stateDot, cont.parDot)   # device vectors, never modified
 
     def step():
         st, par, sd, pd = saved
-        oc.setState(st)
+        ops.set_state(st)
         oc.setPar("Combined Forcing", par)
-        cont.state, cont.par, cont.stateDot, cont.parDot, cont.ds = st.copy(), par, sd.copy(), pd, args.ds
+        cont.state, cont.par, cont.stateDot, cont.parDot, cont.ds = st, par, sd, pd, args.ds
         cont.store()
         solves.clear()
+        R.barrier()
         t = time.perf_counter()
         rc = cont.step()
-        torch.cuda.synchronize()
+        R.barrier()
         return rc, time.perf_counter() - t, list(solves)
 
     for _ in range(args.warmup):
         step()
+    oc.comm_stats()
     recs = [step() for _ in range(args.steps)]
-    ms = sum(r[1] for r in recs) / len(recs) * 1e3
+    comm = oc.comm_stats()
+    ms = R.max(sum(r[1] for r in recs) / len(recs) * 1e3)
+    R.check_agree()
     rc, _, sv = recs[-1]
-    # SpMV roofline of the 1-degree operator: HIP events on the library stream (hot)
+    its = [s.iters for s in sv]
+    # SpMV roofline of the 1-degree operator (this rank's rows): HIP events on the library
+    # stream, hot, after the timed steps
     oc.computeJacobian()
     sp_ms = oc.time_spmv(20)
     from iemic import _lib
     nnz = int(_lib.lib().iemic_graph_nnz(oc._h))
-    bsp = spmv_bytes(nnz, cfg.nrows)
+    nown = oc.layout()["own_rows"]
+    bsp = spmv_bytes(nnz, nown)
+    ell = stencil_ell_bytes(nown // 6, 104, nown)
     achieved = bsp / (sp_ms * 1e-3) / 1e9
-    its = [s.iters for s in sv]
+    real = ell / (sp_ms * 1e-3) / 1e9
+    its_total = max(1, sum(its))
     out = {"metric": "1-degree continuation-step wall time (config C5: predictor + bordered Newton corrector)",
-           "value": round(ms, 1), "unit": "ms/continuation-step", "n_gpus": 1, "steps": args.steps,
+           "value": round(ms, 1), "unit": "ms/continuation-step", "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 1), "higher_is_better": False,
-           "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "scaling": "strong" if R.world > 1 else "none", "vs_baseline": None, "dtype": "f64",
            "data": ("near-solution state: global1 continued on the GPU from rest to Combined Forcing "
                     f"{par0:.5f} with the reference's run/ocean settings (scripts/branch_state.py; "
                     "bench_data/global1_cf05.npz, fp32-rounded); Euler tangent formed untimed"),
            "config": {"workload": f"{args.config} {cfg.n}x{cfg.m}x{cfg.l} Mixing={args.mixing}, one "
-                                  f"continuation step ds={args.ds:g} (Newton tol 1e-2, FGMRES tol 1e-4)",
-                      "rows": cfg.nrows, "nnz": nnz, "krylov_dim": args.krylov, "restarts": args.restarts},
+                                  f"continuation step ds={args.ds:g} (Newton tol 1e-2, FGMRES tol {args.cont_tol:g})",
+                      "rows": cfg.nrows, "nnz_rank0": nnz, "krylov_dim": args.krylov, "restarts": args.restarts},
+           **R.fields(oc),
+           "comm": {"per_fgmres_step": {k: round(v / (its_total * args.steps), 2) for k, v in comm.items()},
+                    "rank": R.rank},
            "continuation": {"rc": rc, "newton_iters": cont.newtonIter, "par": cont.par,
                             "norm_f": cont.normRHStest, "fgmres_iters": its,
-                            "solve_ms": [round(s.t_total_ms, 1) for s in sv]},
-           "roofline": {"kernel": "k_spmv7 (1-degree operator, HIP events, 20 back-to-back launches)",
-                        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes": bsp, "launch_us": round(sp_ms * 1e3, 2)},
+                            "solve_ms": [round(s.t_total_ms, 1) for s in sv],
+                            "vectors": "device (iemic_vec_*, summed over the ranks)"},
+           "roofline": {"kernel": "k_spmv7 (1-degree operator, rank 0's rows, HIP events, 20 back-to-back launches)",
+                        "bound": "hbm", "achieved": round(real, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(real / HBM_PEAK_GBS, 4), "traffic": None, "bytes_basis": "stencil_ell_bytes",
+                        "achieved_csr": round(achieved, 1), "frac_csr": round(achieved / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes": bsp, "stencil_ell_bytes": ell, "launch_us": round(sp_ms * 1e3, 2)},
            "cpu_baseline": None}
-    if not args.no_cpu:
+    if not args.no_cpu and R.world == 1:
         out["cpu_baseline"] = cpu_continuation_sample(cfg, oc, cont, saved, its, args)
-    print(json.dumps(out), flush=True)
+    if R.rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def cpu_continuation_sample(cfg, oc, cont, saved, its, args):
@@ -287,7 +397,7 @@ def cpu_continuation_sample(cfg, oc, cont, saved, its, args):
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
     st, par, sd, pd = saved
-    x = st + args.ds * sd
+    x = cont.ops.to_host(st) + args.ds * cont.ops.to_host(sd)
     o.set_par(19, par + args.ds * pd)        # Combined Forcing (par2int COMB = 19)
     t = time.perf_counter()
     F = o.rhs(x)
@@ -314,15 +424,14 @@ def cpu_continuation_sample(cfg, oc, cont, saved, its, args):
             "timed": True, "extrapolated": True}
 
 
-def bench_coupled(args):
+def bench_coupled(args, R: Ranks):
     """Config C4: the coupled ocean + atmosphere model at 4 degrees (run/coupled: ocean
     96x38x12 with Coupled Temperature = 1, Mixing 1; the atmosphere on the same grid),
     one Newton step of CoupledModel (F, J, the block Gauss-Seidel preconditioner set-up,
-    FGMRES or IDR(s) to tol, update, F).  One GPU (the coupled grid is small)."""
-    import torch
+    FGMRES or IDR(s) to tol, update, F).  On N ranks the ocean is split into Decomp2D
+    subdomains and the atmosphere replicated (CoupledModel.C:274-343); max over ranks."""
     from iemic import config as cf
     from iemic.coupled import RUN_COUPLED_ATMOS, Atmosphere, CoupledModel
-    from iemic.ocean import Ocean
     cfg = cf.preset("coupled4")
     fix = os.path.join(ROOT, "bench_data", "coupled4_cf015.npz")
     branch = args.state == "branch" and os.path.exists(fix)
@@ -334,7 +443,7 @@ def bench_coupled(args):
             xo_b, xa_b, comb = d["x"].astype(np.float64), d["xa"].astype(np.float64), float(d["par"])
     else:
         comb = cfg.start_params["Combined Forcing"]
-    oc = Ocean(cfg, solver_params={"Dyn iterations": args.dyn_iters})
+    oc = R.ocean(cfg, solver_params={"Dyn iterations": args.dyn_iters})
     atm = Atmosphere(oc, {**RUN_COUPLED_ATMOS, "Combined Forcing": comb})
     sp = {"FGMRES iterations": args.krylov, "FGMRES restarts": args.restarts,
           "FGMRES tolerance": args.tol, "Solver": args.solver, "IDR s": args.idr_s}
@@ -357,13 +466,16 @@ def bench_coupled(args):
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    R.barrier()
+    oc.comm_stats()
     recs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         recs.append(step())
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    R.barrier()
+    ms = R.max((time.perf_counter() - t0) / args.steps * 1e3)
+    comm = oc.comm_stats()
+    R.check_agree()
     r = recs[-1]
     seq = []
     if args.newton_seq > 0:
@@ -381,9 +493,11 @@ def bench_coupled(args):
     bsp = spmv_bytes(nnz, cfg.nrows)
     achieved = bsp / (sp_ms * 1e-3) / 1e9
     out = {"metric": "coupled ocean+atmosphere Newton-step wall time (config C4)",
-           "value": round(ms, 3), "unit": "ms/Newton-step", "n_gpus": 1, "steps": args.steps,
+           "value": round(ms, 3), "unit": "ms/Newton-step", "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": False,
-           "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "scaling": "strong" if R.world > 1 else "none", "vs_baseline": None, "dtype": "f64",
+           **R.fields(oc),
+           "comm": {"per_newton_step": {k: round(v / args.steps, 1) for k, v in comm.items()}, "rank": R.rank},
            "data": (("near-solution state of both models: coupled4 continued on the GPU from rest with "
                      "run/coupled's settings to Combined Forcing 0.15 (scripts/coupled_branch_state.py; "
                      "bench_data/coupled4_cf015.npz, fp32-rounded); states reset from host each step")
@@ -401,7 +515,7 @@ def bench_coupled(args):
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                         "algorithmic_bytes": bsp, "launch_us": round(sp_ms * 1e3, 2)},
            "cpu_baseline": None}
-    if not args.no_cpu:
+    if not args.no_cpu and R.world == 1:
         from oracle import atmos_oracle as ao
         from oracle import oracle as orc
         cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -419,7 +533,8 @@ def bench_coupled(args):
             "iters": cb["iters"]}
         out["newton"]["norm_f0_cpu"] = cb["norm_f0"]
         out["newton"]["norm_f1_cpu"] = cb["norm_f1"]
-    print(json.dumps(out), flush=True)
+    if R.rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def launch(args) -> int:
@@ -454,36 +569,25 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world} ranks were started", file=sys.stderr)
         sys.exit(2)
-    if world > 1 and (args.config == "coupled4" or args.mode == "continuation"):
-        print("bench.py: the coupled (C4) and continuation (C5) lines run on one GPU", file=sys.stderr)
-        sys.exit(2)
-    if args.config == "coupled4":
-        return bench_coupled(args)
-    if args.mode == "continuation":
-        return bench_continuation(args)
-    import torch
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    host = args.transport == "host"
-    dist = None
-    ndev = torch.cuda.device_count()
-    if world > 1 and not host and ndev < world:
-        print(f"bench.py: rank {rank}: {world} RCCL ranks need {world} GPUs, {ndev} visible", file=sys.stderr)
-        sys.exit(2)
-    device = local % max(1, ndev) if host else local
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(device)
-        if host:
-            dist.init_process_group("gloo")
+    R = Ranks(args)
+    try:
+        if args.config == "coupled4":
+            bench_coupled(args, R)
+        elif args.mode == "continuation":
+            bench_continuation(args, R)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-    dev = torch.device("cuda", device)
-    torch.cuda.set_device(dev)
+            bench_newton(args, R)
+    finally:
+        R.close()
 
+
+def bench_newton(args, R: Ranks):
+    """The BASELINE metric: one full Newton step of the 2-degree ocean (module docstring)."""
+    import torch
     from iemic import _lib
     from iemic import config as cf
-    from iemic.ocean import Ocean
+    rank, world, dev = R.rank, R.world, R.dev
+    dist = R.dist
 
     cfg = cf.preset(args.config, mixing=args.mixing)
     sp = {"Preconditioner": args.prec, "FGMRES tolerance": args.tol,
@@ -493,23 +597,8 @@ def main():
           "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps,
           "Solver": args.solver, "IDR s": args.idr_s, "TS after dyn pass": args.ts_at}
-    comm_id, tp = None, None
-    if world > 1 and host:
-        from iemic.transport import GlooTransport
-        tp = GlooTransport()
-    elif world > 1:
-        idt = torch.zeros(128, dtype=torch.uint8, device=dev)
-        if rank == 0:
-            idt.copy_(torch.frombuffer(bytearray(Ocean.unique_id()), dtype=torch.uint8))
-        dist.broadcast(idt, 0)
-        comm_id = bytes(idt.cpu().numpy().tobytes())
-    oc = Ocean(cfg, device=device, solver_params=sp, rank=rank, nranks=world, comm_id=comm_id,
-               npx=args.npx, transport=tp)
-    ranks_seen, transport = oc.comm_size()
-    if ranks_seen != world:
-        print(f"bench.py: rank {rank}: the communicator reports {ranks_seen} ranks, WORLD_SIZE {world}",
-              file=sys.stderr)
-        sys.exit(2)
+    oc = R.ocean(cfg, solver_params=sp)
+    ranks_seen, transport = R.ranks_seen, R.transport
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
     fix = os.path.join(ROOT, "bench_data", f"{args.config}_cf05.npz")
     state = args.state if (args.state == "synthetic" or os.path.exists(fix)) else "synthetic"
@@ -537,39 +626,22 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    R.barrier()
     oc.comm_stats()                      # reset the counters: the timed steps only
     infos = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         infos.append(step())
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    R.barrier()
     dt = time.perf_counter() - t0
-    ms = dt / args.steps * 1e3
+    ms = R.max(dt / args.steps * 1e3)
     comm = oc.comm_stats()
     its_total = sum(i.solve.iters for i in infos)
-    if dist:
-        tdev = "cpu" if host else dev
-        tt = torch.tensor([ms], device=tdev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ms = float(tt.item())
-        rs = torch.tensor([ranks_seen, -ranks_seen], device=tdev, dtype=torch.float64)
-        dist.all_reduce(rs, op=dist.ReduceOp.MAX)
-        if int(rs[0]) != world or int(-rs[1]) != world:
-            print(f"bench.py: ranks disagree on the communicator size ({rs.tolist()})", file=sys.stderr)
-            sys.exit(2)
+    R.check_agree()
 
     if args.save_x1:
         # the updated state of the last timed step: each rank's owned rows, summed over ranks
-        x1 = oc.getState()
-        if dist:
-            t1 = torch.from_numpy(x1).to("cpu" if host else dev)
-            dist.all_reduce(t1)
-            x1 = t1.cpu().numpy()
+        x1 = R.gather_ref(oc.getState())
         if rank == 0:
             np.savez(args.save_x1, x0=x0h, x1=x1)
 
@@ -700,8 +772,6 @@ def main():
         out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -844,6 +844,157 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     return inf.solve.converged ? 0 : IEMIC_ENOCONV;
 }
 
+/* ---- device vectors: the Epetra_Vector algebra Continuation.H applies through Utils
+ * (dot / norm / update over the solve map), on vectors in the ext layout; the owned rows
+ * are one contiguous slab, reductions are summed over the ranks ------------------------ */
+namespace iemic {
+__global__ void k_vec_update(double a, const double* __restrict__ x, double b, const double* __restrict__ y,
+                             double cz, double* __restrict__ z, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        double v = a * x[q];
+        if (y) v += b * y[q];
+        if (cz != 0.0) v += cz * z[q];
+        z[q] = v;
+    }
+}
+__global__ void __launch_bounds__(256) k_vec_absmax(const double* __restrict__ x, int64_t N,
+                                                    double* __restrict__ part)
+{
+    __shared__ double sm[4];
+    double v = 0.0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const double a = fabs(x[q]);
+        v = (a > v || a != a) ? a : v;                  /* NaN propagates */
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double u = __shfl_down(v, o, 64);
+        v = (u > v || u != u) ? u : v;
+    }
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = sm[0];
+        for (int w = 1; w < 4; w++) t = (sm[w] > t || sm[w] != sm[w]) ? sm[w] : t;
+        part[blockIdx.x] = t;
+    }
+}
+}  // namespace iemic
+
+extern "C" int iemic_vec_alloc(iemic_ctx* c, double** v)
+{
+    CTX_CHECK(c);
+    if (!v) return IEMIC_EINVAL;
+    *v = nullptr;
+    if (hipMalloc((void**)v, sizeof(double) * c->nerows) != hipSuccess) {
+        *v = nullptr;
+        set_error("iemic_vec_alloc: out of device memory");
+        return IEMIC_ENOMEM;
+    }
+    HIP_OK(hipMemsetAsync(*v, 0, sizeof(double) * c->nerows, c->stream));
+    return 0;
+}
+
+extern "C" int iemic_vec_free(iemic_ctx* c, double* v)
+{
+    CTX_CHECK(c);
+    if (v) HIP_OK(hipFree(v));
+    return 0;
+}
+
+extern "C" int iemic_vec_update(iemic_ctx* c, double a, const double* x, double b, const double* y, double cz,
+                                double* z)
+{
+    CTX_CHECK(c);
+    if (!x || !z) return IEMIC_EINVAL;
+    const int64_t o = NUN * c->own0, NL = c->nlrows;
+    const unsigned G = (unsigned)std::min<int64_t>((NL + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_vec_update, dim3(G), dim3(256), 0, c->stream, a, x + o, b, y ? y + o : nullptr, cz,
+                       z + o, NL);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int iemic_vec_dot(iemic_ctx* c, const double* x, const double* y, double* out)
+{
+    CTX_CHECK(c);
+    if (!x || !y || !out) return IEMIC_EINVAL;
+    return dot_owned(c, x, y, out);
+}
+
+extern "C" int iemic_vec_norm_inf(iemic_ctx* c, const double* x, double* out)
+{
+    CTX_CHECK(c);
+    if (!x || !out) return IEMIC_EINVAL;
+    const int64_t o = NUN * c->own0, NL = c->nlrows;
+    const int nb = (int)std::min<int64_t>((NL + 255) / 256, RED_BLOCKS);
+    hipLaunchKernelGGL(k_vec_absmax, dim3(nb), dim3(256), 0, c->stream, x + o, NL, c->d_part.p);
+    HIP_OK(hipGetLastError());
+    std::vector<double> part(nb);
+    int rc = d2h(c, part.data(), c->d_part.p, sizeof(double) * nb);
+    if (rc) return rc;
+    double mx = 0.0;
+    for (double v : part) mx = (v > mx || v != v) ? v : mx;
+    if (c->nranks > 1) {
+        /* max over the ranks: each rank's value in its own slot, summed */
+        std::vector<double> all((size_t)c->nranks, 0.0);
+        all[(size_t)c->rank] = mx;
+        if ((rc = host_sum(c, all))) return rc;
+        mx = 0.0;
+        for (double v : all) mx = (v > mx || v != v) ? v : mx;
+    }
+    *out = mx;
+    return 0;
+}
+
+extern "C" int iemic_vec_from_ref(iemic_ctx* c, const double* ref, double* v)
+{
+    CTX_CHECK(c);
+    if (!ref || !v) return IEMIC_EINVAL;
+    return put_ref(c, ref, v);
+}
+
+extern "C" int iemic_vec_to_ref(iemic_ctx* c, const double* v, double* ref)
+{
+    CTX_CHECK(c);
+    if (!ref || !v) return IEMIC_EINVAL;
+    return get_ref(c, v, ref);
+}
+
+/* set = 0: v = state; set = 1: state = v (owned rows; halos are refreshed before use) */
+extern "C" int iemic_state_vec(iemic_ctx* c, double* v, int set)
+{
+    CTX_CHECK(c);
+    if (!v) return IEMIC_EINVAL;
+    const int64_t o = NUN * c->own0;
+    if (set) {
+        HIP_OK(hipMemcpyAsync(c->d_x.p + o, v + o, sizeof(double) * c->nlrows, hipMemcpyDeviceToDevice,
+                              c->stream));
+        c->jac_valid = 0;
+    } else {
+        HIP_OK(hipMemcpyAsync(v + o, c->d_x.p + o, sizeof(double) * c->nlrows, hipMemcpyDeviceToDevice,
+                              c->stream));
+    }
+    return 0;
+}
+
+/* F(state) into the device vector F (owned rows) */
+extern "C" int iemic_rhs_vec(iemic_ctx* c, double* F)
+{
+    CTX_CHECK(c);
+    if (!F) return IEMIC_EINVAL;
+    int rc = halo_exchange(c, c->d_x.p, HALO);
+    if (rc) return rc;
+    if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
+    const int64_t o = NUN * c->own0;
+    if (F != c->d_F.p)
+        HIP_OK(hipMemcpyAsync(F + o, c->d_F.p + o, sizeof(double) * c->nlrows, hipMemcpyDeviceToDevice,
+                              c->stream));
+    return 0;
+}
+
 /* mean duration of the SpMV kernel alone (no halo exchange), HIP events on its stream */
 extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
 {

@@ -397,6 +397,7 @@ int intcond_correction(iemic_ctx* c, const double* x_dev);
 int spmv(iemic_ctx* c, double* x, double* y, hipStream_t s);
 int spmv_kernel(iemic_ctx* c, const double* x, double* y);
 double dot(iemic_ctx* c, const double* a, const double* b, int64_t n);
+int dot_owned(iemic_ctx* c, const double* a, const double* b, double* out);
 int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemic_solve_info* info);
 /* opt->method: 0 FGMRES, 1 IDR(s) */
 int krylov_solve(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,

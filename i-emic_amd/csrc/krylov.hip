@@ -664,6 +664,13 @@ static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const
     return 0;
 }
 
+/* a . b over the owned rows of two ext vectors, summed over the ranks (error code) */
+int dot_owned(iemic_ctx* c, const double* a, const double* b, double* out)
+{
+    const int64_t o = NUN * c->own0;
+    return mdot_host(c, a + o, 0, 1, b + o, out);
+}
+
 /* a . b over the owned rows of two ext vectors, summed over the ranks */
 double dot(iemic_ctx* c, const double* a, const double* b, int64_t)
 {

@@ -157,6 +157,15 @@ def lib():
         "iemic_solve": (C.c_int, [vp, PD, PD, P(Krylov), P(SolveInfo)]),
         "iemic_solve_dev": (C.c_int, [vp, vp, vp, P(Krylov), P(SolveInfo)]),
         "iemic_newton_step": (C.c_int, [vp, P(Krylov), P(NewtonInfo)]),
+        "iemic_vec_alloc": (C.c_int, [vp, P(vp)]),
+        "iemic_vec_free": (C.c_int, [vp, vp]),
+        "iemic_vec_update": (C.c_int, [vp, C.c_double, vp, C.c_double, vp, C.c_double, vp]),
+        "iemic_vec_dot": (C.c_int, [vp, vp, vp, PD]),
+        "iemic_vec_norm_inf": (C.c_int, [vp, vp, PD]),
+        "iemic_vec_from_ref": (C.c_int, [vp, PD, vp]),
+        "iemic_vec_to_ref": (C.c_int, [vp, vp, PD]),
+        "iemic_state_vec": (C.c_int, [vp, vp, C.c_int]),
+        "iemic_rhs_vec": (C.c_int, [vp, vp]),
         "iemic_time_spmv": (C.c_int, [vp, C.c_int, PD]),
         "iemic_time_prec": (C.c_int, [vp, C.c_int, PD, PD]),
         "iemic_time_prec_parts": (C.c_int, [vp, C.c_int, PD]),
@@ -221,7 +230,9 @@ EXPORTED = ("iemic_abi_version", "iemic_create", "iemic_create_dist", "iemic_com
             "iemic_set_state_dev",
             "iemic_jacobian", "iemic_rhs", "iemic_diag_b", "iemic_export_csr", "iemic_spmv",
             "iemic_spmv_dev", "iemic_prec_compute", "iemic_prec_apply", "iemic_solve",
-            "iemic_solve_dev", "iemic_newton_step", "iemic_time_spmv", "iemic_time_spmv_cold", "iemic_time_prec",
+            "iemic_solve_dev", "iemic_newton_step", "iemic_vec_alloc", "iemic_vec_free",
+            "iemic_vec_update", "iemic_vec_dot", "iemic_vec_norm_inf", "iemic_vec_from_ref",
+            "iemic_vec_to_ref", "iemic_state_vec", "iemic_rhs_vec", "iemic_time_spmv", "iemic_time_spmv_cold", "iemic_time_prec",
             "iemic_time_prec_parts",
             "iemic_ilu_create", "iemic_ilu_compute", "iemic_ilu_apply", "iemic_ilu_apply_dev",
             "iemic_ilu_stats", "iemic_ilu_destroy",

@@ -10,10 +10,14 @@ normalisation (421-544), step-size control (952-982), reset/restore (1004-1050) 
 secant landing on destinations (858-933).  Parameter names and defaults are the
 reference's (getDefaultInitParameters, Continuation.H:1330-1366).
 
-Vectors are host numpy arrays in the reference row order (the reference's Epetra vector
-algebra runs on the host too); F, J and the solves run on the GPU behind the model.
-Eigenvalue analysis (JDQZ), backtracking (off by default) and user monitors are not
-restated.
+Vector algebra goes through an ops object (the reference's Utils::dot / norm / update on
+Epetra vectors of the solve map): a model with ``vec_ops()`` (the GPU ``Ocean``) supplies
+device vectors in HBM whose dots and norms are summed over its ranks, so the state, tangent,
+dF/dpar and the corrector's two solutions never leave the GPU and the same driver runs on
+every rank of a decomposed model; other models (host numpy vectors in the reference row
+order) get ``HostOps``.  The ops are functional (every result is a new vector), which is
+how the code below reads Continuation.H's Epetra Update calls.  Eigenvalue analysis (JDQZ)
+and user monitors are not restated.
 """
 from __future__ import annotations
 
@@ -42,6 +46,51 @@ DEFAULTS = {
 
 def _sgn(x: float) -> int:
     return (x > 0) - (x < 0)
+
+
+class HostOps:
+    """Vector algebra and model access for a model with host numpy vectors."""
+
+    def __init__(self, model):
+        self.model = model
+
+    @staticmethod
+    def lincomb(a, x, b=0.0, y=None):
+        return a * x + b * y if y is not None else a * x
+
+    @staticmethod
+    def copy(x):
+        return x.copy()
+
+    @staticmethod
+    def dot(x, y) -> float:
+        return float(np.dot(x, y))
+
+    @staticmethod
+    def norm(x) -> float:
+        return float(np.linalg.norm(x))
+
+    @staticmethod
+    def norm_inf(x) -> float:
+        return float(np.max(np.abs(x)))
+
+    def state(self):
+        return self.model.getState("C")
+
+    def set_state(self, v):
+        self.model.setState(v)
+
+    def rhs(self):
+        self.model.computeRHS()
+        return self.model.getRHS("C")
+
+    def solve(self, b):
+        return self.model.solve(b).copy()
+
+
+def ops_for(model):
+    """DeviceOps for a model that keeps its vectors on the GPU, HostOps otherwise."""
+    return model.vec_ops() if hasattr(model, "vec_ops") else HostOps(model)
 
 
 @dataclass
@@ -74,6 +123,7 @@ class Continuation:
         if params:
             p.update(params)
         self.model = model
+        self.ops = ops_for(model)
         self.p = p
         self.parName = p["continuation parameter"]
         self.dsInit = float(p["initial step size"])
@@ -112,26 +162,25 @@ class Continuation:
         self.history: list[StepRecord] = []
 
     # ---- helpers -------------------------------------------------------------------
-    @staticmethod
-    def _norm(v):
-        return float(np.linalg.norm(v))
+    def _norm(self, v):
+        return self.ops.norm(v)
 
     def _set_state(self, x):
-        self.model.setState(x)
+        self.ops.set_state(x)
 
     # ---- Continuation.H:1158-1230 initialize ----------------------------------------
     def initialize(self):
         self.ds = self.dsInit
-        self.model.computeRHS()
-        self.state = self.model.getState("C")
-        self.rhs = self.model.getRHS("C")
+        self.Fcur = self.ops.rhs()
+        self.state = self.ops.state()
+        self.rhs = self.Fcur
         self.par = self.model.getPar(self.parName)
         self.st = _Storage(ds0=self.ds, ds00=self.ds, par0=self.par, par00=self.par,
-                           parDot0=0.0, state0=self.state.copy())
+                           parDot0=0.0, state0=self.state)
         self.destinations = list(self.destinationsBackup)
         self.signMonitor = [0] * len(self.destinations)
         self.secant = False
-        N = len(self.state)
+        N = getattr(self.model, "N", None) or len(self.state)
         if self.normalizeStrategy == "O":
             self.zeta = 1.0 / N
         else:
@@ -149,14 +198,14 @@ class Continuation:
 
     # ---- 389-418 ---------------------------------------------------------------------
     def computeDFDPar(self, mode: str):
+        # mode "A": the residual of the current state is the last one computed (Fcur)
         if mode == "F":
-            self.model.computeRHS()
-        self.rhsCopy = self.model.getRHS("C")
+            self.Fcur = self.ops.rhs()
+        self.rhsCopy = self.Fcur
         self.model.setPar(self.parName, self.par + self.epsilon)
-        self.model.computeRHS()
+        Fe = self.ops.rhs()
         self.model.setPar(self.parName, self.par)
-        Fe = self.model.getRHS("C")
-        self.dFdPar = Fe * (1.0 / self.epsilon) + self.rhsCopy * (-1.0 / self.epsilon)
+        self.dFdPar = self.ops.lincomb(1.0 / self.epsilon, Fe, -1.0 / self.epsilon, self.rhsCopy)
 
     # ---- 300-384 ---------------------------------------------------------------------
     def createInitialTangent(self):
@@ -164,95 +213,99 @@ class Continuation:
         if self.initialTangent in ("E", "S"):
             self.model.preProcess()
             self.model.computeJacobian()
-            self.stateDot = self.model.solve(-self.dFdPar).copy()
+            self.stateDot = self.ops.solve(self.ops.lincomb(-1.0, self.dFdPar))
         else:
-            self.stateDot = -self.dFdPar
+            self.stateDot = self.ops.lincomb(-1.0, self.dFdPar)
         self.normalize()
 
     # ---- 497-544 ---------------------------------------------------------------------
     def normalize(self):
+        ops = self.ops
         if self.normalizeStrategy == "O":
             self.zeta = self.tanScaling / self._norm(self.stateDot)
-            self.stateDot = self.stateDot * self.zeta
+            self.stateDot = ops.lincomb(self.zeta, self.stateDot)
             nrm = self._norm(self.stateDot)
             normComb = math.sqrt(nrm * nrm + 1)
-            self.stateDot = self.stateDot / normComb
+            self.stateDot = ops.lincomb(1.0 / normComb, self.stateDot)
             self.parDot = 1.0 / normComb
         else:
             nrm = self._norm(self.stateDot)
             normComb = math.sqrt(self.zeta * nrm * nrm + 1)
             self.parDot = 1.0 / normComb
-            self.stateDot = self.stateDot * self.parDot
+            self.stateDot = ops.lincomb(self.parDot, self.stateDot)
 
     # ---- 421-494 ---------------------------------------------------------------------
     def createTangent(self, mode: str):
+        ops = self.ops
         if mode == "S":
-            state = self.model.getState("C")
-            self.stateDot = (state - self.st.state0) / self.st.ds0
+            state = ops.state()
+            self.stateDot = ops.lincomb(1.0 / self.st.ds0, state, -1.0 / self.st.ds0, self.st.state0)
             self.par = self.model.getPar(self.parName)
             self.parDot = (self.par - self.st.par0) / self.st.ds0
         else:
             if self.chordHybrid:
                 self.computeDFDPar("F")
                 self.model.computeJacobian()
-                self.stateDot = self.model.solve(-self.dFdPar).copy()
+                self.stateDot = ops.solve(ops.lincomb(-1.0, self.dFdPar))
             elif self.newtonIter != 0:
-                self.stateDot = -self.stateDot
+                self.stateDot = ops.lincomb(-1.0, self.stateDot)
             self.normalize()
 
     # ---- 547-583 ---------------------------------------------------------------------
     def eulerPredictor(self) -> int:
-        self.state = self.state + self.ds * self.stateDot
+        self.state = self.ops.lincomb(1.0, self.state, self.ds, self.stateDot)
         self._set_state(self.state)
         self.par = self.par + self.ds * self.parDot
         self.model.setPar(self.parName, self.par)
-        self.model.computeRHS()
-        return 1 if self._norm(self.model.getRHS("V")) > self.predictorBound else 0
+        self.Fcur = self.ops.rhs()
+        return 1 if self._norm(self.Fcur) > self.predictorBound else 0
 
     # ---- 587-813 ---------------------------------------------------------------------
     def newtonCorrector(self) -> int:
+        ops = self.ops
         res = 100.0
         y = None
         self.newtonIter = 0
         while self.newtonIter < self.maxNewton:
             mode = "F" if self.newtonIter == 0 else "A"
             self.computeDFDPar(mode)
-            R = -self.rhsCopy
+            R = ops.lincomb(-1.0, self.rhsCopy)
             self.normRHS = self._norm(self.rhsCopy)
-            stateDiff = self.model.getState("C") - self.st.state0
+            stateDiff = ops.lincomb(1.0, ops.state(), -1.0, self.st.state0)
             parDiff = self.par - self.st.par0
             if self.normalizeStrategy == "O":
-                rbp = self.ds - float(np.dot(self.stateDot, stateDiff)) * self.zeta - self.parDot * parDiff
+                rbp = self.ds - ops.dot(self.stateDot, stateDiff) * self.zeta - self.parDot * parDiff
             else:
-                rbp = (self.ds * self.ds) - float(np.dot(stateDiff, stateDiff)) * self.zeta - parDiff * parDiff
+                rbp = (self.ds * self.ds) - ops.dot(stateDiff, stateDiff) * self.zeta - parDiff * parDiff
             self.model.computeJacobian()
             # two solves with the same Jacobian (the preconditioner is computed once)
             if not self.chordHybrid:
-                y = self.model.solve(self.dFdPar).copy()
-            z = self.model.solve(R).copy()
+                y = ops.solve(self.dFdPar)
+            z = ops.solve(R)
             if self.normalizeStrategy == "O":
                 if self.chordHybrid:
-                    parDir = ((rbp - self.zeta * float(np.dot(self.stateDot, z))) /
-                              (self.parDot + self.zeta * float(np.dot(self.stateDot, self.stateDot))))
+                    parDir = ((rbp - self.zeta * ops.dot(self.stateDot, z)) /
+                              (self.parDot + self.zeta * ops.dot(self.stateDot, self.stateDot)))
                 else:
-                    parDir = ((rbp - self.zeta * float(np.dot(self.stateDot, z))) /
-                              (self.parDot - self.zeta * float(np.dot(self.stateDot, y))))
+                    parDir = ((rbp - self.zeta * ops.dot(self.stateDot, z)) /
+                              (self.parDot - self.zeta * ops.dot(self.stateDot, y)))
             else:
                 if self.chordHybrid:
-                    parDir = ((rbp - 2 * self.zeta * float(np.dot(stateDiff, z))) /
-                              (2 * parDiff + 2 * (self.zeta / parDiff) * float(np.dot(stateDiff, stateDiff))))
+                    parDir = ((rbp - 2 * self.zeta * ops.dot(stateDiff, z)) /
+                              (2 * parDiff + 2 * (self.zeta / parDiff) * ops.dot(stateDiff, stateDiff)))
                 else:
-                    parDir = ((rbp - 2 * self.zeta * float(np.dot(stateDiff, z))) /
-                              (2 * parDiff - 2 * self.zeta * float(np.dot(stateDiff, y))))
-            stateDir = z + parDir * self.stateDot if self.chordHybrid else z - parDir * y
-            self.state = self.model.getState("C") + stateDir
+                    parDir = ((rbp - 2 * self.zeta * ops.dot(stateDiff, z)) /
+                              (2 * parDiff - 2 * self.zeta * ops.dot(stateDiff, y)))
+            stateDir = (ops.lincomb(1.0, z, parDir, self.stateDot) if self.chordHybrid
+                        else ops.lincomb(1.0, z, -parDir, y))
+            self.state = ops.lincomb(1.0, ops.state(), 1.0, stateDir)
             self._set_state(self.state)
             self.par = self.par + parDir
             self.model.setPar(self.parName, self.par)
             self.newtonIter += 1
             self.sumNewtonIter += 1
-            self.model.computeRHS()
-            self.normRHStest = self._norm(self.model.getRHS("V"))
+            self.Fcur = ops.rhs()
+            self.normRHStest = self._norm(self.Fcur)
             if self.normRHStest > self.predictorBound:
                 return 1
             # no decrease: backtracking along the Newton direction (Continuation.H:724-731)
@@ -265,7 +318,7 @@ class Continuation:
             if self.residualTest == "R":
                 res = self.normRHStest
             else:
-                res = max(abs(parDir), float(np.max(np.abs(stateDir))))
+                res = max(abs(parDir), ops.norm_inf(stateDir))
             if res < self.newtonTol and self.newtonIter >= self.minNewton:
                 break
         if not self.chordHybrid and y is not None:
@@ -284,12 +337,12 @@ class Continuation:
         while self.backTrack != self.numBackTrackingSteps:
             if self.normRHStest < self.normRHS * increase:
                 break
-            self.state = self.model.getState("C") + reduction * stateDir
+            self.state = self.ops.lincomb(1.0, self.ops.state(), reduction, stateDir)
             self._set_state(self.state)
             self.par = self.par + reduction * parDir
             self.model.setPar(self.parName, self.par)
-            self.model.computeRHS()
-            self.normRHStest = self._norm(self.model.getRHS("V"))
+            self.Fcur = self.ops.rhs()
+            self.normRHStest = self._norm(self.Fcur)
             reduction /= 2.0
             self.backTrack += 1
         if self.normRHStest > self.normRHS * increase and self.numBackTrackingSteps > 0:
@@ -299,8 +352,8 @@ class Continuation:
     # ---- 1052-1090 store / restore ----------------------------------------------------
     def store(self):
         self.st.state00 = self.st.state0
-        self.st.state0 = self.model.getState("C")
-        self.st.stateDot0 = None if self.stateDot is None else self.stateDot.copy()
+        self.st.state0 = self.ops.state()
+        self.st.stateDot0 = self.stateDot          # the ops never modify a vector in place
         self.st.par00 = self.st.par0
         self.st.par0 = self.model.getPar(self.parName)
         self.st.ds00 = self.st.ds0
@@ -308,9 +361,9 @@ class Continuation:
         self.st.parDot0 = self.parDot
 
     def restore(self):
-        self.state = self.st.state0.copy()
+        self.state = self.st.state0
         self._set_state(self.state)
-        self.stateDot = None if self.st.stateDot0 is None else self.st.stateDot0.copy()
+        self.stateDot = self.st.stateDot0
         self.par = self.st.par0
         self.model.setPar(self.parName, self.par)
         self.parDot = self.st.parDot0
@@ -393,7 +446,7 @@ class Continuation:
                 self.reset()
                 continue
             self.history.append(StepRecord(self.step_, self.par, self.ds,
-                                           self._norm(self.model.getState("V")),
+                                           self._norm(self.ops.state()),
                                            self.normRHStest, self.newtonIter))
             self.detect()
             self.adjustStep()

@@ -22,7 +22,99 @@ from . import _lib
 from ._lib import IemicError, check, lib, ptr
 from .config import PAR_INDEX, THCMConfig, landmask
 
-__all__ = ["Ocean", "IemicError"]
+__all__ = ["Ocean", "IemicError", "DeviceVec", "DeviceOps"]
+
+
+class DeviceVec:
+    """One fp64 vector in HBM in the model's internal layout (iemic_layout: owned rows of
+    this rank's subdomain), an Epetra_Vector of the solve map.  Buffers are recycled through
+    the owning Ocean's pool, so the continuation's vector algebra allocates nothing per step."""
+    __slots__ = ("oc", "p")
+
+    def __init__(self, oc: "Ocean"):
+        self.oc = oc
+        self.p = oc._vec_take()
+
+    def __del__(self):
+        try:
+            self.oc._vec_give(self.p)
+        except Exception:
+            pass
+
+
+class DeviceOps:
+    """Continuation.H's vector algebra on device vectors (Utils::dot / norm / update over the
+    solve map; collective over the Ocean's ranks).  The functional forms mirror the host ops
+    of iemic.continuation, so the continuation code is the same for both."""
+
+    def __init__(self, oc: "Ocean"):
+        self.oc = oc
+
+    def _h(self):
+        return self.oc._h
+
+    def lincomb(self, a, x, b=0.0, y=None) -> DeviceVec:
+        z = DeviceVec(self.oc)
+        check(lib().iemic_vec_update(self._h(), float(a), x.p, float(b), y.p if y is not None else None,
+                                     0.0, z.p), "iemic_vec_update")
+        return z
+
+    def copy(self, x) -> DeviceVec:
+        return self.lincomb(1.0, x)
+
+    def dot(self, x, y) -> float:
+        v = C.c_double()
+        check(lib().iemic_vec_dot(self._h(), x.p, y.p, C.byref(v)), "iemic_vec_dot")
+        return v.value
+
+    def norm(self, x) -> float:
+        import math
+        return math.sqrt(self.dot(x, x))
+
+    def norm_inf(self, x) -> float:
+        v = C.c_double()
+        check(lib().iemic_vec_norm_inf(self._h(), x.p, C.byref(v)), "iemic_vec_norm_inf")
+        return v.value
+
+    # model side: state, residual, solve without host copies
+    def state(self) -> DeviceVec:
+        v = DeviceVec(self.oc)
+        check(lib().iemic_state_vec(self._h(), v.p, 0), "iemic_state_vec")
+        return v
+
+    def set_state(self, v) -> None:
+        check(lib().iemic_state_vec(self._h(), v.p, 1), "iemic_state_vec")
+
+    def rhs(self) -> DeviceVec:
+        """F(state) (Ocean::computeRHS + getRHS('C'))."""
+        v = DeviceVec(self.oc)
+        check(lib().iemic_rhs_vec(self._h(), v.p), "iemic_rhs_vec")
+        return v
+
+    def solve(self, b) -> DeviceVec:
+        """J x = b (Ocean::solve on the device; the preconditioner is built once per Jacobian)."""
+        oc = self.oc
+        oc.buildPreconditioner()
+        x = DeviceVec(oc)
+        k = oc._krylov()
+        info = _lib.SolveInfo()
+        check(lib().iemic_solve_dev(self._h(), b.p, x.p, C.byref(k), C.byref(info)), "iemic_solve_dev")
+        oc.last_solve = info
+        if oc.solve_hook is not None:
+            oc.solve_hook(info)
+        return x
+
+    def to_host(self, v) -> np.ndarray:
+        """global reference-ordered host vector (this rank's rows; 0 elsewhere)"""
+        out = np.zeros(self.oc.N)
+        check(lib().iemic_vec_to_ref(self._h(), v.p, ptr(out)), "iemic_vec_to_ref")
+        return out
+
+    def from_host(self, x: np.ndarray) -> DeviceVec:
+        v = DeviceVec(self.oc)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        check(lib().iemic_vec_from_ref(self._h(), ptr(x), v.p), "iemic_vec_from_ref")
+        return v
 
 
 class Ocean:
@@ -77,6 +169,8 @@ class Ocean:
         self._F = np.zeros(self.N)
         self._sol = np.zeros(self.N)
         self.last_solve = None
+        self.solve_hook = None          # called with the iemic_solve_info of every solve
+        self._vpool = []                # free device vectors (DeviceVec buffers)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -93,9 +187,28 @@ class Ocean:
                     ib0=int(out[7]), ib1=int(out[8]), npx=int(out[9]), npy=int(out[10]),
                     hx=int(out[11]))
 
+    # ---- device vectors (DeviceOps) ---------------------------------------------------
+    def vec_ops(self) -> DeviceOps:
+        """The device vector algebra a continuation driver uses on this model."""
+        return DeviceOps(self)
+
+    def _vec_take(self) -> C.c_void_p:
+        if self._vpool:
+            return self._vpool.pop()
+        p = C.c_void_p()
+        check(lib().iemic_vec_alloc(self._h, C.byref(p)), "iemic_vec_alloc")
+        return p
+
+    def _vec_give(self, p) -> None:
+        if getattr(self, "_h", None):
+            self._vpool.append(p)
+
     # ---- lifecycle -----------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
+            for p in self._vpool:
+                lib().iemic_vec_free(self._h, p)
+            self._vpool = []
             lib().iemic_destroy(self._h)
             self._h = None
 
@@ -281,6 +394,8 @@ class Ocean:
         check(lib().iemic_solve(self._h, ptr(rhs), ptr(self._sol), C.byref(k), C.byref(info)),
               "iemic_solve")
         self.last_solve = info
+        if self.solve_hook is not None:
+            self.solve_hook(info)
         return self._sol
 
     def preProcess(self) -> None:

@@ -317,6 +317,27 @@ int iemic_solve(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* 
 int iemic_solve_dev(iemic_ctx* ctx, const double* b, double* x, const iemic_krylov* opt,
                     iemic_solve_info* info);
 
+/* ---- device vectors (Continuation.H's vector algebra, Utils::dot / norm / update on the
+ * solve map, Continuation.H:389-813) ---------------------------------------------------
+ * Vectors in the internal layout (iemic_layout: ext length, owned rows significant) on the
+ * context's device, so a continuation driver keeps state, tangent, dF/dpar and the
+ * corrector's solutions in HBM.  dot and norm_inf are summed / maximised over the
+ * context's ranks (collective: every rank calls them in the same order). */
+int iemic_vec_alloc(iemic_ctx* ctx, double** v);                 /* zeroed                 */
+int iemic_vec_free(iemic_ctx* ctx, double* v);
+/* z = a x + b y + c z on the owned rows (y may be NULL; c = 0 does not read z) */
+int iemic_vec_update(iemic_ctx* ctx, double a, const double* x, double b, const double* y, double c,
+                     double* z);
+int iemic_vec_dot(iemic_ctx* ctx, const double* x, const double* y, double* out);
+int iemic_vec_norm_inf(iemic_ctx* ctx, const double* x, double* out);
+/* host global vector in reference order <-> device vector (owned rows) */
+int iemic_vec_from_ref(iemic_ctx* ctx, const double* ref, double* v);
+int iemic_vec_to_ref(iemic_ctx* ctx, const double* v, double* ref);
+/* set = 0: v = state; set = 1: state = v (Model::getState / setState on the device) */
+int iemic_state_vec(iemic_ctx* ctx, double* v, int set);
+/* F(state) into the device vector F (Ocean::computeRHS without the host copy) */
+int iemic_rhs_vec(iemic_ctx* ctx, double* F);
+
 /* ---- one Newton step on the resident state (transient/Newton.H:92-99 form) -----
  * F(x); J(x); precond compute; solve J dx = -F; x += dx; F(x).  Returns ||F|| before /
  * after and the solve info.  Everything stays on the device. */
