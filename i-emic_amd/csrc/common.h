@@ -203,6 +203,7 @@ struct BlockGS {
                                      /* column + row offset of the subdomain's aggregates  */
     DevBuf<double> tsdiag;           /* fine 2x2 T/S blocks (active entries)              */
     DevBuf<double> mg_off[MG_MAX], mg_diag[MG_MAX], mg_fac[MG_MAX], mg_b[MG_MAX], mg_z[MG_MAX];
+    DevBuf<double> mg_zu[MG_MAX];    /* fused up leg (k_mg_up): the post-smoothed iterate      */
     DevBuf<double> mg_cinv;          /* coarsest level: dense inverse (2 ncl)^2          */
     /* subdomains: the coarsest T/S level solved globally (all ranks' coarsest cells plus
      * the cross-subdomain couplings; band LU + inverse on the device, on every rank) */

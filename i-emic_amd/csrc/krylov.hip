@@ -127,29 +127,46 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
 }
 
 
-/* Dynamics defect of the block GS (prec_gs.hip): d = r - A z on the active U/V/W/P rows,
- * 0 on the others.  With z = r on the identity rows and z = 0 on T/S (the state of z
- * after the dynamics pass), r - A z equals rr_D - A_DD z_D of the block iteration, so the
- * full rows of the SpMV are used.  One workgroup per 64 cells; the 64 slots of the four rows
- * are split evenly over the waves (U | U+V | V+W | W+P, 16 each: a wave per equation would
- * leave the U wave with 24 slots and the W wave with 7), the gathers read z directly, and the
- * rows' partials meet in LDS.  z, the flags and d are component-planar (plane stride ps:
- * the gathers of one unknown are unit-stride along i), r is the AoS right-hand side. */
+/* Dynamics defect of the block GS (prec_gs.hip): d = rr - A z on the active U/V/W/P rows,
+ * 0 on the others.  z is the pass iterate, 0 on the identity rows (whose couplings are in
+ * rr, the block right-hand side) and on T/S, so rr - A z equals rr_D - A_DD z_D of the
+ * block iteration.  One workgroup per 64 cells; the 64 slots of the four rows are split
+ * evenly over the waves (U | U+V | V+W | W+P, 16 each), the gathers read z directly, and
+ * the rows' partials meet in LDS.  z, rr, the flags and d are all component-planar (plane
+ * stride ps: unit-stride along i; round 4 read r as 48-byte AoS records).  Skipping the W
+ * row's four T/S slots (z(T, S) = 0) measured slower (24.7 against 22.5 us: the waves'
+ * balance), so they are read. */
 /* on[q]: row sp7_row(S0) + q of the cell is active; an identity row's coefficients are
  * neither loaded nor used (about half the cells are land at 2 degrees).  (Non-temporal
  * coefficient loads measured 35.6 against 26.1 us per defect, scripts/ab_probe.py.) */
+/* The loads of each row are issued in one predicated block (per-slot predicates made the
+ * compiler wait for every load before the next: 64 vmcnt(0) per wave), then the products
+ * are summed in slot order. */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
                                             int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
                                             int64_t ps, double* acc)
 {
+    constexpr int NS = S1 - S0;
+    double v[NS], zz[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) v[s] = zz[s] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (!on[q]) continue;
+#pragma unroll
+        for (int s = S0; s < S1; s++) {
+            const Slot sl = SLOTS[s];
+            if (sp7_row(s) - sp7_row(S0) != q) continue;
+            const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
+            v[s - S0] = val[(int64_t)s * nloc + lc];
+            zz[s - S0] = z[(int64_t)cidx + ps * sl.var];
+        }
+    }
 #pragma unroll
     for (int s = S0; s < S1; s++) {
-        const Slot sl = SLOTS[s];
         const int q = sp7_row(s) - sp7_row(S0);
-        if (!on[q]) continue;
-        const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-        acc[q] += val[(int64_t)s * nloc + lc] * z[(int64_t)cidx + ps * sl.var];
+        if (on[q]) acc[q] += v[s - S0] * zz[s - S0];
     }
 }
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
@@ -192,7 +209,7 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
                      : R == 2 ? red[2][1][cc] + red[3][0][cc]
                               : red[3][1][cc];
     const int64_t cell = e0 + lc0 + cc, e = cell + ps * R;
-    d[e] = knP[e] ? 0.0 : r[NUN * cell + R] - sum;
+    d[e] = knP[e] ? 0.0 : r[e] - sum;
 }
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d)

@@ -595,8 +595,11 @@ __global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__
 
 /* z = r on identity rows and 0 on the others (the apply's starting iterate: no separate
  * memset; halo cells are only read after an exchange, and one rank reads none);
- * rr = r - A(:, known) r(known) on the others (slot bitmask).  z goes to the output (AoS)
- * and to the planar iterate zP, rr to the planar rrP and (rr != null, the T/S sweeps) AoS */
+ * rr = r - A(:, known) r(known) on the others (slot bitmask).  z goes to the output (AoS);
+ * the planar iterate zP starts at 0 on every row, identity rows included: their couplings
+ * are in rr already, so every kernel of the passes reads zP on the active rows only and the
+ * dynamics defect is rr - A zP over all its slots (the T/S columns, 0 in zP until the T/S
+ * solve, not read at all); rr goes to the planar rrP and (rr != null, the T/S sweeps) AoS */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const uint64_t* __restrict__ kmask, const double* __restrict__ r,
                         double* __restrict__ z, double* __restrict__ rr, double* __restrict__ zP,
@@ -611,9 +614,8 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
         const int64_t row = NUN * cell + R;
         acc[R] = r[row];
         kn[R] = known[row] != 0;
-        const double zv = kn[R] ? acc[R] : 0.0;
-        z[row] = zv;
-        zP[PL(cell, R)] = zv;
+        z[row] = kn[R] ? acc[R] : 0.0;
+        zP[PL(cell, R)] = 0.0;
     }
     uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
     if (b[0] | b[1]) {
@@ -1523,17 +1525,34 @@ __host__ __device__ __forceinline__ int64_t mg_columns_of(const TsLev& V, int co
  * recurrence dp_k = F_k dp_{k-1} + g_k and the backward x_k = dp_k - Cp_k x_{k+1} as affine
  * Hillis-Steele scans over the P lanes (log2 P shuffle steps of 2x2 algebra each, no
  * division: the pivots were inverted at set-up).  The factor loads are issued first. */
+/* the 12 line factors of a lane (0 when !on), loadable ahead of the right-hand side */
+struct LineFac {
+    double a0, a1, a2, a3, i0, i1, i2, i3, q0, q1, q2, q3;
+};
+__device__ __forceinline__ LineFac line_fac(const double* __restrict__ f, int64_t cs, bool on)
+{
+    LineFac F{};
+    if (on) {
+        F.a0 = f[0]; F.a1 = f[cs]; F.a2 = f[2 * cs]; F.a3 = f[3 * cs];
+        F.i0 = f[4 * cs]; F.i1 = f[5 * cs]; F.i2 = f[6 * cs]; F.i3 = f[7 * cs];
+        F.q0 = -f[8 * cs]; F.q1 = -f[9 * cs]; F.q2 = -f[10 * cs]; F.q3 = -f[11 * cs];
+    }
+    return F;
+}
+template <int P>
+__device__ __forceinline__ void line_run(const LineFac& F, int k, double rt, double rs, double& xt, double& xs);
 template <int P>
 __device__ __forceinline__ void line_solve(const double* __restrict__ f, int64_t cs, bool on, int k,
                                            double rt, double rs, double& xt, double& xs)
 {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, i0 = 0.0, i1 = 0.0, i2 = 0.0, i3 = 0.0;
-    double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
-    if (on) {
-        a0 = f[0]; a1 = f[cs]; a2 = f[2 * cs]; a3 = f[3 * cs];
-        i0 = f[4 * cs]; i1 = f[5 * cs]; i2 = f[6 * cs]; i3 = f[7 * cs];
-        q0 = -f[8 * cs]; q1 = -f[9 * cs]; q2 = -f[10 * cs]; q3 = -f[11 * cs];
-    }
+    line_run<P>(line_fac(f, cs, on), k, rt, rs, xt, xs);
+}
+template <int P>
+__device__ __forceinline__ void line_run(const LineFac& F, int k, double rt, double rs, double& xt, double& xs)
+{
+    double a0 = F.a0, a1 = F.a1, a2 = F.a2, a3 = F.a3;
+    const double i0 = F.i0, i1 = F.i1, i2 = F.i2, i3 = F.i3;
+    double q0 = F.q0, q1 = F.q1, q2 = F.q2, q3 = F.q3;
     double ct = i0 * rt + i1 * rs, cv = i2 * rt + i3 * rs;
 #pragma unroll
     for (int d = 1; d < P; d <<= 1) {
@@ -1568,14 +1587,14 @@ __device__ __forceinline__ void line_solve(const double* __restrict__ f, int64_t
  * first post-smoothing colour launch, neighbours not yet relaxed in this sweep (smaller
  * colour) read with their aggregate's coarse correction C.z added.  zout (level 0, final
  * sweep): the active T/S rows of the preconditioner output (ext layout) get the result. */
+/* the line solve of column (i, jl) of the given colour from the current iterate (level k of
+ * this lane; on: k < l); corr: neighbours of a smaller colour read with their aggregate's
+ * coarse correction C.z added.  Returns the cell index (0 when !on). */
 template <int P>
-__device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k, const TsLev& C, int corr,
-                                       double* __restrict__ zout)
+__device__ __forceinline__ int64_t zl_col(const TsLev& V, int i, int jl, int k, bool on, int colour,
+                                          const TsLev& C, int corr, double& xt, double& xs)
 {
-    int i, jl;
-    if (!mg_column(V, colour, g, i, jl)) return;           /* whole column groups exit */
     const int64_t cs = V.cstr;
-    const bool on = k < V.l;
     int64_t c = 0;
     double rt = 0.0, rs = 0.0;
     if (on) {
@@ -1597,8 +1616,20 @@ __device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k,
             rs -= V.off[(int64_t)(8 + q) * cs + c] * zs;
         }
     }
-    double xt, xs;
     line_solve<P>(V.fac + c, cs, on, k, rt, rs, xt, xs);
+    return c;
+}
+
+template <int P>
+__device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k, const TsLev& C, int corr,
+                                       double* __restrict__ zout)
+{
+    int i, jl;
+    if (!mg_column(V, colour, g, i, jl)) return;           /* whole column groups exit */
+    const int64_t cs = V.cstr;
+    const bool on = k < V.l;
+    double xt, xs;
+    const int64_t c = zl_col<P>(V, i, jl, k, on, colour, C, corr, xt, xs);
     if (!on) return;
     V.z[c] = xt;
     V.z[cs + c] = xs;
@@ -1695,6 +1726,206 @@ template <int P>
 __global__ void __launch_bounds__(256) k_mg_rc(TsLev F, TsLev C, int shortcut, int relax)
 {
     rc_one<P>(F, C, (blockIdx.x * blockDim.x + threadIdx.x) / P, threadIdx.x % P, shortcut, relax);
+}
+
+/* ---- fused coarse-level visits (two colours, no halos, one sweep): one launch per 2 x 2
+ * aggregate instead of two dependent launches, each workgroup recomputing the colour-1
+ * lines its aggregate's colour-0 cells border (10 line solves for 2 + 2 outputs; the
+ * coarse levels are latency-bound, their arrays L2-resident).  Groups of P lanes: g < 8
+ * the line of neighbour q = g & 3 of colour-0 child h = g >> 2, g = 8, 9 the aggregate's
+ * own colour-1 children.  The arithmetic is that of the unfused launches, operation for
+ * operation (the sums in the same order), so both give the same iterates. */
+template <int P>
+__device__ __forceinline__ void mg_child0(const TsLev& F, int I, int J, int h, int& i, int& jl, bool& in)
+{
+    const int a = h ? 1 - F.jpar : F.jpar;          /* (a + h + jpar) even: colour 0 */
+    in = 2 * I + a < F.n && 2 * J + h < F.mb;
+    i = min(2 * I + a, F.n - 1);
+    jl = min(2 * J + h, F.mb - 1);
+}
+
+/* down leg at level F (first visit, colour 0 relaxed from zero): colour-1 lines, the
+ * restriction of the residual (zero on colour 1, -H z on colour 0: k_mg_rc's shortcut) and,
+ * when relax, the coarse level's colour-0 lines from zero -- k_mg_zl(colour 1) + k_mg_rc */
+template <int P>
+__global__ void __launch_bounds__(10 * P) k_mg_dn(TsLev F, TsLev C, int relax)
+{
+    __shared__ double xv[8][2][P];
+    const int g = threadIdx.x / P, k = threadIdx.x % P;
+    const int I = blockIdx.x % C.n, J = blockIdx.x / C.n;
+    const bool on = k < F.l;
+    const int64_t fs = F.cstr, cs = C.cstr;
+    const int64_t t = on ? mg_cell(C, I, J, k) : 0;
+    /* group 0's operands of the restriction and the coarse line, loaded before the lines */
+    double po[2][8];
+    LineFac cf{};
+    if (g == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            int i, jl;
+            bool in;
+            mg_child0<P>(F, I, J, h, i, jl, in);
+            const int64_t c = mg_cell(F, i, jl, on ? k : 0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                po[h][q] = F.off[(int64_t)q * fs + c];
+                po[h][4 + q] = F.off[(int64_t)(8 + q) * fs + c];
+            }
+        }
+        cf = line_fac(C.fac + t, cs, on && relax && mg_lcolour(C, I, J) == 0);
+    }
+    if (g < 8) {
+        const int h = g >> 2, q = g & 3;
+        int i, jl;
+        bool in;
+        mg_child0<P>(F, I, J, h, i, jl, in);
+        double xt = 0.0, xs = 0.0;
+        if (in) {
+            int ii = i, jj = jl, kk = on ? k : 0;
+            mg_nbc(F, q, ii, jj, kk);
+            if (ii == i && jj == jl) {                 /* clamped: the child itself, weight 0 */
+                if (on) {
+                    const int64_t c = mg_cell(F, i, jl, k);
+                    xt = F.z[c];
+                    xs = F.z[fs + c];
+                }
+            } else {
+                zl_col<P>(F, ii, jj, k, on, 1, F, 0, xt, xs);
+            }
+        }
+        xv[g][0][k] = xt;
+        xv[g][1][k] = xs;
+    } else {
+        const int h = g - 8, a = h ? F.jpar : 1 - F.jpar;   /* colour 1 */
+        const int i = 2 * I + a, jl = 2 * J + h;
+        if (i < F.n && jl < F.mb) {
+            double xt, xs;
+            const int64_t c = zl_col<P>(F, i, jl, k, on, 1, F, 0, xt, xs);
+            if (on) {
+                F.z[c] = xt;
+                F.z[fs + c] = xs;
+            }
+        }
+    }
+    __syncthreads();
+    if (g != 0) return;
+    double rr[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        int i, jl;
+        bool in;
+        mg_child0<P>(F, I, J, h, i, jl, in);
+        double at = 0.0, as = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            at += po[h][q] * xv[4 * h + q][0][k];
+            as += po[h][4 + q] * xv[4 * h + q][1][k];
+        }
+        rr[h][0] = (on && in) ? -at : 0.0;
+        rr[h][1] = (on && in) ? -as : 0.0;
+    }
+    const double bt = rr[0][0] + rr[1][0], bs = rr[0][1] + rr[1][1];
+    if (on) {
+        C.b[t] = bt;
+        C.b[cs + t] = bs;
+    }
+    if (!relax) return;
+    if (mg_lcolour(C, I, J) == 0) {
+        double xt, xs;
+        line_run<P>(cf, k, bt, bs, xt, xs);
+        if (on) {
+            C.z[t] = xt;
+            C.z[cs + t] = xs;
+        }
+    } else if (on) {
+        C.z[t] = 0.0;
+        C.z[cs + t] = 0.0;
+    }
+}
+
+/* up leg at level F (one sweep, colours 1 then 0): the colour-1 lines with the coarse
+ * correction C.z added to their colour-0 neighbours, then the colour-0 lines from the new
+ * colour-1 values -- k_mg_zl(1, corr) + k_mg_zl(0); the result goes to zu (not F.z, which
+ * the neighbouring workgroups still read) */
+template <int P>
+__global__ void __launch_bounds__(10 * P) k_mg_up(TsLev F, TsLev C, double* __restrict__ zu)
+{
+    __shared__ double xv[8][2][P];
+    const int g = threadIdx.x / P, k = threadIdx.x % P;
+    const int I = blockIdx.x % C.n, J = blockIdx.x / C.n;
+    const bool on = k < F.l;
+    const int64_t fs = F.cstr;
+    /* groups 0, 1: their colour-0 child's operands, loaded before the colour-1 lines */
+    int64_t c0 = 0;
+    bool in0 = false;
+    double b0t = 0.0, b0s = 0.0, po[8];
+    LineFac ff{};
+    if (g < 2) {
+        int i, jl;
+        mg_child0<P>(F, I, J, g, i, jl, in0);
+        if (in0 && on) {
+            c0 = mg_cell(F, i, jl, k);
+            b0t = F.b[c0];
+            b0s = F.b[fs + c0];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                po[q] = F.off[(int64_t)q * fs + c0];
+                po[4 + q] = F.off[(int64_t)(8 + q) * fs + c0];
+            }
+        }
+        ff = line_fac(F.fac + c0, fs, in0 && on);
+    }
+    if (g < 8) {
+        const int h = g >> 2, q = g & 3;
+        int i, jl;
+        bool in;
+        mg_child0<P>(F, I, J, h, i, jl, in);
+        double xt = 0.0, xs = 0.0;
+        if (in) {
+            int ii = i, jj = jl, kk = on ? k : 0;
+            mg_nbc(F, q, ii, jj, kk);
+            if (ii == i && jj == jl) {                 /* clamped: the child's old value, weight 0 */
+                if (on) {
+                    const int64_t c = mg_cell(F, i, jl, k);
+                    xt = F.z[c];
+                    xs = F.z[fs + c];
+                }
+            } else {
+                zl_col<P>(F, ii, jj, k, on, 1, C, 1, xt, xs);
+            }
+        }
+        xv[g][0][k] = xt;
+        xv[g][1][k] = xs;
+    } else {
+        const int h = g - 8, a = h ? F.jpar : 1 - F.jpar;
+        const int i = 2 * I + a, jl = 2 * J + h;
+        if (i < F.n && jl < F.mb) {
+            double xt, xs;
+            const int64_t c = zl_col<P>(F, i, jl, k, on, 1, C, 1, xt, xs);
+            if (on) {
+                zu[c] = xt;
+                zu[fs + c] = xs;
+            }
+        }
+    }
+    __syncthreads();
+    if (g >= 2 || !in0) return;                        /* whole groups */
+    /* colour-0 child h = g: its line from the four new colour-1 neighbours (k_mg_zl colour 0) */
+    const int h = g;
+    double rt = b0t, rs = b0s;
+    if (on) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            rt -= po[q] * xv[4 * h + q][0][k];
+            rs -= po[4 + q] * xv[4 * h + q][1][k];
+        }
+    }
+    double xt, xs;
+    line_run<P>(ff, k, rt, rs, xt, xs);
+    if (on) {
+        zu[c0] = xt;
+        zu[fs + c0] = xs;
+    }
 }
 
 /* Level-0 entry: the T/S right-hand side rr_TS - A_TS,D z_D of a tile of TI columns of one
@@ -2491,9 +2722,10 @@ static int mg_setup(iemic_ctx* c)
         for (int lv = 0; lv <= q; lv++) {
             const size_t cs = (size_t)mg_view(c, lv).cstr;
             if (gs.mg_off[lv].alloc(16 * cs) || gs.mg_diag[lv].alloc(4 * cs) || gs.mg_fac[lv].alloc(12 * cs) ||
-                gs.mg_b[lv].alloc(2 * cs) || gs.mg_z[lv].alloc(2 * cs))
+                gs.mg_b[lv].alloc(2 * cs) || gs.mg_z[lv].alloc(2 * cs) || gs.mg_zu[lv].alloc(2 * cs))
                 return IEMIC_ENOMEM;
-            for (DevBuf<double>* bptr : {&gs.mg_off[lv], &gs.mg_diag[lv], &gs.mg_fac[lv], &gs.mg_b[lv], &gs.mg_z[lv]})
+            for (DevBuf<double>* bptr : {&gs.mg_off[lv], &gs.mg_diag[lv], &gs.mg_fac[lv], &gs.mg_b[lv], &gs.mg_z[lv],
+                                         &gs.mg_zu[lv]})
                 HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         }
         const size_t NC = (size_t)2 * n * m * l;
@@ -2686,6 +2918,23 @@ static int mg_coarsest(iemic_ctx* c, int q)
 /* One V-cycle from level q.  first: the level's iterate started at 0 and its colour-0 lines
  * were relaxed by the launch that formed its right-hand side (k_mg_entry / k_mg_rc).
  * zout: the last level-0 sweep writes z(T, S) into the preconditioner output. */
+/* a coarse level visited by the fused launches (k_mg_dn / k_mg_up): two colours, one
+ * sweep, no halo on it or on its coarse level (one rank, or the bands' band-local levels) */
+static bool mg_fused(iemic_ctx* c, int q)
+{
+    BlockGS& gs = c->gs;
+    if (q < 1 || q + 1 >= gs.mg_nlev || std::max(1, gs.mg_sweeps) != 1 || !gs.mg_zu[q].p) return false;
+    const TsLev V = mg_view(c, q), C = mg_view(c, q + 1);
+    return mg_ncolour(V) == 2 && !V.hj && !V.hi && !V.vis && !V.visi && !C.hj && !C.hi && C.l == V.l;
+}
+/* level q as its coarse-correction source: the iterate after its post-smoothing */
+static TsLev mg_final(iemic_ctx* c, int q)
+{
+    TsLev V = mg_view(c, q);
+    if (mg_fused(c, q)) V.z = c->gs.mg_zu[q].p;
+    return V;
+}
+
 static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
 {
     BlockGS& gs = c->gs;
@@ -2693,6 +2942,28 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
     int rc;
     const TsLev V = mg_view(c, q);
     const int nc = mg_ncolour(V), nu = std::max(1, gs.mg_sweeps);
+    if (first && !zout && mg_fused(c, q)) {
+        /* one launch down (colour 1 + restriction + the coarse colour 0), one launch up */
+        const int qc = gs.mg_nlev - 1;
+        const TsLev C = mg_view(c, q + 1);
+        const int P = mg_lanes(V.l);
+        const unsigned g = (unsigned)(C.n * C.mb);
+        const int relax = q + 1 < qc ? 1 : 0;
+        if (P == 16) hipLaunchKernelGGL(k_mg_dn<16>, dim3(g), dim3(160), 0, s, V, C, relax);
+        else if (P == 32) hipLaunchKernelGGL(k_mg_dn<32>, dim3(g), dim3(320), 0, s, V, C, relax);
+        else hipLaunchKernelGGL(k_mg_dn<64>, dim3(g), dim3(640), 0, s, V, C, relax);
+        if (q + 1 == qc) {
+            if ((rc = mg_coarsest(c, q + 1))) return rc;
+        } else if ((rc = mg_vcycle(c, q + 1, true, nullptr))) {
+            return rc;
+        }
+        const TsLev Cf = mg_final(c, q + 1);
+        double* zu = gs.mg_zu[q].p;
+        if (P == 16) hipLaunchKernelGGL(k_mg_up<16>, dim3(g), dim3(160), 0, s, V, Cf, zu);
+        else if (P == 32) hipLaunchKernelGGL(k_mg_up<32>, dim3(g), dim3(320), 0, s, V, Cf, zu);
+        else hipLaunchKernelGGL(k_mg_up<64>, dim3(g), dim3(640), 0, s, V, Cf, zu);
+        return 0;
+    }
     for (int sw = 0; sw < nu; sw++)
         for (int h = (sw == 0 && first) ? 1 : 0; h < nc; h++) {
             if ((rc = mg_halo(c, V))) return rc;
@@ -2712,15 +2983,16 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
     } else if ((rc = mg_vcycle(c, q + 1, true, nullptr))) {
         return rc;
     }
+    const TsLev Cf = mg_final(c, q + 1);
     /* coarse correction: added where the first post-smoothing colours read it, or (level 0
      * of a band group, whose lines also read the neighbour bands' rows) explicitly */
     const bool corr = V.hj == 0 && V.hi == 0;
     if (!corr)
-        hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)V.n * V.mb * V.l)), dim3(256), 0, s, V, C);
+        hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)V.n * V.mb * V.l)), dim3(256), 0, s, V, Cf);
     for (int sw = 0; sw < nu; sw++)
         for (int h = nc - 1; h >= 0; h--) {
             if ((rc = mg_halo(c, V))) return rc;
-            if ((rc = mg_zl(c, V, h, corr && sw == 0 ? &C : nullptr, sw + 1 == nu ? zout : nullptr))) return rc;
+            if ((rc = mg_zl(c, V, h, corr && sw == 0 ? &Cf : nullptr, sw + 1 == nu ? zout : nullptr))) return rc;
         }
     return 0;
 }
@@ -3067,7 +3339,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
      * minimal-residual w (dyn_mr) or the fixed w = dyn_omega */
     if (gs.dyn_mr && gs.dyn_iters > 1) {
         if (band && (rc = halo_exchange_planar(c, zP, NUN, ps, 1))) return rc;
-        if ((rc = spmv_dyn_defect(c, zP, r, gs.knP.p, gs.dres.p))) return rc;
+        if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p))) return rc;
         for (int it = 1; it < gs.dyn_iters; it++) {
             const bool last = it + 1 == gs.dyn_iters;
             if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p))) return rc;
@@ -3083,7 +3355,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     for (int it = 1; !gs.dyn_mr && it < gs.dyn_iters; it++) {
         const bool last = it + 1 == gs.dyn_iters;
         if (band && (rc = halo_exchange_planar(c, zP, NUN, ps, 1))) return rc;   /* w, p of the neighbours */
-        if ((rc = spmv_dyn_defect(c, zP, r, gs.knP.p, gs.dres.p))) return rc;
+        if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p))) return rc;
         if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last)))) return rc;   /* z += w zc */
         if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;
     }
