@@ -227,12 +227,24 @@ struct BlockGS {
     DevBuf<double> colvT;            /* the Schur solution transposed (j * n + i)          */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */
+    /* owned cells with a non-identity row (the rest: land, all six rows identity), ascending:
+     * FGMRES keeps its Arnoldi basis on these cells only (krylov.hip) */
+    DevBuf<int> act;
+    DevBuf<uint8_t> actf;            /* per owned cell: 1 active (k_cell_active)           */
+    int64_t nact = 0;
+    std::vector<uint8_t> act_h;      /* the per-cell flags the list was built from        */
 };
 
 struct Krylov {
     int m = 0;                       /* allocated basis size                            */
     DevBuf<double> V, Z;             /* (m+1) x N and m x N                             */
     DevBuf<double> w, r;
+    /* DCGS2 with the block GS: the Arnoldi basis compressed to the active cells
+     * (BlockGS::act, 6 nact rows per vector), the preconditioner input rf (full, zero on
+     * the land cells) and, for a right-hand side with land-cell entries, t and b' */
+    int mc = 0;
+    int64_t nc = 0;
+    DevBuf<double> Vc, rf, t, bp;
 };
 
 constexpr int RED_BLOCKS = 1024;     /* partial-sum blocks of the reductions            */

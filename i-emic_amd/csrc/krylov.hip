@@ -724,21 +724,71 @@ static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, doubl
     return 0;
 }
 
-static int ensure_krylov(iemic_ctx* c, int m)
+/* the Krylov work space: Z (m x N) and w, r always; the full-length basis V ((m+1) x N) unless
+ * the basis is compressed, then Vc ((m+1) x nc) and the full-length rf, t, b' */
+static int ensure_krylov(iemic_ctx* c, int m, int64_t nc = 0)
 {
-    if (c->kr.m >= m && c->kr.V.p) return 0;
+    Krylov& k = c->kr;
     const int64_t N = c->nerows;
     int rc = 0;
-    rc |= c->kr.V.alloc((size_t)(m + 1) * N);
-    rc |= c->kr.Z.alloc((size_t)m * N);
-    rc |= c->kr.w.alloc(N);
-    rc |= c->kr.r.alloc(N);
-    if (rc) {
-        set_error("fgmres: out of device memory for the Krylov basis");
-        return IEMIC_ENOMEM;
+    if (k.m < m || !k.Z.p) {
+        k.V.free();                  /* sized by m: reallocated below when needed */
+        rc |= k.Z.alloc((size_t)m * N);
+        rc |= k.w.alloc(N);
+        rc |= k.r.alloc(N);
+        if (rc) {
+            set_error("fgmres: out of device memory for the Krylov basis");
+            return IEMIC_ENOMEM;
+        }
+        k.m = m;
     }
-    c->kr.m = m;
+    if (!nc && !k.V.p) {
+        if (k.V.alloc((size_t)(k.m + 1) * N)) {
+            set_error("fgmres: out of device memory for the Krylov basis");
+            return IEMIC_ENOMEM;
+        }
+    }
+    if (nc && (k.mc < m || k.nc < nc || !k.Vc.p)) {
+        rc |= k.Vc.alloc((size_t)(m + 1) * nc);
+        if (!k.rf.p) rc |= k.rf.alloc(N) | k.t.alloc(N) | k.bp.alloc(N);
+        if (rc) {
+            set_error("fgmres: out of device memory for the Krylov basis");
+            return IEMIC_ENOMEM;
+        }
+        k.mc = m;
+        k.nc = nc;
+    }
     return 0;
+}
+
+/* the compressed Arnoldi basis: rows of the active cells act[] (6 per cell), in order */
+__global__ void k_cgather(const double* __restrict__ full, const int* __restrict__ act, int64_t nc,
+                          int64_t own0, double s, double* __restrict__ cmp)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nc;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cl = q / NUN;
+        cmp[q] = s * full[NUN * (own0 + act[cl]) + (q - NUN * cl)];
+    }
+}
+__global__ void k_cscatter(const double* __restrict__ cmp, const int* __restrict__ act, int64_t nc,
+                           int64_t own0, double* __restrict__ full)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nc;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cl = q / NUN;
+        full[NUN * (own0 + act[cl]) + (q - NUN * cl)] = cmp[q];
+    }
+}
+/* t = v on the rows of the inactive (land) cells, 0 elsewhere (owned rows) */
+__global__ void k_land_part(const double* __restrict__ v, const uint8_t* __restrict__ actf, int64_t nloc,
+                            int64_t own0, double* __restrict__ t)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < NUN * nloc;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = NUN * own0 + q;
+        t[r] = actf[q / NUN] ? 0.0 : v[r];
+    }
 }
 
 /* coefficients -> device through the pinned staging area (the previous use of the area
@@ -784,15 +834,25 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     /* vectors are ext-layout (stride NE); kernels touch the owned rows [o, o + NL) */
     const int m = std::max(1, std::min(opt->krylov_dim, MAX_KRYLOV));
     const int64_t NE = c->nerows, o = NUN * c->own0, NL = c->nlrows;
-    int rc = ensure_krylov(c, m);
+    /* DCGS2 with the block GS: the Arnoldi basis on the active cells only.  Land cells are
+     * identity rows of J and of the preconditioner, so with zero land entries in the right-hand
+     * side every Krylov vector is exactly zero there (48 % of the rows at 2 degrees); the two
+     * basis passes per step read and write the active rows only.  A right-hand side with land
+     * entries is first reduced: x_land = b_land, b' = b - J b_land (zero on the land rows). */
+    const BlockGS& gs = c->gs;
+    const bool cmp = opt->orth == 0 && opt->prec == 2 && gs.ready && gs.kind == 2 && gs.nact > 0;
+    const int64_t NC = cmp ? NUN * gs.nact : 0;
+    int rc = ensure_krylov(c, m, NC);
     if (rc) return rc;
     iemic_solve_info inf{};
     auto T0 = std::chrono::steady_clock::now();
-    double* V = c->kr.V.p;
+    double* V = cmp ? nullptr : c->kr.V.p;
+    double* Vc = cmp ? c->kr.Vc.p : nullptr;
     double* Z = c->kr.Z.p;
     double* w = c->kr.w.p;
     double* r = c->kr.r.p;
     const unsigned G = grid_for(NL);
+    const unsigned GC = grid_for(NC);
     std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), h(m + 1), h2(m + 1), y(m);
     std::vector<double> zs(m + 1, 1.0);   /* DCGS2: scale of the stored z_j (1 for DGKS) */
     if (2 * m + 5 > RED_ROWS) {
@@ -819,9 +879,24 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         if (info) *info = inf;
         return 0;
     }
+    const double* b_orig = b;
+    bool land_rhs = false;
+    if (cmp) {
+        /* the preconditioner input: zero on the land rows, the active rows scattered per step */
+        HIP_OK(hipMemsetAsync(c->kr.rf.p, 0, sizeof(double) * NE, c->stream));
+        double* t = c->kr.t.p;
+        hipLaunchKernelGGL(k_land_part, dim3(G), dim3(256), 0, c->stream, b, gs.actf.p, c->nloc, c->own0, t);
+        if (dot(c, t, t, 0) > 0.0) {
+            land_rhs = true;
+            if ((rc = spmv(c, t, w, c->stream))) return rc;
+            hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b + o, -1.0, w + o,
+                               c->kr.bp.p + o, NL);
+            b = c->kr.bp.p;
+        }
+    }
     /* r = b (x0 = 0) */
     HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
-    double beta = bnorm, res = 1.0, res_c0 = 1.0;
+    double beta = land_rhs ? sqrt0(dot(c, b, b, 0)) : bnorm, res = beta / bnorm, res_c0 = res;
     int it = 0;
     /* the safeguard's switch lasts for this solve only */
     struct Restore {
@@ -829,9 +904,13 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         int mr;
         ~Restore() { c->gs.dyn_mr = mr; }
     } restore{c, c->gs.dyn_mr};
-    for (int cycle = 0; cycle <= opt->max_restarts; cycle++) {
+    /* beta = 0: a right-hand side on the land rows only, solved by x = t below */
+    for (int cycle = 0; beta > 0.0 && cycle <= opt->max_restarts; cycle++) {
         const int it_c0 = it;
-        hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r + o, 1.0 / beta, V + o, NL);
+        if (cmp)
+            hipLaunchKernelGGL(k_cgather, dim3(GC), dim3(256), 0, c->stream, r, gs.act.p, NC, c->own0, 1.0 / beta, Vc);
+        else
+            hipLaunchKernelGGL(k_scale_copy, dim3(G), dim3(256), 0, c->stream, r + o, 1.0 / beta, V + o, NL);
         std::fill(g.begin(), g.end(), 0.0);
         g[0] = beta;
         int j = 0;
@@ -919,35 +998,47 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
              * solution update does not read. */
             std::vector<double> htent(m + 1), col(m + 1);
             int ncolf = 0;                 /* finalised columns */
-            const int nbx1 = (int)std::min<int64_t>(RED_BLOCKS, (NL / 2 + 256 * DOT1_E - 1) / (256 * DOT1_E));
+            /* the basis: compressed (Vc, stride NC, from row 0) or the ext vectors' owned rows */
+            double* const Q = cmp ? Vc : V + o;
+            const int64_t LQ = cmp ? NC : NE, NQ = cmp ? NC : NL;
+            const int nbx1 = (int)std::min<int64_t>(RED_BLOCKS, (NQ / 2 + 256 * DOT1_E - 1) / (256 * DOT1_E));
             /* z_jj = M u_jj with u_jj of norm bt_jj: the Hessenberg column of z_jj / bt_jj is
              * the one assembled below, so the solution update divides y_jj by bt_jj */
             std::fill(zs.begin(), zs.end(), 1.0);
             /* iteration jj: [update of jj-1 enqueued before] prec, SpMV, dot pass, coefficients,
              * rows -> pinned slot jj % 2, update */
             auto enqueue = [&](int jj) -> int {
-                double* u = V + (int64_t)jj * NE;
-                double* wv = jj < m ? V + (int64_t)(jj + 1) * NE : nullptr;
+                double* u = Q + (int64_t)jj * LQ;
+                double* wv = jj < m ? Q + (int64_t)(jj + 1) * LQ : nullptr;
                 hipEvent_t* e = ev + 3 * (jj & 1);
                 int rc2;
                 if (jj < m) {
                     double* zj = Z + (int64_t)jj * NE;
+                    /* the full-length input of the preconditioner and output of the SpMV */
+                    double* uf = cmp ? c->kr.rf.p : u - o;
+                    double* wf = cmp ? w : wv - o;
+                    if (cmp)
+                        hipLaunchKernelGGL(k_cscatter, dim3(GC), dim3(256), 0, c->stream, u, gs.act.p, NC,
+                                           c->own0, uf);
                     HIP_OK(hipEventRecord(e[0], c->stream));
                     if (opt->prec > 0) {
-                        if ((rc2 = prec_apply(c, u, zj))) return rc2;
+                        if ((rc2 = prec_apply(c, uf, zj))) return rc2;
                     } else {
-                        HIP_OK(hipMemcpyAsync(zj, u, sizeof(double) * NE, hipMemcpyDeviceToDevice,
+                        HIP_OK(hipMemcpyAsync(zj, uf, sizeof(double) * NE, hipMemcpyDeviceToDevice,
                                               c->stream));
                     }
                     HIP_OK(hipEventRecord(e[1], c->stream));
-                    if ((rc2 = spmv(c, zj, wv, c->stream))) return rc2;
+                    if ((rc2 = spmv(c, zj, wf, c->stream))) return rc2;
                     HIP_OK(hipEventRecord(e[2], c->stream));
+                    if (cmp)
+                        hipLaunchKernelGGL(k_cgather, dim3(GC), dim3(256), 0, c->stream, wf, gs.act.p, NC,
+                                           c->own0, 1.0, wv);
                 }
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
                 const double* wd = wv ? wv : u;
                 hipLaunchKernelGGL(k_dcgs_dot1, dim3(nbx1), dim3(256), sizeof(double) * 4 * (2 * nv + 3),
-                                   c->stream, V + o, NE, nv, u + o, wd + o, NL, c->d_part.p, nbx1);
+                                   c->stream, Q, LQ, nv, u, wd, NQ, c->d_part.p, nbx1);
                 hipLaunchKernelGGL(k_mdot_final, dim3(2 * nv + 3), dim3(256), 0, c->stream, c->d_part.p,
                                    nbx1, 2 * nv + 3, c->d_hbuf.p);
                 if ((rc2 = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc2;
@@ -957,8 +1048,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                                       sizeof(double) * (2 * nv + 5), hipMemcpyDeviceToHost, c->stream));
                 HIP_OK(hipEventRecord(evr[jj & 1], c->stream));
                 if (jj < m)
-                    hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, V + o, NE, nv,
-                                       c->d_hbuf.p + RED_ROWS, u + o, wv + o, NL);
+                    hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, Q, LQ, nv,
+                                       c->d_hbuf.p + RED_ROWS, u, wv, NQ);
                 return 0;
             };
             if ((rc = enqueue(0))) return rc;
@@ -1045,6 +1136,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             inf.safeguard++;
         res_c0 = res;
     }
+    /* the land part of a reduced right-hand side: x = x' + t */
+    if (land_rhs)
+        hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, x + o, 1.0, c->kr.t.p + o, x + o, NL);
+    b = b_orig;
     /* explicit residual (Ocean.C:1140-1150) */
     rc = spmv(c, x, w, c->stream);
     if (rc) return rc;

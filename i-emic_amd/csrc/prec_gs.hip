@@ -111,6 +111,16 @@ __global__ void k_known(const double* __restrict__ val, Lay L, int64_t rowintcon
     }
 }
 
+/* 1 per owned cell (owned index lc) with a non-identity row */
+__global__ void k_cell_active(const uint8_t* __restrict__ known, Lay L, uint8_t* __restrict__ act)
+{
+    OWNED_CELL;
+    bool a = false;
+#pragma unroll
+    for (int r = 0; r < NUN; r++) a |= !known[NUN * cell + r];
+    act[lc] = a ? 1 : 0;
+}
+
 /* 2x2 inverse of [[a b][c d]] restricted to the active unknowns (ia, ib) */
 __device__ __forceinline__ void inv2(double a, double b, double c, double d, bool ia, bool ib,
                                      double* out)
@@ -593,16 +603,17 @@ __global__ void __launch_bounds__(256) k_band_inv_pan(const double* __restrict__
 
 /* ---- apply ------------------------------------------------------------------------ */
 
-/* z = r on identity rows and 0 on the others (the apply's starting iterate: no separate
- * memset; halo cells are only read after an exchange, and one rank reads none);
- * rr = r - A(:, known) r(known) on the others (slot bitmask).  z goes to the output (AoS);
- * the planar iterate zP starts at 0 on every row, identity rows included: their couplings
- * are in rr already, so every kernel of the passes reads zP on the active rows only and the
- * dynamics defect is rr - A zP over all its slots (the T/S columns, 0 in zP until the T/S
- * solve, not read at all); rr goes to the planar rrP and (rr != null, the T/S sweeps) AoS */
+/* The output z = r on identity rows (zall: and 0 on the others -- the T/S sweeps iterate
+ * on z; otherwise the last dynamics pass and the T/S multigrid write every active row);
+ * rr = r - A(:, known) r(known) on the others (slot bitmask), to the planar rrP and
+ * (rr != null, the T/S sweeps) AoS.  The planar iterate zP is 0 on the identity rows and on
+ * T/S (zeroed when the preconditioner is computed, never written there) and the first pass
+ * writes its active dynamics rows before reading them, so the apply does not touch it here:
+ * the identity rows' couplings are in rr, every kernel of the passes reads zP on the active
+ * rows and the dynamics defect is rr - A zP over all its slots */
 __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restrict__ known,
                         const uint64_t* __restrict__ kmask, const double* __restrict__ r,
-                        double* __restrict__ z, double* __restrict__ rr, double* __restrict__ zP,
+                        double* __restrict__ z, double* __restrict__ rr, int zall,
                         double* __restrict__ rrP, Lay L)
 {
     LAY_ALIASES;
@@ -614,8 +625,7 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
         const int64_t row = NUN * cell + R;
         acc[R] = r[row];
         kn[R] = known[row] != 0;
-        z[row] = kn[R] ? acc[R] : 0.0;
-        zP[PL(cell, R)] = 0.0;
+        if (kn[R] || zall) z[row] = kn[R] ? acc[R] : 0.0;
     }
     uint64_t b[2] = {kmask[2 * cell], kmask[2 * cell + 1]};
     if (b[0] | b[1]) {
@@ -3110,6 +3120,8 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     const unsigned gc = (unsigned)((c->nloc + 255) / 256);
     const unsigned gN = (unsigned)std::min<int64_t>((NE + 255) / 256, 4096);
     HIP_OK(hipMemsetAsync(gs.known.p, 1, NE, c->stream));     /* outer halo rows: identity */
+    /* the planar iterate: 0 on the rows no pass writes (identity rows of this Jacobian, T/S) */
+    HIP_OK(hipMemsetAsync(gs.zP.p, 0, sizeof(double) * NE, c->stream));
     hipLaunchKernelGGL(k_known, dim3(gc), dim3(256), 0, c->stream, c->d_val.p, L,
                        (int64_t)c->rowintcon, gs.known.p);
     HIP_OK(hipGetLastError());
@@ -3121,6 +3133,23 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     }
     hipLaunchKernelGGL(k_known_planar, dim3((unsigned)((next + 255) / 256)), dim3(256), 0, c->stream,
                        gs.known.p, gs.knP.p, next);
+    {
+        /* the active-cell list of the compressed Arnoldi basis (rebuilt when the flags change) */
+        if (gs.actf.n < (size_t)c->nloc && gs.actf.alloc(c->nloc)) return IEMIC_ENOMEM;
+        hipLaunchKernelGGL(k_cell_active, dim3(gc), dim3(256), 0, c->stream, gs.known.p, L, gs.actf.p);
+        std::vector<uint8_t> h((size_t)c->nloc);
+        if ((rc = d2h(c, h.data(), gs.actf.p, h.size()))) return rc;
+        if (h != gs.act_h) {
+            std::vector<int> list;
+            list.reserve(h.size());
+            for (int64_t q = 0; q < c->nloc; q++)
+                if (h[q]) list.push_back((int)q);
+            gs.nact = (int64_t)list.size();
+            if (gs.act.n < list.size() + 1 && gs.act.alloc(list.size() + 1)) return IEMIC_ENOMEM;
+            if (!list.empty() && (rc = h2d(c, gs.act.p, list.data(), sizeof(int) * list.size()))) return rc;
+            gs.act_h.swap(h);
+        }
+    }
     {
         /* global column / U/V-point flags: the Schur structure is that of the whole grid */
         const size_t nf = (size_t)2 * c->n * c->m;
@@ -3332,7 +3361,7 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
     /* the halo rows of r hold the neighbours' identity-row values the couplings need */
     if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
     hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
-                       r, z, aos_all ? gs.rr.p : nullptr, zP, gs.rrP.p, L);
+                       r, z, aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
     if ((rc = dyn_solve(c, gs.rrP.p, zP, nullptr, 0.0, zaos_of(gs.dyn_iters == 1)))) return rc;
     if (ts_at == 1 && gs.dyn_iters > 1 && (rc = ts())) return rc;
     /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
