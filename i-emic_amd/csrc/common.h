@@ -230,6 +230,8 @@ struct BlockGS {
     /* owned cells with a non-identity row (the rest: land, all six rows identity), ascending:
      * FGMRES keeps its Arnoldi basis on these cells only (krylov.hip) */
     DevBuf<int> act;
+    DevBuf<int> cmap;                /* per owned cell: its index in act, -1 (land)        */
+    int64_t ric = -1;                /* compressed row of the integral condition (owned)   */
     DevBuf<uint8_t> actf;            /* per owned cell: 1 active (k_cell_active)           */
     int64_t nact = 0;
     std::vector<uint8_t> act_h;      /* the per-cell flags the list was built from        */
@@ -420,6 +422,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
 /* prec.hip */
 int prec_compute(iemic_ctx* c, const iemic_krylov* opt);
 int prec_apply(iemic_ctx* c, const double* r, double* z);
+/* the block GS apply from a compressed input (6 rows per BlockGS::act cell, zero land rows) */
+int gs_apply_c(iemic_ctx* c, const double* rc, double* z);
+/* y = J x written compressed (rows of the active cells only; x full, halo current) */
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc);
 }  // namespace iemic
 
 #endif

@@ -61,12 +61,18 @@ __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, i
         acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
     }
 }
+/* CMP (FGMRES's compressed basis): y holds the rows of the active cells only (cmap: owned
+ * cell -> its index, -1 for land); land cells load no coefficients and a tile without an
+ * active cell exits before staging anything */
+template <bool CMP>
 __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restrict__ val,
                                                const double* __restrict__ x,
-                                               double* __restrict__ y, int nloc, int ntile, int tpr)
+                                               double* __restrict__ y, int nloc, int ntile, int tpr,
+                                               const int* __restrict__ cmap)
 {
     __shared__ double xs[6 * (SP7_T + 2) * NUN];
     __shared__ double red[4][3][SP7_T];
+    __shared__ int cms[SP7_T];
     const int l = X.l, nx = X.nx;
     const int per = (ntile + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -76,6 +82,12 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
     const int nc = min(SP7_T, nx - i0);
     const int lc0 = row * nx + i0;
     const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    int cm = 0;
+    if (CMP) {
+        cm = c < nc ? cmap[lc0 + c] : -1;
+        if (g == 0) cms[c] = cm;
+        if (!__syncthreads_or(cm >= 0)) return;     /* a land tile */
+    }
     /* stage x: 6 grid rows x (nc + 2) cells x 6 unknowns, contiguous runs (the two end
      * cells: the neighbour columns, from the x halo when the x direction is split) */
     {
@@ -93,7 +105,7 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
             xs[(q * (SP7_T + 2) + p) * NUN + var] = x[NUN * cell + var];
         }
     }
-    const bool act = c < nc;
+    const bool act = c < nc && (!CMP || cm >= 0);
     const int64_t lc = lc0 + c;
     double acc[3] = {0.0, 0.0, 0.0};
     double v[26];
@@ -122,7 +134,8 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
         case 4: v = red[2][2][cc] + red[3][0][cc]; break;
         default: v = red[3][1][cc]; break;
         }
-        y[NUN * ((int64_t)HALO * l * nx + lc0) + o] = v;
+        if (!CMP) y[NUN * ((int64_t)HALO * l * nx + lc0) + o] = v;
+        else if (cms[cc] >= 0) y[(int64_t)NUN * cms[cc] + R] = v;
     }
 }
 
@@ -619,6 +632,7 @@ static inline unsigned grid_for(int64_t N)
     return (unsigned)std::min<int64_t>(b, 2048);
 }
 
+static int spmv_intcond(iemic_ctx* c, const double* x, double* yr);
 /* the SpMV kernel(s) alone: x's halo rows must be current */
 int spmv_kernel(iemic_ctx* c, const double* x, double* y)
 {
@@ -634,8 +648,16 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
     const int ntile = (int)(c->nloc / c->nx) * tpr;
     const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-    hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, y, (int)c->nloc, ntile,
-                       tpr);
+    hipLaunchKernelGGL(k_spmv7<false>, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, y, (int)c->nloc, ntile,
+                       tpr, (const int*)nullptr);
+    return spmv_intcond(c, x, c->rowintcon >= 0 ? y + c->rowintcon : nullptr);
+}
+
+/* the dense integral-condition row: *yr = intSign * coeff . x (summed over the ranks; yr its
+ * entry of this rank's output, if it owns it) */
+static int spmv_intcond(iemic_ctx* c, const double* x, double* yr)
+{
+    hipStream_t s = c->stream;
     if (c->su.rowintcon_ref >= 0) {
         /* dense intcond row: y[rowintcon] = intSign * coeff . x (summed over the ranks) */
         const int64_t o = NUN * c->own0;
@@ -647,10 +669,33 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
         if (rc) return rc;
         if (c->rowintcon >= 0)
             hipLaunchKernelGGL(k_scale_copy, dim3(1), dim3(1), 0, s, c->d_red.p + RED_BLOCKS,
-                               (double)c->cfg.int_sign, y + c->rowintcon, (int64_t)1);
+                               (double)c->cfg.int_sign, yr, (int64_t)1);
     }
     HIP_OK(hipGetLastError());
     return 0;
+}
+
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc)
+{
+    if (!c->jac_valid || !c->gs.cmap.p) {
+        set_error("spmv: no Jacobian or no active-cell map");
+        return IEMIC_ESTATE;
+    }
+    hipStream_t s = c->stream;
+    const int tpr = (c->nx + SP7_T - 1) / SP7_T;
+    const int ntile = (int)(c->nloc / c->nx) * tpr;
+    const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
+    hipLaunchKernelGGL(k_spmv7<true>, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, yc, (int)c->nloc,
+                       ntile, tpr, (const int*)c->gs.cmap.p);
+    double* yr = nullptr;
+    if (c->rowintcon >= 0) {
+        if (c->gs.ric < 0) {
+            set_error("spmv: the integral-condition row lies in an inactive cell");
+            return IEMIC_EINVAL;
+        }
+        yr = yc + c->gs.ric;
+    }
+    return spmv_intcond(c, x, yr);
 }
 
 int spmv(iemic_ctx* c, double* x, double* y, hipStream_t)
@@ -725,7 +770,7 @@ static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, doubl
 }
 
 /* the Krylov work space: Z (m x N) and w, r always; the full-length basis V ((m+1) x N) unless
- * the basis is compressed, then Vc ((m+1) x nc) and the full-length rf, t, b' */
+ * the basis is compressed, then Vc ((m+1) x nc) and the full-length t, b' */
 static int ensure_krylov(iemic_ctx* c, int m, int64_t nc = 0)
 {
     Krylov& k = c->kr;
@@ -750,7 +795,7 @@ static int ensure_krylov(iemic_ctx* c, int m, int64_t nc = 0)
     }
     if (nc && (k.mc < m || k.nc < nc || !k.Vc.p)) {
         rc |= k.Vc.alloc((size_t)(m + 1) * nc);
-        if (!k.rf.p) rc |= k.rf.alloc(N) | k.t.alloc(N) | k.bp.alloc(N);
+        if (!k.t.p) rc |= k.t.alloc(N) | k.bp.alloc(N);
         if (rc) {
             set_error("fgmres: out of device memory for the Krylov basis");
             return IEMIC_ENOMEM;
@@ -771,23 +816,14 @@ __global__ void k_cgather(const double* __restrict__ full, const int* __restrict
         cmp[q] = s * full[NUN * (own0 + act[cl]) + (q - NUN * cl)];
     }
 }
-__global__ void k_cscatter(const double* __restrict__ cmp, const int* __restrict__ act, int64_t nc,
-                           int64_t own0, double* __restrict__ full)
+/* t = v on the identity rows (known), 0 elsewhere (owned rows) */
+__global__ void k_known_part(const double* __restrict__ v, const uint8_t* __restrict__ known, int64_t n0,
+                             int64_t nl, double* __restrict__ t)
 {
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nc;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nl;
          q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t cl = q / NUN;
-        full[NUN * (own0 + act[cl]) + (q - NUN * cl)] = cmp[q];
-    }
-}
-/* t = v on the rows of the inactive (land) cells, 0 elsewhere (owned rows) */
-__global__ void k_land_part(const double* __restrict__ v, const uint8_t* __restrict__ actf, int64_t nloc,
-                            int64_t own0, double* __restrict__ t)
-{
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < NUN * nloc;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = NUN * own0 + q;
-        t[r] = actf[q / NUN] ? 0.0 : v[r];
+        const int64_t r = n0 + q;
+        t[r] = known[r] ? v[r] : 0.0;
     }
 }
 
@@ -834,13 +870,15 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     /* vectors are ext-layout (stride NE); kernels touch the owned rows [o, o + NL) */
     const int m = std::max(1, std::min(opt->krylov_dim, MAX_KRYLOV));
     const int64_t NE = c->nerows, o = NUN * c->own0, NL = c->nlrows;
-    /* DCGS2 with the block GS: the Arnoldi basis on the active cells only.  Land cells are
-     * identity rows of J and of the preconditioner, so with zero land entries in the right-hand
-     * side every Krylov vector is exactly zero there (48 % of the rows at 2 degrees); the two
-     * basis passes per step read and write the active rows only.  A right-hand side with land
-     * entries is first reduced: x_land = b_land, b' = b - J b_land (zero on the land rows). */
+    /* DCGS2 with the block GS: the Arnoldi basis on the active cells only.  Identity rows of J
+     * (all rows of a land cell, some of an ocean cell) are identity rows of the preconditioner
+     * too, so with a right-hand side that is zero on them every Krylov vector is exactly zero
+     * there: the basis skips the land cells (48 % of the rows at 2 degrees), the block GS
+     * reads it without the identity-column couplings and the SpMV writes only the active
+     * cells.  A right-hand side with identity-row entries is first reduced: x_k = b_k,
+     * b' = b - J t (t = b on the identity rows), zero on them. */
     const BlockGS& gs = c->gs;
-    const bool cmp = opt->orth == 0 && opt->prec == 2 && gs.ready && gs.kind == 2 && gs.nact > 0;
+    const bool cmp = opt->orth == 0 && opt->prec == 2 && gs.ready && gs.kind == 2 && gs.nact > 0 && gs.cmap.p;
     const int64_t NC = cmp ? NUN * gs.nact : 0;
     int rc = ensure_krylov(c, m, NC);
     if (rc) return rc;
@@ -880,14 +918,12 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
         return 0;
     }
     const double* b_orig = b;
-    bool land_rhs = false;
+    bool known_rhs = false;
     if (cmp) {
-        /* the preconditioner input: zero on the land rows, the active rows scattered per step */
-        HIP_OK(hipMemsetAsync(c->kr.rf.p, 0, sizeof(double) * NE, c->stream));
         double* t = c->kr.t.p;
-        hipLaunchKernelGGL(k_land_part, dim3(G), dim3(256), 0, c->stream, b, gs.actf.p, c->nloc, c->own0, t);
+        hipLaunchKernelGGL(k_known_part, dim3(G), dim3(256), 0, c->stream, b, gs.known.p, o, NL, t);
         if (dot(c, t, t, 0) > 0.0) {
-            land_rhs = true;
+            known_rhs = true;
             if ((rc = spmv(c, t, w, c->stream))) return rc;
             hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, b + o, -1.0, w + o,
                                c->kr.bp.p + o, NL);
@@ -896,7 +932,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     }
     /* r = b (x0 = 0) */
     HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
-    double beta = land_rhs ? sqrt0(dot(c, b, b, 0)) : bnorm, res = beta / bnorm, res_c0 = res;
+    double beta = known_rhs ? sqrt0(dot(c, b, b, 0)) : bnorm, res = beta / bnorm, res_c0 = res;
     int it = 0;
     /* the safeguard's switch lasts for this solve only */
     struct Restore {
@@ -1014,25 +1050,24 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 int rc2;
                 if (jj < m) {
                     double* zj = Z + (int64_t)jj * NE;
-                    /* the full-length input of the preconditioner and output of the SpMV */
-                    double* uf = cmp ? c->kr.rf.p : u - o;
-                    double* wf = cmp ? w : wv - o;
-                    if (cmp)
-                        hipLaunchKernelGGL(k_cscatter, dim3(GC), dim3(256), 0, c->stream, u, gs.act.p, NC,
-                                           c->own0, uf);
                     HIP_OK(hipEventRecord(e[0], c->stream));
-                    if (opt->prec > 0) {
-                        if ((rc2 = prec_apply(c, uf, zj))) return rc2;
+                    if (cmp) {
+                        /* the block GS reads the compressed u, the SpMV writes the compressed w */
+                        if ((rc2 = gs_apply_c(c, u, zj))) return rc2;
+                    } else if (opt->prec > 0) {
+                        if ((rc2 = prec_apply(c, u - o, zj))) return rc2;
                     } else {
-                        HIP_OK(hipMemcpyAsync(zj, uf, sizeof(double) * NE, hipMemcpyDeviceToDevice,
+                        HIP_OK(hipMemcpyAsync(zj, u - o, sizeof(double) * NE, hipMemcpyDeviceToDevice,
                                               c->stream));
                     }
                     HIP_OK(hipEventRecord(e[1], c->stream));
-                    if ((rc2 = spmv(c, zj, wf, c->stream))) return rc2;
+                    if (cmp) {
+                        if ((rc2 = halo_exchange(c, zj, 1))) return rc2;
+                        if ((rc2 = spmv_kernel_c(c, zj, wv))) return rc2;
+                    } else if ((rc2 = spmv(c, zj, wv - o, c->stream))) {
+                        return rc2;
+                    }
                     HIP_OK(hipEventRecord(e[2], c->stream));
-                    if (cmp)
-                        hipLaunchKernelGGL(k_cgather, dim3(GC), dim3(256), 0, c->stream, wf, gs.act.p, NC,
-                                           c->own0, 1.0, wv);
                 }
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
@@ -1136,8 +1171,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             inf.safeguard++;
         res_c0 = res;
     }
-    /* the land part of a reduced right-hand side: x = x' + t */
-    if (land_rhs)
+    /* the identity-row part of a reduced right-hand side: x = x' + t */
+    if (known_rhs)
         hipLaunchKernelGGL(k_axpby, dim3(G), dim3(256), 0, c->stream, 1.0, x + o, 1.0, c->kr.t.p + o, x + o, NL);
     b = b_orig;
     /* explicit residual (Ocean.C:1140-1150) */

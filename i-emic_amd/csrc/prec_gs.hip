@@ -650,6 +650,28 @@ __global__ void k_gs_rr(const double* __restrict__ val, const uint8_t* __restric
     }
 }
 
+/* k_gs_rr for a compressed input (FGMRES's Arnoldi vectors, krylov.hip): r is zero on every
+ * identity row (land cells are not stored, the identity rows of active cells are 0), so the
+ * identity-column couplings vanish and rr = r on the active rows; the output z is 0 on the
+ * identity rows (zall: on every row) */
+__global__ void k_gs_rr_c(const uint8_t* __restrict__ known, const int* __restrict__ cmap,
+                          const double* __restrict__ rc, double* __restrict__ z, double* __restrict__ rr,
+                          int zall, double* __restrict__ rrP, Lay L)
+{
+    LAY_ALIASES;
+    OWNED_CELL;
+    const int cm = cmap[lc];
+#pragma unroll
+    for (int R = 0; R < NUN; R++) {
+        const int64_t row = NUN * cell + R;
+        const bool kn = known[row] != 0;
+        const double v = (kn || cm < 0) ? 0.0 : rc[(int64_t)NUN * cm + R];
+        if (kn || zall) z[row] = 0.0;
+        if (rr) rr[row] = v;
+        rrP[PL(cell, R)] = v;
+    }
+}
+
 /* per owned water column (i, j): 1 in flags[j n + i] if a P row of it is active, 1 in
  * flags[n m + j n + i] if a U or V row is (the host's Schur structure input; band_flags did
  * this on a host copy of all the flags) */
@@ -3147,6 +3169,15 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
             gs.nact = (int64_t)list.size();
             if (gs.act.n < list.size() + 1 && gs.act.alloc(list.size() + 1)) return IEMIC_ENOMEM;
             if (!list.empty() && (rc = h2d(c, gs.act.p, list.data(), sizeof(int) * list.size()))) return rc;
+            std::vector<int> cm((size_t)c->nloc, -1);
+            for (size_t q = 0; q < list.size(); q++) cm[list[q]] = (int)q;
+            if (gs.cmap.n < cm.size() && gs.cmap.alloc(cm.size())) return IEMIC_ENOMEM;
+            if ((rc = h2d(c, gs.cmap.p, cm.data(), sizeof(int) * cm.size()))) return rc;
+            gs.ric = -1;
+            if (c->rowintcon >= 0) {
+                const int64_t cell = c->rowintcon / NUN - c->own0;
+                if (cell >= 0 && cell < c->nloc && cm[cell] >= 0) gs.ric = (int64_t)NUN * cm[cell] + c->rowintcon % NUN;
+            }
             gs.act_h.swap(h);
         }
     }
@@ -3330,7 +3361,11 @@ int gs_time_parts(iemic_ctx* c, int nrep, double* us)
     return rc;
 }
 
-int gs_apply(iemic_ctx* c, const double* r, double* z)
+static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp);
+int gs_apply(iemic_ctx* c, const double* r, double* z) { return gs_apply_impl(c, r, z, false); }
+int gs_apply_c(iemic_ctx* c, const double* rc, double* z) { return gs_apply_impl(c, rc, z, true); }
+
+static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -3358,10 +3393,16 @@ int gs_apply(iemic_ctx* c, const double* r, double* z)
         }
         return ts_solve(c, gs.ts_mg > 0 ? zP : z, z, ts_at == gs.dyn_iters, par);
     };
-    /* the halo rows of r hold the neighbours' identity-row values the couplings need */
-    if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
-    hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
-                       r, z, aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
+    /* the halo rows of r hold the neighbours' identity-row values the couplings need (a
+     * compressed r is zero on every identity row: no couplings, no exchange) */
+    if (cmp) {
+        hipLaunchKernelGGL(k_gs_rr_c, dim3(gc), dim3(256), 0, s, gs.known.p, gs.cmap.p, r, z,
+                           aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
+    } else {
+        if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
+        hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
+                           r, z, aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
+    }
     if ((rc = dyn_solve(c, gs.rrP.p, zP, nullptr, 0.0, zaos_of(gs.dyn_iters == 1)))) return rc;
     if (ts_at == 1 && gs.dyn_iters > 1 && (rc = ts())) return rc;
     /* defect correction on the dynamics block: z_D += w M_D^-1 (rr_D - A_DD z_D), with the
