@@ -285,7 +285,8 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
     rc |= c->d_red.alloc(2048);
     rc |= c->d_part.alloc((size_t)RED_BLOCKS * RED_ROWS);
     rc |= c->d_hbuf.alloc((size_t)2 * RED_ROWS);
-    if (!rc && hipHostMalloc(&c->h_red, sizeof(double) * 2 * RED_ROWS) != hipSuccess) rc = 1;
+    /* coherent: k_dcgs_coef writes the Hessenberg rows straight into it */
+    if (!rc && hipHostMalloc(&c->h_red, sizeof(double) * 2 * RED_ROWS, hipHostMallocCoherent) != hipSuccess) rc = 1;
     if (rc) {
         set_error("iemic_create: out of device memory");
         delete c;

@@ -512,7 +512,8 @@ __global__ void __launch_bounds__(256) k_dcgs_dot1(const double* __restrict__ V,
  * h_jj = (u.w - a.b) / beta, gamma = h_jj / beta; coef = [a | b - gamma a], coef[DCGS_SCAL..] =
  * 1/beta, gamma; beta, h_jj appended to hb (rows 2nv+3, 2nv+4) for the host's Hessenberg
  * column.  A breakdown (beta = 0) gives zero scales; the host stops on it. */
-__global__ void __launch_bounds__(256) k_dcgs_coef(double* __restrict__ hb, int nv, double* __restrict__ coef)
+__global__ void __launch_bounds__(256) k_dcgs_coef(double* __restrict__ hb, int nv, double* __restrict__ coef,
+                                                   double* __restrict__ hrows)
 {
     __shared__ double sm[2 * 4];
     __shared__ double tot[2];
@@ -543,6 +544,12 @@ __global__ void __launch_bounds__(256) k_dcgs_coef(double* __restrict__ hb, int 
         coef[DCGS_SCAL + 1] = gamma;
         hb[2 * nv + 3] = bt;
         hb[2 * nv + 4] = hjj;
+    }
+    /* the rows for the host's Hessenberg column, straight into its pinned (coherent) slot:
+     * no device-to-host copy launch per Arnoldi step */
+    if (hrows) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2 * nv + 5; i += blockDim.x) hrows[i] = hb[i];
     }
 }
 
@@ -1078,9 +1085,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                                    nbx1, 2 * nv + 3, c->d_hbuf.p);
                 if ((rc2 = allreduce_sum(c, c->d_hbuf.p, 2 * nv + 3))) return rc2;
                 hipLaunchKernelGGL(k_dcgs_coef, dim3(1), dim3(256), 0, c->stream, c->d_hbuf.p, nv,
-                                   c->d_hbuf.p + RED_ROWS);
-                HIP_OK(hipMemcpyAsync(c->h_red + (size_t)RED_ROWS * (jj & 1), c->d_hbuf.p,
-                                      sizeof(double) * (2 * nv + 5), hipMemcpyDeviceToHost, c->stream));
+                                   c->d_hbuf.p + RED_ROWS, c->h_red + (size_t)RED_ROWS * (jj & 1));
                 HIP_OK(hipEventRecord(evr[jj & 1], c->stream));
                 if (jj < m)
                     hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, Q, LQ, nv,
