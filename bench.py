@@ -41,7 +41,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PMC_TAG = "r04"         # bench_data/pmc_<tag>.json: per-kernel PMC bytes and trace times of a step
+PMC_TAG = "r05"         # bench_data/pmc_<tag>.json: per-kernel PMC bytes and trace times of a step
 
 
 def pmc_table(config: str):
@@ -655,7 +655,10 @@ def bench_newton(args, R: Ranks):
     nown = lay["own_rows"]
     bsp = spmv_bytes(nnz, nown)
     achieved = bsp / (spmv_ms * 1e-3) / 1e9
-    ell = stencil_ell_bytes(nown // 6, 104, nown)
+    # the in-solve SpMV (k_spmv7<true>) reads the coefficients of the active cells only and
+    # writes their rows (FGMRES's compressed basis); x is read whole: its stencil-ELL minimum
+    nact = oc.active_cells() if args.solver == "FGMRES" and args.orth == "DCGS2" and args.prec == 2 else 0
+    ell = (8 * 104 * nact + 8 * nown + 8 * 6 * nact) if nact else stencil_ell_bytes(nown // 6, 104, nown)
     extra = {}
     if args.spmv_reps > 0 or args.cold_reps > 0:
         oc.setState(x0h)
@@ -673,8 +676,10 @@ def bench_newton(args, R: Ranks):
     tab, why = pmc_table(args.config) if world == 1 else (None, "one GPU only")
     if tab:
         ks = {r["kernel"]: r for r in tab["kernels"]}
-        if "k_spmv7" in ks:
-            traffic = ks["k_spmv7"]["hbm_bytes_per_launch"]
+        for kn in ("k_spmv7<true>", "k_spmv7<false>", "k_spmv7"):
+            if kn in ks:
+                traffic = ks[kn]["hbm_bytes_per_launch"]
+                break
         sb = tab["step_hbm_bytes"]
         step_rf = {"hbm_bytes": sb, "ms": round(ms, 3), "achieved": round(sb / (ms * 1e-3) / 1e9, 1),
                    "frac": round(sb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -759,7 +764,7 @@ def bench_newton(args, R: Ranks):
                      "frac": round(real_gbps / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_basis": "traffic (PMC)" if traffic else "stencil_ell_bytes",
                      "achieved_csr": round(achieved, 1), "frac_csr": round(achieved / HBM_PEAK_GBS, 4),
-                     "algorithmic_bytes": bsp, "stencil_ell_bytes": ell,
+                     "algorithmic_bytes": bsp, "stencil_ell_bytes": ell, "active_cells": nact,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
                      "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp,
                      "step": step_rf, "dominant": dom_rf, **({"table": why} if why else {}), **extra},

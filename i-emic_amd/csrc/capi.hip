@@ -476,6 +476,13 @@ extern "C" int iemic_layout(const iemic_ctx* c, int64_t* out)
     return 0;
 }
 
+extern "C" int iemic_active_cells(const iemic_ctx* c, int64_t* nact)
+{
+    if (!c || !nact) return IEMIC_EINVAL;
+    *nact = c->gs.ready && c->gs.kind == 2 ? c->gs.nact : 0;
+    return 0;
+}
+
 /* communication counters since the last call (halo batches, messages and bytes sent,
  * all-reduces), reset by the call */
 extern "C" int iemic_comm_stats(iemic_ctx* c, int64_t* out4)

@@ -125,6 +125,7 @@ def lib():
         "iemic_comm_unique_id": (C.c_int, [P(C.c_ubyte)]),
         "iemic_layout": (C.c_int, [vp, P64]),
         "iemic_comm_stats": (C.c_int, [vp, P64]),
+        "iemic_active_cells": (C.c_int, [vp, P64]),
         "iemic_comm_size": (C.c_int, [vp, PI, PI]),
         "iemic_allreduce_sum": (C.c_int, [vp, PD, C.c_int64]),
         "iemic_set_comm_timeout": (C.c_int, [vp, C.c_double]),
@@ -218,7 +219,8 @@ def lib():
     return L
 
 
-EXPORTED = ("iemic_abi_version", "iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout", "iemic_comm_stats",
+EXPORTED = ("iemic_abi_version", "iemic_create", "iemic_create_dist", "iemic_comm_unique_id", "iemic_layout",
+            "iemic_comm_stats", "iemic_active_cells",
             "iemic_comm_size", "iemic_allreduce_sum", "iemic_set_comm_timeout",
             "iemic_local_group_new", "iemic_local_group_free", "iemic_create_local",
             "iemic_create_local_2d", "iemic_create_transport", "iemic_decomp2d",

@@ -480,6 +480,12 @@ class Ocean:
         check(lib().iemic_comm_size(self._h, C.byref(n), C.byref(kind)), "iemic_comm_size")
         return n.value, {0: "none", 1: "rccl", 2: "local", 3: "host"}[kind.value]
 
+    def active_cells(self) -> int:
+        """Cells with a non-identity row (iemic_active_cells; 0 before a preconditioner set-up)."""
+        v = C.c_int64()
+        check(lib().iemic_active_cells(self._h, C.byref(v)), "iemic_active_cells")
+        return v.value
+
     def comm_stats(self) -> dict:
         """Communication counters since the previous call (then reset)."""
         out = np.zeros(4, dtype=np.int64)

@@ -271,6 +271,10 @@ int     iemic_landm(const iemic_ctx* ctx, int* out); /* effective (fixed) local 
  * x-halo width.  Internally the owned cells are ordered (j, k, i), i fastest, one
  * contiguous slab between 2 halo rows each side; the x halo (npx > 1) follows them. */
 int     iemic_layout(const iemic_ctx* ctx, int64_t* out);
+/* cells of this rank with a non-identity row (the rest are land: all six rows identity),
+ * from the last preconditioner set-up (iemic_prec_compute / iemic_newton_step; 0 before):
+ * FGMRES keeps its Arnoldi basis and the in-solve SpMV its output on these cells only */
+int     iemic_active_cells(const iemic_ctx* ctx, int64_t* nact);
 /* communication counters since the previous call (then reset): out[0] exchange batches
  * (one per phase of a halo exchange), out[1] messages sent, out[2] bytes sent, out[3]
  * all-reduces */
