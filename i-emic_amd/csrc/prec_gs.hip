@@ -782,14 +782,16 @@ __device__ __forceinline__ int xcd_block(int nwg)
 }
 static inline unsigned xcd_grid(int64_t nwg) { return 8u * (unsigned)((nwg + 7) / 8); }
 
+/* hr: the grid also covers the halo rows jl = -1 and jl = mb (latitude bands: the pass
+ * recomputes the neighbours' edge values it reads instead of exchanging them) */
 template <int LP>
-__device__ __forceinline__ bool col_tile(const Lay& L, int& il, int& jl, int& k, bool& on)
+__device__ __forceinline__ bool col_tile(const Lay& L, int& il, int& jl, int& k, bool& on, int hr = 0)
 {
     constexpr int TI = col_ti<LP>();
     const int tpr = (L.nx + TI - 1) / TI;
-    const int w = xcd_block(tpr * (int)(L.nloc / ((int64_t)L.l * L.nx)));
+    const int w = xcd_block(tpr * ((int)(L.nloc / ((int64_t)L.l * L.nx)) + 2 * hr));
     if (w < 0) return false;
-    jl = w / tpr;
+    jl = w / tpr - hr;
     il = (w % tpr) * TI + (int)threadIdx.x % TI;
     k = (int)threadIdx.x / TI;
     on = k < L.l && il < L.nx;
@@ -986,6 +988,9 @@ __global__ void k_rcol_w(const uint8_t* __restrict__ known, const double* __rest
 
 /* 1 + 3a. ptil (top-down: p_k = A_k + B_k p_k+1) and the column's Schur right-hand side
  * sum_e rcol_e rr_e (summed over the levels in a fixed order), written as k_gs_pcol wrote it */
+/* gsl (latitude bands): the tiles of the halo rows jl = -1, mb (inside the grid) compute
+ * ptil there too, with the W row's couplings from the halo-filled gslot (the owned Jacobian
+ * has no halo rows), so that the U/V kernel needs no exchange of ptil */
 template <int LP>
 __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict__ val,
                                                        const uint8_t* __restrict__ knP,
@@ -993,16 +998,46 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
                                                        const double* __restrict__ rr,
                                                        double* __restrict__ z,
                                                        const int* __restrict__ ocol,
-                                                       double* __restrict__ colv_own, Lay L)
+                                                       double* __restrict__ colv_own, Lay L,
+                                                       const double* __restrict__ gsl)
 {
     LAY_ALIASES;
     constexpr int TI = col_ti<LP>();
     __shared__ double sA[LP][TI], sB[LP][TI], sv[LP][TI];
     int il, jl, k;
     bool on;
-    if (!col_tile<LP>(L, il, jl, k, on)) return;    /* whole idle workgroups */
+    if (!col_tile<LP>(L, il, jl, k, on, gsl ? 1 : 0)) return;    /* whole idle workgroups */
     const int ii = (int)threadIdx.x % TI;
     const int i = L.ib0 + il, j = L.jb0 + jl;
+    const int mbl = (int)(L.nloc / ((int64_t)l * L.nx));
+    if (jl < 0 || jl >= mbl) {
+        /* a halo row: ptil only (rows outside the grid: whole idle workgroups) */
+        if (j < 0 || j >= m) return;
+        double A = 0.0, B = 0.0;
+        bool pa = false;
+        int64_t cell = 0;
+        if (on) {
+            cell = ecell(L, i, j, k);
+            pa = !knP[PL(cell, PP)];
+            if (pa && k < l - 1 && !knP[PL(cell, WW)]) {
+                const double g0 = gsl[GSL * cell + 8], g1 = gsl[GSL * cell + 9];
+                if (g0 != 0.0) {
+                    A = rr[PL(cell, WW)] / g0;
+                    B = -g1 / g0;
+                }
+            }
+        }
+        if (k < LP) {
+            sA[k][ii] = A;
+            sB[k][ii] = B;
+        }
+        __syncthreads();
+        if (!on) return;
+        double p = 0.0;
+        for (int kk = l - 1; kk >= k; kk--) p = sA[kk][ii] + sB[kk][ii] * p;
+        if (pa) z[PL(cell, PP)] = p;
+        return;
+    }
     const int64_t ncell = L.nloc;
     const int ncolb = (int)(L.nloc / l);
     const int t = jl * L.nx + il;
@@ -1184,13 +1219,33 @@ __global__ void k_mr_update(const uint8_t* __restrict__ knP, const double* __res
 
 /* 2 + 4. uv = D^-1 (rr_uv - Guv (ptil + Mz1^T pbar)) in one pass once pbar is known (the
  * Schur right-hand side came from rcol, so uv* is never formed); zo += omega uv */
+/* gsl (latitude bands): threads past the owned cells compute the south halo row's U/V
+ * points too (their P couplings from the halo-filled gslot), into z only, so that the p/w
+ * kernel needs no exchange of uv */
 __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                          const double* __restrict__ uvinv, const double* __restrict__ rr,
                          const double* __restrict__ pbar, double* __restrict__ z, Lay L,
-                         double* __restrict__ zo, double omega, double* __restrict__ zaos)
+                         double* __restrict__ zo, double omega, double* __restrict__ zaos,
+                         const double* __restrict__ gsl)
 {
-    OWNED_CELL;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t lc = t;
+    const int64_t ncell = L.nloc;
     const int n = L.n, m = L.m, periodic = L.periodic;
+    int i, j, k;
+    int64_t cell;
+    const bool halo = t >= L.nloc;
+    if (!halo) {
+        cell = L.own0 + lc;
+        lc_ijk(L, lc, i, j, k);
+    } else {
+        const int64_t q = t - L.nloc;                /* south halo row, (k, i) */
+        if (!gsl || q >= (int64_t)L.l * L.nx || L.jb0 == 0) return;
+        i = L.ib0 + (int)(q % L.nx);
+        k = (int)(q / L.nx);
+        j = L.jb0 - 1;
+        cell = ecell(L, i, j, k);
+    }
     const uint8_t ku = knP[PL(cell, UU)], kv = knP[PL(cell, VV)];
     const bool ua = !ku, va = !kv;
     if (!ua && !va) return;                 /* land: none of the point's operands is read */
@@ -1203,8 +1258,8 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
         const int64_t pc = ecell(L, pi, pj, k);
         const uint8_t kp = knP[PL(pc, PP)];
         const double p = z[PL(pc, PP)] + pbar[(int64_t)pj * n + pi];
-        const double au = val[(int64_t)(S_UP + g4) * ncell + lc];
-        const double av = val[(int64_t)(S_VP + g4) * ncell + lc];
+        const double au = halo ? gsl[GSL * cell + g4] : val[(int64_t)(S_UP + g4) * ncell + lc];
+        const double av = halo ? gsl[GSL * cell + 4 + g4] : val[(int64_t)(S_VP + g4) * ncell + lc];
         const bool use = in && !kp;
         gu += use ? au * p : 0.0;
         gv += use ? av * p : 0.0;
@@ -1217,6 +1272,7 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
     const double nu = d0 * ru + d1 * rv, nv = d2 * ru + d3 * rv;
     if (ua) z[PL(cell, UU)] = nu;
     if (va) z[PL(cell, VV)] = nv;
+    if (halo) return;
     double fu = nu, fv = nv;
     if (zo) {
         if (ua) zo[PL(cell, UU)] = fu = zo[PL(cell, UU)] + omega * nu;
@@ -3275,17 +3331,23 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const int64_t ps = c->next;
     /* ptil and the Schur right-hand side in one column pass (rcol), the U/V points once
      * after the Schur solve, then p and w */
+    /* latitude bands: after the one exchange of rr, the pass computes ptil on both halo rows
+     * and the U/V points of the south one itself (the halo-filled gslot holds their
+     * couplings) instead of exchanging ptil and uv (3 -> 1 exchange batch per pass) */
+    const bool hrow = band && c->npx == 1;
+    const double* gsl = hrow ? gs.gslot.p : nullptr;
+    const unsigned gcth = hrow ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx + 2)) : gct;
     if (band && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
     if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
+        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     else
-        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L);
-    if (band && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
+        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
+    if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
     const double* sb = gs.colv_own.p;
     if (band) {
         HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
@@ -3294,9 +3356,10 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
         sb = gs.colv.p;
     }
     if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s, gs.colvT.p))) return rc;
-    hipLaunchKernelGGL(k_gs_uvp, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
-                       rr, gs.colvT.p, z, L, zo, omega, zaos);
-    if (band && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
+    const unsigned gcu = hrow ? (unsigned)((c->nloc + (int64_t)c->l * c->nx + 255) / 256) : gc;
+    hipLaunchKernelGGL(k_gs_uvp, dim3(gcu), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
+                       rr, gs.colvT.p, z, L, zo, omega, zaos, gsl);
+    if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
     if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
                            gs.colvT.p, z, L, rr, zo, omega, zaos);
