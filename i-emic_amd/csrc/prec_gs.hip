@@ -1272,7 +1272,12 @@ __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restri
     const double nu = d0 * ru + d1 * rv, nv = d2 * ru + d3 * rv;
     if (ua) z[PL(cell, UU)] = nu;
     if (va) z[PL(cell, VV)] = nv;
-    if (halo) return;
+    if (halo) {
+        /* the pass iterate's south halo row too (the T/S right-hand side reads its U/V) */
+        if (zo && ua) zo[PL(cell, UU)] += omega * nu;
+        if (zo && va) zo[PL(cell, VV)] += omega * nv;
+        return;
+    }
     double fu = nu, fv = nv;
     if (zo) {
         if (ua) zo[PL(cell, UU)] = fu = zo[PL(cell, UU)] + omega * nu;
@@ -3449,8 +3454,13 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
      * values from the last pass (every pass for the T/S sweeps, which read z's AoS rows) */
     const bool aos_all = gs.ts_mg <= 0;
     auto zaos_of = [&](bool last) { return (last || aos_all) ? z : nullptr; };
+    /* latitude bands: the last pass also updated the iterate's south halo row U/V (k_gs_uvp),
+     * all the T/S right-hand side reads of it beyond the band (A_TS,D couples U/V at j - 1 and
+     * W in the column): no exchange (the fixed-step passes only) */
+    const bool ts_local = band && c->npx == 1 && gs.ts_mg > 0 && !gs.dyn_mr && ts_at == gs.dyn_iters &&
+                          gs.dyn_iters > 1;
     auto ts = [&]() -> int {
-        if (band && (ts_at < gs.dyn_iters || gs.dyn_iters > 1)) {
+        if (band && !ts_local && (ts_at < gs.dyn_iters || gs.dyn_iters > 1)) {
             rc = gs.ts_mg > 0 ? halo_exchange_planar(c, zP, NUN, ps, 1) : halo_exchange(c, z, 1);
             if (rc) return rc;
         }
