@@ -489,11 +489,11 @@ int comm_verify_plans(iemic_ctx* c)
 {
     if (c->nranks <= 1) return 0;
     const int P = c->nranks;
-    const int spec[3][2] = {{NUN, HALO}, {NUN, 1}, {1, 1}};   /* (width, depth) of the plans */
+    const int spec[4][2] = {{NUN, HALO}, {NUN, 1}, {1, 1}, {1, HALO}};   /* (width, depth) of the plans */
     /* per plan, per ordered pair (a -> b): message count and sum of (k + 1) * length over
      * the k-th message; the sender adds, the receiver subtracts: all zero when they pair */
-    std::vector<double> t((size_t)3 * 2 * P * P, 0.0);
-    for (int q = 0; q < 3; q++) {
+    std::vector<double> t((size_t)4 * 2 * P * P, 0.0);
+    for (int q = 0; q < 4; q++) {
         std::vector<MsgD> px, py;
         plan_ext(c->sub, spec[q][0], spec[q][1], px, py);
         for (const auto* ph : {&px, &py}) {
@@ -514,7 +514,7 @@ int comm_verify_plans(iemic_ctx* c)
     if (!rc) rc = allreduce_sum(c, d.p, (int)t.size());
     if (!rc) rc = d2h(c, t.data(), d.p, sizeof(double) * t.size());
     if (rc) return rc;
-    for (int q = 0; q < 3; q++)
+    for (int q = 0; q < 4; q++)
         for (int a = 0; a < P; a++)
             for (int b = 0; b < P; b++) {
                 const double* e = t.data() + ((size_t)q * 2 * P + a) * P + b;

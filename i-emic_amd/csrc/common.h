@@ -188,6 +188,7 @@ struct BlockGS {
     SchurCR cr;                      /* its cyclic-reduction factors                     */
     int dyn_iters = 1;               /* defect-correction passes on the dynamics block   */
     DevBuf<double> dres, zc;         /* dynamics defect and correction (ext rows)        */
+    DevBuf<double> dvh;              /* bands: U/V/W/P coefficients of the two halo rows  */
     DevBuf<double> dq, dzero, dmr;   /* MR passes: -A_DD zc, a zero vector, dot partials  */
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
@@ -217,6 +218,7 @@ struct BlockGS {
      * longitudes (schur_cr.hip, the explicit "tail" inverse) */
     static constexpr int MG_CR_CELLS = 1024;
     int mg_crd = 0;
+    int mg_local0 = 0;               /* bands: level-0 smoother without the cross-band rows */
     SchurCR mg_cr;
     DevBuf<int> mg_cinfo;            /* its Gauss-Jordan pivot flag                      */
     /* the dynamics passes work on component-planar copies (plane q = unknown q of every ext

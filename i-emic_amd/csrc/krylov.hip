@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
  * are summed in slot order. */
 template <int S0, int S1>
 __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, const double* __restrict__ z,
-                                            int64_t lc, int64_t nloc, const int (*nc)[9], const bool* on,
+                                            int64_t vs, const int (*nc)[9], const bool* on,
                                             int64_t ps, double* acc)
 {
     constexpr int NS = S1 - S0;
@@ -172,7 +172,7 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
             const Slot sl = SLOTS[s];
             if (sp7_row(s) - sp7_row(S0) != q) continue;
             const int cidx = nc[sl.di + 1][(sl.dk + 1) * 3 + (sl.dj + 1)];
-            v[s - S0] = val[(int64_t)s * nloc + lc];
+            v[s - S0] = val[(int64_t)s * vs];
             zz[s - S0] = z[(int64_t)cidx + ps * sl.var];
         }
     }
@@ -182,33 +182,60 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
         if (on[q]) acc[q] += v[s - S0] * zz[s - S0];
     }
 }
+/* hv (latitude bands): tiles past the owned ones compute the defect on the two halo rows
+ * too (their coefficients exchanged once per Jacobian, BlockGS::dvh; z with a 2-deep halo),
+ * so that the next dynamics pass needs no exchange of d.  hs / hn: the south / north halo row
+ * exists (a neighbour band). */
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
                                                   const uint8_t* __restrict__ knP,
-                                                  double* __restrict__ d, int64_t nloc, int nblk, int64_t ps)
+                                                  double* __restrict__ d, int64_t nloc, int nblk, int64_t ps,
+                                                  const double* __restrict__ hv, int nhb, int hs, int hn)
 {
     __shared__ double red[4][2][64];
-    const int per = (nblk + 7) >> 3;
+    const int ntot = nblk + nhb;
+    const int per = (ntot + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile >= nblk) return;
+    if (tile >= ntot) return;
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int64_t lc0 = (int64_t)tile * 64, lc = lc0 + c;
-    const bool act = lc < nloc;
-    const int64_t e0 = (int64_t)HALO * X.l * X.nx;     /* ext cell of owned cell 0 */
+    const int64_t row = (int64_t)X.l * X.nx;             /* cells of one latitude row */
+    const int64_t e0 = (int64_t)HALO * row;              /* ext cell of owned cell 0 */
+    /* u: the cell relative to owned cell 0 (the halo rows at -row .. -1 and nloc .. nloc + row - 1) */
+    int64_t u0, n0;
+    bool halo = tile >= nblk;
+    if (!halo) {
+        u0 = (int64_t)tile * 64;
+        n0 = nloc;
+    } else {
+        u0 = (int64_t)(tile - nblk) * 64;                /* halo index: south row, then north */
+        n0 = 2 * row;
+    }
+    const int64_t h = u0 + c;
+    bool act = h < n0;
+    int64_t u = h;
+    if (halo) {
+        const bool south = h < row;
+        act = act && (south ? hs : hn);
+        u = south ? h - row : nloc + h - row;
+    }
     double acc[2] = {0.0, 0.0};
     if (act) {
-        const int il = (int)(lc % X.nx), k = (int)((lc / X.nx) % X.l), j = X.jb0 + (int)(lc / ((int64_t)X.nx * X.l));
+        const int64_t q = u + row;                       /* >= 0 */
+        const int il = (int)(q % X.nx), k = (int)((q / X.nx) % X.l);
+        const int j = X.jb0 - 1 + (int)(q / row);
         int nc[3][9];
         nb_cells(X, il, j, k, nc);
         /* the wave's two rows: g0 {U, -} g1 {U, V} g2 {V, W} g3 {W, P} */
-        const int64_t cell = e0 + lc;
+        const int64_t cell = e0 + u;
         const int v0 = g == 0 ? 0 : g - 1;
         const bool on[2] = {!knP[cell + ps * v0], g > 0 && !knP[cell + ps * (v0 + 1)]};
-        if (g == 0) dyn_partial<0, 16>(val, z, lc, nloc, nc, on, ps, acc);
-        else if (g == 1) dyn_partial<16, 32>(val, z, lc, nloc, nc, on, ps, acc);
-        else if (g == 2) dyn_partial<32, 48>(val, z, lc, nloc, nc, on, ps, acc);
-        else dyn_partial<48, 64>(val, z, lc, nloc, nc, on, ps, acc);
+        const double* vp = halo ? hv + h : val + u;
+        const int64_t vs = halo ? 2 * row : nloc;
+        if (g == 0) dyn_partial<0, 16>(vp, z, vs, nc, on, ps, acc);
+        else if (g == 1) dyn_partial<16, 32>(vp, z, vs, nc, on, ps, acc);
+        else if (g == 2) dyn_partial<32, 48>(vp, z, vs, nc, on, ps, acc);
+        else dyn_partial<48, 64>(vp, z, vs, nc, on, ps, acc);
     }
     red[g][0][c] = acc[0];
     red[g][1][c] = acc[1];
@@ -216,21 +243,32 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
     /* rows of the waves: g0 {U} g1 {U,V} g2 {V,W} g3 {W,P}; thread = (row, cell), the
      * cell fastest (planar stores) */
     const int R = threadIdx.x >> 6, cc = threadIdx.x & 63;
-    if (lc0 + cc >= nloc) return;
+    const int64_t hh = u0 + cc;
+    if (hh >= n0) return;
+    int64_t uu = hh;
+    if (halo) {
+        const bool south = hh < row;
+        if (!(south ? hs : hn)) return;
+        uu = south ? hh - row : nloc + hh - row;
+    }
     const double sum = R == 0 ? red[0][0][cc] + red[1][0][cc]
                      : R == 1 ? red[1][1][cc] + red[2][0][cc]
                      : R == 2 ? red[2][1][cc] + red[3][0][cc]
                               : red[3][1][cc];
-    const int64_t cell = e0 + lc0 + cc, e = cell + ps * R;
+    const int64_t cell = e0 + uu, e = cell + ps * R;
     d[e] = knP[e] ? 0.0 : r[e] - sum;
 }
 
-int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d)
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d, bool halo)
 {
     const int nblk = (int)((c->nloc + 63) / 64);
-    const unsigned grid = 8u * (unsigned)((nblk + 7) / 8);
+    const int64_t row = (int64_t)c->l * c->nx;
+    const bool hv = halo && c->gs.dvh.p;
+    const int nhb = hv ? (int)((2 * row + 63) / 64) : 0;
+    const unsigned grid = 8u * (unsigned)((nblk + nhb + 7) / 8);
     hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, knP, d,
-                       c->nloc, nblk, (int64_t)c->next);
+                       c->nloc, nblk, (int64_t)c->next, hv ? c->gs.dvh.p : nullptr, nhb,
+                       hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0);
     return 0;
 }
 

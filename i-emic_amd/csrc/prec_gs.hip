@@ -2111,12 +2111,18 @@ __global__ void k_mg_out(TsLev V, double* __restrict__ zout)
 
 /* level 0: the compact T/S couplings and 2x2 blocks (ext layout) into the level layout */
 __global__ void k_mg_pack0(const double* __restrict__ tsoff, const double* __restrict__ tsdiag, Lay L,
-                           int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag)
+                           int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag, int cut)
 {
     OWNED_CELL;
-    const int64_t c = mg_cell(V, i - L.ib0, j - L.jb0, k);
+    const int jl = j - L.jb0;
+    const int64_t c = mg_cell(V, i - L.ib0, jl, k);
+    /* cut: the band-local level 0 drops the couplings to the neighbour bands' rows */
+    const bool cs = cut && jl == 0, cn = cut && jl == V.mb - 1;
 #pragma unroll
-    for (int e = 0; e < 16; e++) off[(int64_t)e * V.cstr + c] = tsoff[(int64_t)e * next + cell];
+    for (int e = 0; e < 16; e++) {
+        const int q = e & 7;
+        off[(int64_t)e * V.cstr + c] = ((q == 2 && cs) || (q == 3 && cn)) ? 0.0 : tsoff[(int64_t)e * next + cell];
+    }
 #pragma unroll
     for (int e = 0; e < 4; e++) diag[(int64_t)e * V.cstr + c] = tsdiag[(int64_t)e * next + cell];
 }
@@ -2370,7 +2376,7 @@ static TsLev mg_view(iemic_ctx* c, int q)
      * across a cut have the other colour; the x wrap only with one x part */
     const int qc = gs.mg_nlev - 1;
     V.periodic = c->cfg.periodic && c->npx == 1;
-    V.hj = (q == 0 && c->npy > 1) ? 1 : 0;
+    V.hj = (q == 0 && c->npy > 1 && !gs.mg_local0) ? 1 : 0;
     V.hi = (q < qc && q <= MG_XHALO_LEVELS && c->npx > 1) ? 1 : 0;
     V.vis = V.hj;
     V.visi = V.hi;
@@ -2758,6 +2764,7 @@ static int mg_setup(iemic_ctx* c)
         return 0;
     }
     if (gs.mg_nlev == 0) {
+        gs.mg_local0 = c->npy > 1 && getenv("IEMIC_MG_LOCAL0") != nullptr;
         /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns); the
          * number of levels is that of the largest subdomain, the same on every rank, so the
          * coarsest grids of the ranks tile the global coarsest problem */
@@ -2828,7 +2835,7 @@ static int mg_setup(iemic_ctx* c)
     {
         const TsLev V0 = mg_view(c, 0);
         hipLaunchKernelGGL(k_mg_pack0, dim3(blocks_for(c->nloc)), dim3(256), 0, s, gs.tsoff.p, gs.tsdiag.p,
-                           lay_of(c), c->next, V0, gs.mg_off[0].p, gs.mg_diag[0].p);
+                           lay_of(c), c->next, V0, gs.mg_off[0].p, gs.mg_diag[0].p, gs.mg_local0);
     }
     for (int q = 1; q < gs.mg_nlev; q++) {
         TsLev F = mg_view(c, q - 1);
@@ -3157,6 +3164,28 @@ static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool si
     return 0;
 }
 
+/* latitude bands: the U/V/W/P rows' coefficients (slots 0 .. 63) of the two halo rows, from
+ * the neighbour bands' first / last owned row (BlockGS::dvh: slot-major, the south row's
+ * cells, then the north row's) */
+static int dyn_halo_coefs(iemic_ctx* c)
+{
+    BlockGS& gs = c->gs;
+    const int64_t row = (int64_t)c->l * c->nx, nloc = c->nloc;
+    constexpr int NDS = 64;
+    if (gs.dvh.n < (size_t)(NDS * 2 * row)) {
+        if (gs.dvh.alloc((size_t)(NDS * 2 * row))) return IEMIC_ENOMEM;
+        HIP_OK(hipMemsetAsync(gs.dvh.p, 0, sizeof(double) * gs.dvh.n, c->stream));
+    }
+    double* v = c->d_val.p;
+    const int so = c->nb[2], no = c->nb[3];
+    std::vector<Msg> y;
+    if (so >= 0) y.push_back({true, so, Seg{v, 0, NDS, row, nloc}});
+    if (no >= 0) y.push_back({false, no, Seg{gs.dvh.p, row, NDS, row, 2 * row}});
+    if (no >= 0) y.push_back({true, no, Seg{v, nloc - row, NDS, row, nloc}});
+    if (so >= 0) y.push_back({false, so, Seg{gs.dvh.p, 0, NDS, row, 2 * row}});
+    return run_msgs(c, y);
+}
+
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
 {
     BlockGS& gs = c->gs;
@@ -3267,6 +3296,7 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         if ((rc = halo_exchange_w(c, gs.uvinv.p, 4, 1))) return rc;
         if ((rc = halo_exchange_w(c, gs.gslot.p, GSL, 1))) return rc;
     }
+    if (c->nranks > 1 && c->npx == 1 && (rc = dyn_halo_coefs(c))) return rc;
     if (c->l <= 64) {
         /* the Schur right-hand side as a linear form in rr (k_gs_ptil_rcol) */
         const int64_t ncolb = c->nloc / c->l;
@@ -3318,8 +3348,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
  * once z is final (the defect correction's update, fused into the pass's last kernels where
  * the column scans run); zaos: the pass's final values (zo's when given) also into the
  * preconditioner output (AoS), on the last pass */
+/* rr_halo: rr's halo rows already hold the neighbours' values (the bands' defect computed
+ * them itself, spmv_dyn_defect) */
 static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0,
-                     double* zaos = nullptr)
+                     double* zaos = nullptr, bool rr_halo = false)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -3342,7 +3374,7 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const bool hrow = band && c->npx == 1;
     const double* gsl = hrow ? gs.gslot.p : nullptr;
     const unsigned gcth = hrow ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx + 2)) : gct;
-    if (band && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
+    if (band && !rr_halo && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
     if (Pl == 16)
         hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
                            gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
@@ -3377,7 +3409,7 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     return 0;
 }
 
-int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d);
+int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d, bool halo = false);
 
 /* GPU time of the apply's parts (HIP events on the library stream, nrep back-to-back
  * launches each, zero data): us[0] one Schur solve (cyclic reduction), us[1] one T/S block
@@ -3495,11 +3527,15 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
                                gs.zc.p, gs.dq.p, zP, gs.dres.p, L, last ? 0 : 1, zaos_of(last));
         }
     }
+    /* latitude bands: the defect on the two halo rows too (from a 2-deep halo of the U/V/W/P
+     * planes), so that the pass needs no exchange of it (2 -> 1 exchange batch per pass) */
+    const bool dhalo = band && c->npx == 1 && gs.dvh.p;
     for (int it = 1; !gs.dyn_mr && it < gs.dyn_iters; it++) {
         const bool last = it + 1 == gs.dyn_iters;
-        if (band && (rc = halo_exchange_planar(c, zP, NUN, ps, 1))) return rc;   /* w, p of the neighbours */
-        if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p))) return rc;
-        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last)))) return rc;   /* z += w zc */
+        if (band && (rc = dhalo ? halo_exchange_planar(c, zP, 4, ps, 2) : halo_exchange_planar(c, zP, NUN, ps, 1)))
+            return rc;   /* w, p of the neighbours */
+        if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p, dhalo))) return rc;
+        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last), dhalo))) return rc;   /* z += w zc */
         if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;
     }
     if (ts_at == gs.dyn_iters && (rc = ts())) return rc;
