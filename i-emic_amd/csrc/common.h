@@ -218,7 +218,8 @@ struct BlockGS {
      * longitudes (schur_cr.hip, the explicit "tail" inverse) */
     static constexpr int MG_CR_CELLS = 1024;
     int mg_crd = 0;
-    int mg_local0 = 0;               /* bands: level-0 smoother without the cross-band rows */
+    int mg_hr = 0;                   /* bands: level 0 has 2 halo rows, and its colour-1   */
+                                     /* lines on them are relaxed here too (mg_vcycle)      */
     SchurCR mg_cr;
     DevBuf<int> mg_cinfo;            /* its Gauss-Jordan pivot flag                      */
     /* the dynamics passes work on component-planar copies (plane q = unknown q of every ext

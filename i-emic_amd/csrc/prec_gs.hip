@@ -1592,26 +1592,32 @@ __device__ __forceinline__ int mg_lcolour(const TsLev& V, int i, int jl)
     return (i + jl + V.jpar) & 1;
 }
 /* g-th owned column of a colour: row jl holds i = 2h + ((colour + jl + jpar) & 1), h <
- * ceil(n'/2), n' = n - 1 on an odd periodic level (whose last column has colour 2 or 3) */
-__device__ __forceinline__ bool mg_column(const TsLev& V, int colour, int g, int& i, int& jl)
+ * ceil(n'/2), n' = n - 1 on an odd periodic level (whose last column has colour 2 or 3).
+ * hr (bands' level 0): the rows run from -1 to mb, the halo row -1 when hr & 1, mb when
+ * hr & 2 (the parity of a negative jl is that of the global row too) */
+__device__ __forceinline__ bool mg_column(const TsLev& V, int colour, int g, int& i, int& jl, int hr = 0)
 {
     const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
+    const int rows = V.mb + (hr ? 2 : 0), j0 = hr ? -1 : 0;
     if (colour < 2) {
         const int per_row = (np + 1) / 2;
-        if (g >= per_row * V.mb) return false;
-        jl = g / per_row;
+        if (g >= per_row * rows) return false;
+        jl = g / per_row + j0;
         i = 2 * (g % per_row) + ((colour + jl + V.jpar) & 1);
-        return i < np;
+    } else {
+        if (g >= rows) return false;
+        jl = g + j0;
+        i = V.n - 1;
+        if (((jl + V.jpar) & 1) != colour - 2) return false;
     }
-    if (g >= V.mb) return false;
-    jl = g;
-    i = V.n - 1;
-    return ((jl + V.jpar) & 1) == colour - 2;
+    if ((jl < 0 && !(hr & 1)) || (jl >= V.mb && !(hr & 2))) return false;
+    return i < np || colour >= 2;
 }
-__host__ __device__ __forceinline__ int64_t mg_columns_of(const TsLev& V, int colour)
+__host__ __device__ __forceinline__ int64_t mg_columns_of(const TsLev& V, int colour, int hr = 0)
 {
     const int np = (V.periodic && (V.n & 1)) ? V.n - 1 : V.n;
-    return colour < 2 ? (int64_t)((np + 1) / 2) * V.mb : V.mb;
+    const int rows = V.mb + (hr ? 2 : 0);
+    return colour < 2 ? (int64_t)((np + 1) / 2) * rows : rows;
 }
 
 /* Line solve of one column, lane = level k (< l when on): g = A'^-1 r, then the forward
@@ -1715,10 +1721,10 @@ __device__ __forceinline__ int64_t zl_col(const TsLev& V, int i, int jl, int k, 
 
 template <int P>
 __device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k, const TsLev& C, int corr,
-                                       double* __restrict__ zout)
+                                       double* __restrict__ zout, int hr)
 {
     int i, jl;
-    if (!mg_column(V, colour, g, i, jl)) return;           /* whole column groups exit */
+    if (!mg_column(V, colour, g, i, jl, hr)) return;       /* whole column groups exit */
     const int64_t cs = V.cstr;
     const bool on = k < V.l;
     double xt, xs;
@@ -1726,7 +1732,7 @@ __device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k,
     if (!on) return;
     V.z[c] = xt;
     V.z[cs + c] = xs;
-    if (zout) {
+    if (zout && jl >= 0 && jl < V.mb) {
         const int64_t e = NUN * ((((int64_t)jl + HALO) * V.l + k) * V.n + i);
         if (V.diag[c] != 0.0) zout[e + TT] = xt;
         if (V.diag[3 * cs + c] != 0.0) zout[e + SS] = xs;
@@ -1734,9 +1740,9 @@ __device__ __forceinline__ void zl_one(const TsLev& V, int colour, int g, int k,
 }
 template <int P>
 __global__ void __launch_bounds__(256) k_mg_zl(TsLev V, int colour, TsLev C, int corr,
-                                              double* __restrict__ zout)
+                                              double* __restrict__ zout, int hr)
 {
-    zl_one<P>(V, colour, (blockIdx.x * blockDim.x + threadIdx.x) / P, threadIdx.x % P, C, corr, zout);
+    zl_one<P>(V, colour, (blockIdx.x * blockDim.x + threadIdx.x) / P, threadIdx.x % P, C, corr, zout, hr);
 }
 
 /* Restriction F -> C (coarse rhs = sum of the children's residuals, fixed order
@@ -2111,18 +2117,12 @@ __global__ void k_mg_out(TsLev V, double* __restrict__ zout)
 
 /* level 0: the compact T/S couplings and 2x2 blocks (ext layout) into the level layout */
 __global__ void k_mg_pack0(const double* __restrict__ tsoff, const double* __restrict__ tsdiag, Lay L,
-                           int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag, int cut)
+                           int64_t next, TsLev V, double* __restrict__ off, double* __restrict__ diag)
 {
     OWNED_CELL;
-    const int jl = j - L.jb0;
-    const int64_t c = mg_cell(V, i - L.ib0, jl, k);
-    /* cut: the band-local level 0 drops the couplings to the neighbour bands' rows */
-    const bool cs = cut && jl == 0, cn = cut && jl == V.mb - 1;
+    const int64_t c = mg_cell(V, i - L.ib0, j - L.jb0, k);
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
-        const int q = e & 7;
-        off[(int64_t)e * V.cstr + c] = ((q == 2 && cs) || (q == 3 && cn)) ? 0.0 : tsoff[(int64_t)e * next + cell];
-    }
+    for (int e = 0; e < 16; e++) off[(int64_t)e * V.cstr + c] = tsoff[(int64_t)e * next + cell];
 #pragma unroll
     for (int e = 0; e < 4; e++) diag[(int64_t)e * V.cstr + c] = tsdiag[(int64_t)e * next + cell];
 }
@@ -2376,7 +2376,7 @@ static TsLev mg_view(iemic_ctx* c, int q)
      * across a cut have the other colour; the x wrap only with one x part */
     const int qc = gs.mg_nlev - 1;
     V.periodic = c->cfg.periodic && c->npx == 1;
-    V.hj = (q == 0 && c->npy > 1 && !gs.mg_local0) ? 1 : 0;
+    V.hj = (q == 0 && c->npy > 1) ? (gs.mg_hr ? 2 : 1) : 0;
     V.hi = (q < qc && q <= MG_XHALO_LEVELS && c->npx > 1) ? 1 : 0;
     V.vis = V.hj;
     V.visi = V.hi;
@@ -2764,7 +2764,8 @@ static int mg_setup(iemic_ctx* c)
         return 0;
     }
     if (gs.mg_nlev == 0) {
-        gs.mg_local0 = c->npy > 1 && getenv("IEMIC_MG_LOCAL0") != nullptr;
+        /* latitude bands, one sweep: level 0 keeps 2 halo rows (mg_vcycle) */
+        gs.mg_hr = c->npy > 1 && c->npx == 1 && std::max(1, gs.mg_sweeps) == 1;
         /* coarsen 2x2 horizontally until the level has <= 128 cells (<= 256 unknowns); the
          * number of levels is that of the largest subdomain, the same on every rank, so the
          * coarsest grids of the ranks tile the global coarsest problem */
@@ -2835,7 +2836,7 @@ static int mg_setup(iemic_ctx* c)
     {
         const TsLev V0 = mg_view(c, 0);
         hipLaunchKernelGGL(k_mg_pack0, dim3(blocks_for(c->nloc)), dim3(256), 0, s, gs.tsoff.p, gs.tsdiag.p,
-                           lay_of(c), c->next, V0, gs.mg_off[0].p, gs.mg_diag[0].p, gs.mg_local0);
+                           lay_of(c), c->next, V0, gs.mg_off[0].p, gs.mg_diag[0].p);
     }
     for (int q = 1; q < gs.mg_nlev; q++) {
         TsLev F = mg_view(c, q - 1);
@@ -2853,6 +2854,24 @@ static int mg_setup(iemic_ctx* c)
         hipLaunchKernelGGL(k_mg_fac, dim3(blocks_for((int64_t)V.n * V.mb)), dim3(256), 0, s, V, gs.mg_fac[q].p);
     }
     HIP_OK(hipGetLastError());
+    if (gs.mg_hr) {
+        /* level 0's couplings, blocks and line factors of the neighbours' edge rows (the
+         * halo-row line solves of mg_vcycle) */
+        const TsLev V = mg_view(c, 0);
+        const int64_t RW = (int64_t)V.n * V.l;
+        const int so = c->nb[2], no = c->nb[3];
+        std::vector<Msg> y;
+        double* const arr[3] = {gs.mg_off[0].p, gs.mg_diag[0].p, gs.mg_fac[0].p};
+        const int ncomp[3] = {16, 4, 12};
+        for (int q = 0; q < 3; q++) {
+            auto row = [&](int jl) { return Seg{arr[q], (V.hj + jl) * RW, ncomp[q], RW, V.cstr}; };
+            if (so >= 0) y.push_back({true, so, row(0)});
+            if (no >= 0) y.push_back({false, no, row(V.mb)});
+            if (no >= 0) y.push_back({true, no, row(V.mb - 1)});
+            if (so >= 0) y.push_back({false, so, row(-1)});
+        }
+        if ((rc = run_msgs(c, y))) return rc;
+    }
     /* coarsest level: its dense operator assembled and inverted on the device (Gauss-Jordan
      * with pivoting in one workgroup, schur_cr.hip, up to 192 unknowns); larger coarsest
      * levels and the bands' global coarsest problem go through the host */
@@ -2970,16 +2989,42 @@ static int mg_halo(iemic_ctx* c, const TsLev& V)
     return run_msgs(c, y);
 }
 
-/* one colour launch of the z-line smoother (C: first post-smoothing sweep, zout: final) */
-static int mg_zl(iemic_ctx* c, const TsLev& V, int colour, const TsLev* C, double* zout)
+/* the bands' level 0 (mg_hr): the iterate's 2 rows next to each neighbour band, and with b
+ * its right-hand side's edge row -- for the halo-row line solves */
+static int mg_halo2(iemic_ctx* c, const TsLev& V, bool with_b)
+{
+    const int64_t RW = (int64_t)V.n * V.l;
+    const int so = c->nb[2], no = c->nb[3];
+    std::vector<Msg> y;
+    for (double* z : {V.z, V.z + V.cstr}) {
+        auto rows = [&](int jl) { return Seg{z, (V.hj + jl) * RW, 1, 2 * RW, 2 * RW}; };
+        if (so >= 0) y.push_back({true, so, rows(0)});
+        if (no >= 0) y.push_back({false, no, rows(V.mb)});
+        if (no >= 0) y.push_back({true, no, rows(V.mb - 2)});
+        if (so >= 0) y.push_back({false, so, rows(-2)});
+    }
+    if (with_b)
+        for (double* b : {V.b, V.b + V.cstr}) {
+            auto row = [&](int jl) { return Seg{b, (V.hj + jl) * RW, 1, RW, RW}; };
+            if (so >= 0) y.push_back({true, so, row(0)});
+            if (no >= 0) y.push_back({false, no, row(V.mb)});
+            if (no >= 0) y.push_back({true, no, row(V.mb - 1)});
+            if (so >= 0) y.push_back({false, so, row(-1)});
+        }
+    return run_msgs(c, y);
+}
+
+/* one colour launch of the z-line smoother (C: first post-smoothing sweep, zout: final;
+ * hr: the halo rows' lines too, mg_column) */
+static int mg_zl(iemic_ctx* c, const TsLev& V, int colour, const TsLev* C, double* zout, int hr = 0)
 {
     hipStream_t s = c->stream;
     const int P = mg_lanes(V.l);
-    const unsigned g = (unsigned)((mg_columns_of(V, colour) * P + 63) / 64);
+    const unsigned g = (unsigned)((mg_columns_of(V, colour, hr) * P + 63) / 64);
     if (!g) return 0;
     const TsLev Cv = C ? *C : V;
     const int corr = C ? 1 : 0;
-    MG_LAUNCH_P64(P, k_mg_zl, g, V, colour, Cv, corr, zout);
+    MG_LAUNCH_P64(P, k_mg_zl, g, V, colour, Cv, corr, zout, hr);
     return 0;
 }
 
@@ -3064,14 +3109,20 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
         else hipLaunchKernelGGL(k_mg_up<64>, dim3(g), dim3(640), 0, s, V, Cf, zu);
         return 0;
     }
+    /* the bands' level 0, one sweep of two colours from the entry kernel: one exchange of 2
+     * rows before each colour-1 launch, which relaxes the halo rows' colour-1 lines too
+     * (the neighbour's own lines, operation for operation), so that the restriction and the
+     * last colour-0 launch read them without another exchange (4 -> 2 batches per V-cycle) */
+    const bool hrel = q == 0 && gs.mg_hr && V.hj == 2 && nu == 1 && nc == 2 && first;
+    const int hr = hrel ? ((c->nb[2] >= 0 ? 1 : 0) | (c->nb[3] >= 0 ? 2 : 0)) : 0;
     for (int sw = 0; sw < nu; sw++)
         for (int h = (sw == 0 && first) ? 1 : 0; h < nc; h++) {
-            if ((rc = mg_halo(c, V))) return rc;
-            if ((rc = mg_zl(c, V, h, nullptr, nullptr))) return rc;
+            if ((rc = hrel ? mg_halo2(c, V, true) : mg_halo(c, V))) return rc;
+            if ((rc = mg_zl(c, V, h, nullptr, nullptr, hrel && h == 1 ? hr : 0))) return rc;
         }
     const int qc = gs.mg_nlev - 1;
     const TsLev C = mg_view(c, q + 1);
-    if ((rc = mg_halo(c, V))) return rc;
+    if (!hrel && (rc = mg_halo(c, V))) return rc;
     {
         const int P = mg_lanes(V.l);
         const int shortcut = (first && nu == 1 && nc == 2) ? 1 : 0;
@@ -3091,8 +3142,14 @@ static int mg_vcycle(iemic_ctx* c, int q, bool first, double* zout)
         hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for((int64_t)V.n * V.mb * V.l)), dim3(256), 0, s, V, Cf);
     for (int sw = 0; sw < nu; sw++)
         for (int h = nc - 1; h >= 0; h--) {
-            if ((rc = mg_halo(c, V))) return rc;
-            if ((rc = mg_zl(c, V, h, corr && sw == 0 ? &Cf : nullptr, sw + 1 == nu ? zout : nullptr))) return rc;
+            if (hrel) {
+                if (h == 1 && (rc = mg_halo2(c, V, false))) return rc;
+            } else if ((rc = mg_halo(c, V))) {
+                return rc;
+            }
+            if ((rc = mg_zl(c, V, h, corr && sw == 0 ? &Cf : nullptr, sw + 1 == nu ? zout : nullptr,
+                            hrel && h == 1 ? hr : 0)))
+                return rc;
         }
     return 0;
 }
