@@ -185,15 +185,20 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
 /* hv (latitude bands): tiles past the owned ones compute the defect on the two halo rows
  * too (their coefficients exchanged once per Jacobian, BlockGS::dvh; z with a 2-deep halo),
  * so that the next dynamics pass needs no exchange of d.  hs / hn: the south / north halo row
- * exists (a neighbour band). */
+ * exists (a neighbour band).  alist: the owned tiles run over the active cells only (the
+ * compressed basis' list, BlockGS::act; about half the cells are land at 2 degrees): d of the
+ * other cells stays 0 (gs_compute zeroes it whenever the list changes). */
 __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
                                                   const uint8_t* __restrict__ knP,
                                                   double* __restrict__ d, int64_t nloc, int nblk, int64_t ps,
-                                                  const double* __restrict__ hv, int nhb, int hs, int hn)
+                                                  const double* __restrict__ hv, int nhb, int hs, int hn,
+                                                  const int* __restrict__ alist, int64_t nown)
 {
     __shared__ double red[4][2][64];
+    __shared__ int64_t us[64];
+    __shared__ int oks[64];
     const int ntot = nblk + nhb;
     const int per = (ntot + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -202,22 +207,22 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
     const int64_t row = (int64_t)X.l * X.nx;             /* cells of one latitude row */
     const int64_t e0 = (int64_t)HALO * row;              /* ext cell of owned cell 0 */
     /* u: the cell relative to owned cell 0 (the halo rows at -row .. -1 and nloc .. nloc + row - 1) */
-    int64_t u0, n0;
-    bool halo = tile >= nblk;
+    const bool halo = tile >= nblk;
+    int64_t h, u;
+    bool act;
     if (!halo) {
-        u0 = (int64_t)tile * 64;
-        n0 = nloc;
+        h = (int64_t)tile * 64 + c;
+        act = h < nown;
+        u = !act ? 0 : (alist ? (int64_t)alist[h] : h);
     } else {
-        u0 = (int64_t)(tile - nblk) * 64;                /* halo index: south row, then north */
-        n0 = 2 * row;
-    }
-    const int64_t h = u0 + c;
-    bool act = h < n0;
-    int64_t u = h;
-    if (halo) {
+        h = (int64_t)(tile - nblk) * 64 + c;             /* halo index: south row, then north */
         const bool south = h < row;
-        act = act && (south ? hs : hn);
+        act = h < 2 * row && (south ? hs : hn);
         u = south ? h - row : nloc + h - row;
+    }
+    if (g == 0) {
+        us[c] = u;
+        oks[c] = act ? 1 : 0;
     }
     double acc[2] = {0.0, 0.0};
     if (act) {
@@ -243,32 +248,28 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
     /* rows of the waves: g0 {U} g1 {U,V} g2 {V,W} g3 {W,P}; thread = (row, cell), the
      * cell fastest (planar stores) */
     const int R = threadIdx.x >> 6, cc = threadIdx.x & 63;
-    const int64_t hh = u0 + cc;
-    if (hh >= n0) return;
-    int64_t uu = hh;
-    if (halo) {
-        const bool south = hh < row;
-        if (!(south ? hs : hn)) return;
-        uu = south ? hh - row : nloc + hh - row;
-    }
+    if (!oks[cc]) return;
     const double sum = R == 0 ? red[0][0][cc] + red[1][0][cc]
                      : R == 1 ? red[1][1][cc] + red[2][0][cc]
                      : R == 2 ? red[2][1][cc] + red[3][0][cc]
                               : red[3][1][cc];
-    const int64_t cell = e0 + uu, e = cell + ps * R;
+    const int64_t cell = e0 + us[cc], e = cell + ps * R;
     d[e] = knP[e] ? 0.0 : r[e] - sum;
 }
 
 int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_t* knP, double* d, bool halo)
 {
-    const int nblk = (int)((c->nloc + 63) / 64);
+    const BlockGS& gs = c->gs;
+    const bool al = gs.act.p && gs.nact > 0;
+    const int64_t nown = al ? gs.nact : c->nloc;
+    const int nblk = (int)((nown + 63) / 64);
     const int64_t row = (int64_t)c->l * c->nx;
-    const bool hv = halo && c->gs.dvh.p;
+    const bool hv = halo && gs.dvh.p;
     const int nhb = hv ? (int)((2 * row + 63) / 64) : 0;
     const unsigned grid = 8u * (unsigned)((nblk + nhb + 7) / 8);
     hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, knP, d,
-                       c->nloc, nblk, (int64_t)c->next, hv ? c->gs.dvh.p : nullptr, nhb,
-                       hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0);
+                       c->nloc, nblk, (int64_t)c->next, hv ? gs.dvh.p : nullptr, nhb,
+                       hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0, al ? gs.act.p : nullptr, nown);
     return 0;
 }
 

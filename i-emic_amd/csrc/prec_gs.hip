@@ -3326,6 +3326,9 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                 if (cell >= 0 && cell < c->nloc && cm[cell] >= 0) gs.ric = (int64_t)NUN * cm[cell] + c->rowintcon % NUN;
             }
             gs.act_h.swap(h);
+            /* the defect (k_spmv_dyn) writes the active cells only: the others' rows 0 */
+            for (DevBuf<double>* bptr : {&gs.dres, &gs.dq})
+                if (bptr->p) HIP_OK(hipMemsetAsync(bptr->p, 0, sizeof(double) * bptr->n, c->stream));
         }
     }
     {
