@@ -47,9 +47,12 @@ template <int S0, int S1>
 __device__ __forceinline__ void sp7_load(const double* __restrict__ val, int64_t nloc, int64_t lc, bool act,
                                          double* v)
 {
+    /* an inactive lane's v is left undefined (its sums are never stored): no merge point
+     * that would wait for the loads before the staging's are issued */
+    if (act) {
 #pragma unroll
-    for (int s = S0; s < S1; s++)
-        v[s - S0] = !act ? 0.0 : __builtin_nontemporal_load(val + (int64_t)s * nloc + lc);
+        for (int s = S0; s < S1; s++) v[s - S0] = __builtin_nontemporal_load(val + (int64_t)s * nloc + lc);
+    }
 }
 template <int S0, int S1>
 __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, int c, double* acc)
@@ -81,39 +84,56 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
     const int k = row % l, jl = row / l, j = X.jb0 + jl;
     const int nc = min(SP7_T, nx - i0);
     const int lc0 = row * nx + i0;
-    const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    const int t = threadIdx.x, c = t & 63;
+    const int g = __builtin_amdgcn_readfirstlane(t >> 6);   /* wave-uniform: scalar branches */
     int cm = 0;
     if (CMP) {
         cm = c < nc ? cmap[lc0 + c] : -1;
         if (g == 0) cms[c] = cm;
         if (!__syncthreads_or(cm >= 0)) return;     /* a land tile */
     }
+    const bool act = c < nc && (!CMP || cm >= 0);
+    const int64_t lc = lc0 + c;
+    double acc[3] = {0.0, 0.0, 0.0};
+    double v[26];
+    /* the coefficient loads first (one predicated block), then the x staging's loads, all
+     * issued before the first LDS store: one memory latency per tile instead of one per
+     * staging round (the staging loop waited for each load before its store) */
+    if (g == 0) sp7_load<0, 26>(val, nloc, lc, act, v);
+    else if (g == 1) sp7_load<26, 52>(val, nloc, lc, act, v);
+    else if (g == 2) sp7_load<52, 78>(val, nloc, lc, act, v);
+    else sp7_load<78, 104>(val, nloc, lc, act, v);
     /* stage x: 6 grid rows x (nc + 2) cells x 6 unknowns, contiguous runs (the two end
      * cells: the neighbour columns, from the x halo when the x direction is split) */
     {
         const int jm = j > 0 ? j - 1 : j, jp = j < X.m - 1 ? j + 1 : j;
         const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
         const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
-        const int per_row = (nc + 2) * NUN;
-        for (int e = t; e < 6 * per_row; e += 256) {
-            const int q = e / per_row, w = e - q * per_row;
-            const int p = w / NUN, var = w - p * NUN;
-            const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
-            const int64_t cell = (p == 0 || p == nc + 1)
-                                     ? xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb)
-                                     : r * nx + i0 + p - 1;
-            xs[(q * (SP7_T + 2) + p) * NUN + var] = x[NUN * cell + var];
+        /* element e of the LDS image is (q (SP7_T + 2) + p) NUN + var: constant divisors */
+        constexpr int PR = (SP7_T + 2) * NUN;
+        constexpr int SPT = (6 * PR + 255) / 256;
+        const int lim = (nc + 2) * NUN;
+        double xv[SPT];
+        int xo[SPT];
+#pragma unroll
+        for (int u = 0; u < SPT; u++) {
+            const int e = t + 256 * u;
+            const int q = e / PR, w = e - q * PR;
+            xo[u] = -1;
+            if (e < 6 * PR && w < lim) {
+                const int p = w / NUN, var = w - p * NUN;
+                const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
+                const int64_t cell = (p == 0 || p == nc + 1)
+                                         ? xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb)
+                                         : r * nx + i0 + p - 1;
+                xo[u] = e;
+                xv[u] = x[NUN * cell + var];
+            }
         }
+#pragma unroll
+        for (int u = 0; u < SPT; u++)
+            if (xo[u] >= 0) xs[xo[u]] = xv[u];
     }
-    const bool act = c < nc && (!CMP || cm >= 0);
-    const int64_t lc = lc0 + c;
-    double acc[3] = {0.0, 0.0, 0.0};
-    double v[26];
-    /* the coefficient loads are issued before the barrier, overlapping the x staging */
-    if (g == 0) sp7_load<0, 26>(val, nloc, lc, act, v);
-    else if (g == 1) sp7_load<26, 52>(val, nloc, lc, act, v);
-    else if (g == 2) sp7_load<52, 78>(val, nloc, lc, act, v);
-    else sp7_load<78, 104>(val, nloc, lc, act, v);
     __syncthreads();
     if (g == 0) sp7_compute<0, 26>(v, xs, c, acc);
     else if (g == 1) sp7_compute<26, 52>(v, xs, c, acc);

@@ -1222,24 +1222,26 @@ __global__ void k_mr_update(const uint8_t* __restrict__ knP, const double* __res
 /* gsl (latitude bands): threads past the owned cells compute the south halo row's U/V
  * points too (their P couplings from the halo-filled gslot), into z only, so that the p/w
  * kernel needs no exchange of uv */
+/* alist: the threads run over the active cells (nown of them; BlockGS::act), the land
+ * cells' U/V points being identity rows */
 __global__ void k_gs_uvp(const double* __restrict__ val, const uint8_t* __restrict__ knP,
                          const double* __restrict__ uvinv, const double* __restrict__ rr,
                          const double* __restrict__ pbar, double* __restrict__ z, Lay L,
                          double* __restrict__ zo, double omega, double* __restrict__ zaos,
-                         const double* __restrict__ gsl)
+                         const double* __restrict__ gsl, const int* __restrict__ alist, int64_t nown)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t lc = t;
     const int64_t ncell = L.nloc;
     const int n = L.n, m = L.m, periodic = L.periodic;
     int i, j, k;
-    int64_t cell;
-    const bool halo = t >= L.nloc;
+    int64_t cell, lc = 0;
+    const bool halo = t >= nown;
     if (!halo) {
+        lc = alist ? (int64_t)alist[t] : t;
         cell = L.own0 + lc;
         lc_ijk(L, lc, i, j, k);
     } else {
-        const int64_t q = t - L.nloc;                /* south halo row, (k, i) */
+        const int64_t q = t - nown;                  /* south halo row, (k, i) */
         if (!gsl || q >= (int64_t)L.l * L.nx || L.jb0 == 0) return;
         i = L.ib0 + (int)(q % L.nx);
         k = (int)(q / L.nx);
@@ -3453,9 +3455,11 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
         sb = gs.colv.p;
     }
     if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s, gs.colvT.p))) return rc;
-    const unsigned gcu = hrow ? (unsigned)((c->nloc + (int64_t)c->l * c->nx + 255) / 256) : gc;
+    const bool al = gs.act.p && gs.nact > 0;
+    const int64_t nown = al ? gs.nact : c->nloc;
+    const unsigned gcu = (unsigned)((nown + (hrow ? (int64_t)c->l * c->nx : 0) + 255) / 256);
     hipLaunchKernelGGL(k_gs_uvp, dim3(gcu), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
-                       rr, gs.colvT.p, z, L, zo, omega, zaos, gsl);
+                       rr, gs.colvT.p, z, L, zo, omega, zaos, gsl, al ? gs.act.p : nullptr, nown);
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
     if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
