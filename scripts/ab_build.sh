@@ -1,8 +1,9 @@
 #!/bin/bash
 # Build kernel variants of the device library for an A/B measurement on one box
 # (scripts/ab_probe.py): each variant is the tree's i-emic_amd/ with a patch applied (a
-# script run in the copy's i-emic_amd/, or a git revision's csrc/ and header for
-# "rev:<commit>"), built into i-emic_amd/lib/libiemic_amd_<name>.so.
+# variant of scripts/ab_patches.sh for "ab:<variant>", a script run in the copy's
+# i-emic_amd/, or a git revision's csrc/ and header for "rev:<commit>"), built into
+# i-emic_amd/lib/libiemic_amd_<name>.so.
 # usage: scripts/ab_build.sh name=spec ...   (spec empty: the tree as it is)
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -20,6 +21,8 @@ for arg in "$@"; do
       git -C "$ROOT" show "$rev:$f" > "$W/i-emic_amd/csrc/$(basename $f)"
     done
     git -C "$ROOT" show "$rev:include/iemic.h" > "$W/include/iemic.h"
+  elif [[ $spec == ab:* ]]; then
+    (cd "$W/i-emic_amd" && bash "$ROOT/scripts/ab_patches.sh" "${spec#ab:}")
   elif [ -n "$spec" ]; then
     (cd "$W/i-emic_amd" && bash "$ROOT/$spec")
   fi
