@@ -318,6 +318,26 @@ def test_fgmres_nonfinite_is_an_error(oracle_lib, Ocean):
         oc.solve(b)
 
 
+def test_nan_state_fails_cleanly(oracle_lib, Ocean):
+    """A NaN state (a diverging Newton iterate) gives a NaN Jacobian.  The preconditioner
+    set-up (its Schur inverses see NaN pivot candidates: k_cr_inv, advisor round 4) or the
+    solve reports an error instead of faulting, and the context stays usable."""
+    from iemic._lib import IemicError
+    c, oc, o, L = make(Ocean, oracle_lib, "natl8", solver_params={"Preconditioner": 2})
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    xn = x.copy()
+    xn[::7] = np.nan
+    oc.setState(xn)
+    oc.computeJacobian()
+    b = cf.synthetic_vector(c, seed=5)
+    with pytest.raises(IemicError):
+        oc.solve(b)
+    oc.setState(x)
+    oc.computeJacobian()
+    sol = oc.solve(b)
+    assert np.all(np.isfinite(sol)) and oc.last_solve.converged == 1
+
+
 def _land_rows(c, L):
     Li = L[1:-1, 1:-1, 1:-1].reshape(-1)
     return np.repeat((Li != 0).astype(float), 6)
