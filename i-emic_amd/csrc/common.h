@@ -428,7 +428,7 @@ int prec_apply(iemic_ctx* c, const double* r, double* z);
 /* the block GS apply from a compressed input (6 rows per BlockGS::act cell, zero land rows) */
 int gs_apply_c(iemic_ctx* c, const double* rc, double* z);
 /* y = J x written compressed (rows of the active cells only; x full, halo current) */
-int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc);
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t after = nullptr);
 }  // namespace iemic
 
 #endif

@@ -741,7 +741,9 @@ static int spmv_intcond(iemic_ctx* c, const double* x, double* yr)
     return 0;
 }
 
-int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc)
+/* after: recorded right after the SpMV kernel, before the integral-condition row's
+ * reduction launches (FGMRES times the SpMV kernel alone with it) */
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t after)
 {
     if (!c->jac_valid || !c->gs.cmap.p) {
         set_error("spmv: no Jacobian or no active-cell map");
@@ -753,6 +755,7 @@ int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc)
     const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
     hipLaunchKernelGGL(k_spmv7<true>, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, yc, (int)c->nloc,
                        ntile, tpr, (const int*)c->gs.cmap.p);
+    if (after) HIP_OK(hipEventRecord(after, s));
     double* yr = nullptr;
     if (c->rowintcon >= 0) {
         if (c->gs.ric < 0) {
@@ -1126,14 +1129,16 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                         HIP_OK(hipMemcpyAsync(zj, u - o, sizeof(double) * NE, hipMemcpyDeviceToDevice,
                                               c->stream));
                     }
-                    HIP_OK(hipEventRecord(e[1], c->stream));
                     if (cmp) {
+                        /* e[1] .. e[2]: the SpMV kernel alone (bench.py's roofline.launch_us) */
                         if ((rc2 = halo_exchange(c, zj, 1))) return rc2;
-                        if ((rc2 = spmv_kernel_c(c, zj, wv))) return rc2;
-                    } else if ((rc2 = spmv(c, zj, wv - o, c->stream))) {
-                        return rc2;
+                        HIP_OK(hipEventRecord(e[1], c->stream));
+                        if ((rc2 = spmv_kernel_c(c, zj, wv, e[2]))) return rc2;
+                    } else {
+                        HIP_OK(hipEventRecord(e[1], c->stream));
+                        if ((rc2 = spmv(c, zj, wv - o, c->stream))) return rc2;
+                        HIP_OK(hipEventRecord(e[2], c->stream));
                     }
-                    HIP_OK(hipEventRecord(e[2], c->stream));
                 }
                 /* dot pass: a = Q^T u, b = Q^T w, u.u, u.w, w.w (Q = V_0..jj-1), summed over ranks */
                 const int nv = jj;
