@@ -672,13 +672,14 @@ def bench_newton(args, R: Ranks):
                                                        args.cold_reps) * 1e3, 2)
             del fl
     # measured per-kernel PMC bytes and trace times of this step (bench_data/pmc_<tag>.json)
-    traffic, step_rf, dom_rf = None, None, None
+    traffic, trace_us, step_rf, dom_rf = None, None, None, None
     tab, why = pmc_table(args.config) if world == 1 else (None, "one GPU only")
     if tab:
         ks = {r["kernel"]: r for r in tab["kernels"]}
         for kn in ("k_spmv7<true>", "k_spmv7<false>", "k_spmv7"):
             if kn in ks:
                 traffic = ks[kn]["hbm_bytes_per_launch"]
+                trace_us = ks[kn]["avg_us"]
                 break
         sb = tab["step_hbm_bytes"]
         step_rf = {"hbm_bytes": sb, "ms": round(ms, 3), "achieved": round(sb / (ms * 1e-3) / 1e9, 1),
@@ -766,7 +767,11 @@ def bench_newton(args, R: Ranks):
                      "achieved_csr": round(achieved, 1), "frac_csr": round(achieved / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes": bsp, "stencil_ell_bytes": ell, "active_cells": nact,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
-                     "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp,
+                     # launch_us: HIP events on the library stream around every in-solve SpMV
+                     # kernel (each interval includes the dispatch and completion latency of
+                     # the event pair); trace_us: the rocprofv3 kernel-trace average of the
+                     # same kernel in the same command (bench_data/pmc_<tag>.json)
+                     "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp, "trace_us": trace_us,
                      "step": step_rf, "dominant": dom_rf, **({"table": why} if why else {}), **extra},
         "cpu_baseline": None,
     }
