@@ -75,6 +75,7 @@ struct iemic_coupled {
     int64_t NL = 0, NA = 0, NC = 0;      /* ocean owned rows, atmosphere rows, packed total  */
     DevBuf<double> xo, yo, ro, zo;       /* ocean ext-layout scratch                         */
     DevBuf<double> V, Z, w, r, tmpa, part, hb;
+    DevBuf<double> hc;                   /* FGMRES: the step's CGS2 coefficients and norm    */
     DevBuf<double> tsurf;            /* n*m surface T of a packed vector (several ranks)  */
     int mk = 0;
     int synced = 0;
@@ -672,6 +673,25 @@ __global__ void k_cscale(double s, const double* __restrict__ x, double* __restr
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x)
         y[q] = s * x[q];
 }
+/* y -= sum_v c_v X_v with the coefficients in device memory (CGS2 pass without a host trip) */
+__global__ void k_cupdate_m(const double* __restrict__ X, int64_t ld, int nv, const double* __restrict__ c,
+                            double* __restrict__ y, int64_t N)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x) {
+        double s = y[q];
+        for (int v = 0; v < nv; v++) s += -c[v] * X[(int64_t)v * ld + q];
+        y[q] = s;
+    }
+}
+/* y *= 1 / sqrt(nrm2) from the device-resident squared norm (unchanged when it is not > 0) */
+__global__ void k_cscale_dev(const double* __restrict__ nrm2, double* __restrict__ y, int64_t N)
+{
+    const double n2 = *nrm2;
+    if (!(n2 > 0.0)) return;
+    const double s = 1.0 / sqrt(n2);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (int64_t)gridDim.x * blockDim.x)
+        y[q] = s * y[q];
+}
 
 }  // namespace
 }  // namespace iemic
@@ -1262,6 +1282,7 @@ extern "C" int iemic_coupled_create(iemic_coupled** out, iemic_ctx* oc, iemic_at
     rc |= cm->r.alloc(cm->NC);
     rc |= cm->part.alloc((size_t)KB * (MAX_KRYLOV + 2));
     rc |= cm->hb.alloc((size_t)2 * MAX_KRYLOV + 8);
+    rc |= cm->hc.alloc((size_t)2 * MAX_KRYLOV + 8);
     if (!rc && hipHostMalloc(&cm->h_red, sizeof(double) * (2 * MAX_KRYLOV + 8)) != hipSuccess) rc = 1;
     if (rc) {
         delete cm;
@@ -1369,6 +1390,17 @@ double cdot_host(iemic_coupled* cm, const double* V, int64_t ld, int nv, const d
 }  // namespace
 
 namespace {
+/* cdot_host's reduction left on the device: out[0..nv] (summed over the ranks) */
+int cdot_dev(iemic_coupled* cm, const double* V, int64_t ld, int nv, const double* w, double* out)
+{
+    hipStream_t s = cm->oc->stream;
+    const int64_t N = cm->oc->rank == 0 ? cm->NC : cm->NL;
+    hipLaunchKernelGGL(k_cdots, dim3(KB, nv + 1), dim3(256), 0, s, V, ld, nv, w, N, cm->part.p);
+    hipLaunchKernelGGL(k_cfinal, dim3(nv + 1), dim3(256), 0, s, (const double*)cm->part.p, nv + 1, out);
+    if (cm->oc->nranks > 1) return allreduce_sum(cm->oc, out, nv + 1);
+    return 0;
+}
+
 LinC make_linc(double a, const std::vector<double>& cs, const std::vector<const double*>& xs)
 {
     LinC L{};
@@ -1619,24 +1651,29 @@ extern "C" int iemic_coupled_solve(iemic_coupled* cm, const double* b_host, doub
             if ((rc = cpl_prec(cm, vj, zj, opt->prec > 0))) return rc;
             if ((rc = cpl_apply(cm, zj, vn))) return rc;
             (void)tp;
-            /* CGS2: h = V^T w, w -= V h, twice */
+            /* CGS2: h = V^T w, w -= V h, twice, then the norm and the scaling, with the
+             * coefficients on the device and one host round trip for all of them (round 4:
+             * three, each leaving the GPU idle) */
+            double* hc0 = cm->hc.p;
+            double* hc1 = cm->hc.p + (j + 1);
+            double* hcn = cm->hc.p + 2 * (j + 1);
             for (int pass = 0; pass < 2; pass++) {
-                cdot_host(cm, V, NC, j + 1, vn, (pass ? h2 : h).data());
-                std::vector<double>& hv = pass ? h2 : h;
-                for (int i = 0; i <= j; i++) tmp[i] = -hv[i];
-                (void)hipMemcpyAsync(cm->hb.p + MAX_KRYLOV + 4, tmp.data(), sizeof(double) * (j + 1),
-                                     hipMemcpyHostToDevice, s);
-                hipLaunchKernelGGL(k_cupdate, dim3(G), dim3(256), 0, s, (const double*)V, NC, j + 1,
-                                   (const double*)(cm->hb.p + MAX_KRYLOV + 4), 1.0, vn, NC);
+                double* hv = pass ? hc1 : hc0;
+                if ((rc = cdot_dev(cm, V, NC, j + 1, vn, hv))) return rc;
+                hipLaunchKernelGGL(k_cupdate_m, dim3(G), dim3(256), 0, s, (const double*)V, NC, j + 1,
+                                   (const double*)hv, vn, NC);
             }
-            for (int i = 0; i <= j; i++) h[i] += h2[i];
-            const double hn2 = cdot_host(cm, nullptr, 0, 0, vn, tmp.data());
+            if ((rc = cdot_dev(cm, nullptr, 0, 0, vn, hcn))) return rc;
+            hipLaunchKernelGGL(k_cscale_dev, dim3(G), dim3(256), 0, s, (const double*)hcn, vn, NC);
+            HIP_OK(hipMemcpyAsync(cm->h_red, cm->hc.p, sizeof(double) * (2 * (j + 1) + 1), hipMemcpyDeviceToHost, s));
+            HIP_OK(hipStreamSynchronize(s));
+            for (int i = 0; i <= j; i++) h[i] = cm->h_red[i] + cm->h_red[j + 1 + i];
+            const double hn2 = cm->h_red[2 * (j + 1)];
             if (!std::isfinite(hn2)) {
                 set_error("coupled FGMRES: non-finite value in the Krylov basis");
                 return IEMIC_ERANGE;
             }
             const double hn = std::sqrt(std::max(hn2, 0.0));
-            if (hn > 0) hipLaunchKernelGGL(k_cscale, dim3(G), dim3(256), 0, s, 1.0 / hn, (const double*)vn, vn, NC);
             for (int i = 0; i <= j; i++) H[(size_t)i * m + j] = h[i];
             H[(size_t)(j + 1) * m + j] = hn;
             for (int i = 0; i < j; i++) {
