@@ -81,7 +81,13 @@ struct iemic_coupled {
     int synced = 0;
     double pars[18] = {};                /* CommPars of the last synchronisation            */
     double* h_red = nullptr;
-    ~iemic_coupled() { if (h_red) (void)hipHostFree(h_red); }
+    hipEvent_t ev[2] = {nullptr, nullptr};  /* FGMRES: a step's coefficients in h_red         */
+    ~iemic_coupled()
+    {
+        if (h_red) (void)hipHostFree(h_red);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
 
 namespace iemic {
@@ -1282,8 +1288,10 @@ extern "C" int iemic_coupled_create(iemic_coupled** out, iemic_ctx* oc, iemic_at
     rc |= cm->r.alloc(cm->NC);
     rc |= cm->part.alloc((size_t)KB * (MAX_KRYLOV + 2));
     rc |= cm->hb.alloc((size_t)2 * MAX_KRYLOV + 8);
-    rc |= cm->hc.alloc((size_t)2 * MAX_KRYLOV + 8);
-    if (!rc && hipHostMalloc(&cm->h_red, sizeof(double) * (2 * MAX_KRYLOV + 8)) != hipSuccess) rc = 1;
+    rc |= cm->hc.alloc((size_t)2 * (2 * MAX_KRYLOV + 8));
+    for (hipEvent_t& e : cm->ev)
+        if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = 1;
+    if (!rc && hipHostMalloc(&cm->h_red, sizeof(double) * 2 * (2 * MAX_KRYLOV + 8)) != hipSuccess) rc = 1;
     if (rc) {
         delete cm;
         set_error("iemic_coupled_create: out of device memory");
@@ -1642,34 +1650,44 @@ extern "C" int iemic_coupled_solve(iemic_coupled* cm, const double* b_host, doub
         hipLaunchKernelGGL(k_cscale, dim3(G), dim3(256), 0, s, 1.0 / beta, (const double*)r, V, NC);
         std::fill(g.begin(), g.end(), 0.0);
         g[0] = beta;
-        int j = 0;
-        for (; j < m; j++) {
-            double* vj = V + (int64_t)j * NC;
-            double* zj = Z + (int64_t)j * NC;
-            double* vn = V + (int64_t)(j + 1) * NC;
-            auto tp = std::chrono::steady_clock::now();
-            if ((rc = cpl_prec(cm, vj, zj, opt->prec > 0))) return rc;
-            if ((rc = cpl_apply(cm, zj, vn))) return rc;
-            (void)tp;
-            /* CGS2: h = V^T w, w -= V h, twice, then the norm and the scaling, with the
-             * coefficients on the device and one host round trip for all of them (round 4:
-             * three, each leaving the GPU idle) */
-            double* hc0 = cm->hc.p;
-            double* hc1 = cm->hc.p + (j + 1);
-            double* hcn = cm->hc.p + 2 * (j + 1);
+        /* step jj enqueued: preconditioner, operator, CGS2 with the coefficients on the
+         * device, the new vector scaled on the device, its coefficients copied into half
+         * jj & 1 of the pinned h_red; the host enqueues step jj + 1 before it reads step jj
+         * (the work of a step after the last one of a cycle is discarded) */
+        const size_t HH = 2 * MAX_KRYLOV + 8;
+        auto enqueue = [&](int jj) -> int {
+            double* vj = V + (int64_t)jj * NC;
+            double* zj = Z + (int64_t)jj * NC;
+            double* vn = V + (int64_t)(jj + 1) * NC;
+            int rc2;
+            if ((rc2 = cpl_prec(cm, vj, zj, opt->prec > 0))) return rc2;
+            if ((rc2 = cpl_apply(cm, zj, vn))) return rc2;
+            double* hc0 = cm->hc.p + (size_t)(jj & 1) * HH;
+            double* hc1 = hc0 + (jj + 1);
+            double* hcn = hc0 + 2 * (jj + 1);
             for (int pass = 0; pass < 2; pass++) {
                 double* hv = pass ? hc1 : hc0;
-                if ((rc = cdot_dev(cm, V, NC, j + 1, vn, hv))) return rc;
-                hipLaunchKernelGGL(k_cupdate_m, dim3(G), dim3(256), 0, s, (const double*)V, NC, j + 1,
+                if ((rc2 = cdot_dev(cm, V, NC, jj + 1, vn, hv))) return rc2;
+                hipLaunchKernelGGL(k_cupdate_m, dim3(G), dim3(256), 0, s, (const double*)V, NC, jj + 1,
                                    (const double*)hv, vn, NC);
             }
-            if ((rc = cdot_dev(cm, nullptr, 0, 0, vn, hcn))) return rc;
+            if ((rc2 = cdot_dev(cm, nullptr, 0, 0, vn, hcn))) return rc2;
             hipLaunchKernelGGL(k_cscale_dev, dim3(G), dim3(256), 0, s, (const double*)hcn, vn, NC);
-            HIP_OK(hipMemcpyAsync(cm->h_red, cm->hc.p, sizeof(double) * (2 * (j + 1) + 1), hipMemcpyDeviceToHost, s));
-            HIP_OK(hipStreamSynchronize(s));
-            for (int i = 0; i <= j; i++) h[i] = cm->h_red[i] + cm->h_red[j + 1 + i];
-            const double hn2 = cm->h_red[2 * (j + 1)];
+            HIP_OK(hipMemcpyAsync(cm->h_red + (size_t)(jj & 1) * HH, hc0, sizeof(double) * (2 * (jj + 1) + 1),
+                                  hipMemcpyDeviceToHost, s));
+            HIP_OK(hipEventRecord(cm->ev[jj & 1], s));
+            return 0;
+        };
+        int j = 0;
+        if ((rc = enqueue(0))) return rc;
+        for (; j < m; j++) {
+            if (j + 1 < m && (rc = enqueue(j + 1))) return rc;
+            HIP_OK(hipEventSynchronize(cm->ev[j & 1]));
+            const double* hr = cm->h_red + (size_t)(j & 1) * HH;
+            for (int i = 0; i <= j; i++) h[i] = hr[i] + hr[j + 1 + i];
+            const double hn2 = hr[2 * (j + 1)];
             if (!std::isfinite(hn2)) {
+                (void)hipStreamSynchronize(s);
                 set_error("coupled FGMRES: non-finite value in the Krylov basis");
                 return IEMIC_ERANGE;
             }
