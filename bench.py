@@ -115,6 +115,8 @@ def parse():
                         "earlier lets the T/S multigrid run on a second stream beside the rest")
     p.add_argument("--spmv-reps", type=int, default=0,
                    help="extra back-to-back (hot Infinity Cache) SpMV launches, reported apart")
+    p.add_argument("--no-stream", action="store_true",
+                   help="skip the STREAM-copy probe (scripts/gpu_pmc.sh: its 1 GiB copies are no part of the step)")
     p.add_argument("--cold-reps", type=int, default=0,
                    help="extra SpMV launches after an Infinity Cache flush, reported apart")
     p.add_argument("--no-cpu", action="store_true")
@@ -697,7 +699,7 @@ def bench_newton(args, R: Ranks):
     # STREAM-copy rate of this box: device-to-device copy of 1 GiB, read +
     # write bytes / time, median of 5 -- the achievable HBM rate beside the 8 TB/s spec
     stream = None
-    if rank == 0:
+    if rank == 0 and not args.no_stream:
         a = torch.empty(1 << 27, dtype=torch.float64, device=dev)
         b = torch.empty_like(a)
         a.fill_(1.0)

@@ -14,10 +14,10 @@ done
 echo "calib ok"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/bench_$ctr -o run \
-      -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 > gpurun_out/pmc/bench_$ctr.log 2>&1 || { echo "bench $ctr failed"; exit 1; }
+      -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 --no-stream > gpurun_out/pmc/bench_$ctr.log 2>&1 || { echo "bench $ctr failed"; exit 1; }
 done
 echo "bench pmc ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/bench_trace -o run \
-    -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 > gpurun_out/pmc/bench_trace.log 2>&1 \
+    -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 --no-stream > gpurun_out/pmc/bench_trace.log 2>&1 \
     || { echo "bench trace failed"; exit 1; }
 echo "bench trace ok"

@@ -78,7 +78,7 @@ def main():
     dom = out[0]["kernel"] if out else None
     print(json.dumps({
         "tag": tag, "src_digest": src_digest(), "config": "global2",
-        "condition": ("bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0: context set-up plus one "
+        "condition": ("bench.py --steps 1 --warmup 0 --no-cpu --newton-seq 0 --no-stream: context set-up plus one "
                       "benchmark Newton step (global2 branch state), in-solve, warm caches; PMC passes "
                       "FETCH_SIZE and WRITE_SIZE in separate runs, avg_us from a kernel-trace run of the "
                       "same command"),
