@@ -189,6 +189,8 @@ struct BlockGS {
     int dyn_iters = 1;               /* defect-correction passes on the dynamics block   */
     DevBuf<double> dres, zc;         /* dynamics defect and correction (ext rows)        */
     DevBuf<double> dvh;              /* bands: U/V/W/P coefficients of the two halo rows  */
+    DevBuf<double> dvb;              /* the active cells' U/V/W/P coefficients, blocked:  */
+                                     /* [act / 64][slot][act % 64] (the defect's stream)  */
     DevBuf<double> dq, dzero, dmr;   /* MR passes: -A_DD zc, a zero vector, dot partials  */
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */

@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
                                                   const uint8_t* __restrict__ knP,
                                                   double* __restrict__ d, int64_t nloc, int nblk, int64_t ps,
                                                   const double* __restrict__ hv, int nhb, int hs, int hn,
-                                                  const int* __restrict__ alist, int64_t nown)
+                                                  const int* __restrict__ alist, int64_t nown,
+                                                  const double* __restrict__ vb)
 {
     __shared__ double red[4][2][64];
     __shared__ int64_t us[64];
@@ -255,8 +256,9 @@ __global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __rest
         const int64_t cell = e0 + u;
         const int v0 = g == 0 ? 0 : g - 1;
         const bool on[2] = {!knP[cell + ps * v0], g > 0 && !knP[cell + ps * (v0 + 1)]};
-        const double* vp = halo ? hv + h : val + u;
-        const int64_t vs = halo ? 2 * row : nloc;
+        /* vb: the active cells' coefficients blocked per tile (h = tile 64 + c) */
+        const double* vp = halo ? hv + h : (vb ? vb + (int64_t)tile * 4096 + c : val + u);
+        const int64_t vs = halo ? 2 * row : (vb ? 64 : nloc);
         if (g == 0) dyn_partial<0, 16>(vp, z, vs, nc, on, ps, acc);
         else if (g == 1) dyn_partial<16, 32>(vp, z, vs, nc, on, ps, acc);
         else if (g == 2) dyn_partial<32, 48>(vp, z, vs, nc, on, ps, acc);
@@ -289,7 +291,8 @@ int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_
     const unsigned grid = 8u * (unsigned)((nblk + nhb + 7) / 8);
     hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, knP, d,
                        c->nloc, nblk, (int64_t)c->next, hv ? gs.dvh.p : nullptr, nhb,
-                       hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0, al ? gs.act.p : nullptr, nown);
+                       hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0, al ? gs.act.p : nullptr, nown,
+                       al && gs.dvb.p ? gs.dvb.p : nullptr);
     return 0;
 }
 

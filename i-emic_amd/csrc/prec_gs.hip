@@ -3223,6 +3223,16 @@ static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool si
     return 0;
 }
 
+/* dvb[(h / 64) 4096 + s 64 + h % 64] = val[s nloc + act[h]] (0 past the last active cell) */
+__global__ void k_dyn_pack(const double* __restrict__ val, const int* __restrict__ act, int64_t nact,
+                           int64_t nloc, double* __restrict__ dvb, int64_t n)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t blk = t >> 12, s = (t >> 6) & 63, l = t & 63, h = blk * 64 + l;
+    dvb[t] = h < nact ? val[s * nloc + act[h]] : 0.0;
+}
+
 /* latitude bands: the U/V/W/P rows' coefficients (slots 0 .. 63) of the two halo rows, from
  * the neighbour bands' first / last owned row (BlockGS::dvh: slot-major, the south row's
  * cells, then the north row's) */
@@ -3359,6 +3369,17 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
         if ((rc = halo_exchange_w(c, gs.gslot.p, GSL, 1))) return rc;
     }
     if (c->nranks > 1 && c->npx == 1 && (rc = dyn_halo_coefs(c))) return rc;
+    if (gs.nact > 0 && gs.act.p) {
+        /* the defect's coefficient stream: the active cells' 64 U/V/W/P slots, blocked per
+         * 64 active cells, so a workgroup reads one contiguous 32 KB run and no land lines */
+        const int64_t nb = (gs.nact + 63) / 64;
+        if (gs.dvb.n < (size_t)(nb * 64 * 64)) {
+            if (gs.dvb.alloc((size_t)(nb * 64 * 64))) return IEMIC_ENOMEM;
+        }
+        hipLaunchKernelGGL(k_dyn_pack, dim3(blocks_for(nb * 64 * 64)), dim3(256), 0, c->stream, c->d_val.p,
+                           (const int*)gs.act.p, gs.nact, c->nloc, gs.dvb.p, nb * 64 * 64);
+        HIP_OK(hipGetLastError());
+    }
     if (c->l <= 64) {
         /* the Schur right-hand side as a linear form in rr (k_gs_ptil_rcol) */
         const int64_t ncolb = c->nloc / c->l;
