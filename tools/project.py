@@ -50,7 +50,10 @@ def main():
     hdr = " | ".join(f"t_b {b} / t_ar {a} us" for b, a in lat)
     print(f"| N | FGMRES steps | kernels us / step | batches / step | all-reduces / step | {hdr} |")
     print("|---|---|---|---|---|" + "---|" * len(lat))
-    scale = newton_ms / (t1 * steps / 1e3 + setup_ms)       # traced -> untraced
+    # traced -> untraced, on the one-GPU run's FGMRES steps (the trace may hold several
+    # Newton steps: `steps` counts all of its FGMRES steps)
+    it1 = next((it for N, it, _, _ in runs if N == 1), steps)
+    scale = newton_ms / (t1 * it1 / 1e3 + setup_ms)
     for N, it, nb, nar in runs:
         kern = 0.0
         for k, v in step.items():
