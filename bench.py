@@ -123,7 +123,7 @@ def parse():
     p.add_argument("--save-x1", default=None,
                    help="write the state after the last timed Newton step (gathered from all ranks) "
                         "and the starting state to this .npz (rank 0), for parity checks")
-    p.add_argument("--cpu-samples", type=int, default=5,
+    p.add_argument("--cpu-samples", type=int, default=10,
                    help="timed CPU Newton steps (the line reports their median and spread)")
     p.add_argument("--cpu-warmup", type=int, default=2,
                    help="untimed CPU Newton steps before the timed ones (SURVEY §8d: 2)")
@@ -133,21 +133,57 @@ def parse():
     p.add_argument("--ds", type=float, default=0.1, help="continuation step size (--mode continuation)")
     p.add_argument("--cont-tol", type=float, default=1e-4,
                    help="FGMRES tolerance of the continuation's solves (run/ocean solver_params.xml: 1e-4)")
+    p.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
     p.add_argument("--cpu-iters", type=int, default=8,
                    help="FGMRES iterations of the bounded CPU sample (--mode continuation)")
     return p.parse_args()
 
 
 def cpu_baseline(cfg, L, x, args):
+    """The CPU baseline of the Newton line (cpu_baseline_run), in a child process started
+    after the GPU work: a fresh interpreter that loads numpy and the oracle only (no torch, no
+    HIP), so its OpenMP runtime starts with the binding below and no other thread pool shares
+    the cores.  OMP_PROC_BIND=close, OMP_PLACES=cores (unless the caller set them): one thread
+    per core of the process's affinity mask, pinned for the whole run."""
+    import subprocess
+    import tempfile
+    env = dict(os.environ)
+    env.setdefault("OMP_PROC_BIND", "close")
+    env.setdefault("OMP_PLACES", "cores")
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "state.npz")
+        np.savez(path, x=x, L=L)
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", path, "--config", args.config,
+               "--mixing", str(args.mixing), "--tol", repr(args.tol), "--krylov", str(args.krylov),
+               "--restarts", str(args.restarts), "--ts-sweeps", str(args.ts_sweeps),
+               "--dyn-iters", str(args.dyn_iters), "--dyn-omega", repr(args.dyn_omega),
+               "--ts-mg", str(args.ts_mg), "--ts-at", str(args.ts_at),
+               "--cpu-samples", str(args.cpu_samples), "--cpu-warmup", str(args.cpu_warmup)]
+        out = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, check=True, text=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def cpu_baseline_child(args):
+    """bench.py --cpu-child <npz>: the CPU baseline process (cpu_baseline)"""
+    from iemic import config as cf
+    cfg = cf.preset(args.config, mixing=args.mixing)
+    with np.load(args.cpu_child, allow_pickle=False) as d:
+        x, L = d["x"], d["L"]
+    print(json.dumps(cpu_baseline_run(cfg, L, x, args)), flush=True)
+
+
+def cpu_baseline_run(cfg, L, x, args):
     """The oracle port timed on the host cores for one full Newton step of the same
     workload with the same algorithm: F and J assembly, the block Gauss-Seidel set-up (4
     damped defect-correction passes on the dynamics block, one T/S aggregation-multigrid
     V-cycle with z-line smoothing: oracle/prec_oracle.c, the GPU apply's CPU twin; Schur by
     band LU), FGMRES(krylov) with restarts to the same tolerance (CGS2), x += dx, new F.
-    args.cpu_warmup untimed steps, then args.cpu_samples timed steps; the value is their
-    median (10 after 2 warm-ups; 5 keep the default line within minutes)."""
+    args.cpu_warmup untimed steps, then args.cpu_samples timed steps (10 after 2
+    warm-ups); the value is their median."""
     from oracle import oracle as orc
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    bind = f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}, OMP_PLACES={os.environ.get('OMP_PLACES', 'unset')}"
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
     samples = []
     nwarm = max(0, args.cpu_warmup)
@@ -176,11 +212,11 @@ def cpu_baseline(cfg, L, x, args):
     return {
         "value": round(med, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
         "samples_ms": [round(v, 1) for v in ms], "spread_ms": round(ms[-1] - ms[0], 1),
-        "warmup": nwarm,
+        "spread_frac": round((ms[-1] - ms[0]) / med, 4), "warmup": nwarm,
+        "binding": bind, "affinity_cpus": aff,
         "sample": (f"median of {len(ms)} timed full Newton steps after {nwarm} untimed warm-up steps "
-                   f"(SURVEY §8d asks for 10 after 2 warm-ups; {len(ms)} keep the line within minutes) "
-                   f"on the oracle C port "
-                   f"(OpenMP {cores} threads), same state and algorithm; last: F {t_rhs*1e3:.0f} ms, "
+                   f"on the oracle C port (OpenMP {cores} threads, {bind}; a child process without "
+                   f"torch), same state and algorithm; last: F {t_rhs*1e3:.0f} ms, "
                    f"J {t_jac*1e3:.0f} ms, block GS set-up {t_prec*1e3:.0f} ms (dyn x{args.dyn_iters}, "
                    f"T/S multigrid x{args.ts_mg}), FGMRES({args.krylov}) {its} iterations to {rel:.1e} "
                    f"in {t_solve:.1f} s"),
@@ -564,6 +600,9 @@ def launch(args) -> int:
 
 def main():
     args = parse()
+    if args.cpu_child:
+        cpu_baseline_child(args)
+        return
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         sys.exit(launch(args))
@@ -657,8 +696,9 @@ def bench_newton(args, R: Ranks):
     nown = lay["own_rows"]
     bsp = spmv_bytes(nnz, nown)
     achieved = bsp / (spmv_ms * 1e-3) / 1e9
-    # the in-solve SpMV (k_spmv7<true>) reads the coefficients of the active cells only and
-    # writes their rows (FGMRES's compressed basis); x is read whole: its stencil-ELL minimum
+    # the in-solve SpMV (k_spmv7c) reads the coefficients of the active cells only (packed per
+    # Jacobian, BlockGS::spc) and writes their rows (FGMRES's compressed basis); x is read
+    # whole: its stencil-ELL minimum
     nact = oc.active_cells() if args.solver == "FGMRES" and args.orth == "DCGS2" and args.prec == 2 else 0
     ell = (8 * 104 * nact + 8 * nown + 8 * 6 * nact) if nact else stencil_ell_bytes(nown // 6, 104, nown)
     extra = {}
@@ -678,7 +718,7 @@ def bench_newton(args, R: Ranks):
     tab, why = pmc_table(args.config) if world == 1 else (None, "one GPU only")
     if tab:
         ks = {r["kernel"]: r for r in tab["kernels"]}
-        for kn in ("k_spmv7<true>", "k_spmv7<false>", "k_spmv7"):
+        for kn in ("k_spmv7c", "k_spmv7<true>", "k_spmv7"):
             if kn in ks:
                 traffic = ks[kn]["hbm_bytes_per_launch"]
                 trace_us = ks[kn]["avg_us"]
@@ -769,10 +809,11 @@ def bench_newton(args, R: Ranks):
                      "achieved_csr": round(achieved, 1), "frac_csr": round(achieved / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes": bsp, "stencil_ell_bytes": ell, "active_cells": nact,
                      "ell_gbps": round(ell / (spmv_ms * 1e-3) / 1e9, 1),
-                     # launch_us: HIP events on the library stream around every in-solve SpMV
-                     # kernel (each interval includes the dispatch and completion latency of
-                     # the event pair); trace_us: the rocprofv3 kernel-trace average of the
-                     # same kernel in the same command (bench_data/pmc_<tag>.json)
+                     # launch_us: HIP events of every in-solve SpMV launch of the timed steps,
+                     # recorded by the dispatch itself (hipExtLaunchKernelGGL start / stop
+                     # events on the library stream: the kernel's own begin and end);
+                     # trace_us: the rocprofv3 kernel-trace average of the same kernel in the
+                     # same command (bench_data/pmc_<tag>.json)
                      "launch_us": round(spmv_ms * 1e3, 2), "launches": n_sp, "trace_us": trace_us,
                      "step": step_rf, "dominant": dom_rf, **({"table": why} if why else {}), **extra},
         "cpu_baseline": None,

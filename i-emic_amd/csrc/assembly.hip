@@ -12,6 +12,7 @@
  */
 #include <cmath>
 #include <vector>
+#include <utility>
 
 #include "common.h"
 
@@ -214,6 +215,18 @@ int assemble_jacobian(iemic_ctx* c, const double* x_dev)
 {
     int rc = mix_control(c, x_dev);
     if (rc) return rc;
+    BlockGS& gs = c->gs;
+    if (gs.ready && gs.kind == 2) {
+        /* the block GS reads its set-up Jacobian (BlockGS::vp): assemble into the other buffer */
+        if (gs.vp == c->d_val.p) {
+            if (gs.vold.n != c->d_val.n && gs.vold.alloc(c->d_val.n)) {
+                set_error("assemble_jacobian: out of device memory for the second Jacobian buffer");
+                return IEMIC_ENOMEM;
+            }
+            std::swap(c->d_val, gs.vold);
+        }
+        gs.coef_stale = 1;
+    }
     Geo g = c->geo();
     dim3 blk(128), grd((unsigned)((c->nloc + 127) / 128), NUN);
     hipLaunchKernelGGL(k_jacobian, grd, blk, 0, c->stream, g, x_dev, c->d_val.p, c->nloc,

@@ -10,9 +10,14 @@
  * libm the reference uses, so every per-cell expression evaluated on the device is
  * bit-identical to the reference; all per-cell and per-row work runs on the GPU.
  */
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -26,6 +31,47 @@ void set_error(const std::string& s) { g_err = s; }
 using namespace iemic;
 
 extern "C" const char* iemic_last_error(void) { return g_err.c_str(); }
+
+/* Fatal-signal trace: on SIGSEGV / SIGBUS / SIGILL / SIGFPE the library writes the native
+ * backtrace of the faulting thread to stderr (backtrace_symbols_fd: no allocation), then
+ * restores the handler that was installed before (Python's faulthandler, a profiler's, or the
+ * default) and lets the fault recur into it, so the process still ends as it would have.
+ * Installed once, at the first context creation; IEMIC_SEGV_TRACE=0 leaves the handlers alone. */
+namespace {
+constexpr int kTraceSigs[4] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE};
+struct sigaction g_prev_act[4];
+
+void fatal_trace(int sig, siginfo_t* si, void*)
+{
+    static const char hdr[] = "\niemic: fatal signal in the process; native backtrace of the faulting thread:\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, n, 2);
+    for (int q = 0; q < 4; q++)
+        if (kTraceSigs[q] == sig) sigaction(sig, &g_prev_act[q], nullptr);
+    /* a fault raised by the hardware recurs when the instruction is re-executed on return;
+     * a signal sent by a process is re-sent */
+    if (!si || si->si_code <= 0) raise(sig);
+}
+
+void install_fatal_trace()
+{
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* e = std::getenv("IEMIC_SEGV_TRACE");
+        if (e && e[0] == '0') return;
+        void* warm[2];
+        (void)backtrace(warm, 2);            /* loads the unwinder outside any handler */
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof(sa));
+        sa.sa_sigaction = fatal_trace;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigemptyset(&sa.sa_mask);
+        for (int q = 0; q < 4; q++) sigaction(kTraceSigs[q], &sa, &g_prev_act[q]);
+    });
+}
+}  // namespace
 
 extern "C" int iemic_abi_version(void) { return IEMIC_ABI_VERSION; }
 
@@ -49,6 +95,7 @@ iemic_ctx::~iemic_ctx()
     if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
     stream = side = nullptr;
+    if (group) iemic::local_group_leave(this);   /* the group outlives its last context */
     /* device buffers are members: released after this body, with the stream drained */
 }
 
@@ -197,6 +244,7 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
 {
     if (!out || !grid || !landm) return IEMIC_EINVAL;
     *out = nullptr;
+    install_fatal_trace();
     int ndev = iemic_device_count();
     if (ndev <= 0) {
         set_error("iemic_create: no HIP device available (the library never runs on the CPU)");

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "common.h"
+#include "local_group.h"
 
 namespace iemic {
 
@@ -35,50 +36,7 @@ namespace iemic {
         }                                                                                \
     } while (0)
 
-/* ---- in-process group (test facility) ------------------------------------------------
- * Several band contexts of one problem in one process (one host thread each, e.g. on one
- * GPU, where RCCL refuses duplicate devices): collectives are host-staged through a shared
- * object with a reusable barrier.  Sums are taken in rank order, so results do not depend
- * on thread timing. */
-struct LocalGroup {
-    int P;
-    std::mutex mu;
-    std::condition_variable cv;
-    int arrived = 0, generation = 0;
-    std::vector<std::vector<double>> slot;
-    std::vector<double*> vec;
-    std::vector<iemic_ctx*> ctxs;
-    /* point-to-point mailbox: (src, dst, k) -> the k-th message src sent to dst in a batch */
-    std::map<std::tuple<int, int, int>, std::vector<double>> box;
-    explicit LocalGroup(int p) : P(p), slot(p), vec(p, nullptr), ctxs(p, nullptr) {}
-    /* false when the other ranks did not all arrive within timeout_s (the caller withdraws
-     * and reports; the group is unusable afterwards, as a communicator after an abort) */
-    bool barrier(double timeout_s)
-    {
-        std::unique_lock<std::mutex> lk(mu);
-        const int gen = generation;
-        if (++arrived == P) {
-            arrived = 0;
-            generation++;
-            cv.notify_all();
-            return true;
-        }
-        if (cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return generation != gen; }))
-            return true;
-        arrived--;
-        return false;
-    }
-};
-
-static int group_barrier(iemic_ctx* c, LocalGroup* g, const char* what)
-{
-    if (g->barrier(c->comm_timeout_s)) return 0;
-    set_error(std::string("rank group: ") + what + " on rank " + std::to_string(c->rank) +
-              ": the other ranks did not arrive within " + std::to_string(c->comm_timeout_s) +
-              " s (a rank skipped the collective or its exchange plan differs)");
-    return IEMIC_EDEVICE;
-}
-
+/* ---- in-process group (test facility; local_group.h) ------------------------------- */
 static int host_allreduce(iemic_ctx* c, double* dev, int count)
 {
     std::vector<double> h(count);
@@ -94,31 +52,42 @@ static int host_allreduce(iemic_ctx* c, double* dev, int count)
 static int local_allreduce(iemic_ctx* c, double* dev, int count)
 {
     LocalGroup* g = (LocalGroup*)c->group;
-    auto& mine = g->slot[c->rank];
-    mine.resize(count);
-    int rc = d2h(c, mine.data(), dev, sizeof(double) * count);
+    std::vector<double> h(count);
+    int rc = d2h(c, h.data(), dev, sizeof(double) * count);
     if (rc) return rc;
-    if ((rc = group_barrier(c, g, "all-reduce"))) return rc;
-    std::vector<double> sum(count, 0.0);
-    for (int r = 0; r < g->P; r++) {
-        if (g->slot[r].size() != (size_t)count) {
-            set_error("rank group: all-reduce of " + std::to_string(count) + " doubles on rank " +
-                      std::to_string(c->rank) + ", " + std::to_string(g->slot[r].size()) + " on rank " +
-                      std::to_string(r));
-            return IEMIC_EINVAL;
-        }
-        for (int q = 0; q < count; q++) sum[q] += g->slot[r][q];
+    std::string err;
+    if (g->sum(c->rank, h.data(), h.data(), count, c->comm_timeout_s, err)) {
+        set_error(err);
+        return err.find("did not arrive") != std::string::npos ? IEMIC_EDEVICE : IEMIC_EINVAL;
     }
-    if ((rc = group_barrier(c, g, "all-reduce"))) return rc;
-    return h2d(c, dev, sum.data(), sizeof(double) * count);
+    return h2d(c, dev, h.data(), sizeof(double) * count);
+}
+
+static int group_barrier(iemic_ctx* c, LocalGroup* g, const char* what)
+{
+    if (g->barrier(c->comm_timeout_s)) return 0;
+    std::string err;
+    LocalGroup::timed_out(err, what, c->rank, c->comm_timeout_s);
+    set_error(err);
+    return IEMIC_EDEVICE;
 }
 
 void* local_group_new(int nranks) { return nranks > 0 ? new LocalGroup(nranks) : nullptr; }
-void local_group_free(void* g) { delete (LocalGroup*)g; }
+/* the owner gives the group up; it is deleted now, or by the last context still attached */
+void local_group_free(void* g)
+{
+    if (g && ((LocalGroup*)g)->release()) delete (LocalGroup*)g;
+}
 void local_group_join(iemic_ctx* c, void* g)
 {
     c->group = g;
-    ((LocalGroup*)g)->ctxs[c->rank] = c;
+    ((LocalGroup*)g)->attach(c->rank);
+}
+void local_group_leave(iemic_ctx* c)
+{
+    LocalGroup* g = (LocalGroup*)c->group;
+    c->group = nullptr;
+    if (g && g->detach(c->rank)) delete g;
 }
 
 int comm_unique_id(unsigned char* id128)
@@ -301,30 +270,27 @@ static int run_local(iemic_ctx* c, const std::vector<Msg>& ops)
         std::vector<double> h(seg_count(op.s));
         HIP_OK(hipMemcpyAsync(h.data(), buf[q], sizeof(double) * h.size(), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
-        std::lock_guard<std::mutex> lk(g->mu);
-        g->box[std::make_tuple(c->rank, op.peer, ksend[op.peer]++)] = std::move(h);
+        g->post(c->rank, op.peer, ksend[op.peer]++, std::move(h));
     }
     if ((rc = group_barrier(c, g, "halo batch"))) return rc;
-    for (size_t q = 0; q < ops.size(); q++) {
+    bool ok = true;
+    for (size_t q = 0; q < ops.size() && ok; q++) {
         const Msg& op = ops[q];
         if (op.send) continue;
         std::vector<double> h;
-        {
-            std::lock_guard<std::mutex> lk(g->mu);
-            auto it = g->box.find(std::make_tuple(op.peer, c->rank, krecv[op.peer]++));
-            if (it == g->box.end() || it->second.size() != seg_count(op.s)) {
-                set_error("rank group: unmatched receive");
-                return IEMIC_EINVAL;
-            }
-            h = std::move(it->second);
-            g->box.erase(it);
-        }
+        if (!(ok = g->take(op.peer, c->rank, krecv[op.peer]++, seg_count(op.s), h))) break;
         HIP_OK(hipMemcpyAsync(buf[q], h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
     }
-    if ((rc = unstage_recvs(c, ops, buf))) return rc;
+    if (ok && (rc = unstage_recvs(c, ops, buf))) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
-    return group_barrier(c, g, "halo batch");
+    /* the second meeting also after an unmatched receive, so the peers are not left waiting */
+    if ((rc = group_barrier(c, g, "halo batch"))) return rc;
+    if (!ok) {
+        set_error("rank group: unmatched receive on rank " + std::to_string(c->rank));
+        return IEMIC_EINVAL;
+    }
+    return 0;
 }
 
 /* the caller's host transport: all sends (staged), all receives, wait, unpack */

@@ -240,6 +240,25 @@ struct BlockGS {
     DevBuf<uint8_t> actf;            /* per owned cell: 1 active (k_cell_active)           */
     int64_t nact = 0;
     std::vector<uint8_t> act_h;      /* the per-cell flags the list was built from        */
+    /* the compressed SpMV (krylov.hip k_spmv7c): the active cells' 104 coefficients packed
+     * slot-major over the active list (row stride spc_ld = nact rounded up to 16 cells, so
+     * no coefficient line holds a land cell), and the grid tiles that hold an active cell
+     * (4 ints each: tile, first and last active lane, 0) */
+    DevBuf<double> spc;
+    int64_t spc_ld = 0;
+    DevBuf<int> atl;
+    int natile = 0;
+    /* the Jacobian the apply reads: the set-up one (prec_gs.hip gs_refresh).  A Jacobian
+     * assembled while the block GS is set up goes into the other buffer (assemble_jacobian
+     * swaps iemic_ctx::d_val with vold), so the preconditioner stays the operator of its
+     * set-up Jacobian on every rank, as the reference's extracted blocks do */
+    const double* vp = nullptr;
+    DevBuf<double> vold;
+    /* a Jacobian was assembled since the set-up: the compressed SpMV's stream spc and the
+     * identity-row check are redone before the next apply or solve (gs_refresh) */
+    int coef_stale = 0;
+    int cmp_ok = 0;                  /* the active list matches the Jacobian's identity rows */
+    DevBuf<double> chk;              /* gs_refresh: identity-row mismatches (1 double)     */
 };
 
 struct Krylov {
@@ -405,6 +424,7 @@ int comm_unique_id(unsigned char* id128);
 void* local_group_new(int nranks);
 void local_group_free(void* g);
 void local_group_join(iemic_ctx* c, void* g);
+void local_group_leave(iemic_ctx* c);
 void comm_destroy(iemic_ctx* c);
 
 /* assembly.hip */
@@ -429,8 +449,10 @@ int prec_compute(iemic_ctx* c, const iemic_krylov* opt);
 int prec_apply(iemic_ctx* c, const double* r, double* z);
 /* the block GS apply from a compressed input (6 rows per BlockGS::act cell, zero land rows) */
 int gs_apply_c(iemic_ctx* c, const double* rc, double* z);
+/* repack the block GS's coefficient copies after a new Jacobian (BlockGS::coef_stale) */
+int gs_refresh(iemic_ctx* c);
 /* y = J x written compressed (rows of the active cells only; x full, halo current) */
-int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t after = nullptr);
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 }  // namespace iemic
 
 #endif

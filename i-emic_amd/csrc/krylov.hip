@@ -19,6 +19,8 @@
 #include <chrono>
 #include <cmath>
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 
 namespace iemic {
@@ -64,18 +66,13 @@ __device__ __forceinline__ void sp7_compute(const double* v, const double* xs, i
         acc[sp7_row(s) - sp7_row(S0)] += v[s - S0] * xs[(q * (SP7_T + 2) + (c + 1 + sl.di)) * NUN + sl.var];
     }
 }
-/* CMP (FGMRES's compressed basis): y holds the rows of the active cells only (cmap: owned
- * cell -> its index, -1 for land); land cells load no coefficients and a tile without an
- * active cell exits before staging anything */
-template <bool CMP>
+/* the full SpMV (FGMRES's compressed basis uses k_spmv7c below) */
 __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restrict__ val,
                                                const double* __restrict__ x,
-                                               double* __restrict__ y, int nloc, int ntile, int tpr,
-                                               const int* __restrict__ cmap)
+                                               double* __restrict__ y, int nloc, int ntile, int tpr)
 {
     __shared__ double xs[6 * (SP7_T + 2) * NUN];
     __shared__ double red[4][3][SP7_T];
-    __shared__ int cms[SP7_T];
     const int l = X.l, nx = X.nx;
     const int per = (ntile + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -86,13 +83,7 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
     const int lc0 = row * nx + i0;
     const int t = threadIdx.x, c = t & 63;
     const int g = __builtin_amdgcn_readfirstlane(t >> 6);   /* wave-uniform: scalar branches */
-    int cm = 0;
-    if (CMP) {
-        cm = c < nc ? cmap[lc0 + c] : -1;
-        if (g == 0) cms[c] = cm;
-        if (!__syncthreads_or(cm >= 0)) return;     /* a land tile */
-    }
-    const bool act = c < nc && (!CMP || cm >= 0);
+    const bool act = c < nc;
     const int64_t lc = lc0 + c;
     double acc[3] = {0.0, 0.0, 0.0};
     double v[26];
@@ -154,11 +145,111 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
         case 4: v = red[2][2][cc] + red[3][0][cc]; break;
         default: v = red[3][1][cc]; break;
         }
-        if (!CMP) y[NUN * ((int64_t)HALO * l * nx + lc0) + o] = v;
-        else if (cms[cc] >= 0) y[(int64_t)NUN * cms[cc] + R] = v;
+        y[NUN * ((int64_t)HALO * l * nx + lc0) + o] = v;
     }
 }
 
+/* k_spmv7c: the in-solve SpMV of FGMRES's compressed basis (round 6).  k_spmv7<true> read the
+ * slot-major Jacobian and skipped land lanes, but a 128-byte coefficient line holds 16 cells,
+ * so the lines of mixed land / water runs were fetched whole: 128.9 MB of coefficient lines
+ * for 100.7 MB of active coefficients at 2 degrees (147 MB of counter bytes per launch, 1.25x).
+ * Here the coefficients come from BlockGS::spc, the active cells' 104 slots packed slot-major
+ * over the active list (row stride ld), so the active lanes of a tile read one contiguous
+ * run per slot that no land cell shares.  Only the tiles that hold an active cell are
+ * launched (BlockGS::atl, dealt to the 8 XCDs in contiguous runs), and x is staged only over
+ * the columns the tile's active cells reach (first active lane - 1 .. last + 1). */
+__global__ void __launch_bounds__(256) k_spmv7c(SubLay X, const double* __restrict__ spc, int64_t ld,
+                                                const double* __restrict__ x, double* __restrict__ y,
+                                                const int4* __restrict__ atl, int natile, int tpr,
+                                                const int* __restrict__ cmap)
+{
+    __shared__ double xs[6 * (SP7_T + 2) * NUN];
+    __shared__ double red[4][3][SP7_T];
+    __shared__ int cms[SP7_T], lof[SP7_T];
+    const int l = X.l, nx = X.nx;
+    const int per = (natile + 7) >> 3;
+    const int pos = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (pos >= natile) return;
+    const int4 td = atl[pos];
+    const int tile = td.x, clo = td.y, chi = td.z;
+    const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
+    const int k = row % l, jl = row / l, j = X.jb0 + jl;
+    const int nc = min(SP7_T, nx - i0);
+    const int lc0 = row * nx + i0;
+    const int t = threadIdx.x, c = t & 63;
+    const int g = __builtin_amdgcn_readfirstlane(t >> 6);   /* wave-uniform: scalar branches */
+    const int cm = (c >= clo && c <= chi) ? cmap[lc0 + c] : -1;
+    const int a0 = cmap[lc0 + clo];                          /* the tile's first active cell */
+    const bool act = cm >= 0;
+    if (g == 0) {
+        cms[c] = cm;
+        if (act) lof[cm - a0] = c;                           /* active cell -> its lane */
+    }
+    double acc[3] = {0.0, 0.0, 0.0};
+    double v[26];
+    /* coefficient loads, then the staging loads, all issued before the first LDS store */
+    if (g == 0) sp7_load<0, 26>(spc, ld, cm, act, v);
+    else if (g == 1) sp7_load<26, 52>(spc, ld, cm, act, v);
+    else if (g == 2) sp7_load<52, 78>(spc, ld, cm, act, v);
+    else sp7_load<78, 104>(spc, ld, cm, act, v);
+    {
+        const int jm = j > 0 ? j - 1 : j, jp = j < X.m - 1 ? j + 1 : j;
+        const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
+        const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
+        constexpr int PR = (SP7_T + 2) * NUN;
+        constexpr int SPT = (6 * PR + 255) / 256;
+        /* staged cells p = clo .. chi + 2 (cell i0 + p - 1) of each grid row */
+        const int wlo = clo * NUN, whi = (chi + 3) * NUN;
+        double xv[SPT];
+        int xo[SPT];
+#pragma unroll
+        for (int u = 0; u < SPT; u++) {
+            const int e = t + 256 * u;
+            const int q = e / PR, w = e - q * PR;
+            xo[u] = -1;
+            if (e < 6 * PR && w >= wlo && w < whi) {
+                const int p = w / NUN, var = w - p * NUN;
+                const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
+                const int64_t cell = (p == 0 || p == nc + 1)
+                                         ? xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb)
+                                         : r * nx + i0 + p - 1;
+                xo[u] = e;
+                xv[u] = x[NUN * cell + var];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SPT; u++)
+            if (xo[u] >= 0) xs[xo[u]] = xv[u];
+    }
+    __syncthreads();
+    if (act) {
+        if (g == 0) sp7_compute<0, 26>(v, xs, c, acc);
+        else if (g == 1) sp7_compute<26, 52>(v, xs, c, acc);
+        else if (g == 2) sp7_compute<52, 78>(v, xs, c, acc);
+        else sp7_compute<78, 104>(v, xs, c, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) red[g][q][c] = acc[q];
+    __syncthreads();
+    /* rows of the groups: g0 {U,V} g1 {V,W} g2 {W,P,T} g3 {T,S}; the tile's active cells are
+     * consecutive in the compressed vector, so its rows [6 cm(clo), 6 cm(chi) + 6) are one
+     * contiguous run: thread o writes entry o of it */
+    const int na = cms[chi] - a0 + 1;
+    for (int o = t; o < na * NUN; o += 256) {
+        const int ac = o / NUN, R = o - ac * NUN;
+        const int cc = lof[ac];
+        double vv;
+        switch (R) {
+        case 0: vv = red[0][0][cc]; break;
+        case 1: vv = red[0][1][cc] + red[1][0][cc]; break;
+        case 2: vv = red[1][1][cc] + red[2][0][cc]; break;
+        case 3: vv = red[2][1][cc]; break;
+        case 4: vv = red[2][2][cc] + red[3][0][cc]; break;
+        default: vv = red[3][1][cc]; break;
+        }
+        y[(int64_t)NUN * a0 + o] = vv;
+    }
+}
 
 /* Dynamics defect of the block GS (prec_gs.hip): d = rr - A z on the active U/V/W/P rows,
  * 0 on the others.  z is the pass iterate, 0 on the identity rows (whose couplings are in
@@ -289,7 +380,7 @@ int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_
     const bool hv = halo && gs.dvh.p;
     const int nhb = hv ? (int)((2 * row + 63) / 64) : 0;
     const unsigned grid = 8u * (unsigned)((nblk + nhb + 7) / 8);
-    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), c->d_val.p, z, r, knP, d,
+    hipLaunchKernelGGL(k_spmv_dyn, dim3(grid), dim3(256), 0, c->stream, sub_lay(c), gs.vp, z, r, knP, d,
                        c->nloc, nblk, (int64_t)c->next, hv ? gs.dvh.p : nullptr, nhb,
                        hv && c->nb[2] >= 0 ? 1 : 0, hv && c->nb[3] >= 0 ? 1 : 0, al ? gs.act.p : nullptr, nown,
                        al && gs.dvb.p ? gs.dvb.p : nullptr);
@@ -717,8 +808,8 @@ int spmv_kernel(iemic_ctx* c, const double* x, double* y)
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
     const int ntile = (int)(c->nloc / c->nx) * tpr;
     const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-    hipLaunchKernelGGL(k_spmv7<false>, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, y, (int)c->nloc, ntile,
-                       tpr, (const int*)nullptr);
+    hipLaunchKernelGGL(k_spmv7, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, y, (int)c->nloc, ntile,
+                       tpr);
     return spmv_intcond(c, x, c->rowintcon >= 0 ? y + c->rowintcon : nullptr);
 }
 
@@ -744,21 +835,22 @@ static int spmv_intcond(iemic_ctx* c, const double* x, double* yr)
     return 0;
 }
 
-/* after: recorded right after the SpMV kernel, before the integral-condition row's
- * reduction launches (FGMRES times the SpMV kernel alone with it) */
-int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t after)
+/* ev0 / ev1 (optional): the kernel's own start and end (hipExtLaunchKernelGGL records them
+ * from the dispatch itself, so FGMRES times the SpMV kernel alone, as the trace does) */
+int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t ev0, hipEvent_t ev1)
 {
-    if (!c->jac_valid || !c->gs.cmap.p) {
-        set_error("spmv: no Jacobian or no active-cell map");
+    const BlockGS& gs = c->gs;
+    if (!c->jac_valid || !gs.cmap.p || !gs.spc.p || !gs.atl.p || gs.coef_stale) {
+        set_error("spmv: no Jacobian, no active-cell map or stale packed coefficients");
         return IEMIC_ESTATE;
     }
     hipStream_t s = c->stream;
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
-    const int ntile = (int)(c->nloc / c->nx) * tpr;
-    const unsigned grid = 8u * (unsigned)((ntile + 7) / 8);
-    hipLaunchKernelGGL(k_spmv7<true>, dim3(grid), dim3(256), 0, s, sub_lay(c), c->d_val.p, x, yc, (int)c->nloc,
-                       ntile, tpr, (const int*)c->gs.cmap.p);
-    if (after) HIP_OK(hipEventRecord(after, s));
+    const unsigned grid = 8u * (unsigned)((gs.natile + 7) / 8);
+    if (gs.natile > 0)
+        hipExtLaunchKernelGGL(k_spmv7c, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c),
+                              (const double*)gs.spc.p, gs.spc_ld, x, yc, (const int4*)gs.atl.p, gs.natile, tpr,
+                              (const int*)gs.cmap.p);
     double* yr = nullptr;
     if (c->rowintcon >= 0) {
         if (c->gs.ric < 0) {
@@ -950,9 +1042,12 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
      * cells.  A right-hand side with identity-row entries is first reduced: x_k = b_k,
      * b' = b - J t (t = b on the identity rows), zero on them. */
     const BlockGS& gs = c->gs;
-    const bool cmp = opt->orth == 0 && opt->prec == 2 && gs.ready && gs.kind == 2 && gs.nact > 0 && gs.cmap.p;
+    int rc = opt->prec > 0 ? gs_refresh(c) : 0;
+    if (rc) return rc;
+    const bool cmp = opt->orth == 0 && opt->prec == 2 && gs.ready && gs.kind == 2 && gs.nact > 0 && gs.cmap.p &&
+                     gs.cmp_ok && gs.spc.p && gs.atl.p;
     const int64_t NC = cmp ? NUN * gs.nact : 0;
-    int rc = ensure_krylov(c, m, NC);
+    rc = ensure_krylov(c, m, NC);
     if (rc) return rc;
     iemic_solve_info inf{};
     auto T0 = std::chrono::steady_clock::now();
@@ -1135,8 +1230,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     if (cmp) {
                         /* e[1] .. e[2]: the SpMV kernel alone (bench.py's roofline.launch_us) */
                         if ((rc2 = halo_exchange(c, zj, 1))) return rc2;
-                        HIP_OK(hipEventRecord(e[1], c->stream));
-                        if ((rc2 = spmv_kernel_c(c, zj, wv, e[2]))) return rc2;
+                        if ((rc2 = spmv_kernel_c(c, zj, wv, e[1], e[2]))) return rc2;
                     } else {
                         HIP_OK(hipEventRecord(e[1], c->stream));
                         if ((rc2 = spmv(c, zj, wv - o, c->stream))) return rc2;

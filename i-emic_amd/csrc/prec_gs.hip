@@ -3175,7 +3175,7 @@ static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool si
         const TsLev V0 = mg_view(c, 0);
         const int P = mg_lanes(c->l);
         const unsigned ge = (unsigned)(((c->nx + MG_TI - 1) / MG_TI) * V0.mb);
-        MG_LAUNCH_P(P, k_mg_entry, ge, c->d_val.p, gs.knP.p, gs.kmask.p, gs.rrP.p, zd, L, V0);
+        MG_LAUNCH_P(P, k_mg_entry, ge, gs.vp, gs.knP.p, gs.kmask.p, gs.rrP.p, zd, L, V0);
         if (side) {
             HIP_OK(hipEventRecord(c->ev_fork, s));
             HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
@@ -3197,7 +3197,7 @@ static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool si
     if (ts_compact(c)) {
         /* colour-compacted symmetric red-black sweeps */
         const int nblk = (int)((c->nloc + 63) / 64);
-        hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, c->d_val.p,
+        hipLaunchKernelGGL(k_gs_bts2, dim3(8u * (unsigned)((nblk + 7) / 8)), dim3(128), 0, s, gs.vp,
                            gs.known.p, gs.kmask.p, gs.rr.p, z, gs.bc.p, gs.zt.p, gs.zs.p, L, gs.bts.p, nblk);
         const unsigned gh = (unsigned)((c->nloc / 2 + 255) / 256);
         const int seq[4] = {0, 1, 1, 0};
@@ -3208,7 +3208,7 @@ static int ts_solve(iemic_ctx* c, const double* zd, double* z, bool out, bool si
         hipLaunchKernelGGL(k_ts_scatter, dim3(gc), dim3(256), 0, s, gs.known.p, gs.zt.p, gs.zs.p, z, L);
     } else {
         /* symmetric sweeps: colours forward then backward */
-        hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.rr.p, z,
+        hipLaunchKernelGGL(k_gs_bts, dim3(gc), dim3(256), 0, s, gs.vp, gs.known.p, gs.rr.p, z,
                            gs.bts.p, L);
         const bool four = c->cfg.periodic && (n & 1);
         const int seq2[4] = {0, 1, 1, 0}, seq4[8] = {0, 1, 2, 3, 3, 2, 1, 0};
@@ -3233,6 +3233,33 @@ __global__ void k_dyn_pack(const double* __restrict__ val, const int* __restrict
     dvb[t] = h < nact ? val[s * nloc + act[h]] : 0.0;
 }
 
+/* spc[s ld + a] = val[s nloc + act[a]] (0 in the row's padding): the compressed SpMV's stream */
+__global__ void k_spmv_pack(const double* __restrict__ val, const int* __restrict__ act, int64_t nact,
+                            int64_t ld, int64_t nloc, double* __restrict__ spc)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)NSLOT * ld) return;
+    const int64_t s = t / ld, a = t - s * ld;
+    spc[t] = a < nact ? val[s * nloc + act[a]] : 0.0;
+}
+
+/* gs_refresh: *nd += 1 for every owned row whose identity flag (k_known's rule) in the
+ * current Jacobian differs from the set-up's */
+__global__ void k_known_diff(const double* __restrict__ val, Lay L, int64_t rowintcon,
+                             const uint8_t* __restrict__ known, double* __restrict__ nd)
+{
+    OWNED_CELL;
+    int diff = 0;
+    for (int r = 0; r < NUN; r++) {
+        bool id = val[(int64_t)ROW_BEGIN[r] * ncell + lc] == 1.0;
+        for (int s = ROW_BEGIN[r] + 1; id && s < ROW_BEGIN[r + 1]; s++)
+            id = val[(int64_t)s * ncell + lc] == 0.0;
+        const uint8_t k = (id && NUN * cell + r != rowintcon) ? 1 : 0;
+        diff += k != known[NUN * cell + r];
+    }
+    if (diff) atomicAdd(nd, (double)diff);
+}
+
 /* latitude bands: the U/V/W/P rows' coefficients (slots 0 .. 63) of the two halo rows, from
  * the neighbour bands' first / last owned row (BlockGS::dvh: slot-major, the south row's
  * cells, then the north row's) */
@@ -3253,6 +3280,45 @@ static int dyn_halo_coefs(iemic_ctx* c)
     if (no >= 0) y.push_back({true, no, Seg{v, nloc - row, NDS, row, nloc}});
     if (so >= 0) y.push_back({false, so, Seg{gs.dvh.p, 0, NDS, row, 2 * row}});
     return run_msgs(c, y);
+}
+
+/* The compressed SpMV's coefficient stream (k_spmv7c): the active cells' 104 slots of the
+ * current Jacobian, packed at every set-up and by gs_refresh after every later Jacobian */
+static int gs_pack_spc(iemic_ctx* c)
+{
+    BlockGS& gs = c->gs;
+    if (gs.nact <= 0 || !gs.act.p) return 0;
+    gs.spc_ld = (gs.nact + 15) / 16 * 16;
+    if (gs.spc.n < (size_t)(NSLOT * gs.spc_ld) && gs.spc.alloc((size_t)(NSLOT * gs.spc_ld))) return IEMIC_ENOMEM;
+    hipLaunchKernelGGL(k_spmv_pack, dim3(blocks_for(NSLOT * gs.spc_ld)), dim3(256), 0, c->stream, c->d_val.p,
+                       (const int*)gs.act.p, gs.nact, gs.spc_ld, c->nloc, gs.spc.p);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+/* A Jacobian assembled while the block GS is set up (Ocean::solve reuses the preconditioner
+ * until preProcess flags a rebuild, Ocean.C:790-801, 1360-1374).  The preconditioner stays the
+ * operator of the set-up Jacobian, as TRIOS::BlockPreconditioner's extracted blocks do: the
+ * assembly wrote into the second Jacobian buffer (assemble_jacobian) and the apply reads the
+ * set-up one through BlockGS::vp, together with the copies made from it (gslot, dvh, dvb).
+ * What follows the new Jacobian: the compressed SpMV's stream, and whether the set-up's land
+ * cells are still identity rows (else the compressed basis would drop live rows: summed over
+ * the ranks, so every rank takes the same branch). */
+int gs_refresh(iemic_ctx* c)
+{
+    BlockGS& gs = c->gs;
+    if (!gs.coef_stale || !gs.ready || gs.kind != 2) return 0;
+    gs.coef_stale = 0;
+    if (gs.chk.n < 1 && gs.chk.alloc(1)) return IEMIC_ENOMEM;
+    HIP_OK(hipMemsetAsync(gs.chk.p, 0, sizeof(double), c->stream));
+    hipLaunchKernelGGL(k_known_diff, dim3((unsigned)((c->nloc + 255) / 256)), dim3(256), 0, c->stream,
+                       c->d_val.p, lay_of(c), (int64_t)c->rowintcon, gs.known.p, gs.chk.p);
+    int rc = allreduce_sum(c, gs.chk.p, 1);
+    if (rc) return rc;
+    double nd = 0.0;
+    if ((rc = d2h(c, &nd, gs.chk.p, sizeof(double)))) return rc;
+    if (nd != 0.0) gs.cmp_ok = 0;
+    return gs_pack_spc(c);
 }
 
 int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
@@ -3337,6 +3403,28 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                 const int64_t cell = c->rowintcon / NUN - c->own0;
                 if (cell >= 0 && cell < c->nloc && cm[cell] >= 0) gs.ric = (int64_t)NUN * cm[cell] + c->rowintcon % NUN;
             }
+            /* the compressed SpMV's tiles (k_spmv7c): 64 cells along i of one grid row, those
+             * holding an active cell, with their first and last active lane */
+            {
+                const int nx = c->nx, tpr = (nx + 63) / 64;
+                const int64_t nrow = c->nloc / nx;
+                std::vector<int> tl;
+                for (int64_t row = 0; row < nrow; row++)
+                    for (int ti = 0; ti < tpr; ti++) {
+                        const int i0 = ti * 64, nc = std::min(64, nx - i0);
+                        int lo = -1, hi = -1;
+                        for (int cc = 0; cc < nc; cc++)
+                            if (h[row * nx + i0 + cc]) {
+                                if (lo < 0) lo = cc;
+                                hi = cc;
+                            }
+                        if (lo < 0) continue;
+                        tl.insert(tl.end(), {(int)(row * tpr + ti), lo, hi, 0});
+                    }
+                gs.natile = (int)(tl.size() / 4);
+                if (gs.atl.n < tl.size() + 4 && gs.atl.alloc(tl.size() + 4)) return IEMIC_ENOMEM;
+                if (!tl.empty() && (rc = h2d(c, gs.atl.p, tl.data(), sizeof(int) * tl.size()))) return rc;
+            }
             gs.act_h.swap(h);
             /* the defect (k_spmv_dyn) writes the active cells only: the others' rows 0 */
             for (DevBuf<double>* bptr : {&gs.dres, &gs.dq})
@@ -3380,6 +3468,11 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                            (const int*)gs.act.p, gs.nact, c->nloc, gs.dvb.p, nb * 64 * 64);
         HIP_OK(hipGetLastError());
     }
+    if ((rc = gs_pack_spc(c))) return rc;
+    /* the apply reads this Jacobian (a later one is assembled into the other buffer) */
+    gs.vp = c->d_val.p;
+    gs.coef_stale = 0;
+    gs.cmp_ok = 1;
     if (c->l <= 64) {
         /* the Schur right-hand side as a linear form in rr (k_gs_ptil_rcol) */
         const int64_t ncolb = c->nloc / c->l;
@@ -3459,13 +3552,13 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const unsigned gcth = hrow ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx + 2)) : gct;
     if (band && !rr_halo && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
     if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
                            gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
                            gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     else
-        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gcth), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
                            gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
     const double* sb = gs.colv_own.p;
@@ -3479,17 +3572,17 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const bool al = gs.act.p && gs.nact > 0;
     const int64_t nown = al ? gs.nact : c->nloc;
     const unsigned gcu = (unsigned)((nown + (hrow ? (int64_t)c->l * c->nx : 0) + 255) / 256);
-    hipLaunchKernelGGL(k_gs_uvp, dim3(gcu), dim3(256), 0, s, c->d_val.p, gs.knP.p, gs.uvinv.p,
+    hipLaunchKernelGGL(k_gs_uvp, dim3(gcu), dim3(256), 0, s, gs.vp, gs.knP.p, gs.uvinv.p,
                        rr, gs.colvT.p, z, L, zo, omega, zaos, gsl, al ? gs.act.p : nullptr, nown);
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
     if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
                            gs.colvT.p, z, L, rr, zo, omega, zaos);
     else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
                            gs.colvT.p, z, L, rr, zo, omega, zaos);
     else
-        hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, c->d_val.p, gs.knP.p,
+        hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
                            gs.colvT.p, z, L, rr, zo, omega, zaos);
     return 0;
 }
@@ -3559,7 +3652,8 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
     const bool band = c->nranks > 1;
     const int64_t ps = c->next;
     double* zP = gs.zP.p;
-    int rc = 0;
+    int rc = gs_refresh(c);
+    if (rc) return rc;
     /* the T/S block is solved with the right-hand side rr_TS - A_TS,D z_D of the dynamics
      * iterate after ts_at passes (default: after the last; the CPU twin: orc_gs_apply); the
      * later passes neither read nor write the T/S rows */
@@ -3590,7 +3684,7 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
                            aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
     } else {
         if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
-        hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, c->d_val.p, gs.known.p, gs.kmask.p,
+        hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, gs.vp, gs.known.p, gs.kmask.p,
                            r, z, aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
     }
     if ((rc = dyn_solve(c, gs.rrP.p, zP, nullptr, 0.0, zaos_of(gs.dyn_iters == 1)))) return rc;

@@ -399,3 +399,59 @@ def test_unmatched_exchange_fails_fast(oracle_lib):
     for o in ocs:
         o.close()
     _lib.lib().iemic_local_group_free(group)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 4])
+def test_reused_preconditioner_after_new_jacobian(oracle_lib, nranks):
+    """Ocean::solve reuses the preconditioner until preProcess flags a rebuild (Ocean.C:790-801,
+    1360-1374), and TRIOS::BlockPreconditioner keeps applying the blocks it extracted from the
+    set-up Jacobian.  The block GS is set up at state x, then J is assembled at x2 (into the
+    second Jacobian buffer):
+    * the apply is bitwise the apply before the new Jacobian, on every band: the bands'
+      halo-row recomputation and the owners' kernels read the same set-up Jacobian;
+    * the solve with the reused preconditioner (compressed basis, SpMV of J(x2) from the
+      repacked stream) solves the new system: ||b - J(x2) s|| <= 1e-8 ||b|| with the oracle's
+      J(x2); and a rebuilt preconditioner (preProcess) still gives the same solution."""
+    from iemic import _lib
+    from iemic.ocean import Ocean
+    name = "global4"
+    c = cf.preset(name, mixing=0)
+    L0 = golden_landm(name)
+    L = mask_fix(oracle_lib, c, L0)
+    o = oracle_lib.Oracle(c.ref_dict(), L, c.par_list())
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    x2 = cf.synthetic_state(c, L, seed=11, amp_ts=2e-3)
+    r = cf.synthetic_vector(c, seed=3)
+    b1, b2 = -o.rhs(x), -o.rhs(x2)
+    sp = {"Preconditioner": 2, "FGMRES tolerance": 1e-10, "FGMRES iterations": 1000}
+
+    def fn(rk, group):
+        kw = dict(local_group=group, rank=rk, nranks=nranks, npx=1) if group is not None else {}
+        oc = Ocean(c, landm=L0, solver_params=sp, **kw)
+        oc.setState(x)
+        oc.computeJacobian()
+        oc.solve(b1)                           # builds the block GS at x
+        z0 = oc.applyPrecon(r).copy()
+        oc.setState(x2)
+        oc.computeJacobian()                   # J(x2), the preconditioner stays that of x
+        z1 = oc.applyPrecon(r).copy()
+        s2 = oc.solve(b2).copy()
+        info = oc.last_solve
+        oc.preProcess()
+        s3 = oc.solve(b2).copy()
+        lay = oc.layout()
+        oc.close()
+        return dict(lay=lay, z0=z0, z1=z1, s2=s2, s3=s3, conv=info.converged)
+
+    res = [fn(0, None)] if nranks == 1 else _run_bands(nranks, fn)
+    s2, s3 = np.zeros(c.nrows), np.zeros(c.nrows)
+    for q in res:
+        rows = np.array(owned_rows(c, q["lay"]))
+        np.testing.assert_array_equal(q["z1"][rows].view(np.int64), q["z0"][rows].view(np.int64))
+        assert q["conv"] == 1
+        s2[rows] = q["s2"][rows]
+        s3[rows] = q["s3"][rows]
+    ov2, _ = o.jacobian(x2)
+    nb = np.linalg.norm(b2)
+    assert np.linalg.norm(b2 - o.spmv(ov2, s2)) <= 1e-8 * nb
+    assert np.linalg.norm(b2 - o.spmv(ov2, s3)) <= 1e-8 * nb
