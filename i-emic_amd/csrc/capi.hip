@@ -106,7 +106,7 @@ int upload_forcing_tables(iemic_ctx* c)
     std::vector<double> t = c->su.forcing_tables();
     HIP_OK(hipMemcpyAsync(c->d_ftab.p, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice,
                           c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return compute_forcing(c);
 }
 
@@ -264,6 +264,10 @@ static int create_impl(iemic_ctx** out, const iemic_grid* grid, const int* landm
         return IEMIC_EINVAL;
     }
     iemic_ctx* c = new iemic_ctx();
+    if (const char* e = std::getenv("IEMIC_COMM_TIMEOUT")) {
+        const double v = std::atof(e);
+        if (v > 0.0) c->comm_timeout_s = v;
+    }
     c->cfg = *grid;
     c->device = std::min(std::max(grid->device, 0), ndev - 1);
     if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -487,7 +491,7 @@ extern "C" int iemic_set_par(iemic_ctx* c, int idx, double value)
     c->jac_valid = 0;
     int rc = upload_forcing_tables(c);
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 
@@ -747,7 +751,7 @@ extern "C" int iemic_jacobian(iemic_ctx* c)
     int rc = halo_exchange(c, c->d_x.p, HALO);
     if (rc) return rc;
     if ((rc = assemble_jacobian(c, c->d_x.p))) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 
@@ -758,7 +762,7 @@ extern "C" int iemic_rhs(iemic_ctx* c, double* F)
     if (rc) return rc;
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
     if (F) return get_ref(c, c->d_F.p, F);
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 
@@ -803,7 +807,7 @@ extern "C" int iemic_prec_compute(iemic_ctx* c, const iemic_krylov* opt)
     CTX_CHECK(c);
     int rc = prec_compute(c, opt);
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 
@@ -867,29 +871,29 @@ extern "C" int iemic_newton_step(iemic_ctx* c, const iemic_krylov* opt, iemic_ne
     int rc = halo_exchange(c, c->d_x.p, HALO);
     if (rc) return rc;
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     inf.t_rhs_ms += ms(t);
     inf.norm_f0 = std::sqrt(dot(c, c->d_F.p, c->d_F.p, 0));   /* NaN stays NaN */
     t = clk::now();
     if ((rc = assemble_jacobian(c, c->d_x.p))) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     inf.t_jac_ms = ms(t);
     t = clk::now();
     if (opt->prec > 0) {
         if ((rc = prec_compute(c, opt))) return rc;
-        HIP_OK(hipStreamSynchronize(c->stream));
+        DEV_SYNC(c);
     }
     inf.t_prec_ms = ms(t);
     hipLaunchKernelGGL(k_neg, dim3(G), dim3(256), 0, c->stream, c->d_F.p + o, c->d_tmp1.p + o, NL);
     t = clk::now();
     if ((rc = krylov_solve(c, c->d_tmp1.p, c->d_tmp2.p, opt, &inf.solve))) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     inf.t_solve_ms = ms(t);
     hipLaunchKernelGGL(k_newton_update, dim3(G), dim3(256), 0, c->stream, c->d_x.p + o, c->d_tmp2.p + o, NL);
     t = clk::now();
     if ((rc = halo_exchange(c, c->d_x.p, HALO))) return rc;
     if ((rc = assemble_rhs(c, c->d_x.p, c->d_F.p))) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     inf.t_rhs_ms += ms(t);
     inf.norm_f1 = std::sqrt(dot(c, c->d_F.p, c->d_F.p, 0));   /* NaN stays NaN */
     c->jac_valid = 1;
@@ -1070,7 +1074,7 @@ extern "C" int iemic_time_spmv(iemic_ctx* c, int nrep, double* ms_per_launch)
         if (rc) return rc;
     }
     HIP_OK(hipEventRecord(e1, c->stream));
-    HIP_OK(hipEventSynchronize(e1));
+    DEV_WAIT_EVENT(c, e1);
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     *ms_per_launch = ms / nrep;
@@ -1090,13 +1094,13 @@ extern "C" int iemic_time_prec(iemic_ctx* c, int nrep, double* ms_per_apply, dou
     HIP_OK(hipMemsetAsync(c->d_tmp1.p, 0, sizeof(double) * c->nerows, c->stream));
     int rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);   /* warm */
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     const auto t0 = std::chrono::steady_clock::now();
     HIP_OK(hipEventRecord(e0, c->stream));
     for (int r = 0; r < nrep && !rc; r++) rc = prec_apply(c, c->d_tmp1.p, c->d_tmp2.p);
     HIP_OK(hipEventRecord(e1, c->stream));
     const double host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    HIP_OK(hipEventSynchronize(e1));
+    DEV_WAIT_EVENT(c, e1);
     if (rc) return rc;
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
@@ -1154,7 +1158,7 @@ extern "C" int iemic_time_spmv_cold(iemic_ctx* c, int nrep, void* flush, int64_t
         HIP_OK(hipEventRecord(e0, c->stream));
         if ((rc = spmv_kernel(c, c->d_x.p, c->d_tmp2.p))) return rc;
         HIP_OK(hipEventRecord(e1, c->stream));
-        HIP_OK(hipEventSynchronize(e1));
+        DEV_WAIT_EVENT(c, e1);
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, e0, e1));
         tot += ms;

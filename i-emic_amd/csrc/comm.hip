@@ -139,22 +139,29 @@ int comm_size(const iemic_ctx* c, int* size, int* kind)
     return 0;
 }
 
-/* Bounded wait for the RCCL work enqueued on the stream (fail-fast for the first
- * all-reduce and the first halo batch of a context, where a plan mismatch or a missing peer
- * would otherwise hang the process until an outside time limit): polls the stream and the
- * communicator's asynchronous error; on an error or after comm_timeout_s the communicator is
- * aborted (its kernels see the abort flag and return) and the call fails naming `what`. */
-static int rccl_wait(iemic_ctx* c, const std::string& what)
+/* Bounded wait for the RCCL work enqueued on the stream (or up to event e): polls the
+ * stream / event and the communicator's asynchronous error; on an error or after
+ * comm_timeout_s the communicator is aborted (its kernels see the abort flag and return) and
+ * the call fails naming `what`.  Every host wait of an RCCL context goes through here
+ * (dev_wait), so a peer that never posts a matching call -- at the first collective or at one
+ * of a plan first used in the middle of a solve -- ends the call instead of hanging the
+ * process.  The first 200 polls spin (the FGMRES loop waits on every iteration: no sleep
+ * latency), then the poll backs off to 20 us and later 1 ms. */
+static int rccl_wait(iemic_ctx* c, const std::string& what, hipEvent_t e = nullptr)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     ncclComm_t comm = (ncclComm_t)c->comm;
     for (int it = 0;; it++) {
-        const hipError_t q = hipStreamQuery(c->stream);
+        const hipError_t q = e ? hipEventQuery(e) : hipStreamQuery(c->stream);
         if (q == hipSuccess) return 0;
         if (q != hipErrorNotReady) {
             set_error(what + ": " + hipGetErrorString(q));
             return IEMIC_EDEVICE;
+        }
+        if (it < 200) {
+            std::this_thread::yield();
+            continue;
         }
         ncclResult_t ae = ncclSuccess;
         const bool failed = ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess &&
@@ -170,8 +177,18 @@ static int rccl_wait(iemic_ctx* c, const std::string& what)
                       "; communicator aborted");
             return IEMIC_EDEVICE;
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(it < 1000 ? 20 : 1000));
+        std::this_thread::sleep_for(std::chrono::microseconds(it < 5000 ? 20 : 1000));
     }
+}
+
+/* the host waits of the library: for the stream (e null) or an event; bounded under RCCL */
+int dev_wait(iemic_ctx* c, hipEvent_t e, const char* what)
+{
+    if (!c->comm) {
+        HIP_OK(e ? hipEventSynchronize(e) : hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    return rccl_wait(c, std::string("wait in ") + what, e);
 }
 
 static int rccl_live(iemic_ctx* c)

@@ -240,13 +240,13 @@ struct BlockGS {
     DevBuf<uint8_t> actf;            /* per owned cell: 1 active (k_cell_active)           */
     int64_t nact = 0;
     std::vector<uint8_t> act_h;      /* the per-cell flags the list was built from        */
-    /* the compressed SpMV (krylov.hip k_spmv7c): the active cells' 104 coefficients packed
-     * slot-major over the active list (row stride spc_ld = nact rounded up to 16 cells, so
-     * no coefficient line holds a land cell), and the grid tiles that hold an active cell
-     * (4 ints each: tile, first and last active lane, 0) */
+    /* the compressed SpMV (krylov.hip k_spmv7c): the active cells' 104 coefficients blocked
+     * per tile (prec_gs.hip k_spmv_pack: no coefficient line holds a land cell or another
+     * tile's), and the grid tiles that hold an active cell (8 ints each: tile, first | last
+     * active lane << 8, first active cell, active cells, 64-bit active-lane mask, 0, 0) */
     DevBuf<double> spc;
-    int64_t spc_ld = 0;
     DevBuf<int> atl;
+    DevBuf<int> apos;                /* per active cell: its tile's index in atl            */
     int natile = 0;
     /* the Jacobian the apply reads: the set-up one (prec_gs.hip gs_refresh).  A Jacobian
      * assembled while the block GS is set up goes into the other buffer (assemble_jacobian
@@ -310,10 +310,11 @@ struct iemic_ctx {
     iemic::DevBuf<double> d_stage;   /* packed strided messages (RCCL)                    */
     std::vector<double> h_stage;     /* host-staged messages (group / host transport)     */
     int64_t stat[4] = {0, 0, 0, 0};  /* exchange batches, messages, bytes sent, all-reduces */
-    /* fail-fast (comm.hip): the first all-reduce and the first halo batch of a context are
-     * waited for with this bound (RCCL: stream + async-error polling, then ncclCommAbort;
-     * in-process group: timed barriers, always); bits of comm_checked: 1 all-reduce, 2 halo */
-    double comm_timeout_s = 60.0;
+    /* fail-fast (comm.hip): every host wait of an RCCL context (stream / event + async-error
+     * polling, then ncclCommAbort) and every barrier of the in-process group is bounded by
+     * this (IEMIC_COMM_TIMEOUT or 300 s at creation); the first all-reduce and halo batch
+     * name their batch (bits of comm_checked: 1 all-reduce, 2 halo) */
+    double comm_timeout_s = 300.0;
     int comm_checked = 0;
     iemic::host::Setup su;           /* grid tables, parameters, effective mask */
     /* device tables */
@@ -343,20 +344,32 @@ struct iemic_ctx {
 };
 
 namespace iemic {
+/* the host waits for the stream (e null) or an event: bounded under RCCL (comm.hip) */
+int dev_wait(iemic_ctx* c, hipEvent_t e, const char* what);
+#define DEV_SYNC(c)                                                     \
+    do {                                                                \
+        const int rs_ = ::iemic::dev_wait((c), nullptr, __func__);      \
+        if (rs_) return rs_;                                            \
+    } while (0)
+#define DEV_WAIT_EVENT(c, e)                                            \
+    do {                                                                \
+        const int rs_ = ::iemic::dev_wait((c), (e), __func__);          \
+        if (rs_) return rs_;                                            \
+    } while (0)
 /* Stream-ordered copies: every transfer goes through the context's stream and is complete
  * on return (the stream is non-blocking, so the legacy null stream must never be used). */
 inline int h2d(iemic_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!bytes) return 0;
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 inline int d2h(iemic_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!bytes) return 0;
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     return 0;
 }
 /* two timing events, destroyed on every return path */
@@ -377,7 +390,7 @@ struct EventPair {
  * this context is still in flight when control goes back to the caller. */
 struct StreamGuard {
     iemic_ctx* c;
-    ~StreamGuard() { if (c && c->stream) (void)hipStreamSynchronize(c->stream); }
+    ~StreamGuard() { if (c && c->stream) (void)dev_wait(c, nullptr, "return"); }
 };
 
 /* the subdomain layout handed to the structured-grid kernels */

@@ -1051,7 +1051,7 @@ extern "C" int iemic_atmos_rhs(iemic_atmos* a, double* F)
     int rc = atm_rhs_dev(a);
     if (rc) return rc;
     if (F) return d2h(a->oc, F, a->d_F.p, sizeof(double) * a->dim);
-    HIP_OK(hipStreamSynchronize(a->oc->stream));
+    DEV_SYNC(a->oc);
     return 0;
 }
 /* Atmosphere::computeJacobian (911-1126) */
@@ -1061,7 +1061,7 @@ extern "C" int iemic_atmos_jacobian(iemic_atmos* a)
     if (hipSetDevice(a->oc->device) != hipSuccess) return IEMIC_EDEVICE;
     int rc = atm_jac_dev(a);
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(a->oc->stream));
+    DEV_SYNC(a->oc);
     return 0;
 }
 /* the local rows as ELL (dim-1 rows x 7: values, columns, -1 unused); the dense q-integral
@@ -1324,7 +1324,7 @@ extern "C" int iemic_coupled_synchronize(iemic_coupled* cm)
     if (hipSetDevice(cm->oc->device) != hipSuccess) return IEMIC_EDEVICE;
     int rc = cpl_sync(cm);
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(cm->oc->stream));
+    DEV_SYNC(cm->oc);
     return 0;
 }
 
@@ -1391,7 +1391,10 @@ double cdot_host(iemic_coupled* cm, const double* V, int64_t ld, int nv, const d
         return out[nv];
     }
     (void)hipMemcpyAsync(cm->h_red, cm->hb.p, sizeof(double) * (nv + 1), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
+    if (dev_wait(cm->oc, nullptr, "coupled dots")) {
+        for (int i = 0; i <= nv; i++) out[i] = std::nan("");
+        return out[nv];
+    }
     for (int i = 0; i <= nv; i++) out[i] = cm->h_red[i];
     return out[nv];
 }
@@ -1682,12 +1685,12 @@ extern "C" int iemic_coupled_solve(iemic_coupled* cm, const double* b_host, doub
         if ((rc = enqueue(0))) return rc;
         for (; j < m; j++) {
             if (j + 1 < m && (rc = enqueue(j + 1))) return rc;
-            HIP_OK(hipEventSynchronize(cm->ev[j & 1]));
+            DEV_WAIT_EVENT(cm->oc, cm->ev[j & 1]);
             const double* hr = cm->h_red + (size_t)(j & 1) * HH;
             for (int i = 0; i <= j; i++) h[i] = hr[i] + hr[j + 1 + i];
             const double hn2 = hr[2 * (j + 1)];
             if (!std::isfinite(hn2)) {
-                (void)hipStreamSynchronize(s);
+                (void)dev_wait(cm->oc, nullptr, "coupled fgmres");
                 set_error("coupled FGMRES: non-finite value in the Krylov basis");
                 return IEMIC_ERANGE;
             }

@@ -149,77 +149,87 @@ __global__ void __launch_bounds__(256) k_spmv7(SubLay X, const double* __restric
     }
 }
 
-/* k_spmv7c: the in-solve SpMV of FGMRES's compressed basis (round 6).  k_spmv7<true> read the
- * slot-major Jacobian and skipped land lanes, but a 128-byte coefficient line holds 16 cells,
- * so the lines of mixed land / water runs were fetched whole: 128.9 MB of coefficient lines
- * for 100.7 MB of active coefficients at 2 degrees (147 MB of counter bytes per launch, 1.25x).
- * Here the coefficients come from BlockGS::spc, the active cells' 104 slots packed slot-major
- * over the active list (row stride ld), so the active lanes of a tile read one contiguous
- * run per slot that no land cell shares.  Only the tiles that hold an active cell are
- * launched (BlockGS::atl, dealt to the 8 XCDs in contiguous runs), and x is staged only over
- * the columns the tile's active cells reach (first active lane - 1 .. last + 1). */
-__global__ void __launch_bounds__(256) k_spmv7c(SubLay X, const double* __restrict__ spc, int64_t ld,
+/* k_spmv7c: the in-solve SpMV of FGMRES's compressed basis (round 6).  k_spmv7 reads the
+ * slot-major Jacobian, whose 128-byte coefficient lines hold 16 cells: the lines of mixed land /
+ * water runs are fetched whole (at 2 degrees 128.9 MB of coefficient lines for 100.7 MB of
+ * active coefficients; round 5's land-skipping variant moved 147 MB per launch, 1.25x).
+ *  - Coefficients: BlockGS::spc holds the active cells' 104 slots blocked per tile -- the na
+ *    active cells of a tile (consecutive in the compressed order, from a0) as one contiguous
+ *    run of 104 na doubles, slot s of the tile's r-th active cell at 104 a0 + s na + r -- so a
+ *    workgroup streams one run that no land cell and no other tile shares (PMC: 117.1 MB per
+ *    launch against 117.7 MB algorithmic; slot-major packing over the active list: 124.9 MB,
+ *    3.4 us slower).
+ *  - Tiles: only the 64-cell tiles (one grid row) that hold an active cell are launched
+ *    (BlockGS::atl: tile, first / last active lane, a0, na and the 64-bit active-lane mask, so
+ *    a lane finds its compressed index by a popcount instead of a dependent load), dealt to
+ *    the 8 XCDs in contiguous runs.
+ *  - x: the six (dj, dk) neighbour rows' interior cells are contiguous runs in x and in the
+ *    LDS image, copied by LDS-DMA (global_load_lds_dwordx4, no VGPR destination: 94 instead
+ *    of 104 VGPRs, 5 waves per SIMD instead of 4; 32.5 -> 29.2 us), pieces beyond the active
+ *    cells' reach skipped; the two end cells of each row by plain loads.
+ * Same sums in the same order as k_spmv7: the compressed rows are bitwise its rows. */
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+__global__ void __launch_bounds__(256) k_spmv7c(SubLay X, const double* __restrict__ spc,
                                                 const double* __restrict__ x, double* __restrict__ y,
-                                                const int4* __restrict__ atl, int natile, int tpr,
-                                                const int* __restrict__ cmap)
+                                                const int4* __restrict__ atl, int natile, int tpr)
 {
     __shared__ double xs[6 * (SP7_T + 2) * NUN];
     __shared__ double red[4][3][SP7_T];
-    __shared__ int cms[SP7_T], lof[SP7_T];
+    __shared__ int lof[SP7_T];
     const int l = X.l, nx = X.nx;
     const int per = (natile + 7) >> 3;
     const int pos = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     if (pos >= natile) return;
-    const int4 td = atl[pos];
-    const int tile = td.x, clo = td.y, chi = td.z;
+    const int4 td = atl[2 * pos], tm = atl[2 * pos + 1];
+    const int tile = td.x, clo = td.y & 255, chi = td.y >> 8, a0 = td.z;
+    /* the tile's active lanes: a 64-bit mask, so a lane finds its compressed index without a
+     * dependent load (cm = a0 + active lanes below it) */
+    const uint64_t amask = (uint64_t)(uint32_t)tm.x | ((uint64_t)(uint32_t)tm.y << 32);
     const int row = tile / tpr, i0 = (tile - row * tpr) * SP7_T;
     const int k = row % l, jl = row / l, j = X.jb0 + jl;
     const int nc = min(SP7_T, nx - i0);
-    const int lc0 = row * nx + i0;
     const int t = threadIdx.x, c = t & 63;
     const int g = __builtin_amdgcn_readfirstlane(t >> 6);   /* wave-uniform: scalar branches */
-    const int cm = (c >= clo && c <= chi) ? cmap[lc0 + c] : -1;
-    const int a0 = cmap[lc0 + clo];                          /* the tile's first active cell */
-    const bool act = cm >= 0;
-    if (g == 0) {
-        cms[c] = cm;
-        if (act) lof[cm - a0] = c;                           /* active cell -> its lane */
-    }
+    const bool act = (amask >> c) & 1;
+    const int cm = act ? a0 + __builtin_popcountll(amask & ((1ull << c) - 1)) : -1;
+    if (g == 0 && act) lof[cm - a0] = c;                    /* active cell -> its lane */
     double acc[3] = {0.0, 0.0, 0.0};
     double v[26];
     /* coefficient loads, then the staging loads, all issued before the first LDS store */
-    if (g == 0) sp7_load<0, 26>(spc, ld, cm, act, v);
-    else if (g == 1) sp7_load<26, 52>(spc, ld, cm, act, v);
-    else if (g == 2) sp7_load<52, 78>(spc, ld, cm, act, v);
-    else sp7_load<78, 104>(spc, ld, cm, act, v);
+    const double* vb = spc + (int64_t)NSLOT * a0;
+    const int64_t vs = td.w, vo = cm - a0;
+    if (g == 0) sp7_load<0, 26>(vb, vs, vo, act, v);
+    else if (g == 1) sp7_load<26, 52>(vb, vs, vo, act, v);
+    else if (g == 2) sp7_load<52, 78>(vb, vs, vo, act, v);
+    else sp7_load<78, 104>(vb, vs, vo, act, v);
     {
+        /* the interior cells i0 .. i0 + nc - 1 of each of the six grid rows are one contiguous
+         * run of nc * 48 bytes in x and in the LDS image: copied by LDS-DMA in 1 KiB pieces (a
+         * wave-instruction of 16 bytes per lane, no VGPR destination), the pieces outside the
+         * active cells' reach skipped; the two end cells of each row (the neighbour columns,
+         * from the x halo when the x direction is split) by 72 plain loads */
         const int jm = j > 0 ? j - 1 : j, jp = j < X.m - 1 ? j + 1 : j;
         const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
         const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
-        constexpr int PR = (SP7_T + 2) * NUN;
-        constexpr int SPT = (6 * PR + 255) / 256;
-        /* staged cells p = clo .. chi + 2 (cell i0 + p - 1) of each grid row */
-        const int wlo = clo * NUN, whi = (chi + 3) * NUN;
-        double xv[SPT];
-        int xo[SPT];
-#pragma unroll
-        for (int u = 0; u < SPT; u++) {
-            const int e = t + 256 * u;
-            const int q = e / PR, w = e - q * PR;
-            xo[u] = -1;
-            if (e < 6 * PR && w >= wlo && w < whi) {
-                const int p = w / NUN, var = w - p * NUN;
-                const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
-                const int64_t cell = (p == 0 || p == nc + 1)
-                                         ? xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb)
-                                         : r * nx + i0 + p - 1;
-                xo[u] = e;
-                xv[u] = x[NUN * cell + var];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < SPT; u++)
-            if (xo[u] >= 0) xs[xo[u]] = xv[u];
+        const int lane = t & 63, nb = nc * NUN * 8;
+        const int blo = max(0, (clo - 1) * NUN * 8), bhi = min(nb, (chi + 2) * NUN * 8);
+        for (int u = g; u < 18; u += 4) {
+            const int q = u / 3, h = u - 3 * q;
+            if (h * 1024 >= bhi || (h + 1) * 1024 <= blo) continue;        /* wave-uniform */
+            const int byte = h * 1024 + lane * 16;
+            const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
+            if (byte < nb)
+                __builtin_amdgcn_global_load_lds((glb_void*)(x + NUN * (r * nx + i0) + byte / 8),
+                                                 (lds_void*)(xs + (q * (SP7_T + 2) + 1) * NUN + h * 128), 16, 0, 0);
+    }
+        if (t < 72) {
+            const int q = t / 12, side = (t / NUN) & 1, var = t - NUN * (t / NUN);
+            const int p = side ? nc + 1 : 0;
+            const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
+            const int64_t cell = xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb);
+            xs[(q * (SP7_T + 2) + p) * NUN + var] = x[NUN * cell + var];
+    }
     }
     __syncthreads();
     if (act) {
@@ -234,7 +244,7 @@ __global__ void __launch_bounds__(256) k_spmv7c(SubLay X, const double* __restri
     /* rows of the groups: g0 {U,V} g1 {V,W} g2 {W,P,T} g3 {T,S}; the tile's active cells are
      * consecutive in the compressed vector, so its rows [6 cm(clo), 6 cm(chi) + 6) are one
      * contiguous run: thread o writes entry o of it */
-    const int na = cms[chi] - a0 + 1;
+    const int na = td.w;
     for (int o = t; o < na * NUN; o += 256) {
         const int ac = o / NUN, R = o - ac * NUN;
         const int cc = lof[ac];
@@ -848,9 +858,8 @@ int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t ev0, hip
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
     const unsigned grid = 8u * (unsigned)((gs.natile + 7) / 8);
     if (gs.natile > 0)
-        hipExtLaunchKernelGGL(k_spmv7c, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c),
-                              (const double*)gs.spc.p, gs.spc_ld, x, yc, (const int4*)gs.atl.p, gs.natile, tpr,
-                              (const int*)gs.cmap.p);
+        hipExtLaunchKernelGGL(k_spmv7c, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c), (const double*)gs.spc.p,
+                              x, yc, (const int4*)gs.atl.p, gs.natile, tpr);
     double* yr = nullptr;
     if (c->rowintcon >= 0) {
         if (c->gs.ric < 0) {
@@ -885,7 +894,7 @@ static int mdot_host(iemic_ctx* c, const double* V, int64_t ldv, int nvec, const
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * nout, hipMemcpyDeviceToHost,
                           c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     for (int i = 0; i < nout; i++) out[i] = c->h_red[i];
     return 0;
 }
@@ -926,7 +935,7 @@ static int orth_pass(iemic_ctx* c, const double* V, int64_t ldv, int nvec, doubl
     if ((rc = allreduce_sum(c, c->d_hbuf.p + nvec + 1, 1))) return rc;
     HIP_OK(hipMemcpyAsync(c->h_red, c->d_hbuf.p, sizeof(double) * (nvec + 2), hipMemcpyDeviceToHost,
                           c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    DEV_SYNC(c);
     for (int i = 0; i < nvec; i++) h[i] = c->h_red[i];
     *ww0 = c->h_red[nvec];
     *ww1 = c->h_red[nvec + 1];
@@ -1256,7 +1265,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             if ((rc = enqueue(0))) return rc;
             for (int jj = 0; jj <= m; jj++) {
                 if (jj < m && (rc = enqueue(jj + 1))) return rc;
-                HIP_OK(hipEventSynchronize(evr[jj & 1]));
+                DEV_WAIT_EVENT(c, evr[jj & 1]);
                 if (jj < m) {
                     float a1 = 0.f, a2 = 0.f;
                     hipEvent_t* e = ev + 3 * (jj & 1);
@@ -1270,7 +1279,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 const double* hr = c->h_red + (size_t)RED_ROWS * (jj & 1);
                 const double uu = hr[2 * nv], uw = hr[2 * nv + 1];
                 if (!std::isfinite(uu) || !std::isfinite(uw)) {
-                    (void)hipStreamSynchronize(c->stream);
+                    (void)dev_wait(c, nullptr, "fgmres");
                     return nonfinite();
                 }
                 const double bt = hr[2 * nv + 3], hjj = hr[2 * nv + 4];
@@ -1307,7 +1316,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
             }
             /* the speculative iteration and its copy into the pinned slots finish before the
              * slots are reused as the staging area of the solution update */
-            HIP_OK(hipStreamSynchronize(c->stream));
+            DEV_SYNC(c);
             j = ncolf;
         }
         /* y = H \ g ; x += Z y */

@@ -3233,14 +3233,18 @@ __global__ void k_dyn_pack(const double* __restrict__ val, const int* __restrict
     dvb[t] = h < nact ? val[s * nloc + act[h]] : 0.0;
 }
 
-/* spc[s ld + a] = val[s nloc + act[a]] (0 in the row's padding): the compressed SpMV's stream */
-__global__ void k_spmv_pack(const double* __restrict__ val, const int* __restrict__ act, int64_t nact,
-                            int64_t ld, int64_t nloc, double* __restrict__ spc)
+/* the compressed SpMV's stream (krylov.hip k_spmv7c): the active cells of tile pos (a0 ..
+ * a0 + na - 1) hold one contiguous run spc[104 a0 ..), slot s of active cell a at
+ * 104 a0 + s na + (a - a0) */
+__global__ void k_spmv_pack(const double* __restrict__ val, const int* __restrict__ act,
+                                const int* __restrict__ apos, const int4* __restrict__ atl, int64_t nact,
+                                int64_t nloc, double* __restrict__ spc)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)NSLOT * ld) return;
-    const int64_t s = t / ld, a = t - s * ld;
-    spc[t] = a < nact ? val[s * nloc + act[a]] : 0.0;
+    if (t >= (int64_t)NSLOT * nact) return;
+    const int64_t s = t / nact, a = t - s * nact;
+    const int4 td = atl[2 * apos[a]];
+    spc[(int64_t)NSLOT * td.z + s * td.w + (a - td.z)] = val[s * nloc + act[a]];
 }
 
 /* gs_refresh: *nd += 1 for every owned row whose identity flag (k_known's rule) in the
@@ -3288,10 +3292,10 @@ static int gs_pack_spc(iemic_ctx* c)
 {
     BlockGS& gs = c->gs;
     if (gs.nact <= 0 || !gs.act.p) return 0;
-    gs.spc_ld = (gs.nact + 15) / 16 * 16;
-    if (gs.spc.n < (size_t)(NSLOT * gs.spc_ld) && gs.spc.alloc((size_t)(NSLOT * gs.spc_ld))) return IEMIC_ENOMEM;
-    hipLaunchKernelGGL(k_spmv_pack, dim3(blocks_for(NSLOT * gs.spc_ld)), dim3(256), 0, c->stream, c->d_val.p,
-                       (const int*)gs.act.p, gs.nact, gs.spc_ld, c->nloc, gs.spc.p);
+    if (gs.spc.n < (size_t)(NSLOT * gs.nact) && gs.spc.alloc((size_t)(NSLOT * gs.nact))) return IEMIC_ENOMEM;
+    hipLaunchKernelGGL(k_spmv_pack, dim3(blocks_for(NSLOT * gs.nact)), dim3(256), 0, c->stream, c->d_val.p,
+                       (const int*)gs.act.p, (const int*)gs.apos.p, (const int4*)gs.atl.p, gs.nact, c->nloc,
+                       gs.spc.p);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -3404,26 +3408,34 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                 if (cell >= 0 && cell < c->nloc && cm[cell] >= 0) gs.ric = (int64_t)NUN * cm[cell] + c->rowintcon % NUN;
             }
             /* the compressed SpMV's tiles (k_spmv7c): 64 cells along i of one grid row, those
-             * holding an active cell, with their first and last active lane */
+             * holding an active cell: tile, first | last active lane << 8, the first active
+             * cell a0, the active cells na, the 64-bit active-lane mask (8 ints each) */
             {
                 const int nx = c->nx, tpr = (nx + 63) / 64;
                 const int64_t nrow = c->nloc / nx;
-                std::vector<int> tl;
+                std::vector<int> tl, ap((size_t)gs.nact, 0);
                 for (int64_t row = 0; row < nrow; row++)
                     for (int ti = 0; ti < tpr; ti++) {
                         const int i0 = ti * 64, nc = std::min(64, nx - i0);
                         int lo = -1, hi = -1;
+                        uint64_t mask = 0;
                         for (int cc = 0; cc < nc; cc++)
                             if (h[row * nx + i0 + cc]) {
                                 if (lo < 0) lo = cc;
                                 hi = cc;
+                                mask |= (uint64_t)1 << cc;
                             }
                         if (lo < 0) continue;
-                        tl.insert(tl.end(), {(int)(row * tpr + ti), lo, hi, 0});
+                        const int a0 = cm[row * nx + i0 + lo], na = cm[row * nx + i0 + hi] - a0 + 1;
+                        for (int a = a0; a < a0 + na; a++) ap[a] = (int)(tl.size() / 8);
+                        tl.insert(tl.end(), {(int)(row * tpr + ti), lo | (hi << 8), a0, na, (int)(uint32_t)mask,
+                                             (int)(uint32_t)(mask >> 32), 0, 0});
                     }
-                gs.natile = (int)(tl.size() / 4);
-                if (gs.atl.n < tl.size() + 4 && gs.atl.alloc(tl.size() + 4)) return IEMIC_ENOMEM;
+                gs.natile = (int)(tl.size() / 8);
+                if (gs.atl.n < tl.size() + 8 && gs.atl.alloc(tl.size() + 8)) return IEMIC_ENOMEM;
                 if (!tl.empty() && (rc = h2d(c, gs.atl.p, tl.data(), sizeof(int) * tl.size()))) return rc;
+                if (gs.apos.n < ap.size() + 1 && gs.apos.alloc(ap.size() + 1)) return IEMIC_ENOMEM;
+                if (!ap.empty() && (rc = h2d(c, gs.apos.p, ap.data(), sizeof(int) * ap.size()))) return rc;
             }
             gs.act_h.swap(h);
             /* the defect (k_spmv_dyn) writes the active cells only: the others' rows 0 */

@@ -151,6 +151,8 @@ class Ocean:
         else:
             rc = lib().iemic_create(C.byref(h), C.byref(self._grid), ptr(L, C.c_int))
         check(rc, "iemic_create")
+        self._vlive = 0                 # DeviceVecs handed out and not yet given back
+        self._closing = False
         self._h = h
         self.N = lib().iemic_nrows(h)
         # Belos solver parameters (Ocean::getDefaultInitParameters, Ocean.C:2232-2237)
@@ -193,22 +195,45 @@ class Ocean:
         return DeviceOps(self)
 
     def _vec_take(self) -> C.c_void_p:
+        if self._closing:
+            raise IemicError("Ocean is closed")
+        self._vlive += 1
         if self._vpool:
             return self._vpool.pop()
         p = C.c_void_p()
-        check(lib().iemic_vec_alloc(self._h, C.byref(p)), "iemic_vec_alloc")
+        rc = lib().iemic_vec_alloc(self._h, C.byref(p))
+        if rc:
+            self._vlive -= 1
+        check(rc, "iemic_vec_alloc")
         return p
 
     def _vec_give(self, p) -> None:
-        if getattr(self, "_h", None):
+        """a DeviceVec's buffer back: into the pool, or freed when the Ocean was closed (the
+        context then lives until the last vector is gone)"""
+        if not getattr(self, "_h", None):
+            return
+        self._vlive -= 1
+        if self._closing:
+            lib().iemic_vec_free(self._h, p)
+            if self._vlive <= 0:
+                self._destroy()
+        else:
             self._vpool.append(p)
 
     # ---- lifecycle -----------------------------------------------------------------
     def close(self):
-        if getattr(self, "_h", None):
+        """Frees the pooled vectors and the context; a context with DeviceVecs still alive
+        (a continuation's saved state, say) is destroyed when the last of them is released."""
+        if getattr(self, "_h", None) and not self._closing:
             for p in self._vpool:
                 lib().iemic_vec_free(self._h, p)
             self._vpool = []
+            self._closing = True
+            if self._vlive <= 0:
+                self._destroy()
+
+    def _destroy(self):
+        if getattr(self, "_h", None):
             lib().iemic_destroy(self._h)
             self._h = None
 

@@ -283,11 +283,13 @@ int     iemic_comm_stats(iemic_ctx* ctx, int64_t* out4);
  * transport: 0 none, 1 RCCL, 2 in-process group, 3 host transport (reports its nranks).
  * The reference queries Epetra_Comm::NumProc (e.g. THCM.C:404, 1717). */
 int     iemic_comm_size(const iemic_ctx* ctx, int* size, int* transport);
-/* Fail-fast bound (seconds, default 60) for this context's first all-reduce and first halo
- * batch over RCCL (stream and ncclCommGetAsyncError polled; on an error or timeout the
- * communicator is aborted and the call returns IEMIC_EDEVICE naming the batch and peers) and
- * for every barrier of the in-process group.  Exchange plans are checked to pair up across
- * the ranks when a context is created (a mismatch fails iemic_create_* with IEMIC_EINVAL). */
+/* Fail-fast bound (seconds) for every host wait of this context over RCCL (the stream or
+ * event polled together with ncclCommGetAsyncError; on an error or timeout the communicator
+ * is aborted and the call returns IEMIC_EDEVICE naming the wait, and for the first all-reduce
+ * and halo batch the batch and peers) and for every barrier of the in-process group.  The
+ * default, also for the collectives inside iemic_create_*, is the environment variable
+ * IEMIC_COMM_TIMEOUT when set, else 300 s.  Exchange plans are checked to pair up across the
+ * ranks when a context is created (a mismatch fails iemic_create_* with IEMIC_EINVAL). */
 int     iemic_set_comm_timeout(iemic_ctx* ctx, double seconds);
 /* Epetra_Comm::SumAll (e.g. Ocean::getColumnIntegral's column sums, Ocean.C:1851-1895):
  * buf (host, count doubles) summed over the context's ranks in place; collective */

@@ -40,6 +40,8 @@ typedef struct {
     int ts_at;                       /* T/S right-hand side after this many dynamics passes */
     double dyn_omega;
     double *dres, *zc;
+    int dyn_krylov;                  /* 1: the dynamics passes as right-preconditioned GMRES */
+    double *kv, *kz;                 /* its basis (dyn_iters + 1) and M_D^-1 images (dyn_iters) */
     void* mg;
 } gs_t;
 
@@ -92,7 +94,7 @@ void orc_gs_destroy(void* h)
     if (!g) return;
     free(g->known); free(g->colid); free(g->ij_of_col); free(g->pinned); free(g->band);
     free(g->piv); free(g->uvinv); free(g->tsinv); free(g->pw); free(g->rr); free(g->bts);
-    free(g->colv); free(g->band0); free(g->dres); free(g->zc);
+    free(g->colv); free(g->band0); free(g->dres); free(g->zc); free(g->kv); free(g->kz);
     mg_free(g->mg);
     free(g);
 }
@@ -879,6 +881,99 @@ void orc_gs_ts_at(void* h, int ts_at)
     ((gs_t*)h)->ts_at = ts_at;
 }
 
+/* Study variant (CPU twin only, not on the GPU; DESIGN.md §4 "inner acceleration"):
+ * dyn_krylov = 1 makes the dyn_iters applications of M_D a right-preconditioned GMRES on the
+ * dynamics block A_DD z_D = rr_D (from z_D = 0; classical Gram-Schmidt twice) instead of the
+ * damped defect-correction passes (the reference accelerates its sub-solves by GMRESR,
+ * TRIOS_BlockPreconditioner.C:1479-1611) */
+void orc_gs_dyn_krylov(void* h, int on)
+{
+    gs_t* g = (gs_t*)h;
+    g->dyn_krylov = on ? 1 : 0;
+    if (on && !g->kv) {
+        g->kv = (double*)calloc((size_t)(g->dyn_iters + 1) * g->N, sizeof(double));
+        g->kz = (double*)calloc((size_t)g->dyn_iters * g->N, sizeof(double));
+    }
+}
+
+static double dyn_dot(const gs_t* g, const double* a, const double* b)
+{
+    double s = 0.0;
+    for (int64_t row = 0; row < g->N; row++)
+        if (row % NUN <= PP && !g->known[row]) s += a[row] * b[row];
+    return s;
+}
+
+/* z_D from GMRES(k) on the dynamics block, k = dyn_iters applications of dyn_solve */
+static void dyn_gmres(gs_t* g, double* z)
+{
+    const int k = g->dyn_iters;
+    const int64_t N = g->N;
+    double H[17][16], cs[16], sn[16], e[17], y[16];
+    memset(H, 0, sizeof(H));
+    memset(e, 0, sizeof(e));
+    double* V = g->kv;
+    double* Z = g->kz;
+    /* v0 = rr_D / beta (the rows the dynamics solve reads: U/V/W/P of the active rows) */
+    for (int64_t row = 0; row < N; row++) V[row] = (row % NUN <= PP && !g->known[row]) ? g->rr[row] : 0.0;
+    const double beta = sqrt(dyn_dot(g, V, V));
+    if (!(beta > 0.0)) return;
+    for (int64_t row = 0; row < N; row++) V[row] /= beta;
+    e[0] = beta;
+    int nk = 0;
+    for (int j = 0; j < k; j++) {
+        double* vj = V + (int64_t)j * N;
+        double* zj = Z + (int64_t)j * N;
+        double* w = V + (int64_t)(j + 1) * N;
+        memset(zj, 0, sizeof(double) * N);
+        dyn_solve(g, vj, zj);
+        /* w = A_DD zj: the defect of zj against a zero right-hand side, negated */
+        double* rrs = g->rr;
+        static double* zero = NULL;
+        static int64_t nz = 0;
+        if (nz < N) { free(zero); zero = (double*)calloc(N, sizeof(double)); nz = N; }
+        g->rr = zero;
+        dyn_defect(g, zj, w);
+        g->rr = rrs;
+        for (int64_t row = 0; row < N; row++) w[row] = -w[row];
+        for (int pass = 0; pass < 2; pass++)
+            for (int i = 0; i <= j; i++) {
+                const double hij = dyn_dot(g, V + (int64_t)i * N, w);
+                H[i][j] += hij;
+                for (int64_t row = 0; row < N; row++) w[row] -= hij * V[(int64_t)i * N + row];
+            }
+        const double hn = sqrt(dyn_dot(g, w, w));
+        H[j + 1][j] = hn;
+        if (hn > 0.0)
+            for (int64_t row = 0; row < N; row++) w[row] /= hn;
+        for (int i = 0; i < j; i++) {
+            const double a = H[i][j], b = H[i + 1][j];
+            H[i][j] = cs[i] * a + sn[i] * b;
+            H[i + 1][j] = -sn[i] * a + cs[i] * b;
+        }
+        const double a = H[j][j], b = H[j + 1][j], d = sqrt(a * a + b * b);
+        cs[j] = d > 0.0 ? a / d : 1.0;
+        sn[j] = d > 0.0 ? b / d : 0.0;
+        H[j][j] = d;
+        H[j + 1][j] = 0.0;
+        e[j + 1] = -sn[j] * e[j];
+        e[j] = cs[j] * e[j];
+        nk = j + 1;
+        if (hn == 0.0) break;
+    }
+    for (int i = nk - 1; i >= 0; i--) {
+        double s = e[i];
+        for (int q = i + 1; q < nk; q++) s -= H[i][q] * y[q];
+        y[i] = H[i][i] != 0.0 ? s / H[i][i] : 0.0;
+    }
+    for (int64_t row = 0; row < N; row++) {
+        if (row % NUN > PP || g->known[row]) continue;
+        double s = 0.0;
+        for (int q = 0; q < nk; q++) s += y[q] * Z[(int64_t)q * N + row];
+        z[row] = s;
+    }
+}
+
 void orc_gs_apply(void* h, const double* r, double* z)
 {
     gs_t* g = (gs_t*)h;
@@ -896,12 +991,17 @@ void orc_gs_apply(void* h, const double* r, double* z)
         g->rr[row] = acc;
     }
     double* rr = g->rr;
-    dyn_solve(g, rr, z);
+    const int ts_at = (g->ts_at >= 1 && g->ts_at < g->dyn_iters) ? g->ts_at : g->dyn_iters;
+    if (g->dyn_krylov && g->dyn_iters > 1) {
+        dyn_gmres(g, z);
+        ts_rhs(g, z);
+    } else {
+        dyn_solve(g, rr, z);
+    }
     /* defect correction: z_D += omega M_D^-1 (rr - A z)_D; the T/S right-hand side
      * rr_TS - A_TS,D z_D is formed after ts_at passes (default: all of them) */
-    const int ts_at = (g->ts_at >= 1 && g->ts_at < g->dyn_iters) ? g->ts_at : g->dyn_iters;
-    if (ts_at == 1) ts_rhs(g, z);
-    for (int it = 1; it < g->dyn_iters; it++) {
+    if (ts_at == 1 && !g->dyn_krylov) ts_rhs(g, z);
+    for (int it = 1; !g->dyn_krylov && it < g->dyn_iters; it++) {
         dyn_defect(g, z, g->dres);
         memset(g->zc, 0, sizeof(double) * N);
         dyn_solve(g, g->dres, g->zc);

@@ -85,3 +85,26 @@ def test_unrestated_mixing_rejected(built):
     oc.setPar("MIXP", 1.0)
     with pytest.raises(_lib.IemicError, match="neutral physics"):
         oc.computeRHS()
+
+
+@pytest.mark.gpu
+def test_device_vectors_outlive_close(built):
+    """Ocean.close() with DeviceVecs still alive (a continuation's saved state, say): the
+    pool is freed at once, the context stays valid for the live vectors and is destroyed
+    when the last one is released, so no device buffer leaks and none is freed twice."""
+    from iemic.ocean import Ocean
+    c = cf.preset("test6x6x4", mixing=0)
+    oc = Ocean(c)
+    ops = oc.vec_ops()
+    oc.setState(cf.synthetic_state(c, oc.landmask().reshape(c.l + 2, c.m + 2, c.n + 2), amp_ts=1e-3))
+    a = ops.state()
+    b = ops.copy(a)
+    del b                                       # back into the pool
+    assert len(oc._vpool) == 1 and oc._vlive == 1
+    oc.close()
+    assert oc._vpool == [] and oc._h is not None
+    assert ops.dot(a, a) > 0.0                  # the context still serves the live vector
+    del a
+    assert oc._h is None
+    with pytest.raises(_lib.IemicError):
+        ops.state()

@@ -455,3 +455,41 @@ def test_reused_preconditioner_after_new_jacobian(oracle_lib, nranks):
     nb = np.linalg.norm(b2)
     assert np.linalg.norm(b2 - o.spmv(ov2, s2)) <= 1e-8 * nb
     assert np.linalg.norm(b2 - o.spmv(ov2, s3)) <= 1e-8 * nb
+
+
+def test_mid_solve_mismatch_fails_fast():
+    """Fail-fast in the middle of a solve (comm.hip: every barrier of the in-process group,
+    every host wait of an RCCL context is bounded): both ranks run FGMRES without reaching its
+    tolerance, rank 1 with 10 steps, rank 0 with 40, so rank 0's collectives from step 11 on
+    have no partner.  Rank 0's solve returns an error within the 2 s bound instead of hanging,
+    and every rank returns."""
+    import time
+    from iemic import _lib
+    from iemic.ocean import Ocean
+    c = cf.preset("natl8", mixing=0)
+    L0 = golden_landm("natl8")
+    x = cf.synthetic_state(c, L0, amp_ts=1e-3)
+    b = cf.synthetic_vector(c, seed=9)
+
+    def fn(r, group):
+        sp = {"Preconditioner": 2, "FGMRES tolerance": 1e-30, "FGMRES restarts": 0,
+              "FGMRES iterations": 40 if r == 0 else 10}
+        oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=2, npx=1, solver_params=sp)
+        _lib.check(_lib.lib().iemic_set_comm_timeout(oc._h, 2.0), "set_comm_timeout")
+        oc.setState(x)
+        oc.computeJacobian()
+        t0 = time.perf_counter()
+        err = None
+        try:
+            oc.solve(b)
+        except _lib.IemicError as e:
+            err = str(e)
+        dt = time.perf_counter() - t0
+        oc.close()
+        return dict(msg=err, dt=dt)
+
+    t0 = time.perf_counter()
+    res = _run_bands(2, fn)
+    assert time.perf_counter() - t0 < 60.0
+    assert res[0]["msg"] is not None, res
+    assert res[0]["dt"] < 20.0, res
