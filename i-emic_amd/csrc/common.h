@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -271,6 +272,7 @@ struct Krylov {
     int mc = 0;
     int64_t nc = 0;
     DevBuf<double> Vc, rf, t, bp;
+    int zclean = 0;                  /* Z is zero on the identity rows of the current set-up */
 };
 
 constexpr int RED_BLOCKS = 1024;     /* partial-sum blocks of the reductions            */
@@ -372,6 +374,12 @@ inline int d2h(iemic_ctx* c, void* dst, const void* src, size_t bytes)
     DEV_SYNC(c);
     return 0;
 }
+/* p[0 .. n) = 0 by a kernel of the library.  Used instead of hipMemsetAsync on the solve
+ * path: the HIP runtime dispatches a memset as its own blit kernel, and rocprofv3's kernel
+ * tracer (rocprofiler-sdk 7.2) faulted inside its dispatch intercept when several host
+ * threads issued those concurrently (eight in-process band ranks) */
+__global__ void k_zero(double* __restrict__ p, int64_t n);
+inline int dev_zero(iemic_ctx* c, double* p, int64_t n);
 /* two timing events, destroyed on every return path */
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -388,6 +396,14 @@ struct EventPair {
 };
 /* Drains the stream when an entry point returns, also on error paths, so no kernel of
  * this context is still in flight when control goes back to the caller. */
+inline int dev_zero(iemic_ctx* c, double* p, int64_t n)
+{
+    if (n <= 0) return 0;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_zero, dim3(g), dim3(256), 0, c->stream, p, n);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
 struct StreamGuard {
     iemic_ctx* c;
     ~StreamGuard() { if (c && c->stream) (void)dev_wait(c, nullptr, "return"); }
@@ -461,7 +477,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt,
 int prec_compute(iemic_ctx* c, const iemic_krylov* opt);
 int prec_apply(iemic_ctx* c, const double* r, double* z);
 /* the block GS apply from a compressed input (6 rows per BlockGS::act cell, zero land rows) */
-int gs_apply_c(iemic_ctx* c, const double* rc, double* z);
+/* staged: rc is already in the block GS's planar right-hand side (k_dcgs_update) */
+int gs_apply_c(iemic_ctx* c, const double* rc, double* z, bool staged = false);
 /* repack the block GS's coefficient copies after a new Jacobian (BlockGS::coef_stale) */
 int gs_refresh(iemic_ctx* c);
 /* y = J x written compressed (rows of the active cells only; x full, halo current) */

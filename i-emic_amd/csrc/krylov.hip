@@ -398,6 +398,12 @@ int spmv_dyn_defect(iemic_ctx* c, const double* z, const double* r, const uint8_
 }
 
 /* ---- reductions / BLAS-1 ------------------------------------------------------------ */
+__global__ void k_zero(double* __restrict__ p, int64_t n)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        p[q] = 0.0;
+}
+
 
 __device__ __forceinline__ double block_sum(double v, double* sm)
 {
@@ -722,10 +728,16 @@ __global__ void __launch_bounds__(256) k_dcgs_coef(double* __restrict__ hb, int 
  * 1/beta (lagged normalisation) keeps every candidate at the scale of a normalised Arnoldi
  * vector, so its norm never compounds the earlier subdiagonals (no overflow / false breakdown
  * over long cycles). */
+/* rrP (the compressed basis with the block GS): the new candidate w -- the next step's
+ * preconditioner input -- also goes straight into the block GS's planar right-hand side
+ * (rows 2e, 2e + 1 of w are unknowns R, R + 1 of active cell act[2e / 6]), so the apply
+ * skips its entry kernel k_gs_rr_c */
 __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ V, int64_t ldv,
                                                      int nvec, const double* __restrict__ coef,
                                                      double* __restrict__ u, double* __restrict__ w,
-                                                     int64_t N)
+                                                     int64_t N, const int* __restrict__ act = nullptr,
+                                                     int64_t own0 = 0, int64_t ps = 0,
+                                                     double* __restrict__ rrP = nullptr)
 {
     /* two consecutive elements per lane (16-byte loads; N even), four basis vectors per step */
     constexpr int UN = 4;
@@ -763,7 +775,13 @@ __global__ void __launch_bounds__(256) k_dcgs_update(const double* __restrict__ 
         }
         const double2 ue = u2[e], we = w2[e];
         u2[e] = make_double2((ue.x - sux) * inv_beta, (ue.y - suy) * inv_beta);
-        w2[e] = make_double2((we.x - swx - gamma * ue.x) * inv_beta, (we.y - swy - gamma * ue.y) * inv_beta);
+        const double2 wn = make_double2((we.x - swx - gamma * ue.x) * inv_beta, (we.y - swy - gamma * ue.y) * inv_beta);
+        w2[e] = wn;
+        if (rrP) {
+            const int64_t a = e / 3, R = 2 * e - 6 * a, cell = own0 + act[a];
+            rrP[cell + R * ps] = wn.x;
+            rrP[cell + (R + 1) * ps] = wn.y;
+        }
     }
 }
 
@@ -950,6 +968,7 @@ static int ensure_krylov(iemic_ctx* c, int m, int64_t nc = 0)
     const int64_t N = c->nerows;
     int rc = 0;
     if (k.m < m || !k.Z.p) {
+        k.zclean = 0;
         k.V.free();                  /* sized by m: reallocated below when needed */
         rc |= k.Z.alloc((size_t)m * N);
         rc |= k.w.alloc(N);
@@ -1058,6 +1077,15 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     const int64_t NC = cmp ? NUN * gs.nact : 0;
     rc = ensure_krylov(c, m, NC);
     if (rc) return rc;
+    /* the staged applies (gs_apply_c after an update pass) leave the identity rows of the
+     * preconditioned vectors Z alone: zero them once per set-up (kr.zclean), the other
+     * solvers may have left values there */
+    if (cmp && !c->kr.zclean) {
+        if ((rc = dev_zero(c, c->kr.Z.p, (int64_t)m * NE))) return rc;
+        c->kr.zclean = 1;
+    } else if (!cmp) {
+        c->kr.zclean = 0;
+    }
     iemic_solve_info inf{};
     auto T0 = std::chrono::steady_clock::now();
     double* V = cmp ? nullptr : c->kr.V.p;
@@ -1085,7 +1113,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
     for (int q = 0; q < 6; q++) HIP_OK(hipEventCreate(&ev[q]));
     for (int q = 6; q < 8; q++) HIP_OK(hipEventCreateWithFlags(&evs.e[q], hipEventDisableTiming));
 
-    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
+    if ((rc = dev_zero(c, x, NE))) return rc;
     double bnorm = sqrt0(dot(c, b, b, 0));
     if (!std::isfinite(bnorm)) return nonfinite();
     if (!(bnorm > 0)) {
@@ -1228,8 +1256,10 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                     double* zj = Z + (int64_t)jj * NE;
                     HIP_OK(hipEventRecord(e[0], c->stream));
                     if (cmp) {
-                        /* the block GS reads the compressed u, the SpMV writes the compressed w */
-                        if ((rc2 = gs_apply_c(c, u, zj))) return rc2;
+                        /* the block GS reads the compressed u (staged into its planar right-hand
+                         * side by the previous update pass, jj > 0), the SpMV writes the
+                         * compressed w */
+                        if ((rc2 = gs_apply_c(c, u, zj, jj > 0))) return rc2;
                     } else if (opt->prec > 0) {
                         if ((rc2 = prec_apply(c, u - o, zj))) return rc2;
                     } else {
@@ -1259,7 +1289,8 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                 HIP_OK(hipEventRecord(evr[jj & 1], c->stream));
                 if (jj < m)
                     hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, Q, LQ, nv,
-                                       c->d_hbuf.p + RED_ROWS, u, wv, NQ);
+                                       c->d_hbuf.p + RED_ROWS, u, wv, NQ, cmp ? (const int*)gs.act.p : nullptr,
+                                       c->own0, (int64_t)c->next, cmp ? gs.rrP.p : nullptr);
                 return 0;
             };
             if ((rc = enqueue(0))) return rc;
@@ -1510,7 +1541,7 @@ int idrs(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, iemi
         if (!(nn > 0.0)) return nonfinite();
         hipLaunchKernelGGL(k_scale_copy, dim3(GR), dim3(256), 0, c->stream, Pi(j) + o, 1.0 / nn, Pi(j) + o, NL);
     }
-    HIP_OK(hipMemsetAsync(x, 0, sizeof(double) * NE, c->stream));
+    if ((rc = dev_zero(c, x, NE))) return rc;
     HIP_OK(hipMemcpyAsync(r, b, sizeof(double) * NE, hipMemcpyDeviceToDevice, c->stream));
     const double normb = sqrt0(dot(c, b, b, 0));
     if (!std::isfinite(normb)) return nonfinite();

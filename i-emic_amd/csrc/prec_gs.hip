@@ -3040,7 +3040,7 @@ static int mg_coarsest(iemic_ctx* c, int q)
     if (gs.mg_glob) {
         /* gather the bands' right-hand sides, own rows of X b */
         const int64_t ncl = N / 2;
-        HIP_OK(hipMemsetAsync(gs.mg_gvec.p, 0, sizeof(double) * gs.mg_gN, s));
+        if ((rc = dev_zero(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
         hipLaunchKernelGGL(k_mg_gput, dim3(blocks_for(ncl)), dim3(256), 0, s, gs.mg_b[q].p, ncl,
                            gs.mg_n[q], c->l, gs.mg_gGX, gs.mg_gI0, gs.mg_gJ0, gs.mg_gvec.p);
         if ((rc = allreduce_sum(c, gs.mg_gvec.p, gs.mg_gN))) return rc;
@@ -3485,6 +3485,9 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.vp = c->d_val.p;
     gs.coef_stale = 0;
     gs.cmp_ok = 1;
+    /* the staged applies write rrP on the active cells only, and leave z's identity rows */
+    HIP_OK(hipMemsetAsync(gs.rrP.p, 0, sizeof(double) * gs.rrP.n, c->stream));
+    c->kr.zclean = 0;
     if (c->l <= 64) {
         /* the Schur right-hand side as a linear form in rr (k_gs_ptil_rcol) */
         const int64_t ncolb = c->nloc / c->l;
@@ -3651,11 +3654,11 @@ int gs_time_parts(iemic_ctx* c, int nrep, double* us)
     return rc;
 }
 
-static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp);
+static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp, bool staged = false);
 int gs_apply(iemic_ctx* c, const double* r, double* z) { return gs_apply_impl(c, r, z, false); }
-int gs_apply_c(iemic_ctx* c, const double* rc, double* z) { return gs_apply_impl(c, rc, z, true); }
+int gs_apply_c(iemic_ctx* c, const double* rc, double* z, bool staged) { return gs_apply_impl(c, rc, z, true, staged); }
 
-static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
+static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp, bool staged)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -3692,8 +3695,11 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp)
     /* the halo rows of r hold the neighbours' identity-row values the couplings need (a
      * compressed r is zero on every identity row: no couplings, no exchange) */
     if (cmp) {
-        hipLaunchKernelGGL(k_gs_rr_c, dim3(gc), dim3(256), 0, s, gs.known.p, gs.cmap.p, r, z,
-                           aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
+        /* staged: the update pass wrote rrP (its land entries stay 0 since the set-up, the
+         * identity rows of z were zeroed per set-up: Krylov::zclean) */
+        if (!staged || aos_all)
+            hipLaunchKernelGGL(k_gs_rr_c, dim3(gc), dim3(256), 0, s, gs.known.p, gs.cmap.p, r, z,
+                               aos_all ? gs.rr.p : nullptr, aos_all ? 1 : 0, gs.rrP.p, L);
     } else {
         if (band && (rc = halo_exchange(c, const_cast<double*>(r), 1))) return rc;
         hipLaunchKernelGGL(k_gs_rr, dim3(gc), dim3(256), 0, s, gs.vp, gs.known.p, gs.kmask.p,

@@ -86,20 +86,25 @@ void dgetrf_(void) { fprintf(stderr, "thcm_ref: dgetrf_ stub called\n"); abort()
 void dgetri_(void) { fprintf(stderr, "thcm_ref: dgetri_ stub called\n"); abort(); }
 void dgecon_(void) { fprintf(stderr, "thcm_ref: dgecon_ stub called\n"); abort(); }
 
-/* Serial restatement of THCM.C:2704-2737: area-weighted surface mean of qfun2 over
- * ocean points of the top layer.  y points at y(1:m), landm at landm(0:n+1,0:m+1,0:l+1). */
+/* The C++ callback the Fortran forcing calls (THCM.C:2704-2737, serial case): the mean of
+ * qfun2 over the wet surface cells, weighted by cos(latitude).  Accumulated latitude by
+ * latitude, west to east, product before sum, as the reference does, so the sums are bitwise
+ * the reference's.  y: y(1:m); landm: landm(0:n+1, 0:m+1, 0:l+1), the surface is level l. */
 void thcm_forcing_integral_(double* qfun2, double* y, int* landm, double* fsint)
 {
-    int n = g_n, m = g_m, l = g_l;
-    double lsint = 0.0, lfsint = 0.0;
-    for (int j = 0; j < m; j++)
-        for (int i = 0; i < n; i++) {
-            int pl = (l * (m + 2) + (j + 1)) * (n + 2) + (i + 1);
-            int pq = j * n + i;
-            lfsint = qfun2[pq] * cos(y[j]) * (1 - landm[pl]) + lfsint;
-            lsint = cos(y[j]) * (1 - landm[pl]) + lsint;
+    const int nx = g_n, ny = g_m, top = g_l;
+    double area = 0.0, flux = 0.0;
+    for (int jj = 1; jj <= ny; jj++) {
+        const double w = cos(y[jj - 1]);
+        const int* wetrow = landm + ((size_t)top * (ny + 2) + jj) * (nx + 2);
+        const double* frow = qfun2 + (size_t)(jj - 1) * nx;
+        for (int ii = 1; ii <= nx; ii++) {
+            const double wet = (double)(1 - wetrow[ii]);
+            flux = frow[ii - 1] * w * wet + flux;
+            area = w * wet + area;
         }
-    *fsint = lfsint / lsint;
+    }
+    *fsint = flux / area;
 }
 
 /* ---- run a closure on a big-stack thread -------------------------------------- */
