@@ -309,7 +309,7 @@ __device__ __forceinline__ void dyn_partial(const double* __restrict__ val, cons
  * exists (a neighbour band).  alist: the owned tiles run over the active cells only (the
  * compressed basis' list, BlockGS::act; about half the cells are land at 2 degrees): d of the
  * other cells stays 0 (gs_compute zeroes it whenever the list changes). */
-__global__ void __launch_bounds__(256) k_spmv_dyn(SubLay X, const double* __restrict__ val,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_spmv_dyn(SubLay X, const double* __restrict__ val,
                                                   const double* __restrict__ z,
                                                   const double* __restrict__ r,
                                                   const uint8_t* __restrict__ knP,
