@@ -41,7 +41,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "i-emic_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PMC_TAG = "r05"         # bench_data/pmc_<tag>.json: per-kernel PMC bytes and trace times of a step
+PMC_TAG = "r06"         # bench_data/pmc_<tag>.json: per-kernel PMC bytes and trace times of a step
 
 
 def pmc_table(config: str):

@@ -1288,7 +1288,7 @@ int fgmres(iemic_ctx* c, const double* b, double* x, const iemic_krylov* opt, ie
                                    c->d_hbuf.p + RED_ROWS, c->h_red + (size_t)RED_ROWS * (jj & 1));
                 HIP_OK(hipEventRecord(evr[jj & 1], c->stream));
                 if (jj < m)
-                    hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, Q, LQ, nv,
+                    hipLaunchKernelGGL(k_dcgs_update, dim3((unsigned)std::min<int64_t>(4096, (NQ / 2 + 255) / 256)), dim3(256), 0, c->stream, Q, LQ, nv,
                                        c->d_hbuf.p + RED_ROWS, u, wv, NQ, cmp ? (const int*)gs.act.p : nullptr,
                                        c->own0, (int64_t)c->next, cmp ? gs.rrP.p : nullptr);
                 return 0;

@@ -28,6 +28,8 @@
 # | dyn_occ4 | defect capped at 4 waves per SIMD | rejected (slower) | round 5 (f500835) |
 # | dyn_occ5 | defect capped at 5 waves per SIMD | rejected (slower) | round 5 (f500835) |
 # | dyn_t | load-policy flips (temporal / non-temporal) | the tree keeps the faster policy of each | round 4 |
+# | upd_fit | DCGS2 update pass on a grid fitted to the compressed basis | adopted (117.3 -> 117.1 ms) | round 6 (54c7f0e) |
+# | dot1_e2 (re-test) | 2 elements per lane on the compressed basis (709 workgroups) | rejected (117.3 -> 118.7 ms) | round 6 (54c7f0e) |
 # | gemvw_t | load-policy flips (temporal / non-temporal) | the tree keeps the faster policy of each | round 4 |
 # | mg_unfused | coarse T/S levels by the unfused launches (k_mg_zl + k_mg_rc) | the fused k_mg_dn / k_mg_up adopted | round 5 (f500835) |
 # | mg_wg64 | z-line / restriction launches in 64-thread workgroups | adopted (T/S 112 → 103 µs per apply) | round 4 |
@@ -735,6 +737,20 @@ for p, old, nmax in (('csrc/schur_cr.hip', '    for (int c = threadIdx.x; c < M;
     }}"""
     s=s.replace(old,new)
     open(p,'w').write(s)
+PY
+}
+
+ab_upd_fit() {
+# DCGS2 update pass on a grid fitted to the compressed basis (one 16-byte element per lane)
+# instead of 1024 workgroups striding over it (1.4 elements per lane at 2 degrees)
+python3 - <<'PY'
+p='csrc/krylov.hip'
+s=open(p).read()
+old="hipLaunchKernelGGL(k_dcgs_update, dim3(1024), dim3(256), 0, c->stream, Q, LQ, nv,"
+new="hipLaunchKernelGGL(k_dcgs_update, dim3((unsigned)std::min<int64_t>(4096, (NQ / 2 + 255) / 256)), dim3(256), 0, c->stream, Q, LQ, nv,"
+assert old in s
+s=s.replace(old,new)
+open(p,'w').write(s)
 PY
 }
 
