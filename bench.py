@@ -113,6 +113,9 @@ def parse():
     p.add_argument("--ts-at", type=int, default=0,
                    help="form the T/S right-hand side after this many dynamics passes (0: the last); "
                         "earlier lets the T/S multigrid run on a second stream beside the rest")
+    p.add_argument("--schur-passes", type=int, default=0,
+                   help="only the first this many dynamics passes solve the Schur system "
+                        "(the later correction passes take pbar = 0; 0: every pass)")
     p.add_argument("--spmv-reps", type=int, default=0,
                    help="extra back-to-back (hot Infinity Cache) SpMV launches, reported apart")
     p.add_argument("--no-stream", action="store_true",
@@ -157,7 +160,7 @@ def cpu_baseline(cfg, L, x, args):
                "--mixing", str(args.mixing), "--tol", repr(args.tol), "--krylov", str(args.krylov),
                "--restarts", str(args.restarts), "--ts-sweeps", str(args.ts_sweeps),
                "--dyn-iters", str(args.dyn_iters), "--dyn-omega", repr(args.dyn_omega),
-               "--ts-mg", str(args.ts_mg), "--ts-at", str(args.ts_at),
+               "--ts-mg", str(args.ts_mg), "--ts-at", str(args.ts_at), "--schur-passes", str(args.schur_passes),
                "--cpu-samples", str(args.cpu_samples), "--cpu-warmup", str(args.cpu_warmup)]
         out = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, check=True, text=True).stdout
     return json.loads(out.strip().splitlines()[-1])
@@ -197,7 +200,7 @@ def cpu_baseline_run(cfg, L, x, args):
         t_jac = time.perf_counter() - t
         t = time.perf_counter()
         P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
-                        ts_mg=args.ts_mg, ts_at=args.ts_at)
+                        ts_mg=args.ts_mg, ts_at=args.ts_at, schur_passes=args.schur_passes)
         t_prec = time.perf_counter() - t
         t = time.perf_counter()
         dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=args.tol, m=args.krylov,
@@ -637,7 +640,8 @@ def bench_newton(args, R: Ranks):
           "Dyn iterations": args.dyn_iters,
           "Dyn damping": args.dyn_omega, "Dyn minimal residual": args.dyn_mr,
           "TS multigrid cycles": args.ts_mg, "Multigrid sweeps": args.mg_sweeps,
-          "Solver": args.solver, "IDR s": args.idr_s, "TS after dyn pass": args.ts_at}
+          "Solver": args.solver, "IDR s": args.idr_s, "TS after dyn pass": args.ts_at,
+          "Schur passes": args.schur_passes}
     oc = R.ocean(cfg, solver_params=sp)
     ranks_seen, transport = R.ranks_seen, R.transport
     L = oc.landmask().reshape(cfg.l + 2, cfg.m + 2, cfg.n + 2)
@@ -781,6 +785,7 @@ def bench_newton(args, R: Ranks):
                    "state": (f"branch (bench_data/{args.config}_cf05.npz, CF 0.5)" if state == "branch"
                              else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
+                   "schur_passes": args.schur_passes,
                    "parallelism": (f"decomp2d {lay['npx']}x{lay['npy']}" if world > 1 else "single"),
                    "transport": transport if world > 1 else "none",
                    "subdomain_rank0": {"cols": [lay["ib0"], lay["ib1"]], "rows": [lay["jb0"], lay["jb1"]]}},

@@ -196,6 +196,7 @@ struct BlockGS {
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
     int ts_at = 0;                   /* T/S rhs after this many passes (0: after all)     */
+    int schur_passes = 0;            /* passes from this one on skip the Schur solve (0: none) */
     /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local): level q
      * has mg_n[q] x mg_m[q] x l cells in the k-contiguous level layout (prec_gs.hip TsLev;
      * level 0 packed from tsoff/tsdiag) with 16 couplings, the 2x2 block, the z-line
@@ -231,6 +232,7 @@ struct BlockGS {
     DevBuf<uint8_t> knP;
     DevBuf<double> zP, rrP;
     DevBuf<double> colvT;            /* the Schur solution transposed (j * n + i)          */
+    DevBuf<double> colvZ;            /* zeros of colvT's size: pbar of a pass without Schur  */
     DevBuf<double> rr, bts, colv, colv2, colv_own; /* work: Schur rhs (colv_own; bands:  */
                                      /* summed into colv), solution colv2               */
     /* owned cells with a non-identity row (the rest: land, all six rows identity), ascending:

@@ -2323,6 +2323,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     rc |= gs.S9.alloc((size_t)9 * NC);
     rc |= gs.colv2.alloc(NC);
     rc |= gs.colvT.alloc(NC);
+    rc |= gs.colvZ.alloc(NC);
     rc |= gs.colv_own.alloc(NC);
     rc |= gs.colv.alloc(NC);
     rc |= gs.own_pos.alloc(NC);
@@ -2333,6 +2334,7 @@ int build_structure(iemic_ctx* c, const std::vector<double>& flags)
     }
     if ((rc = h2d(c, gs.col_of_ij.p, colid.data(), sizeof(int) * colid.size()))) return rc;
     if ((rc = h2d(c, gs.ij_of_col.p, ij_of_col.data(), sizeof(int) * NC))) return rc;
+    HIP_OK(hipMemsetAsync(gs.colvZ.p, 0, sizeof(double) * NC, c->stream));
     if ((rc = h2d(c, gs.pinned.p, pin.data(), NC))) return rc;
     if ((rc = h2d(c, gs.own_pos.p, own.data(), sizeof(int) * NC))) return rc;
     if ((rc = h2d(c, gs.ocol.p, ocol.data(), sizeof(int) * ocol.size()))) return rc;
@@ -3522,6 +3524,7 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
     gs.dyn_mr = opt ? (opt->dyn_mr != 0) : 0;
     gs.dyn_omega = opt && opt->dyn_omega > 0.0 ? opt->dyn_omega : 1.0;
     gs.ts_at = opt ? std::max(0, opt->ts_at) : 0;
+    gs.schur_passes = opt ? std::max(0, opt->schur_passes) : 0;
     if (gs.dyn_iters > 1 && gs.dres.n < (size_t)NE) {
         if (gs.dres.alloc(NE) || gs.zc.alloc(NE) || gs.dq.alloc(NE) || gs.dzero.alloc(NE) ||
             gs.dmr.alloc(2 * MR_NB + 2))
@@ -3541,8 +3544,10 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
  * preconditioner output (AoS), on the last pass */
 /* rr_halo: rr's halo rows already hold the neighbours' values (the bands' defect computed
  * them itself, spmv_dyn_defect) */
+/* schur = false: pbar = 0 (no Schur right-hand side reduction, no Schur solve; the later
+ * correction passes of BlockGS::schur_passes, the CPU twin's orc_gs_schur_passes) */
 static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0,
-                     double* zaos = nullptr, bool rr_halo = false)
+                     double* zaos = nullptr, bool rr_halo = false, bool schur = true)
 {
     BlockGS& gs = c->gs;
     const Lay L = lay_of(c);
@@ -3577,28 +3582,29 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
                            gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
     const double* sb = gs.colv_own.p;
-    if (band) {
+    const double* pbT = schur ? gs.colvT.p : gs.colvZ.p;
+    if (band && schur) {
         HIP_OK(hipMemcpyAsync(gs.colv.p, gs.colv_own.p, sizeof(double) * c->n * c->m,
                               hipMemcpyDeviceToDevice, s));
         if ((rc = allreduce_sum(c, gs.colv.p, c->n * c->m))) return rc;
         sb = gs.colv.p;
     }
-    if ((rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s, gs.colvT.p))) return rc;
+    if (schur && (rc = cr_solve(c, gs.cr, sb, gs.colv2.p, s, gs.colvT.p))) return rc;
     const bool al = gs.act.p && gs.nact > 0;
     const int64_t nown = al ? gs.nact : c->nloc;
     const unsigned gcu = (unsigned)((nown + (hrow ? (int64_t)c->l * c->nx : 0) + 255) / 256);
     hipLaunchKernelGGL(k_gs_uvp, dim3(gcu), dim3(256), 0, s, gs.vp, gs.knP.p, gs.uvinv.p,
-                       rr, gs.colvT.p, z, L, zo, omega, zaos, gsl, al ? gs.act.p : nullptr, nown);
+                       rr, pbT, z, L, zo, omega, zaos, gsl, al ? gs.act.p : nullptr, nown);
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* uv below the band */
     if (Pl == 16)
         hipLaunchKernelGGL(k_gs_pw_t<16>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.colvT.p, z, L, rr, zo, omega, zaos);
+                           pbT, z, L, rr, zo, omega, zaos);
     else if (Pl == 32)
         hipLaunchKernelGGL(k_gs_pw_t<32>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.colvT.p, z, L, rr, zo, omega, zaos);
+                           pbT, z, L, rr, zo, omega, zaos);
     else
         hipLaunchKernelGGL(k_gs_pw_t<64>, dim3(gct), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.colvT.p, z, L, rr, zo, omega, zaos);
+                           pbT, z, L, rr, zo, omega, zaos);
     return 0;
 }
 
@@ -3732,7 +3738,9 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp, boo
         if (band && (rc = dhalo ? halo_exchange_planar(c, zP, 4, ps, 2) : halo_exchange_planar(c, zP, NUN, ps, 1)))
             return rc;   /* w, p of the neighbours */
         if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p, dhalo))) return rc;
-        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last), dhalo))) return rc;   /* z += w zc */
+        const bool schur = gs.schur_passes <= 0 || it < gs.schur_passes;
+        if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last), dhalo, schur)))
+            return rc;   /* z += w zc */
         if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;
     }
     if (ts_at == gs.dyn_iters && (rc = ts())) return rc;

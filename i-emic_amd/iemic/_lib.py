@@ -58,7 +58,7 @@ class Krylov(C.Structure):
                 ("dyn_iters", C.c_int), ("method", C.c_int), ("ts_mg", C.c_int),
                 ("mg_sweeps", C.c_int), ("dyn_omega", C.c_double), ("dyn_mr", C.c_int),
                 ("idr_s", C.c_int), ("idr_angle", C.c_double), ("idr_replace", C.c_int),
-                ("ts_at", C.c_int)]
+                ("ts_at", C.c_int), ("schur_passes", C.c_int)]
 
 
 class SolveInfo(C.Structure):

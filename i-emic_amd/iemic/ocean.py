@@ -160,7 +160,8 @@ class Ocean:
               "Preconditioner": 2, "TS sweeps": 12, "Orthogonalization": "DCGS2",
               "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
               "Solver": "FGMRES", "IDR s": 4, "IDR angle": 0.7, "IDR replace residuals": False,
-              "Multigrid sweeps": 1, "TS after dyn pass": 0}
+              "Multigrid sweeps": 1, "TS after dyn pass": 0,
+              "Schur passes": 0}
         if solver_params:
             sp.update(solver_params)
         self.solver_params = sp
@@ -395,7 +396,8 @@ class Ocean:
                            int(sp["TS multigrid cycles"]), int(sp["Multigrid sweeps"]),
                            float(sp["Dyn damping"]), int(bool(sp["Dyn minimal residual"])),
                            int(sp["IDR s"]), float(sp["IDR angle"]),
-                           int(bool(sp["IDR replace residuals"])), int(sp["TS after dyn pass"]))
+                           int(bool(sp["IDR replace residuals"])), int(sp["TS after dyn pass"]),
+                           int(sp["Schur passes"]))
 
     def buildPreconditioner(self, force: bool = False) -> None:
         """Ocean::buildPreconditioner (Ocean.C:1360-1374): recompute only when flagged."""

@@ -41,6 +41,8 @@ typedef struct {
     double dyn_omega;
     double *dres, *zc;
     int dyn_krylov;                  /* 1: the dynamics passes as right-preconditioned GMRES */
+    int schur_passes;                /* passes from this one on skip the Schur solve (pbar = 0); 0: none */
+    int skip_schur;
     double *kv, *kz;                 /* its basis (dyn_iters + 1) and M_D^-1 images (dyn_iters) */
     void* mg;
 } gs_t;
@@ -393,9 +395,9 @@ static void dyn_solve(gs_t* g, const double* rr, double* z)
             if (kn[NUN * c + PP]) continue;
             s += g->pw[c] * (duv_uv(g, i, j, k, z) - rr[NUN * c + PP]);
         }
-        g->colv[q] = g->pinned[q] ? 0.0 : s;
+        g->colv[q] = (g->pinned[q] || g->skip_schur) ? 0.0 : s;
     }
-    {
+    if (!g->skip_schur) {
         const int ncol = g->ncol, bl = g->bl, bu = g->bu, W = 2 * bl + bu + 1;
         const double* ab = g->band;
         double* b = g->colv;
@@ -886,6 +888,10 @@ void orc_gs_ts_at(void* h, int ts_at)
  * dynamics block A_DD z_D = rr_D (from z_D = 0; classical Gram-Schmidt twice) instead of the
  * damped defect-correction passes (the reference accelerates its sub-solves by GMRESR,
  * TRIOS_BlockPreconditioner.C:1479-1611) */
+/* correction passes from schur_passes on (0: none) skip the exact Schur solve: the GPU's
+ * BlockGS::schur_passes (iemic_krylov.schur_passes, prec_gs.hip dyn_solve's schur flag) */
+void orc_gs_schur_passes(void* h, int k) { ((gs_t*)h)->schur_passes = k > 0 ? k : 0; }
+
 void orc_gs_dyn_krylov(void* h, int on)
 {
     gs_t* g = (gs_t*)h;
@@ -1004,7 +1010,9 @@ void orc_gs_apply(void* h, const double* r, double* z)
     for (int it = 1; !g->dyn_krylov && it < g->dyn_iters; it++) {
         dyn_defect(g, z, g->dres);
         memset(g->zc, 0, sizeof(double) * N);
+        g->skip_schur = g->schur_passes > 0 && it >= g->schur_passes;
         dyn_solve(g, g->dres, g->zc);
+        g->skip_schur = 0;
         for (int64_t row = 0; row < N; row++)
             if (row % NUN <= PP && !kn[row]) z[row] += g->dyn_omega * g->zc[row];
         if (it + 1 == ts_at) ts_rhs(g, z);

@@ -99,12 +99,14 @@ def test_subdomains_in_one_process(oracle_lib, name, nranks, npx):
     assert abs(res[0]["info"].norm_f1 - f1) <= 1e-9 * f1 + 1e-14 * f0
 
 
-@pytest.mark.parametrize("nranks,npx", [(2, 1), (8, 1), (4, 0), (8, 0)])
-def test_subdomains_global2_newton_mixing(oracle_lib, nranks, npx):
+@pytest.mark.parametrize("nranks,npx,schur_passes", [(2, 1, 0), (8, 1, 0), (4, 0, 0), (8, 0, 0),
+                                                     (4, 1, 2), (8, 0, 2)])
+def test_subdomains_global2_newton_mixing(oracle_lib, nranks, npx, schur_passes):
     """The bench workload split as the multi-GPU bench splits it (global 2 deg, Mixing = 1,
     default solver: block GS with 4 damped defect passes, T/S multigrid per subdomain;
-    npx = 0: the reference's Decomp2D, 2 x 2 and 4 x 2): the distributed Newton step
-    converges and solves the linearised system of the whole problem."""
+    npx = 0: the reference's Decomp2D, 2 x 2 and 4 x 2; schur_passes 2: the last two passes
+    without the Schur reduction): the distributed Newton step converges and solves the
+    linearised system of the whole problem."""
     from iemic.ocean import Ocean
     c = cf.preset("global2", mixing=1)
     L0 = cf.init_landmask(c, cf.landmask(c))
@@ -116,7 +118,8 @@ def test_subdomains_global2_newton_mixing(oracle_lib, nranks, npx):
     def fn(r, group):
         from iemic import _lib
         oc = Ocean(c, landm=L0, local_group=group, rank=r, nranks=nranks, npx=npx,
-                   solver_params={"FGMRES iterations": 100, "FGMRES restarts": 20})
+                   solver_params={"FGMRES iterations": 100, "FGMRES restarts": 20,
+                                  "Schur passes": schur_passes})
         oc.setState(x)
         info = oc.newtonStep()
         lay = oc.layout()

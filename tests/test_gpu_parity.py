@@ -183,6 +183,29 @@ def test_block_gs_early_ts_matches_cpu(oracle_lib, Ocean, name, ts_at):
     assert np.max(np.abs(z0 - zc)) > 1e-6 * np.max(np.abs(zc))
 
 
+@pytest.mark.parametrize("name,sp_k", [("global4", 1), ("global4", 2), ("global2", 2), ("global2", 3)])
+def test_block_gs_schur_passes_matches_cpu(oracle_lib, Ocean, name, sp_k):
+    """Only the first sp_k of the 4 dynamics passes solve the Schur system (the later
+    correction passes take pbar = 0, no Schur reduction or solve) == the CPU twin with the
+    same schur_passes; and it differs from every pass solving it."""
+    c, oc, o, L = make(Ocean, oracle_lib, name, mixing=1,
+                       solver_params={"Preconditioner": 2, "Schur passes": sp_k})
+    sp = oc.solver_params
+    x = cf.synthetic_state(c, L, amp_ts=1e-3)
+    oc.setState(x)
+    oc.computeJacobian()
+    oc.buildPreconditioner(force=True)
+    ov, _ = o.jacobian(x)
+    kw = dict(dyn_iters=sp["Dyn iterations"], dyn_omega=sp["Dyn damping"], ts_mg=sp["TS multigrid cycles"])
+    r = cf.synthetic_vector(c, seed=3)
+    z = oc.applyPrecon(r)
+    zc = oracle_lib.BlockGS(o, ov, 3, schur_passes=sp_k, **kw).apply(r)
+    z0 = oracle_lib.BlockGS(o, ov, 3, **kw).apply(r)
+    assert np.all(np.isfinite(z))
+    assert np.max(np.abs(z - zc)) <= 1e-8 * np.max(np.abs(zc))
+    assert np.max(np.abs(z0 - zc)) > 1e-6 * np.max(np.abs(zc))
+
+
 @pytest.mark.parametrize("mixing", [0, 1])
 def test_block_gs_apply_global2(oracle_lib, Ocean, mixing):
     """The same at the bench size (2 degrees, 192x76x16, 8,996 water columns: 192 blocks of
