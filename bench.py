@@ -113,7 +113,7 @@ def parse():
     p.add_argument("--ts-at", type=int, default=0,
                    help="form the T/S right-hand side after this many dynamics passes (0: the last); "
                         "earlier lets the T/S multigrid run on a second stream beside the rest")
-    p.add_argument("--schur-passes", type=int, default=0,
+    p.add_argument("--schur-passes", type=int, default=2,
                    help="only the first this many dynamics passes solve the Schur system "
                         "(the later correction passes take pbar = 0; 0: every pass)")
     p.add_argument("--spmv-reps", type=int, default=0,
@@ -448,7 +448,7 @@ def cpu_continuation_sample(cfg, oc, cont, saved, its, args):
     t_jac = time.perf_counter() - t
     t = time.perf_counter()
     P = orc.BlockGS(o, val, args.ts_sweeps, dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega,
-                    ts_mg=args.ts_mg)
+                    ts_mg=args.ts_mg, schur_passes=args.schur_passes)
     t_prec = time.perf_counter() - t
     t = time.perf_counter()
     _, k, _, _ = P.fgmres(np.ascontiguousarray(-F), tol=1e-30, m=args.cpu_iters, maxit=args.cpu_iters)
@@ -562,7 +562,7 @@ def bench_coupled(args, R: Ranks):
         cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         cb = orc.coupled_newton_step(cfg, L, xo, xa, comb, ao.COUPLED_RUN_PARAMS, ts_sweeps=args.ts_sweeps,
                                      dyn_iters=args.dyn_iters, dyn_omega=args.dyn_omega, ts_mg=args.ts_mg,
-                                     tol=args.tol, m=args.krylov, maxit=args.krylov * (args.restarts + 1))
+                                     schur_passes=args.schur_passes, tol=args.tol, m=args.krylov, maxit=args.krylov * (args.restarts + 1))
         out["cpu_baseline"] = {
             "value": round(cb["total"] * 1e3, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
             "sample": (f"timed, one full coupled Newton step on the CPU restatements ({cores} OpenMP threads "

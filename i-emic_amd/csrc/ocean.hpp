@@ -80,7 +80,7 @@ class Ocean {
         rhs_ = std::make_shared<Vector>(N_);
         sol_ = std::make_shared<Vector>(N_);
         /* Belos defaults of Ocean::getDefaultInitParameters (Ocean.C:2232-2237) */
-        krylov_ = iemic_krylov{1e-8, 500, 0, 2, 12, 0, 4, /*method FGMRES*/ 0, 1, 1, 0.95, 0, 4, 0.7, 0, 0, 0};
+        krylov_ = iemic_krylov{1e-8, 500, 0, 2, 12, 0, 4, /*method FGMRES*/ 0, 1, 1, 0.95, 0, 4, 0.7, 0, 0, /*Schur passes*/ 2};
     }
     ~Ocean() { iemic_destroy(ctx_); }
     Ocean(const Ocean&) = delete;

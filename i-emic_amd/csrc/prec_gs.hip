@@ -991,7 +991,8 @@ __global__ void k_rcol_w(const uint8_t* __restrict__ known, const double* __rest
 /* gsl (latitude bands): the tiles of the halo rows jl = -1, mb (inside the grid) compute
  * ptil there too, with the W row's couplings from the halo-filled gslot (the owned Jacobian
  * has no halo rows), so that the U/V kernel needs no exchange of ptil */
-template <int LP>
+/* RC = false: ptil only (a pass without the Schur solve needs no right-hand side for it) */
+template <int LP, bool RC = true>
 __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict__ val,
                                                        const uint8_t* __restrict__ knP,
                                                        const double* __restrict__ rcol,
@@ -1045,31 +1046,36 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
     bool pa = false;
     int64_t cell = 0;
     if (on) {
-        int64_t nc9[9];
-#pragma unroll
-        for (int e = 0; e < 9; e++) {
-            int i2 = i + e % 3 - 1, j2 = j + e / 3 - 1;
-            if (!hnb(i2, j2, n, m, periodic)) { i2 = i; j2 = j; }
-            nc9[e] = ecell(L, i2, j2, k);
-        }
-        cell = nc9[4];
-        const double* R = rcol + (int64_t)k * ncolb + t;
-        const int64_t es = (int64_t)l * ncolb;
+        cell = ecell(L, i, j, k);
         const uint8_t kp = knP[PL(cell, PP)], kw = knP[PL(cell, WW)];
         pa = !kp;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        if constexpr (RC) {
+            int64_t nc9[9];
 #pragma unroll
-        for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[PL(nc9[e], WW)];
-        if (pa) {
-            /* the corner and own-P coefficients vanish on an inactive P row (land): not read */
-#pragma unroll
-            for (int q4 = 0; q4 < 4; q4++) {
-                /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
-                const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
-                a1 += R[(9 + q4) * es] * rr[PL(qc, UU)];
-                a2 += R[(13 + q4) * es] * rr[PL(qc, VV)];
+            for (int e = 0; e < 9; e++) {
+                int i2 = i + e % 3 - 1, j2 = j + e / 3 - 1;
+                if (!hnb(i2, j2, n, m, periodic)) { i2 = i; j2 = j; }
+                nc9[e] = ecell(L, i2, j2, k);
             }
-            a2 += R[17 * es] * rr[PL(cell, PP)];
+            const double* R = rcol + (int64_t)k * ncolb + t;
+            const int64_t es = (int64_t)l * ncolb;
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int e = 0; e < 9; e++) a0 += R[e * es] * rr[PL(nc9[e], WW)];
+            if (pa) {
+                /* the corner and own-P coefficients vanish on an inactive P row (land): not read */
+#pragma unroll
+                for (int q4 = 0; q4 < 4; q4++) {
+                    /* corner q4 = (i - (q4 & 1), j - (q4 >> 1)): neighbour (1 - (q4 >> 1)) * 3 + 1 - (q4 & 1) */
+                    const int64_t qc = nc9[(1 - ((q4 >> 1) & 1)) * 3 + 1 - (q4 & 1)];
+                    a1 += R[(9 + q4) * es] * rr[PL(qc, UU)];
+                    a2 += R[(13 + q4) * es] * rr[PL(qc, VV)];
+                }
+                a2 += R[17 * es] * rr[PL(cell, PP)];
+            }
+            v = a0 + (a1 + a2);
+        }
+        if (pa) {
             if (k < l - 1 && !kw) {
                 const double g0 = val[(int64_t)S_WP0 * ncell + (cell - L.own0)];
                 const double g1 = val[(int64_t)S_WP1 * ncell + (cell - L.own0)];
@@ -1079,19 +1085,18 @@ __global__ void __launch_bounds__(1024) k_gs_ptil_rcol(const double* __restrict_
                 }
             }
         }
-        v = a0 + (a1 + a2);
     }
     if (k < LP) {
         sA[k][ii] = A;
         sB[k][ii] = B;
-        sv[k][ii] = v;
+        if constexpr (RC) sv[k][ii] = v;
     }
     __syncthreads();
     if (!on) return;
     double p = 0.0;
     for (int kk = l - 1; kk >= k; kk--) p = sA[kk][ii] + sB[kk][ii] * p;
     if (pa) z[PL(cell, PP)] = p;
-    if (k == 0) {
+    if (RC && k == 0) {
         const int q = ocol[j * n + i];
         double s = 0.0;
         for (int kk = 0; kk < l; kk++) s += sv[kk][ii];
@@ -3571,15 +3576,13 @@ static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nul
     const double* gsl = hrow ? gs.gslot.p : nullptr;
     const unsigned gcth = hrow ? xcd_grid(((c->nx + cti - 1) / cti) * (ncolb / c->nx + 2)) : gct;
     if (band && !rr_halo && (rc = halo_exchange_planar(c, const_cast<double*>(rr), NUN, ps, 1))) return rc;   /* rr around the band */
-    if (Pl == 16)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<16>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
-    else if (Pl == 32)
-        hipLaunchKernelGGL(k_gs_ptil_rcol<32>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
-    else
-        hipLaunchKernelGGL(k_gs_ptil_rcol<64>, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p,
-                           gs.rcol.p, rr, z, gs.ocol.p, gs.colv_own.p, L, gsl);
+    {
+        auto kp = Pl == 16 ? (schur ? k_gs_ptil_rcol<16, true> : k_gs_ptil_rcol<16, false>)
+                : Pl == 32 ? (schur ? k_gs_ptil_rcol<32, true> : k_gs_ptil_rcol<32, false>)
+                           : (schur ? k_gs_ptil_rcol<64, true> : k_gs_ptil_rcol<64, false>);
+        hipLaunchKernelGGL(kp, dim3(gcth), bct, 0, s, gs.vp, gs.knP.p, gs.rcol.p, rr, z, gs.ocol.p,
+                           gs.colv_own.p, L, gsl);
+    }
     if (band && !hrow && (rc = halo_exchange_planar(c, z, NUN, ps, 1))) return rc;   /* ptil above the band */
     const double* sb = gs.colv_own.p;
     const double* pbT = schur ? gs.colvT.p : gs.colvZ.p;

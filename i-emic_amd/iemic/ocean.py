@@ -161,7 +161,7 @@ class Ocean:
               "Dyn iterations": 4, "Dyn damping": 0.95, "Dyn minimal residual": False, "TS multigrid cycles": 1,
               "Solver": "FGMRES", "IDR s": 4, "IDR angle": 0.7, "IDR replace residuals": False,
               "Multigrid sweeps": 1, "TS after dyn pass": 0,
-              "Schur passes": 0}
+              "Schur passes": 2}
         if solver_params:
             sp.update(solver_params)
         self.solver_params = sp

@@ -605,7 +605,7 @@ class BlockILU:
 # coupled ocean + atmosphere Newton step on the CPU (CoupledModel.C, bench cpu_baseline)
 
 def coupled_newton_step(cfg, landm, xo, xa, comb, atm_params, ts_sweeps=12, dyn_iters=4,
-                        dyn_omega=0.95, ts_mg=1, tol=1e-8, m=100, maxit=600):
+                        dyn_omega=0.95, ts_mg=1, tol=1e-8, m=100, maxit=600, schur_passes=0):
     """One Newton step of CoupledModel (solving scheme 'C', preconditioning 'F') on the CPU
     restatements: synchronize (Ocean::synchronize(atmos): T, q, A, dimensional P over water,
     CommPars; Atmosphere: SST), F and J of the ocean (thcm_oracle.c in coupled mode) and of
@@ -652,7 +652,8 @@ def coupled_newton_step(cfg, landm, xo, xa, comb, atm_params, ts_sweeps=12, dyn_
     A = sp.bmat([[Jo, Coa], [Cao, Ja]]).tocsr()
     t_jac = time.perf_counter() - t
     t = time.perf_counter()
-    G = BlockGS(o, val, ts_sweeps, dyn_iters=dyn_iters, dyn_omega=dyn_omega, ts_mg=ts_mg)
+    G = BlockGS(o, val, ts_sweeps, dyn_iters=dyn_iters, dyn_omega=dyn_omega, ts_mg=ts_mg,
+                schur_passes=schur_passes)
     lu = spla.splu(Ja)
     t_prec = time.perf_counter() - t
 
