@@ -142,17 +142,68 @@ def parse():
     return p.parse_args()
 
 
+def quiet_cores(n, dt=0.5):
+    """n CPUs of this process's affinity mask on n distinct physical cores, the least busy
+    ones over dt seconds of /proc/stat (a shared host's other jobs load some cores: pinning the
+    baseline's threads to cores 0..n-1 made its samples spread by 26 %).  Returns (cpus, the
+    busiest chosen core's busy fraction), or (None, None) where /proc is not readable."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+
+        def stat():
+            out = {}
+            with open("/proc/stat") as f:
+                for ln in f:
+                    if ln.startswith("cpu") and ln[3].isdigit():
+                        a = ln.split()
+                        v = [int(t) for t in a[1:]]
+                        out[int(a[0][3:])] = (v[3] + v[4], sum(v))
+            return out
+
+        s0 = stat()
+        time.sleep(dt)
+        s1 = stat()
+        busy = {}
+        for c in aff:
+            if c in s0 and c in s1:
+                tot = s1[c][1] - s0[c][1]
+                busy[c] = 1.0 - (s1[c][0] - s0[c][0]) / tot if tot > 0 else 0.0
+        core = {}
+        for c in busy:
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                    sib = f.read().strip()
+            except OSError:
+                sib = str(c)
+            core.setdefault(sib, []).append(c)
+        # a core's load is its busiest sibling's; one CPU (the lowest sibling) per core
+        ranked = sorted(((max(busy[c] for c in cs), min(cs)) for cs in core.values()))
+        if len(ranked) < n:
+            return None, None
+        pick = ranked[:n]
+        return sorted(c for _, c in pick), round(max(b for b, _ in pick), 3)
+    except (OSError, ValueError, AttributeError):
+        return None, None
+
+
 def cpu_baseline(cfg, L, x, args):
     """The CPU baseline of the Newton line (cpu_baseline_run), in a child process started
     after the GPU work: a fresh interpreter that loads numpy and the oracle only (no torch, no
     HIP), so its OpenMP runtime starts with the binding below and no other thread pool shares
-    the cores.  OMP_PROC_BIND=close, OMP_PLACES=cores (unless the caller set them): one thread
-    per core of the process's affinity mask, pinned for the whole run."""
+    the cores.  OMP_PROC_BIND=close over explicit places: one thread per physical core, the
+    OMP_NUM_THREADS least busy cores of the affinity mask (quiet_cores), pinned for the whole
+    run (OMP_PLACES=cores when /proc cannot tell, or when the caller set OMP_PLACES)."""
     import subprocess
     import tempfile
     env = dict(os.environ)
     env.setdefault("OMP_PROC_BIND", "close")
-    env.setdefault("OMP_PLACES", "cores")
+    if "OMP_PLACES" not in env:
+        cpus, load = quiet_cores(int(env.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        if cpus:
+            env["OMP_PLACES"] = ",".join("{%d}" % c for c in cpus)
+            env["IEMIC_CPU_PICK"] = f"{len(cpus)} least busy cores (busiest {load:.0%} over 0.5 s before)"
+        else:
+            env["OMP_PLACES"] = "cores"
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "state.npz")
         np.savez(path, x=x, L=L)
@@ -185,7 +236,9 @@ def cpu_baseline_run(cfg, L, x, args):
     warm-ups); the value is their median."""
     from oracle import oracle as orc
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    bind = f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}, OMP_PLACES={os.environ.get('OMP_PLACES', 'unset')}"
+    places = os.environ.get('OMP_PLACES', 'unset')
+    pick = os.environ.get("IEMIC_CPU_PICK")
+    bind = f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}, OMP_PLACES={places if not pick else pick}"
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     o = orc.Oracle(cfg.ref_dict(), L, cfg.par_list())
     samples = []
@@ -210,13 +263,16 @@ def cpu_baseline_run(cfg, L, x, args):
         if it >= nwarm:
             samples.append(time.perf_counter() - T0)
         del P
-    ms = sorted(v * 1e3 for v in samples)
+    order = [v * 1e3 for v in samples]
+    ms = sorted(order)
     med = float(np.median(ms))
+    q1, q3 = (float(v) for v in np.percentile(ms, [25, 75]))
     return {
         "value": round(med, 1), "unit": "ms/Newton-step", "cores": cores, "kind": "port",
-        "samples_ms": [round(v, 1) for v in ms], "spread_ms": round(ms[-1] - ms[0], 1),
-        "spread_frac": round((ms[-1] - ms[0]) / med, 4), "warmup": nwarm,
-        "binding": bind, "affinity_cpus": aff,
+        "samples_ms": [round(v, 1) for v in ms], "samples_in_order_ms": [round(v, 1) for v in order],
+        "spread_ms": round(ms[-1] - ms[0], 1),
+        "spread_frac": round((ms[-1] - ms[0]) / med, 4), "iqr_frac": round((q3 - q1) / med, 4),
+        "warmup": nwarm, "binding": bind, "places": places, "affinity_cpus": aff,
         "sample": (f"median of {len(ms)} timed full Newton steps after {nwarm} untimed warm-up steps "
                    f"on the oracle C port (OpenMP {cores} threads, {bind}; a child process without "
                    f"torch), same state and algorithm; last: F {t_rhs*1e3:.0f} ms, "
@@ -414,7 +470,7 @@ def bench_continuation(args, R: Ranks):
            "comm": {"per_fgmres_step": {k: round(v / (its_total * args.steps), 2) for k, v in comm.items()},
                     "rank": R.rank},
            "continuation": {"rc": rc, "newton_iters": cont.newtonIter, "par": cont.par,
-                            "norm_f": cont.normRHStest, "fgmres_iters": its,
+                            "norm_f": cont.normRHStest, "norm_rhs": cont.normRHS, "fgmres_iters": its,
                             "solve_ms": [round(s.t_total_ms, 1) for s in sv],
                             "vectors": "device (iemic_vec_*, summed over the ranks)"},
            "roofline": {"kernel": "k_spmv7 (1-degree operator, rank 0's rows, HIP events, 20 back-to-back launches)",
