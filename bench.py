@@ -114,8 +114,8 @@ def parse():
                    help="form the T/S right-hand side after this many dynamics passes (0: the last); "
                         "earlier lets the T/S multigrid run on a second stream beside the rest")
     p.add_argument("--schur-passes", type=int, default=2,
-                   help="only the first this many dynamics passes solve the Schur system "
-                        "(the later correction passes take pbar = 0; 0: every pass)")
+                   help="this many dynamics passes solve the Schur system: the first k - 1 and the last "
+                        "(the others take pbar = 0; 0: every pass)")
     p.add_argument("--spmv-reps", type=int, default=0,
                    help="extra back-to-back (hot Infinity Cache) SpMV launches, reported apart")
     p.add_argument("--no-stream", action="store_true",

@@ -196,7 +196,7 @@ struct BlockGS {
     int dyn_mr = 0;                  /* 1: minimal-residual step length per correction   */
     double dyn_omega = 1.0;          /* fixed step of the correction passes (dyn_mr = 0) */
     int ts_at = 0;                   /* T/S rhs after this many passes (0: after all)     */
-    int schur_passes = 0;            /* passes from this one on skip the Schur solve (0: none) */
+    int schur_passes = 0;            /* passes solving the Schur system: first k-1 + last (0: all) */
     /* T/S aggregation multigrid (2x2 horizontal aggregates, full depth, band-local): level q
      * has mg_n[q] x mg_m[q] x l cells in the k-contiguous level layout (prec_gs.hip TsLev;
      * level 0 packed from tsoff/tsdiag) with 16 couplings, the 2x2 block, the z-line

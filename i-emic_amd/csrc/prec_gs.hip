@@ -3549,8 +3549,18 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
  * preconditioner output (AoS), on the last pass */
 /* rr_halo: rr's halo rows already hold the neighbours' values (the bands' defect computed
  * them itself, spmv_dyn_defect) */
-/* schur = false: pbar = 0 (no Schur right-hand side reduction, no Schur solve; the later
- * correction passes of BlockGS::schur_passes, the CPU twin's orc_gs_schur_passes) */
+/* schur = false: pbar = 0 (no Schur right-hand side reduction, no Schur solve; the passes
+ * gs_pass_schur leaves out) */
+/* does dynamics pass it (0 .. dyn_iters - 1) solve the Schur system?  schur_passes k: the first
+ * k - 1 passes and the last (k = 1: the first only; 0 or >= dyn_iters: every pass).  The twin
+ * at 2 degrees: every pass 203 FGMRES steps; the first and the last 203; the first two 207;
+ * the first and the third 205; the first only 300 (profiles/r06_prec_study.md) */
+static bool gs_pass_schur(const BlockGS& gs, int it)
+{
+    const int k = gs.schur_passes, n = gs.dyn_iters;
+    return it == 0 || k <= 0 || k >= n || (k >= 2 && (it < k - 1 || it == n - 1));
+}
+
 static int dyn_solve(iemic_ctx* c, const double* rr, double* z, double* zo = nullptr, double omega = 0.0,
                      double* zaos = nullptr, bool rr_halo = false, bool schur = true)
 {
@@ -3741,7 +3751,7 @@ static int gs_apply_impl(iemic_ctx* c, const double* r, double* z, bool cmp, boo
         if (band && (rc = dhalo ? halo_exchange_planar(c, zP, 4, ps, 2) : halo_exchange_planar(c, zP, NUN, ps, 1)))
             return rc;   /* w, p of the neighbours */
         if ((rc = spmv_dyn_defect(c, zP, gs.rrP.p, gs.knP.p, gs.dres.p, dhalo))) return rc;
-        const bool schur = gs.schur_passes <= 0 || it < gs.schur_passes;
+        const bool schur = gs_pass_schur(gs, it);
         if ((rc = dyn_solve(c, gs.dres.p, gs.zc.p, zP, gs.dyn_omega, zaos_of(last), dhalo, schur)))
             return rc;   /* z += w zc */
         if (it + 1 == ts_at && it + 1 < gs.dyn_iters && (rc = ts())) return rc;

@@ -101,9 +101,10 @@ typedef struct {
                                  /* many dynamics passes (0: after the last); earlier, */
                                  /* the T/S multigrid runs on a second stream beside   */
                                  /* the remaining passes (one rank)                    */
-    int schur_passes;            /* block GS: only the first this many dynamics passes */
-                                 /* solve the 2-D Schur system exactly, the later      */
-                                 /* correction passes take pbar = 0 (0: every pass)     */
+    int schur_passes;            /* block GS: this many of the dynamics passes solve   */
+                                 /* the 2-D Schur system exactly, the first k - 1 and  */
+                                 /* the last (k = 1: the first); the others take       */
+                                 /* pbar = 0 (0 or >= dyn_iters: every pass)           */
 } iemic_krylov;
 
 typedef struct {

@@ -483,6 +483,7 @@ def _load_gs():
         lib.orc_gs_ts_at.argtypes = [C.c_void_p, C.c_int]
         lib.orc_gs_dyn_krylov.argtypes = [C.c_void_p, C.c_int]
         lib.orc_gs_schur_passes.argtypes = [C.c_void_p, C.c_int]
+        lib.orc_gs_schur_mask.argtypes = [C.c_void_p, C.c_int]
         lib.orc_fgmres_gs.argtypes = [C.c_int, P64, PI, PD, C.c_void_p, PD, PD, C.c_double,
                                       C.c_int, C.c_int, PD, PD]
         lib._gs_ready = True
@@ -494,7 +495,7 @@ class BlockGS:
 
     def __init__(self, o: "Oracle", val, ts_sweeps: int = 3, dyn_iters: int = 1,
                  dyn_omega: float = 1.0, ts_mg: int = 0, ts_at: int = 0, dyn_krylov: int = 0,
-                 schur_passes: int = 0):
+                 schur_passes: int = 0, schur_mask: int = 0):
         """ts_sweeps plain T/S sweeps, or (ts_mg > 0) the GPU's default variant: dyn_iters
         defect-correction passes of step dyn_omega on the dynamics block and ts_mg
         aggregation-multigrid V-cycles with z-line smoothing on the T/S block; the T/S
@@ -516,6 +517,7 @@ class BlockGS:
         lib.orc_gs_ts_at(self.h, ts_at)
         lib.orc_gs_dyn_krylov(self.h, dyn_krylov)
         lib.orc_gs_schur_passes(self.h, schur_passes)
+        lib.orc_gs_schur_mask(self.h, schur_mask)   # study: which correction passes solve it
         self.ncol = lib.orc_gs_ncol(self.h)
         self.band = lib.orc_gs_band(self.h)
 

@@ -41,7 +41,8 @@ typedef struct {
     double dyn_omega;
     double *dres, *zc;
     int dyn_krylov;                  /* 1: the dynamics passes as right-preconditioned GMRES */
-    int schur_passes;                /* passes from this one on skip the Schur solve (pbar = 0); 0: none */
+    int schur_passes;                /* passes that solve the Schur system: the first k - 1 and the last (0: all) */
+    int schur_mask;                  /* study: bit k set = correction pass k solves it (0: schur_passes decides) */
     int skip_schur;
     double *kv, *kz;                 /* its basis (dyn_iters + 1) and M_D^-1 images (dyn_iters) */
     void* mg;
@@ -888,9 +889,11 @@ void orc_gs_ts_at(void* h, int ts_at)
  * dynamics block A_DD z_D = rr_D (from z_D = 0; classical Gram-Schmidt twice) instead of the
  * damped defect-correction passes (the reference accelerates its sub-solves by GMRESR,
  * TRIOS_BlockPreconditioner.C:1479-1611) */
-/* correction passes from schur_passes on (0: none) skip the exact Schur solve: the GPU's
- * BlockGS::schur_passes (iemic_krylov.schur_passes, prec_gs.hip dyn_solve's schur flag) */
+/* the exact Schur solve in schur_passes of the dynamics passes only: the first k - 1 and the
+ * last (k = 1: the first; 0 or >= dyn_iters: all); the others take pbar = 0.  The GPU's
+ * BlockGS::schur_passes (iemic_krylov.schur_passes, prec_gs.hip gs_pass_schur) */
 void orc_gs_schur_passes(void* h, int k) { ((gs_t*)h)->schur_passes = k > 0 ? k : 0; }
+void orc_gs_schur_mask(void* h, int mask) { ((gs_t*)h)->schur_mask = mask; }
 
 void orc_gs_dyn_krylov(void* h, int on)
 {
@@ -1010,7 +1013,13 @@ void orc_gs_apply(void* h, const double* r, double* z)
     for (int it = 1; !g->dyn_krylov && it < g->dyn_iters; it++) {
         dyn_defect(g, z, g->dres);
         memset(g->zc, 0, sizeof(double) * N);
-        g->skip_schur = g->schur_passes > 0 && it >= g->schur_passes;
+        {
+            /* schur_passes k: the first k - 1 passes and the last solve it (k = 1: the first
+             * only; 0 or >= dyn_iters: every pass) -- the GPU's gs_pass_schur */
+            const int k = g->schur_passes, last = it + 1 == g->dyn_iters;
+            const int solve = k <= 0 || k >= g->dyn_iters || (k >= 2 && (it < k - 1 || last));
+            g->skip_schur = g->schur_mask ? !((g->schur_mask >> it) & 1) : !solve;
+        }
         dyn_solve(g, g->dres, g->zc);
         g->skip_schur = 0;
         for (int64_t row = 0; row < N; row++)

@@ -31,7 +31,7 @@ def main():
         t = time.perf_counter()
         P = orc.BlockGS(o, val, 12, dyn_iters=v.get("dyn_iters", 4), dyn_omega=v.get("dyn_omega", 0.95),
                         ts_mg=v.get("ts_mg", 1), dyn_krylov=v.get("dyn_krylov", 0),
-                        schur_passes=v.get("schur_passes", 0))
+                        schur_passes=v.get("schur_passes", 0), schur_mask=v.get("schur_mask", 0))
         dx, its, rel, _ = P.fgmres(np.ascontiguousarray(-F), tol=1e-8, m=90, maxit=90 * 21)
         print(json.dumps({"config": name, **v, "fgmres_steps": its, "rel": rel,
                           "s": round(time.perf_counter() - t, 1)}), flush=True)

@@ -104,8 +104,8 @@ def test_subdomains_in_one_process(oracle_lib, name, nranks, npx):
 def test_subdomains_global2_newton_mixing(oracle_lib, nranks, npx, schur_passes):
     """The bench workload split as the multi-GPU bench splits it (global 2 deg, Mixing = 1,
     default solver: block GS with 4 damped defect passes, T/S multigrid per subdomain;
-    npx = 0: the reference's Decomp2D, 2 x 2 and 4 x 2; schur_passes 2: the last two passes
-    without the Schur reduction): the distributed Newton step converges and solves the
+    npx = 0: the reference's Decomp2D, 2 x 2 and 4 x 2; schur_passes 2: the middle two
+    passes without the Schur reduction): the distributed Newton step converges and solves the
     linearised system of the whole problem."""
     from iemic.ocean import Ocean
     c = cf.preset("global2", mixing=1)

@@ -187,9 +187,10 @@ def test_block_gs_early_ts_matches_cpu(oracle_lib, Ocean, name, ts_at):
 
 @pytest.mark.parametrize("name,sp_k", [("global4", 1), ("global4", 3), ("global2", 0), ("global2", 3)])
 def test_block_gs_schur_passes_matches_cpu(oracle_lib, Ocean, name, sp_k):
-    """Only the first sp_k of the 4 dynamics passes solve the Schur system (the later
-    correction passes take pbar = 0, no Schur reduction or solve; 0: every pass) == the CPU
-    twin with the same schur_passes; and it differs from the default (the first 2)."""
+    """sp_k of the 4 dynamics passes solve the Schur system, the first sp_k - 1 and the last
+    (1: the first only; 0: every pass); the others take pbar = 0, no Schur reduction or solve.
+    == the CPU twin with the same schur_passes; and it differs from the default (2: the first
+    and the last)."""
     c, oc, o, L = make(Ocean, oracle_lib, name, mixing=1,
                        solver_params={"Preconditioner": 2, "Schur passes": sp_k})
     sp = oc.solver_params
