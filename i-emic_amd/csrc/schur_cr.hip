@@ -79,8 +79,45 @@ __global__ void k_cr_expand(const double* __restrict__ S9, const int* __restrict
  * trick), so the result is written out through the two permutations (row p_k of the
  * storage is row k of the inverse, storage column k is its column p_k).  The step loop is
  * unrolled over blocks of TR steps, so the register column of k is a compile-time index;
- * the pivot row's register row is selected under a branch on its row lane.  Two barriers
- * per step (the LDS vectors are double-buffered by step parity).  A zero pivot sets *info. */
+ * the pivot row's register row is selected under a branch on its row lane.
+ * One barrier per step (round 6; two before): the owners of column k + 1 write it to LDS and
+ * search its pivot right after their step-k update, and every thread takes the pivot row's
+ * entries of its own columns from the lane of thread (p's row lane, its column lane) -- the
+ * threads of one column lane are TR consecutive lanes of one wave -- by a cross-lane read
+ * instead of a second LDS round.  Same operations in the same order: the inverse is bitwise
+ * the two-barrier kernel's.  A zero pivot sets *info. */
+template <int TR, int RA, int RB>
+__device__ __forceinline__ void cr_inv_pivot(const double* cv, unsigned used, int m, int k, int tr,
+                                             double* __restrict__ pcol, int* __restrict__ s_p,
+                                             int* __restrict__ piv_row, int* __restrict__ step_of,
+                                             int* __restrict__ info)
+{
+    double best = -1.0;
+    int bi = m;
+#pragma unroll
+    for (int x = 0; x < RA; x++) {
+        const int i = tr + TR * x;
+        const double v = cv[x];
+        if (i < m) pcol[i] = v;
+        /* a NaN candidate counts as 0, so some unused row is always taken and step_of /
+         * piv_row stay a permutation (the zero pivot sets *info) */
+        const double av = (i < m && !((used >> x) & 1u)) ? (v == v ? fabs(v) : 0.0) : -1.0;
+        if (av > best) { best = av; bi = i; }
+    }
+#pragma unroll
+    for (int o = 1; o < TR; o <<= 1) {
+        const double ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (tr == 0) {
+        if (!(best > 0.0)) *info = 1;
+        *s_p = bi;
+        piv_row[k] = bi;
+        step_of[bi < m ? bi : 0] = k;
+    }
+}
+
 template <int TR, int RA, int RB>
 __global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ src, int s0, int sstep,
                                                      double* __restrict__ dst, int m, int* __restrict__ info)
@@ -89,7 +126,8 @@ __global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ s
     const double* A = src + (size_t)(s0 + blockIdx.x * sstep) * mm;
     double* X = dst + (size_t)blockIdx.x * mm;
     const int t = threadIdx.x, tr = t % TR, tc = t / TR;
-    __shared__ double pcol[2][TR * RA], prow[2][32 * RB];
+    const int lbase = (t & 63) - tr;                    /* lane of thread (0, tc) in this wave */
+    __shared__ double pcol[2][TR * RA];
     __shared__ int s_p[2];
     __shared__ int piv_row[TR * RA], step_of[TR * RA];
     double a[RA][RB];
@@ -101,65 +139,43 @@ __global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ s
             a[x][y] = (i < m && j < m) ? A[i + (size_t)j * m] : 0.0;
         }
     unsigned used = 0;                                 /* bit x: row tr + TR x was a pivot */
+    if (tc == 0) {                                     /* column 0: LDS and its pivot */
+        double cv[RA];
+#pragma unroll
+        for (int x = 0; x < RA; x++) cv[x] = a[x][0];
+        cr_inv_pivot<TR, RA, RB>(cv, used, m, 0, tr, pcol[0], &s_p[0], piv_row, step_of, info);
+    }
 #pragma unroll
     for (int kbr = 0; kbr < RA; kbr++) {
         const int yk = kbr * TR / 32;                   /* register column of k (compile time) */
+        const int ykn = ((kbr + 1) * TR / 32) < RB ? (kbr + 1) * TR / 32 : RB - 1;   /* of the next block's first */
         for (int kk = 0; kk < TR; kk++) {
             const int k = kbr * TR + kk;
             if (k >= m) break;
             const int sel = k & 1, kc = k & 31;
-            /* 1. pivot search in column k (TR lanes of one wave), column k -> LDS */
-            if (tc == kc) {
-                double best = -1.0;
-                int bi = m;
-#pragma unroll
-                for (int x = 0; x < RA; x++) {
-                    const int i = tr + TR * x;
-                    const double v = a[x][yk];
-                    if (i < m) pcol[sel][i] = v;
-                    /* a NaN candidate counts as 0, so some unused row is always taken and
-                     * step_of / piv_row stay a permutation (the zero pivot sets *info) */
-                    const double av = (i < m && !((used >> x) & 1u)) ? (v == v ? fabs(v) : 0.0) : -1.0;
-                    if (av > best) { best = av; bi = i; }
-                }
-#pragma unroll
-                for (int o = 1; o < TR; o <<= 1) {
-                    const double ob = __shfl_xor(best, o, 64);
-                    const int oi = __shfl_xor(bi, o, 64);
-                    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-                }
-                if (tr == 0) {
-                    if (!(best > 0.0)) *info = 1;
-                    s_p[sel] = bi;
-                    piv_row[k] = bi;
-                    step_of[bi < m ? bi : 0] = k;
-                }
-            }
-            __syncthreads();
+            __syncthreads();                            /* column k and its pivot in LDS */
             const int p = __builtin_amdgcn_readfirstlane(s_p[sel]);
             const int pr = p % TR, pa = p / TR;
-            /* 2. row p -> LDS */
-            if (tr == pr) {
-                used |= 1u << pa;
+            if (tr == pr) used |= 1u << pa;
+            /* the pivot row's entries of this thread's columns: thread (pr, tc)'s registers */
+            double prw[RB];
 #pragma unroll
-                for (int x = 0; x < RA; x++)
-                    if (x == pa)
+            for (int y = 0; y < RB; y++) {
+                double mine = a[0][y];
 #pragma unroll
-                        for (int y = 0; y < RB; y++) {
-                            const int j = tc + 32 * y;
-                            if (j < m) prow[sel][j] = a[x][y];
-                        }
+                for (int x = 1; x < RA; x++)
+                    if (x == pa) mine = a[x][y];
+                prw[y] = __shfl(mine, lbase + pr, 64);
             }
-            __syncthreads();
-            /* 3. scale row p, eliminate column k from the other rows; column k keeps the
+            /* scale row p, eliminate column k from the other rows; column k keeps the
              * inverse's column (1 / piv in row p, -a(i, k) / piv elsewhere) */
-            const double piv = prow[sel][k];
+            const double piv = pcol[sel][p];
             const double inv = piv != 0.0 ? 1.0 / piv : 0.0;
             double pr_s[RB];
 #pragma unroll
             for (int y = 0; y < RB; y++) {
                 const int j = tc + 32 * y;
-                pr_s[y] = j < m ? prow[sel][j] * inv : 0.0;
+                pr_s[y] = j < m ? prw[y] * inv : 0.0;
             }
             const bool colk = tc == kc;
 #pragma unroll
@@ -178,6 +194,14 @@ __global__ void __launch_bounds__(32 * TR) k_cr_inv(const double* __restrict__ s
                     if (x == pa)
 #pragma unroll
                         for (int y = 0; y < RB; y++) a[x][y] = (y == yk && colk) ? inv : pr_s[y];
+            }
+            /* column k + 1 (updated above) to LDS and its pivot, by its owners */
+            if (k + 1 < m && tc == ((k + 1) & 31)) {
+                double cv[RA];
+#pragma unroll
+                for (int x = 0; x < RA; x++) cv[x] = kk + 1 < TR ? a[x][yk] : a[x][ykn];
+                cr_inv_pivot<TR, RA, RB>(cv, used, m, k + 1, tr, pcol[sel ^ 1], &s_p[sel ^ 1], piv_row,
+                                         step_of, info);
             }
         }
     }

@@ -16,7 +16,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("IEMIC_LIB", "libiemic_amd.so"))
 
 IEMIC_ENODEV = -19
-ABI_VERSION = 5             # IEMIC_ABI_VERSION of include/iemic.h this binding mirrors
+ABI_VERSION = 6             # IEMIC_ABI_VERSION of include/iemic.h this binding mirrors
 IEMIC_ENOCONV = 1           # iemic_newton_step: applied, but the solve missed its tolerance
 
 

@@ -47,7 +47,7 @@ extern "C" {
  * size or meaning (5: iemic_solve_info gained `safeguard` in round 4, the device vector
  * algebra of round 5); a caller built against another header must refuse to run:
  *   if (iemic_abi_version() != IEMIC_ABI_VERSION) abort(); */
-#define IEMIC_ABI_VERSION 5
+#define IEMIC_ABI_VERSION 6
 int iemic_abi_version(void);
 
 typedef struct iemic_ctx iemic_ctx;
