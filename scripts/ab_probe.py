@@ -39,7 +39,7 @@ def main():
         return
     x0 = torch.from_numpy(x).cuda()
     L_ = _lib.lib()
-    times, iters, prec, f1 = [], [], [], None
+    times, iters, prec, f1, sp = [], [], [], None, []
     for q in range(nsteps + 1):
         _lib.check(L_.iemic_set_state_dev(oc._h, x0.data_ptr()), "set_state_dev")
         torch.cuda.synchronize()
@@ -50,12 +50,15 @@ def main():
             times.append((time.perf_counter() - t) * 1e3)
             iters.append(info.solve.iters)
             prec.append(info.t_prec_ms)
+            if info.solve.n_spmv:
+                sp.append(info.solve.t_spmv_ms * 1e3 / info.solve.n_spmv)
             f1 = info.norm_f1
     out["newton_ms"] = round(float(np.median(times)), 2)
     out["newton_ms_all"] = [round(t, 2) for t in times]
     out["fgmres_iters"] = iters
     out["prec_setup_ms"] = round(float(np.median(prec)), 3)
     out["norm_f1"] = repr(f1)
+    out["spmv_insolve_us"] = round(float(np.median(sp)), 2) if sp else None
     print(json.dumps(out), flush=True)
 
 
