@@ -35,8 +35,6 @@ namespace iemic {
  * wave per equation (24/22/7/11/20/20), so the waves of a tile finish together; their row
  * partials meet in LDS and the 384 results of the tile are stored contiguously. */
 constexpr int SP7_T = 64;
-/* the in-solve SpMV as the persistent k_spmv7p (true) or one workgroup per tile, k_spmv7c */
-constexpr bool SP7_PERSIST = true;
 __host__ __device__ constexpr int sp7_row(int s)
 {
     return s < 24 ? 0 : s < 46 ? 1 : s < 53 ? 2 : s < 64 ? 3 : s < 84 ? 4 : 5;
@@ -260,132 +258,6 @@ __global__ void __launch_bounds__(256) k_spmv7c(SubLay X, const double* __restri
         default: vv = red[3][1][cc]; break;
         }
         y[(int64_t)NUN * a0 + o] = vv;
-    }
-}
-
-/* k_spmv7p: k_spmv7c as a persistent kernel (round 6).  The grid is what the chip holds at
- * once (5 workgroups per CU); each workgroup walks the active tiles of its XCD's contiguous
- * run with a stride, and issues the next tile's coefficient loads and x staging (all of it by
- * LDS-DMA, the end cells too: no load waits for a register) as soon as the current tile's
- * products are in LDS, so they stream while the current tile's rows are summed and written,
- * and no workgroup is launched per tile.  Same sums in the same order: bitwise k_spmv7c. */
-struct Sp7Tile {
-    int tile, clo, chi, a0, na;
-    uint64_t amask;
-};
-__device__ __forceinline__ Sp7Tile sp7_tile(const int4* __restrict__ atl, int pos)
-{
-    const int4 td = atl[2 * pos], tm = atl[2 * pos + 1];
-    Sp7Tile T;
-    T.tile = td.x;
-    T.clo = td.y & 255;
-    T.chi = td.y >> 8;
-    T.a0 = td.z;
-    T.na = td.w;
-    T.amask = (uint64_t)(uint32_t)tm.x | ((uint64_t)(uint32_t)tm.y << 32);
-    return T;
-}
-/* the tile's coefficient loads into v and its x image into xs (interior runs and end cells by
- * LDS-DMA); lof: active cell -> lane */
-__device__ __forceinline__ void sp7_issue(const SubLay& X, const double* __restrict__ spc,
-                                          const double* __restrict__ x, const Sp7Tile& T, int tpr, int t,
-                                          int g, double* v, double* xs, int* lof)
-{
-    asm volatile("" : "+v"(t));                             /* lane addresses formed per tile */
-    const int l = X.l, nx = X.nx, c = t & 63, lane = t & 63;
-    const int row = T.tile / tpr, i0 = (T.tile - row * tpr) * SP7_T;
-    const int k = row % l, jl = row / l, j = X.jb0 + jl;
-    const int nc = min(SP7_T, nx - i0);
-    const bool act = (T.amask >> c) & 1;
-    const int cm = act ? __builtin_popcountll(T.amask & ((1ull << c) - 1)) : -1;
-    if (g == 0 && act) lof[cm] = c;
-    const double* vb = spc + (int64_t)NSLOT * T.a0;
-    const int64_t vs = T.na, vo = cm;
-    if (g == 0) sp7_load<0, 26>(vb, vs, vo, act, v);
-    else if (g == 1) sp7_load<26, 52>(vb, vs, vo, act, v);
-    else if (g == 2) sp7_load<52, 78>(vb, vs, vo, act, v);
-    else sp7_load<78, 104>(vb, vs, vo, act, v);
-    const int jm = j > 0 ? j - 1 : j, jp = j < X.m - 1 ? j + 1 : j;
-    const int km = k > 0 ? k - 1 : k, kp = k < l - 1 ? k + 1 : k;
-    const int rj[6] = {jm, j, jp, j, j, jp}, rk[6] = {k, k, k, km, kp, km};
-    const int nb = nc * NUN * 8;
-    const int blo = max(0, (T.clo - 1) * NUN * 8), bhi = min(nb, (T.chi + 2) * NUN * 8);
-    for (int u = g; u < 18; u += 4) {
-        const int q = u / 3, h = u - 3 * q;
-        if (h * 1024 >= bhi || (h + 1) * 1024 <= blo) continue;        /* wave-uniform */
-        const int byte = h * 1024 + lane * 16;
-        const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
-        if (byte < nb)
-            __builtin_amdgcn_global_load_lds((glb_void*)(x + NUN * (r * nx + i0) + byte / 8),
-                                             (lds_void*)(xs + (q * (SP7_T + 2) + 1) * NUN + h * 128), 16, 0, 0);
-    }
-    /* end cells: (row q, side) pair u holds 6 doubles = 12 dwords, lanes 0..11 one dword each */
-    for (int u = g; u < 12; u += 4) {
-        const int q = u >> 1, side = u & 1;
-        const int p = side ? nc + 1 : 0;
-        const int64_t r = (int64_t)(rj[q] - X.jb0 + HALO) * l + rk[q];
-        const int64_t cell = xnb_cell(r, i0 + p - 1, X.n, X.ib0, nx, X.hx, X.periodic, X.xb);
-        if (lane < 12)
-            __builtin_amdgcn_global_load_lds((glb_void*)((const float*)(x + NUN * cell) + lane),
-                                             (lds_void*)(xs + (q * (SP7_T + 2) + p) * NUN), 4, 0, 0);
-    }
-}
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_spmv7p(SubLay X, const double* __restrict__ spc,
-                                                const double* __restrict__ x, double* __restrict__ y,
-                                                const int4* __restrict__ atl, int natile, int tpr)
-{
-    __shared__ double xs[6 * (SP7_T + 2) * NUN];
-    __shared__ double red[4][3][SP7_T];
-    __shared__ int lof[2][SP7_T];
-    const int per = (natile + 7) >> 3;
-    const int nbx = (int)(gridDim.x >> 3);
-    const int base = (int)(blockIdx.x & 7) * per, end = min(base + per, natile);
-    int pos = base + (int)(blockIdx.x >> 3);
-    if (pos >= end) return;
-    const int t = threadIdx.x, c = t & 63;
-    const int g = __builtin_amdgcn_readfirstlane(t >> 6);   /* wave-uniform: scalar branches */
-    double v[26];
-    Sp7Tile T = sp7_tile(atl, pos);
-    sp7_issue(X, spc, x, T, tpr, t, g, v, xs, lof[0]);
-    int par = 0;
-    for (;;) {
-        __syncthreads();                                    /* tile pos: v, xs and lof landed */
-        const int pn = pos + nbx;
-        const bool more = pn < end;
-        int cl = c;
-        asm volatile("" : "+v"(cl));                        /* no lane addresses hoisted out of the loop */
-        const bool act = (T.amask >> cl) & 1;
-        double acc[3] = {0.0, 0.0, 0.0};
-        if (act) {
-            if (g == 0) sp7_compute<0, 26>(v, xs, cl, acc);
-            else if (g == 1) sp7_compute<26, 52>(v, xs, cl, acc);
-            else if (g == 2) sp7_compute<52, 78>(v, xs, cl, acc);
-            else sp7_compute<78, 104>(v, xs, cl, acc);
-        }
-#pragma unroll
-        for (int q = 0; q < 3; q++) red[g][q][cl] = acc[q];
-        __syncthreads();                                    /* partials in LDS, xs free */
-        /* this tile's rows, then the next tile's loads (v is dead while the rows are summed) */
-        const int* lo = lof[par];
-        for (int o = t; o < T.na * NUN; o += 256) {
-            const int ac = o / NUN, R = o - ac * NUN;
-            const int cc = lo[ac];
-            double vv;
-            switch (R) {
-            case 0: vv = red[0][0][cc]; break;
-            case 1: vv = red[0][1][cc] + red[1][0][cc]; break;
-            case 2: vv = red[1][1][cc] + red[2][0][cc]; break;
-            case 3: vv = red[2][1][cc]; break;
-            case 4: vv = red[2][2][cc] + red[3][0][cc]; break;
-            default: vv = red[3][1][cc]; break;
-            }
-            y[(int64_t)NUN * T.a0 + o] = vv;
-        }
-        if (!more) break;
-        pos = pn;
-        T = sp7_tile(atl, pn);
-        par ^= 1;
-        sp7_issue(X, spc, x, T, tpr, t, g, v, xs, lof[par]);
     }
 }
 
@@ -1002,20 +874,7 @@ int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t ev0, hip
     }
     hipStream_t s = c->stream;
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
-    if (gs.natile > 0 && SP7_PERSIST) {
-        /* the workgroups the chip holds at once, a multiple of the 8 XCDs */
-        static int resident = 0;
-        if (!resident) {
-            int occ = 0, ncu = 0, dev = 0;
-            HIP_OK(hipGetDevice(&dev));
-            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spmv7p, 256, 0));
-            HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            resident = std::max(8, (occ * ncu) / 8 * 8);
-        }
-        const unsigned grid = (unsigned)std::min<int64_t>(resident, 8 * (int64_t)((gs.natile + 7) / 8));
-        hipExtLaunchKernelGGL(k_spmv7p, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c), (const double*)gs.spc.p,
-                              x, yc, (const int4*)gs.atl.p, gs.natile, tpr);
-    } else if (gs.natile > 0) {
+    if (gs.natile > 0) {
         const unsigned grid = 8u * (unsigned)((gs.natile + 7) / 8);
         hipExtLaunchKernelGGL(k_spmv7c, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c), (const double*)gs.spc.p,
                               x, yc, (const int4*)gs.atl.p, gs.natile, tpr);

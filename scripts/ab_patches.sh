@@ -29,8 +29,7 @@
 # | dyn_occ5 | defect capped at 5 waves per SIMD | rejected (slower) | round 5 (f500835) |
 # | dyn_t | load-policy flips (temporal / non-temporal) | the tree keeps the faster policy of each | round 4 |
 # | upd_fit | DCGS2 update pass on a grid fitted to the compressed basis | adopted (117.3 -> 117.1 ms) | round 6 (54c7f0e) |
-# | sp7c | the in-solve SpMV as one workgroup per tile (k_spmv7c) instead of the persistent k_spmv7p | A/B | round 6 |
-# | sp7p4 | the persistent SpMV without the 5-waves cap (106 VGPRs, 4 waves per SIMD, no spill) | A/B | round 6 |
+# | rev:180a20a | the in-solve SpMV as a persistent kernel (k_spmv7p; its patches sp7c / sp7p4 there) | rejected: 33.3-34.1 vs 29.1 us per launch | round 6 (180a20a) |
 # | dot1_e2 (re-test) | 2 elements per lane on the compressed basis (709 workgroups) | rejected (117.3 -> 118.7 ms) | round 6 (54c7f0e) |
 # | gemvw_t | load-policy flips (temporal / non-temporal) | the tree keeps the faster policy of each | round 4 |
 # | mg_unfused | coarse T/S levels by the unfused launches (k_mg_zl + k_mg_rc) | the fused k_mg_dn / k_mg_up adopted | round 5 (f500835) |
@@ -52,17 +51,6 @@
 #
 # usage: (cd <copy>/i-emic_amd && bash <repo>/scripts/ab_patches.sh <variant>)
 set -e
-
-ab_sp7c() {
-# the in-solve SpMV as one workgroup per tile (k_spmv7c)
-sed -i 's/^constexpr bool SP7_PERSIST = true;/constexpr bool SP7_PERSIST = false;/' csrc/krylov.hip
-grep -q "SP7_PERSIST = false" csrc/krylov.hip
-}
-
-ab_sp7p4() {
-# the persistent SpMV without the 5-waves-per-SIMD cap
-sed -i 's/__attribute__((amdgpu_waves_per_eu(5, 8))) k_spmv7p/k_spmv7p/' csrc/krylov.hip
-}
 
 ab_bts_t() {
 # T/S right-hand side coefficients with the default (temporal) load policy
