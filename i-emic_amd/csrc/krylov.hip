@@ -874,11 +874,10 @@ int spmv_kernel_c(iemic_ctx* c, const double* x, double* yc, hipEvent_t ev0, hip
     }
     hipStream_t s = c->stream;
     const int tpr = (c->nx + SP7_T - 1) / SP7_T;
-    if (gs.natile > 0) {
-        const unsigned grid = 8u * (unsigned)((gs.natile + 7) / 8);
+    const unsigned grid = 8u * (unsigned)((gs.natile + 7) / 8);
+    if (gs.natile > 0)
         hipExtLaunchKernelGGL(k_spmv7c, dim3(grid), dim3(256), 0, s, ev0, ev1, 0, sub_lay(c), (const double*)gs.spc.p,
                               x, yc, (const int4*)gs.atl.p, gs.natile, tpr);
-    }
     double* yr = nullptr;
     if (c->rowintcon >= 0) {
         if (c->gs.ric < 0) {
