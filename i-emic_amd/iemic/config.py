@@ -75,6 +75,7 @@ class THCMConfig:
     integral_j: int = -1
     coupled_t: int = 0            # "Coupled Temperature" (coupled_T, THCM.C:232)
     coupled_s: int = 0            # "Coupled Salinity" (coupled_S)
+    fix_pressure_points: bool = False  # "Fix Pressure Points" (THCM.C:2201-2238): not restated
     refine: int = 1               # synthetic horizontal refinement of the mask
     refine_l: int = 0             # target layer count for vertical remap (0: none)
     start_params: Dict[str, float] = dataclasses.field(default_factory=dict)
@@ -86,6 +87,15 @@ class THCMConfig:
     @property
     def nrows(self) -> int:
         return NUN * self.ncell
+
+    def validate(self) -> None:
+        """Refuse, by name, the THCM options the device library does not restate (the model
+        would otherwise silently run another problem)."""
+        if self.fix_pressure_points:
+            raise NotImplementedError(
+                "THCM 'Fix Pressure Points' (THCM::fixPressurePoints, THCM.C:2201-2238) is not "
+                "restated: the device model pins the pressure null space in the Schur solve "
+                "instead; every reference run XML leaves it false (THCM.C:2792)")
 
     def par_list(self):
         """(index, value) pairs of the starting parameters, THCM::setParameter order."""

@@ -130,6 +130,7 @@ class Ocean:
         in-process test facility.  npx: x parts (0: the reference's Decomp2D factorisation,
         1: latitude bands, the default on every transport: x cuts through the zonal flow cost
         FGMRES steps)."""
+        cfg.validate()
         self.cfg = cfg
         L = landmask(cfg) if landm is None else landm
         L = np.ascontiguousarray(L, dtype=np.int32).reshape(-1)
