@@ -105,7 +105,7 @@ def parse():
     p.add_argument("--idr-s", type=int, default=4)
     p.add_argument("--dyn-iters", type=int, default=None,
                    help="defect-correction passes on the dynamics block of the block GS (default 4; "
-                        "6 at 1 degree, where the passes without the Schur solve pay: DESIGN.md section 4)")
+                        "8 at 1 degree, where the passes without the Schur solve pay: DESIGN.md section 4)")
     p.add_argument("--dyn-omega", type=float, default=0.95, help="step of the correction passes")
     p.add_argument("--dyn-mr", action="store_true", help="minimal-residual step per pass")
     p.add_argument("--ts-mg", type=int, default=1,
@@ -142,7 +142,7 @@ def parse():
                    help="FGMRES iterations of the bounded CPU sample (--mode continuation)")
     a = p.parse_args()
     if a.dyn_iters is None:
-        a.dyn_iters = 6 if a.config == "global1" else 4
+        a.dyn_iters = 8 if a.config == "global1" else 4
     return a
 
 
