@@ -841,7 +841,7 @@ def bench_newton(args, R: Ranks):
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
                    "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
-                   "schur": "cyclic reduction (fp64, exact)",
+                   "schur": ("cyclic reduction (fp64, exact)" + (f" in {args.schur_passes} of the {args.dyn_iters} dynamics passes (the first {args.schur_passes - 1} and the last)" if 0 < args.schur_passes < args.dyn_iters else "")),
                    "state": (f"branch (bench_data/{args.config}_cf05.npz, CF 0.5)" if state == "branch"
                              else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
