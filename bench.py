@@ -146,6 +146,15 @@ def parse():
     return a
 
 
+def schur_where(k, n):
+    """which of the n dynamics passes solve the Schur system (iemic_krylov.schur_passes k)"""
+    if k <= 0 or k >= n:
+        return ", every dynamics pass"
+    if k == 1:
+        return f", the first of the {n} dynamics passes only"
+    return f", {k} of the {n} dynamics passes (the first {k - 1} and the last)"
+
+
 def quiet_cores(n, dt=0.5):
     """n CPUs of this process's affinity mask on n distinct physical cores, the least busy
     ones over dt seconds of /proc/stat (a shared host's other jobs load some cores: pinning the
@@ -841,7 +850,7 @@ def bench_newton(args, R: Ranks):
                    "krylov_dim": args.krylov, "restarts": args.restarts, "orth": args.orth,
                    "solver": args.solver if args.solver == "FGMRES" else f"IDR({args.idr_s})",
                    "ts_sweeps": args.ts_sweeps, "dyn_iters": args.dyn_iters, "dyn_omega": args.dyn_omega, "dyn_mr": args.dyn_mr,
-                   "schur": ("cyclic reduction (fp64, exact)" + (f" in {args.schur_passes} of the {args.dyn_iters} dynamics passes (the first {args.schur_passes - 1} and the last)" if 0 < args.schur_passes < args.dyn_iters else "")),
+                   "schur": "cyclic reduction (fp64, exact)" + schur_where(args.schur_passes, args.dyn_iters),
                    "state": (f"branch (bench_data/{args.config}_cf05.npz, CF 0.5)" if state == "branch"
                              else f"synthetic (splitmix64 seed 20261015, T/S amp {args.amp_ts:g})"),
                    "ts_mg": args.ts_mg, "mg_sweeps": args.mg_sweeps, "ts_at": args.ts_at,
