@@ -152,7 +152,8 @@ def schur_where(k, n):
         return ", every dynamics pass"
     if k == 1:
         return f", the first of the {n} dynamics passes only"
-    return f", {k} of the {n} dynamics passes (the first {k - 1} and the last)"
+    first = "the first" if k == 2 else f"the first {k - 1}"
+    return f", {k} of the {n} dynamics passes ({first} and the last)"
 
 
 def quiet_cores(n, dt=0.5):
