@@ -935,7 +935,14 @@ static void dyn_gmres(gs_t* g, double* z)
         double* zj = Z + (int64_t)j * N;
         double* w = V + (int64_t)(j + 1) * N;
         memset(zj, 0, sizeof(double) * N);
+        {
+            /* the Schur solve in the applications schur_passes selects (gs_pass_schur) */
+            const int kk = g->schur_passes, last = j + 1 == k;
+            const int solve = j == 0 || kk <= 0 || kk >= k || (kk >= 2 && (j < kk - 1 || last));
+            g->skip_schur = !solve;
+        }
         dyn_solve(g, vj, zj);
+        g->skip_schur = 0;
         /* w = A_DD zj: the defect of zj against a zero right-hand side, negated */
         double* rrs = g->rr;
         static double* zero = NULL;
