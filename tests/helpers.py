@@ -184,3 +184,12 @@ def emul_get_deps(e: "Emul") -> np.ndarray:
     e.lib.emul_get_deps.argtypes = [C.c_void_p, P(C.c_double)]
     e.lib.emul_get_deps(e.h, _lib.ptr(out))
     return out
+
+
+def free_port() -> int:
+    """A TCP port nothing listens on now (for gloo rendezvous on 127.0.0.1): fixed ports
+    collide when several test workers (pytest -n) start process groups at once."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]

@@ -110,7 +110,8 @@ def _worker(rank, nranks, npx, name, port, q):
 def test_subdomain_assembly_matches_oracle(oracle_lib, emul, name, nranks, npx):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29600 + 10 * nranks + npx + (hash(name) % 100)
+    from helpers import free_port
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, nranks, npx, name, port, q)) for r in range(nranks)]
     for p in procs:
         p.start()

@@ -18,7 +18,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from helpers import golden_landm, mask_fix
+from helpers import free_port, golden_landm, mask_fix
 from iemic import config as cf
 
 pytestmark = pytest.mark.gpu
@@ -250,7 +250,8 @@ def test_rccl_ranks(oracle_lib, npx):
         pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, npx, 29811 + npx, q)) for r in range(2)]
+    port = free_port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, npx, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
@@ -319,7 +320,8 @@ def test_transport_processes(oracle_lib, name, nranks, npx):
     gathered update solves the whole linearised system to 1e-8."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_transport_worker, args=(r, nranks, npx, name, 29830 + nranks, q))
+    port = free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, nranks, npx, name, port, q))
              for r in range(nranks)]
     for p in procs:
         p.start()
