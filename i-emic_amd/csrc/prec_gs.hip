@@ -3438,7 +3438,6 @@ int gs_compute(iemic_ctx* c, const iemic_krylov* opt)
                         tl.insert(tl.end(), {(int)(row * tpr + ti), lo | (hi << 8), a0, na, (int)(uint32_t)mask,
                                              (int)(uint32_t)(mask >> 32), 0, 0});
                     }
-                spmv_tiles_by_xcd(tl, ap);
                 gs.natile = (int)(tl.size() / 8);
                 if (gs.atl.n < tl.size() + 8 && gs.atl.alloc(tl.size() + 8)) return IEMIC_ENOMEM;
                 if (!tl.empty() && (rc = h2d(c, gs.atl.p, tl.data(), sizeof(int) * tl.size()))) return rc;
